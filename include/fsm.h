@@ -1,0 +1,147 @@
+/*
+ * fsm.h — C ABI of the MI355X spark-fsm engine (libfsm.so).
+ *
+ * This is the drop-in boundary for the two hot-path entry points of the
+ * reference (paths relative to /root/reference/src/main/scala/de/kp/spark/fsm):
+ *
+ *   SPADE.extractRDDPatterns(dataset: RDD[(Int,String)], support: Double,
+ *                            dfs: Boolean = true, stats: Boolean = true)
+ *       : List[de.kp.core.spade.Pattern]                       SPADE.scala:36
+ *     -> fsm_db_from_spmf(ctx, FSM_MODE_SPADE, ...) + fsm_spade_mine(...)
+ *
+ *   TSR.extractRDDRules(dataset: RDD[(Int,String)], k: Int, minconf: Double)
+ *       : List[de.kp.core.tsr.Rule]                            TSR.scala:31
+ *     -> fsm_db_from_spmf(ctx, FSM_MODE_TSR, ...) + fsm_tsr_mine(...)
+ *
+ * The JVM side collects the RDD once (sids + SPMF lines) and hands plain
+ * arrays across; see INTEGRATION.md for the JNI binding.  No C++ exception
+ * crosses this boundary: every entry point returns 0 on success or a nonzero
+ * FSM_E* code, with a message in fsm_last_error(ctx).  Parse errors that make
+ * the reference throw (SPADE.scala:161-168,194; TSR.scala:41,135) return
+ * FSM_EPARSE, which the Scala shim rethrows as a java.lang.Exception so that
+ * TrainActor (TrainActor.scala:65-67) records FAILURE exactly as today.
+ *
+ * Ownership: input arrays are borrowed for the duration of the call; result
+ * objects are owned by the library until freed.  Threading: calls block; a
+ * context owns its HIP stream and device buffers; distinct contexts may be
+ * used from distinct threads (the reference runs concurrent requests on one
+ * SparkContext, RequestContext.scala:30).
+ */
+#ifndef SPARK_FSM_AMD_FSM_H
+#define SPARK_FSM_AMD_FSM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSM_ABI_VERSION 1
+
+/* status codes */
+#define FSM_OK 0
+#define FSM_EINVAL 1    /* invalid argument (null pointer, k < 1, bad mode, ...) */
+#define FSM_EPARSE 2    /* input the reference would throw on (SPADE.scala:161-194, TSR.scala:41-135) */
+#define FSM_EDEVICE 3   /* HIP runtime / kernel failure, or no usable gfx950 device */
+#define FSM_ENOMEM 4    /* host or device allocation failed */
+#define FSM_ECOMM 5     /* RCCL failure (multi-GPU) */
+#define FSM_ELIMIT 6    /* input exceeds an engine limit (e.g. > 4096 eids per sequence) */
+
+typedef struct fsm_ctx fsm_ctx;
+typedef struct fsm_db fsm_db;
+
+typedef enum { FSM_MODE_SPADE = 0, FSM_MODE_TSR = 1 } fsm_mode;
+
+typedef struct {
+    int32_t device;          /* local HIP device ordinal */
+    int32_t nranks;          /* 1: single GPU; >1: SPADE prefix classes sharded over ranks */
+    int32_t rank;            /* this process's rank in [0, nranks) */
+    int32_t verbose;         /* 1: per-level trace on stderr */
+    uint8_t unique_id[128];  /* RCCL unique id (fsm_comm_unique_id on rank 0), nranks > 1 */
+    int64_t mem_budget;      /* device bytes for lattice frontier slabs; 0 = 1/2 of free HBM */
+} fsm_opts;
+
+/* SPADE result: the patterns of List[Pattern] in CSR form.  Pattern p has
+ * itemsets set_off[pat_off[p]] .. set_off[pat_off[p+1]]; itemset s has items
+ * items[set_off[s]] .. items[set_off[s+1]] in ascending order.  Pattern order is
+ * the engine's discovery order (the reference's is also discovery order). */
+typedef struct {
+    int64_t n;
+    int32_t* support;        /* absolute support (#sequence ids) */
+    int64_t* pat_off;        /* [n+1] */
+    int64_t* set_off;        /* [n_sets+1] */
+    int32_t* items;          /* [n_items] */
+    int64_t n_sets;
+    int64_t n_items;
+    int64_t total;           /* sequences.count() of the input (SPADE.scala:46) */
+    int32_t minsup;          /* absolute threshold max(1, ceil(support*total)) */
+} fsm_patterns;
+
+/* TSR result: the rules of List[Rule] (getItemset1/getItemset2,
+ * getAbsoluteSupport, getConfidence, TSRActor.scala:55-59). */
+typedef struct {
+    int64_t n;
+    int32_t* support;        /* getAbsoluteSupport */
+    double* confidence;      /* getConfidence */
+    int64_t* ante_off;       /* [n+1] */
+    int32_t* ante;           /* getItemset1 */
+    int64_t* cons_off;       /* [n+1] */
+    int32_t* cons;           /* getItemset2 */
+    int64_t total;           /* number of input sequences (TSRActor.scala:52) */
+    int32_t final_minsup;
+} fsm_rules;
+
+/* Replaces algorithm.printStatistics() (SPADE.scala:136). */
+typedef struct {
+    int64_t joins;              /* candidate id-list joins per SURVEY A.2 (incl. infrequent) */
+    int64_t patterns;           /* frequent patterns found */
+    int64_t classes;            /* prefix equivalence classes processed */
+    int64_t batches;            /* class batches (kernel rounds) */
+    int64_t entries;            /* class-row entries streamed by the count kernel */
+    int64_t bytes_join_equiv;   /* sum 12*(|Li|+|Lj|) + 12*|Lout| */
+    int64_t bytes_streamed;     /* bytes the count+emit kernels read/write once per entry */
+    int64_t expansions;         /* TSR: expandL + expandR evaluations */
+    int64_t rules;              /* TSR: rules returned */
+    double ms_flatten;          /* host parse + flatten (fsm_db_*) */
+    double ms_upload;           /* host -> HBM copy of the flattened DB */
+    double ms_f1;               /* SPADE: F1 histogram + root row filter */
+    double ms_f2;               /* SPADE: root pair-count matrix (F2) */
+    double ms_lattice;          /* SPADE: class batches below the root */
+    double ms_mine;             /* whole fsm_*_mine call */
+    double ms_count_kernel;     /* device time of the class pair-count kernel */
+    double ms_emit_kernel;      /* device time of the child-row emission kernel */
+    int64_t count_launches;
+    int64_t mask_words;         /* W: u64 words per eid mask of this DB */
+    int64_t bytes_count_alg;    /* count kernel algorithmic bytes: entries * (12 + 8W) */
+} fsm_stats;
+
+int fsm_abi_version(void);
+int fsm_comm_unique_id(uint8_t out[128]);
+
+int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out);
+void fsm_ctx_destroy(fsm_ctx* ctx);
+const char* fsm_last_error(const fsm_ctx* ctx);
+int fsm_get_stats(const fsm_ctx* ctx, fsm_stats* out);
+
+/* Flatten an SPMF-format dataset (one line per sequence id, as produced by
+ * SPMFHandler.sequence2SPMF) once and upload it to HBM.  mode selects the
+ * reference parser: SPADE.scala:145-212 or TSR.scala:41,109-143. */
+int fsm_db_from_spmf(fsm_ctx* ctx, int32_t mode, const int32_t* sids, const char* const* lines,
+                     const int64_t* lens, int64_t n, fsm_db** out);
+/* Pre-tokenized variant: sequence r has tokens tokens[seq_off[r] .. seq_off[r+1]]
+ * where -1 ends an itemset, -2 ends the sequence, other values are items
+ * (implicit timestamps 1,2,3,...). */
+int fsm_db_from_tokens(fsm_ctx* ctx, int32_t mode, const int32_t* sids, const int64_t* seq_off,
+                       const int64_t* tokens, int64_t n, fsm_db** out);
+void fsm_db_free(fsm_db* db);
+
+int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_patterns** out);
+void fsm_patterns_free(fsm_patterns* p);
+
+int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** out);
+void fsm_rules_free(fsm_rules* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,79 @@
+// device_util.hip — three-phase exclusive scan (tile scan -> scan of tile sums
+// -> add), 2048 elements per 256-thread tile, wave64 shuffles + LDS.
+#include "device_util.h"
+
+namespace fsm {
+namespace {
+
+constexpr int kScanT = 256;
+constexpr int kScanV = 8;
+constexpr int kScanTile = kScanT * kScanV;
+
+template <class T>
+__global__ __launch_bounds__(kScanT) void k_scan_tile(const T* __restrict__ in, uint64_t* __restrict__ out,
+                                                      uint64_t* __restrict__ tile_sum, size_t n) {
+    __shared__ uint64_t wsum[kScanT / 64];
+    const size_t base = size_t(blockIdx.x) * kScanTile + size_t(threadIdx.x) * kScanV;
+    uint64_t v[kScanV];
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanV; ++k) {
+        const size_t i = base + size_t(k);
+        v[k] = i < n ? uint64_t(in[i]) : 0ull;
+        s += v[k];
+    }
+    const uint64_t incl = wave_incl_scan(s);
+    const unsigned wave = threadIdx.x >> 6;
+    if (lane_id() == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t woff = 0;
+    for (unsigned w = 0; w < wave; ++w) woff += wsum[w];
+    uint64_t run = woff + incl - s;
+#pragma unroll
+    for (int k = 0; k < kScanV; ++k) {
+        const size_t i = base + size_t(k);
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == kScanT - 1) tile_sum[blockIdx.x] = woff + incl;
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_add(uint64_t* __restrict__ out, const uint64_t* __restrict__ tile_off,
+                                                     size_t n) {
+    const uint64_t add = tile_off[blockIdx.x];
+    const size_t base = size_t(blockIdx.x) * kScanTile + size_t(threadIdx.x) * kScanV;
+#pragma unroll
+    for (int k = 0; k < kScanV; ++k) {
+        const size_t i = base + size_t(k);
+        if (i < n) out[i] += add;
+    }
+}
+
+template <class T> void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s) {
+    if (n == 0) {
+        FSM_HIP(hipMemsetAsync(out, 0, sizeof(uint64_t), s));
+        return;
+    }
+    const size_t nt = (n + kScanTile - 1) / kScanTile;
+    if (nt == 1) {
+        hipLaunchKernelGGL(k_scan_tile<T>, dim3(1), dim3(kScanT), 0, s, in, out, out + n, n);
+        FSM_HIP(hipGetLastError());
+        return;
+    }
+    DevBuf sums((nt) * sizeof(uint64_t));
+    DevBuf offs((nt + 1) * sizeof(uint64_t));
+    hipLaunchKernelGGL(k_scan_tile<T>, dim3(unsigned(nt)), dim3(kScanT), 0, s, in, out, sums.as<uint64_t>(), n);
+    FSM_HIP(hipGetLastError());
+    scan_impl<uint64_t>(sums.as<uint64_t>(), offs.as<uint64_t>(), nt, s);
+    hipLaunchKernelGGL(k_scan_add, dim3(unsigned(nt)), dim3(kScanT), 0, s, out, offs.as<uint64_t>(), n);
+    FSM_HIP(hipGetLastError());
+    FSM_HIP(hipMemcpyAsync(out + n, offs.as<uint64_t>() + nt, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    FSM_HIP(hipStreamSynchronize(s));  // sums/offs are released on return
+}
+
+}  // namespace
+
+void scan_exclusive(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint32_t>(in, out, n, s); }
+void scan_exclusive(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint64_t>(in, out, n, s); }
+
+}  // namespace fsm

@@ -1,0 +1,203 @@
+// fsm_api.cpp — the extern "C" boundary (include/fsm.h).  Every entry point
+// catches everything: no C++ exception crosses the ABI, failures come back as
+// FSM_E* codes with the message in fsm_last_error (the Scala shim turns them
+// into java.lang.Exception so TrainActor records FAILURE, TrainActor.scala:65-67).
+#include <cstdlib>
+#include <new>
+
+#include "fsm_internal.h"
+
+using fsm::Error;
+
+namespace {
+
+thread_local std::string g_err;  // errors before a context exists
+
+int fail(fsm_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg; else g_err = msg;
+    return code;
+}
+
+template <class F> int guarded(fsm_ctx* ctx, F&& f) {
+    try {
+        if (ctx) ctx->err.clear();
+        f();
+        return FSM_OK;
+    } catch (const Error& e) {
+        return fail(ctx, e.code, e.what());
+    } catch (const std::bad_alloc&) {
+        return fail(ctx, FSM_ENOMEM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(ctx, FSM_EDEVICE, e.what());
+    } catch (...) {
+        return fail(ctx, FSM_EDEVICE, "unknown error");
+    }
+}
+
+int make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out) {
+    if (!ctx || !out) return fail(ctx, FSM_EINVAL, "null argument");
+    *out = nullptr;
+    if (src.n < 0 || (src.n > 0 && !src.sids)) return fail(ctx, FSM_EINVAL, "bad record arrays");
+    if (mode != FSM_MODE_SPADE && mode != FSM_MODE_TSR) return fail(ctx, FSM_EINVAL, "mode must be SPADE(0) or TSR(1)");
+    fsm_db* db = new (std::nothrow) fsm_db();
+    if (!db) return fail(ctx, FSM_ENOMEM, "host allocation failed");
+    db->ctx = ctx;
+    db->mode = mode;
+    const int rc = guarded(ctx, [&] {
+        FSM_HIP(hipSetDevice(ctx->opts.device));
+        const double t0 = fsm::now_ms();
+        if (mode == FSM_MODE_SPADE) fsm::flatten_spade(src, db->spade);
+        else fsm::flatten_tsr(src, db->tsr);
+        const double t1 = fsm::now_ms();
+        if (mode == FSM_MODE_SPADE) fsm::spade_upload(ctx, db);
+        else fsm::tsr_upload(ctx, db);
+        ctx->stats.ms_flatten = t1 - t0;
+        ctx->stats.ms_upload = fsm::now_ms() - t1;
+    });
+    if (rc != FSM_OK) {
+        fsm_db_free(db);
+        return rc;
+    }
+    *out = db;
+    return FSM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fsm_abi_version(void) { return FSM_ABI_VERSION; }
+
+int fsm_comm_unique_id(uint8_t out[128]) {
+    if (!out) return FSM_EINVAL;
+    std::memset(out, 0, 128);
+    return fail(nullptr, FSM_ECOMM, "multi-rank SPADE is not built into this library yet");
+}
+
+int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
+    if (!out) return FSM_EINVAL;
+    *out = nullptr;
+    fsm_ctx* ctx = new (std::nothrow) fsm_ctx();
+    if (!ctx) return fail(nullptr, FSM_ENOMEM, "host allocation failed");
+    if (opts) ctx->opts = *opts;
+    if (ctx->opts.nranks <= 0) ctx->opts.nranks = 1;
+    const int rc = guarded(ctx, [&] {
+        if (ctx->opts.nranks != 1)
+            throw Error(FSM_ECOMM, "multi-rank SPADE is not built into this library yet");
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+            throw Error(FSM_EDEVICE, "no HIP device available (libfsm requires an MI355X / gfx950 GPU)");
+        if (ctx->opts.device < 0 || ctx->opts.device >= ndev)
+            throw Error(FSM_EINVAL, "device ordinal " + std::to_string(ctx->opts.device) + " out of range");
+        FSM_HIP(hipSetDevice(ctx->opts.device));
+        hipDeviceProp_t prop;
+        FSM_HIP(hipGetDeviceProperties(&prop, ctx->opts.device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            throw Error(FSM_EDEVICE, std::string("libfsm is built for gfx950; device is ") + prop.gcnArchName);
+        FSM_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    });
+    if (rc != FSM_OK) {
+        g_err = ctx->err;
+        fsm_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return FSM_OK;
+}
+
+void fsm_ctx_destroy(fsm_ctx* ctx) {
+    if (!ctx) return;
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* fsm_last_error(const fsm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int fsm_get_stats(const fsm_ctx* ctx, fsm_stats* out) {
+    if (!ctx || !out) return FSM_EINVAL;
+    *out = ctx->stats;
+    return FSM_OK;
+}
+
+int fsm_db_from_spmf(fsm_ctx* ctx, int32_t mode, const int32_t* sids, const char* const* lines, const int64_t* lens,
+                     int64_t n, fsm_db** out) {
+    if (n > 0 && (!lines || !lens)) return fail(ctx, FSM_EINVAL, "null lines/lens");
+    fsm::Source src;
+    src.sids = sids;
+    src.lines = lines;
+    src.lens = lens;
+    src.n = n;
+    return make_db(ctx, mode, src, out);
+}
+
+int fsm_db_from_tokens(fsm_ctx* ctx, int32_t mode, const int32_t* sids, const int64_t* seq_off,
+                       const int64_t* tokens, int64_t n, fsm_db** out) {
+    if (n > 0 && (!seq_off || (!tokens && seq_off[n] > 0))) return fail(ctx, FSM_EINVAL, "null token arrays");
+    fsm::Source src;
+    src.sids = sids;
+    src.seq_off = seq_off;
+    src.tokens = tokens;
+    src.n = n;
+    return make_db(ctx, mode, src, out);
+}
+
+void fsm_db_free(fsm_db* db) {
+    if (!db) return;
+    fsm::spade_release(db);
+    fsm::tsr_release(db);
+    delete db;
+}
+
+int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_patterns** out) {
+    (void)dfs;  // DFS vs BFS only changes the discovery order, not the pattern set
+    if (!ctx || !db || !out) return fail(ctx, FSM_EINVAL, "null argument");
+    *out = nullptr;
+    if (db->ctx != ctx) return fail(ctx, FSM_EINVAL, "db belongs to another context");
+    if (db->mode != FSM_MODE_SPADE) return fail(ctx, FSM_EINVAL, "db was not flattened for SPADE");
+    return guarded(ctx, [&] {
+        FSM_HIP(hipSetDevice(ctx->opts.device));
+        const double fl = ctx->stats.ms_flatten, up = ctx->stats.ms_upload;
+        ctx->stats = fsm_stats{};
+        ctx->stats.ms_flatten = fl;
+        ctx->stats.ms_upload = up;
+        fsm::spade_mine(ctx, db, support, out);
+    });
+}
+
+int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** out) {
+    if (!ctx || !db || !out) return fail(ctx, FSM_EINVAL, "null argument");
+    *out = nullptr;
+    if (db->ctx != ctx) return fail(ctx, FSM_EINVAL, "db belongs to another context");
+    if (db->mode != FSM_MODE_TSR) return fail(ctx, FSM_EINVAL, "db was not flattened for TSR");
+    if (k < 1) return fail(ctx, FSM_EINVAL, "TSR: k must be >= 1 (got " + std::to_string(k) + ")");
+    return guarded(ctx, [&] {
+        FSM_HIP(hipSetDevice(ctx->opts.device));
+        const double fl = ctx->stats.ms_flatten, up = ctx->stats.ms_upload;
+        ctx->stats = fsm_stats{};
+        ctx->stats.ms_flatten = fl;
+        ctx->stats.ms_upload = up;
+        fsm::tsr_mine(ctx, db, k, minconf, out);
+    });
+}
+
+void fsm_patterns_free(fsm_patterns* p) {
+    if (!p) return;
+    std::free(p->support);
+    std::free(p->pat_off);
+    std::free(p->set_off);
+    std::free(p->items);
+    std::free(p);
+}
+
+void fsm_rules_free(fsm_rules* r) {
+    if (!r) return;
+    std::free(r->support);
+    std::free(r->confidence);
+    std::free(r->ante_off);
+    std::free(r->ante);
+    std::free(r->cons_off);
+    std::free(r->cons);
+    std::free(r);
+}
+
+}  // extern "C"

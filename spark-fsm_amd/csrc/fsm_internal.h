@@ -1,0 +1,137 @@
+// fsm_internal.h — shared host-side types of libfsm (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/fsm.h"
+
+namespace fsm {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define FSM_HIP(x)                                                                        \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess)                                                             \
+            throw ::fsm::Error(FSM_EDEVICE, std::string(#x) + " failed: " + hipGetErrorString(e_) + \
+                                                " (" __FILE__ ":" + std::to_string(__LINE__) + ")"); \
+    } while (0)
+
+inline double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// Owning device allocation (hipMalloc) with RAII.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t n) { alloc(n); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void alloc(size_t n) {
+        release();
+        if (n == 0) n = 16;
+        hipError_t e = hipMalloc(&p, n);
+        if (e != hipSuccess) {
+            p = nullptr;
+            throw Error(FSM_ENOMEM, "hipMalloc(" + std::to_string(n) + " bytes) failed: " +
+                                        hipGetErrorString(e));
+        }
+        bytes = n;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// ---------------------------------------------------------------- flat DBs
+// SPADE: one row per distinct sequence id (records with equal sids merged, as
+// IDListBitmap.registerBit(sid, ts) merges them, SPADE.scala:74,90); entries
+// are the distinct items of the row (ascending dense id) with the bitmask of
+// the row's rank-compressed timestamps (eids) at which they occur.
+struct FlatSpade {
+    int64_t total = 0;                 // input records = sequences.count()
+    int W = 1;                         // u64 words per eid mask (power of two)
+    std::vector<int32_t> item_val;     // dense item id -> item value (ascending)
+    std::vector<uint32_t> row_off;     // [rows+1]
+    std::vector<uint32_t> ent_item;    // dense item id
+    std::vector<uint64_t> ent_mask;    // [entries * W]
+};
+
+// TSR: one row per sequence (sid == position), entries = distinct items with
+// their first / last itemset index (the Vertical maps, TSR.scala:52-94).
+struct FlatTsr {
+    int64_t total = 0;
+    std::vector<int32_t> item_val;
+    std::vector<uint32_t> row_off;     // [total+1]
+    std::vector<uint32_t> ent_item;
+    std::vector<uint32_t> ent_first;
+    std::vector<uint32_t> ent_last;
+};
+
+struct Source {
+    // exactly one of (lines, tokens) is set
+    const int32_t* sids = nullptr;
+    const char* const* lines = nullptr;
+    const int64_t* lens = nullptr;
+    const int64_t* seq_off = nullptr;
+    const int64_t* tokens = nullptr;
+    int64_t n = 0;
+};
+
+void flatten_spade(const Source& src, FlatSpade& out);
+void flatten_tsr(const Source& src, FlatTsr& out);
+
+}  // namespace fsm
+
+struct SpadeDevDB;
+struct TsrDevDB;
+
+struct fsm_ctx {
+    fsm_opts opts{};
+    std::string err;
+    fsm_stats stats{};
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    void* comm = nullptr;  // ncclComm_t when nranks > 1
+};
+
+struct fsm_db {
+    fsm_ctx* ctx = nullptr;
+    int mode = 0;
+    fsm::FlatSpade spade;
+    fsm::FlatTsr tsr;
+    SpadeDevDB* spade_dev = nullptr;
+    TsrDevDB* tsr_dev = nullptr;
+};
+
+namespace fsm {
+// engines (spade_engine.hip / tsr_engine.hip)
+void spade_upload(fsm_ctx* ctx, fsm_db* db);
+void spade_release(fsm_db* db);
+void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out);
+void tsr_upload(fsm_ctx* ctx, fsm_db* db);
+void tsr_release(fsm_db* db);
+void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** out);
+}  // namespace fsm

@@ -1,0 +1,805 @@
+// spade_engine.hip — SPADE frequent-sequence mining on MI355X (SURVEY §8a rows
+// a2-a5; the [EXT] SpadeAlgorithm of SPADE.scala:132-135).
+//
+// Layout.  Every prefix equivalence class [P] lives in HBM as a horizontal
+// "class-row" set: one row per sequence containing P, holding one entry per
+// member m of [P] (m = P->x or P x) present in that sequence:
+//     mem  u32  member id = rank(x) << 1 | type   (type 0 = sequence-ext, 1 = itemset-ext)
+//     lohi u32  first | last set eid of the entry's mask (16 bits each)
+//     pos  u32  offset-in-row << 16 | row length  (rows are contiguous runs)
+//     mask u64[W] eid bitmask (the id-list entry (sid, eids) of member m)
+// The entries of member m across all rows of the class ARE its id-list L(m).
+//
+// Kernels (one launch each per class batch; a batch = hundreds..thousands of
+// classes of one DFS frontier):
+//   k_count   every (entry i, entry j) pair of a row evaluates the temporal /
+//             equality join predicate of SURVEY A.2 and bumps the pair's
+//             support counter: ALL n^2 candidate joins of a class in a single
+//             streaming pass over its entries (vs n^2 separate list merges).
+//   k_freq_*  one wave per member row of the counter matrix: ballot the
+//             frequent candidates (support >= minsup), give them child member
+//             ids (wave prefix popcount), compact them for the host.
+//   k_emit    writes the child classes' rows (the joined id-lists of the
+//             frequent candidates) straight into the next frontier slab.
+// The root class is the flattened DB restricted to frequent items (F1 = k_f1,
+// row filter = k_root_*); its pair-count matrix is the F2 matrix (K2).
+#include <algorithm>
+#include <cstdio>
+#include <numeric>
+#include <memory>
+#include <cmath>
+#include <cstdlib>
+
+#include "device_util.h"
+
+struct SpadeDevDB {
+    fsm::DevBuf row_off;  // u32 [R+1]
+    fsm::DevBuf item;     // u32 [E]
+    fsm::DevBuf mask;     // u64 [E*W]
+    int64_t R = 0, E = 0, U = 0;
+    int W = 1;
+};
+
+namespace fsm {
+namespace {
+
+constexpr uint32_t kSeq = 0, kItm = 1;
+constexpr uint32_t kChunk = 2048;  // class entries per workgroup work item
+constexpr int kBlock = 256;
+
+struct DClass {
+    uint32_t ebegin, nent, D, cbase;
+    uint64_t cnt_off;
+};
+struct DWork {
+    uint32_t cls, e0, e1, pad;
+};
+struct DRow {
+    uint32_t cls, mi;
+};
+struct DChild {
+    uint32_t ebegin, cap;
+};
+struct FreqRec {
+    uint32_t row, slot, sup, cid;
+};
+
+struct SlabPtrs {
+    uint32_t* mem;
+    uint32_t* lohi;
+    uint32_t* pos;
+    uint64_t* mask;
+};
+
+// ------------------------------------------------------------------ kernels
+
+// K1: F1 histogram = distinct-sid support per item (entries are distinct per
+// (row, item)).  SPADE.scala:113-126 `idList.getSupport()`.
+__global__ __launch_bounds__(kBlock) void k_f1(const uint32_t* __restrict__ item, uint64_t e0, uint64_t e1,
+                                               uint32_t* __restrict__ f1) {
+    for (uint64_t e = e0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < e1;
+         e += uint64_t(gridDim.x) * blockDim.x)
+        atomicAdd(&f1[item[e]], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_root_count(const uint32_t* __restrict__ row_off,
+                                                       const uint32_t* __restrict__ item,
+                                                       const uint32_t* __restrict__ rank, uint64_t r0, uint64_t r1,
+                                                       uint32_t* __restrict__ cnt, uint32_t* __restrict__ flag) {
+    const uint64_t r = r0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= r1) return;
+    uint32_t c = 0;
+    for (uint32_t e = row_off[r]; e < row_off[r + 1]; ++e) c += rank[item[e]] != kNone;
+    cnt[r - r0] = c;
+    if (c > 0xFFFFu) atomicOr(flag, 1u);
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_root_write(const uint32_t* __restrict__ row_off,
+                                                       const uint32_t* __restrict__ item,
+                                                       const uint64_t* __restrict__ mask,
+                                                       const uint32_t* __restrict__ rank, uint64_t r0, uint64_t r1,
+                                                       const uint64_t* __restrict__ off, SlabPtrs o) {
+    const uint64_t r = r0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= r1) return;
+    const uint64_t ob = off[r - r0];
+    const uint32_t len = uint32_t(off[r - r0 + 1] - ob);
+    uint32_t k = 0;
+    for (uint32_t e = row_off[r]; e < row_off[r + 1]; ++e) {
+        const uint32_t rk = rank[item[e]];
+        if (rk == kNone) continue;
+        uint64_t m[W];
+        load_mask<W>(mask + size_t(e) * W, m);
+        const uint64_t d = ob + k;
+        o.mem[d] = rk << 1 | kSeq;
+        o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+        o.pos[d] = (k << 16) | len;
+        store_mask<W>(o.mask + size_t(d) * W, m);
+        ++k;
+    }
+}
+
+template <int W> __device__ __forceinline__ bool and_nonzero(const uint64_t (&a)[W], const uint64_t* __restrict__ b) {
+    uint64_t bm[W];
+    load_mask<W>(b, bm);
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) acc |= a[k] & bm[k];
+    return acc != 0;
+}
+
+// K2/K3/K4: all candidate joins of every class of the batch, one pass.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_count(const DWork* __restrict__ work, const DClass* __restrict__ cls,
+                                                  const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
+                                                  const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
+                                                  uint32_t* __restrict__ cnt) {
+    const DWork w = work[blockIdx.x];
+    const DClass c = cls[w.cls];
+    for (uint32_t e = w.e0 + threadIdx.x; e < w.e1; e += blockDim.x) {
+        const uint32_t mi = mem[e], p = pos[e];
+        const uint32_t lo_i = lohi[e] & 0xFFFFu;
+        const uint32_t ti = mi & 1u, ri = mi >> 1;
+        const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
+        uint64_t mk[W];
+        load_mask<W>(mask + size_t(e) * W, mk);
+        uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi) * c.D;
+        for (uint32_t q = 0; q < rl; ++q) {
+            const uint32_t f = rb + q;
+            const uint32_t mj = mem[f];
+            const uint32_t tj = mj & 1u, rj = mj >> 1;
+            if (tj == kSeq) {
+                // P x -> y  /  P->x -> y : bits of L(j) strictly after first bit of L(i)
+                if ((lohi[f] >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
+                // P->(x y), y > x : L(i) & L(j)
+                if (ti == kSeq && rj > ri && and_nonzero<W>(mk, mask + size_t(f) * W))
+                    atomicAdd(rowc + (rj << 1 | 1u), 1u);
+            } else if (ti == kItm && rj > ri && and_nonzero<W>(mk, mask + size_t(f) * W)) {
+                // P(x y), y > x
+                atomicAdd(rowc + (rj << 1 | 1u), 1u);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ rows, uint32_t nrows,
+                                                       const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
+                                                       uint32_t minsup, uint32_t* __restrict__ rowcnt) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (g >= nrows) return;
+    const DRow r = rows[g];
+    const DClass c = cls[r.cls];
+    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi) * c.D;
+    uint32_t n = 0;
+    for (uint32_t s = 0; s < c.D; s += 64) {
+        const uint32_t slot = s + lane_id();
+        const uint32_t v = slot < c.D ? base[slot] : 0u;
+        n += __popcll(__ballot(v >= minsup));
+    }
+    if (lane_id() == 0) rowcnt[g] = n;
+}
+
+__global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ rows, uint32_t nrows,
+                                                       const DClass* __restrict__ cls, uint32_t* __restrict__ cnt,
+                                                       uint32_t minsup, const uint64_t* __restrict__ rowoff,
+                                                       FreqRec* __restrict__ out) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (g >= nrows) return;
+    const DRow r = rows[g];
+    const DClass c = cls[r.cls];
+    uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi) * c.D;
+    uint64_t o = rowoff[g];
+    uint32_t nrank = 0;
+    const unsigned lane = lane_id();
+    const uint64_t lead_lt = (1ull << (lane & ~1u)) - 1ull;
+    for (uint32_t s = 0; s < c.D; s += 64) {
+        const uint32_t slot = s + lane;
+        const uint32_t v = slot < c.D ? base[slot] : 0u;
+        const bool fr = slot < c.D && v >= minsup;
+        const bool partner = __shfl_xor(int(fr), 1, 64) != 0;
+        const uint64_t lead = __ballot((fr || partner) && !(lane & 1u));
+        const uint32_t crank = nrank + uint32_t(__popcll(lead & lead_lt));
+        const uint32_t cid = fr ? (crank << 1 | (slot & 1u)) : kNone;
+        if (slot < c.D) base[slot] = cid;
+        const uint64_t fb = __ballot(fr);
+        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{g, slot, v, cid};
+        o += uint64_t(__popcll(fb));
+        nrank += uint32_t(__popcll(lead));
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work, const DClass* __restrict__ cls,
+                                                 const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
+                                                 const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
+                                                 const uint32_t* __restrict__ ids, const uint32_t* __restrict__ child_of,
+                                                 const DChild* __restrict__ ch, uint32_t* __restrict__ cursor,
+                                                 SlabPtrs o) {
+    const DWork w = work[blockIdx.x];
+    const DClass c = cls[w.cls];
+    for (uint32_t e = w.e0 + threadIdx.x; e < w.e1; e += blockDim.x) {
+        const uint32_t mi = mem[e];
+        const uint32_t cc = child_of[c.cbase + mi];
+        if (cc == kNone) continue;
+        const uint32_t p = pos[e];
+        const uint32_t lo_i = lohi[e] & 0xFFFFu;
+        const uint32_t ti = mi & 1u, ri = mi >> 1;
+        const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
+        uint64_t mk[W];
+        load_mask<W>(mask + size_t(e) * W, mk);
+        const uint32_t* rid = ids + c.cnt_off + uint64_t(mi) * c.D;
+        uint32_t n = 0;
+        for (uint32_t q = 0; q < rl; ++q) {
+            const uint32_t f = rb + q;
+            const uint32_t mj = mem[f];
+            const uint32_t tj = mj & 1u, rj = mj >> 1;
+            if (tj == kSeq) {
+                if ((lohi[f] >> 16) > lo_i && rid[rj << 1] != kNone) ++n;
+                if (ti == kSeq && rj > ri && rid[rj << 1 | 1u] != kNone && and_nonzero<W>(mk, mask + size_t(f) * W)) ++n;
+            } else if (ti == kItm && rj > ri && rid[rj << 1 | 1u] != kNone &&
+                       and_nonzero<W>(mk, mask + size_t(f) * W)) {
+                ++n;
+            }
+        }
+        if (n == 0) continue;
+        const uint32_t base = ch[cc].ebegin + atomicAdd(&cursor[cc], n);
+        uint32_t k = 0;
+        const uint32_t lw = lo_i >> 6, lb = lo_i & 63u;
+        for (uint32_t q = 0; q < rl; ++q) {
+            const uint32_t f = rb + q;
+            const uint32_t mj = mem[f];
+            const uint32_t tj = mj & 1u, rj = mj >> 1;
+            const uint32_t hj = lohi[f] >> 16;
+            if (tj == kSeq && hj > lo_i) {
+                const uint32_t cid = rid[rj << 1];
+                if (cid != kNone) {
+                    uint64_t m[W];
+                    load_mask<W>(mask + size_t(f) * W, m);
+#pragma unroll
+                    for (int x = 0; x < W; ++x) {
+                        if (uint32_t(x) < lw) m[x] = 0;
+                        else if (uint32_t(x) == lw) m[x] = lb == 63u ? 0ull : (m[x] & (~0ull << (lb + 1u)));
+                    }
+                    const uint32_t d = base + k;
+                    o.mem[d] = cid;
+                    o.lohi[d] = mask_lo<W>(m) | (hj << 16);
+                    o.pos[d] = (k << 16) | n;
+                    store_mask<W>(o.mask + size_t(d) * W, m);
+                    ++k;
+                }
+            }
+            if (rj > ri && ti == tj) {
+                const uint32_t cid = rid[rj << 1 | 1u];
+                if (cid != kNone) {
+                    uint64_t m[W];
+                    load_mask<W>(mask + size_t(f) * W, m);
+                    uint64_t acc = 0;
+#pragma unroll
+                    for (int x = 0; x < W; ++x) {
+                        m[x] &= mk[x];
+                        acc |= m[x];
+                    }
+                    if (acc) {
+                        const uint32_t d = base + k;
+                        o.mem[d] = cid;
+                        o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+                        o.pos[d] = (k << 16) | n;
+                        store_mask<W>(o.mask + size_t(d) * W, m);
+                        ++k;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------- host side
+
+struct Slab {
+    DevBuf mem, lohi, pos, mask;
+    uint64_t cap = 0;
+    void alloc(uint64_t n, int W) {
+        mem.alloc(n * 4);
+        lohi.alloc(n * 4);
+        pos.alloc(n * 4);
+        mask.alloc(n * 8 * uint64_t(W));
+        cap = n;
+    }
+    SlabPtrs ptrs() const { return SlabPtrs{mem.as<uint32_t>(), lohi.as<uint32_t>(), pos.as<uint32_t>(), mask.as<uint64_t>()}; }
+};
+
+struct ClassMeta {
+    std::vector<uint32_t> rank_item;  // rank -> dense item id
+    std::vector<int32_t> node_of;     // member id -> pattern node (-1: absent)
+    uint32_t D = 0;
+    uint64_t cnt_off = 0;
+    uint32_t ebegin = 0, nent = 0, cbase = 0;
+};
+
+struct ChildInfo {
+    uint32_t pcls = 0, pmi = 0;
+    std::vector<uint32_t> rank_item;
+    std::vector<int32_t> node_of;
+    uint32_t D = 0;
+    uint64_t cap = 0;
+};
+
+struct PNode {
+    int32_t parent;
+    uint32_t item;
+    uint32_t type;
+    uint32_t support;
+};
+
+struct Batch {
+    Slab slab;
+    std::vector<ClassMeta> cls;
+    DevBuf d_cls, d_work, cnt;
+    uint32_t nwork = 0;
+    uint64_t n_cnt = 0, cbase_total = 0;
+    std::vector<ChildInfo> children;
+    std::vector<std::pair<size_t, size_t>> groups;
+    size_t next_group = 0;
+};
+
+struct Miner {
+    fsm_ctx* ctx;
+    SpadeDevDB* db;
+    hipStream_t s;
+    int W;
+    uint32_t minsup;
+    uint64_t budget;
+    std::vector<PNode> nodes;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_count, ev_emit;
+
+    uint64_t entry_bytes() const { return 12ull + 8ull * uint64_t(W); }
+
+    template <class T> void upload(DevBuf& d, const std::vector<T>& h) {
+        d.alloc(h.size() * sizeof(T));
+        if (!h.empty()) FSM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+
+    std::pair<hipEvent_t, hipEvent_t> ev_pair() {
+        hipEvent_t a, b;
+        FSM_HIP(hipEventCreate(&a));
+        FSM_HIP(hipEventCreate(&b));
+        return {a, b};
+    }
+
+    // work items + class descriptors for a batch whose classes have ebegin/nent set
+    void prepare(Batch& b) {
+        std::vector<DClass> dc(b.cls.size());
+        std::vector<DWork> wk;
+        uint64_t off = 0, cb = 0;
+        for (size_t c = 0; c < b.cls.size(); ++c) {
+            ClassMeta& m = b.cls[c];
+            m.cnt_off = off;
+            m.cbase = uint32_t(cb);
+            off += uint64_t(m.D) * m.D;
+            cb += m.D;
+            dc[c] = DClass{m.ebegin, m.nent, m.D, m.cbase, m.cnt_off};
+            for (uint32_t e = 0; e < m.nent; e += kChunk)
+                wk.push_back(DWork{uint32_t(c), m.ebegin + e, m.ebegin + std::min(m.nent, e + kChunk), 0});
+        }
+        if (cb >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
+        b.n_cnt = off;
+        b.cbase_total = cb;
+        b.nwork = uint32_t(wk.size());
+        upload(b.d_cls, dc);
+        upload(b.d_work, wk);
+    }
+
+    void stats_for_class(const ClassMeta& m) {
+        uint64_t S = 0, I = 0, sS = 0, sI = 0;
+        for (uint32_t mi = 0; mi < m.D; ++mi) {
+            const int32_t nd = m.node_of[mi];
+            if (nd < 0) continue;
+            const uint64_t sup = nodes[size_t(nd)].support;
+            if ((mi & 1u) == kSeq) { ++S; sS += sup; } else { ++I; sI += sup; }
+        }
+        fsm_stats& st = ctx->stats;
+        st.joins += int64_t(S * S + I * S + (S ? S * (S - 1) / 2 : 0) + (I ? I * (I - 1) / 2 : 0));
+        const uint64_t in = 2 * S * sS + S * sI + I * sS + (S ? (S - 1) * sS : 0) + (I ? (I - 1) * sI : 0);
+        st.bytes_join_equiv += int64_t(12 * in);
+        st.classes += 1;
+    }
+
+    // count kernel + frequent-candidate extraction; fills b.children / b.groups
+    void count_and_freq(Batch& b) {
+        prepare(b);
+        for (auto& m : b.cls) stats_for_class(m);
+        fsm_stats& st = ctx->stats;
+        st.batches += 1;
+        uint64_t tot_ent = 0;
+        for (auto& m : b.cls) tot_ent += m.nent;
+        st.entries += int64_t(tot_ent);
+        st.bytes_streamed += int64_t(tot_ent * entry_bytes());
+        st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
+        b.cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
+        FSM_HIP(hipMemsetAsync(b.cnt.p, 0, b.n_cnt * 4, s));
+        if (b.nwork) {
+            auto ev = ev_pair();
+            FSM_HIP(hipEventRecord(ev.first, s));
+            const SlabPtrs sp = b.slab.ptrs();
+#define FSM_COUNT(WW)                                                                                   \
+    hipLaunchKernelGGL(k_count<WW>, dim3(b.nwork), dim3(kBlock), 0, s, b.d_work.as<DWork>(),           \
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.cnt.as<uint32_t>())
+            switch (W) {
+                case 1: FSM_COUNT(1); break;
+                case 2: FSM_COUNT(2); break;
+                case 4: FSM_COUNT(4); break;
+                case 8: FSM_COUNT(8); break;
+                case 16: FSM_COUNT(16); break;
+                case 32: FSM_COUNT(32); break;
+                default: FSM_COUNT(64); break;
+            }
+#undef FSM_COUNT
+            FSM_HIP(hipGetLastError());
+            FSM_HIP(hipEventRecord(ev.second, s));
+            ev_count.push_back(ev);
+            st.count_launches += 1;
+        }
+        // member rows of the counter matrix
+        std::vector<DRow> rows;
+        for (size_t c = 0; c < b.cls.size(); ++c)
+            for (uint32_t mi = 0; mi < b.cls[c].D; ++mi)
+                if (b.cls[c].node_of[mi] >= 0) rows.push_back(DRow{uint32_t(c), mi});
+        const uint32_t nrows = uint32_t(rows.size());
+        DevBuf d_rows, rowcnt((size_t(nrows) + 1) * 4), rowoff((size_t(nrows) + 1) * 8);
+        upload(d_rows, rows);
+        const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
+        if (nrows) {
+            hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
+                               b.d_cls.as<DClass>(), b.cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
+            FSM_HIP(hipGetLastError());
+        }
+        scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
+        uint64_t nfreq = 0;
+        FSM_HIP(hipMemcpyAsync(&nfreq, rowoff.as<uint64_t>() + nrows, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        std::vector<FreqRec> recs(nfreq);
+        if (nfreq) {
+            DevBuf d_recs(nfreq * sizeof(FreqRec));
+            hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
+                               b.d_cls.as<DClass>(), b.cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(),
+                               d_recs.as<FreqRec>());
+            FSM_HIP(hipGetLastError());
+            FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nfreq * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipStreamSynchronize(s));
+        }
+        // children (new pattern nodes) in deterministic (row, slot) order
+        b.children.clear();
+        for (size_t q = 0; q < recs.size();) {
+            const uint32_t row = recs[q].row;
+            const DRow pr = rows[row];
+            const ClassMeta& pm = b.cls[pr.cls];
+            size_t q2 = q;
+            uint32_t maxcid = 0;
+            while (q2 < recs.size() && recs[q2].row == row) { maxcid = std::max(maxcid, recs[q2].cid); ++q2; }
+            ChildInfo ch;
+            ch.pcls = pr.cls;
+            ch.pmi = pr.mi;
+            const uint32_t R2 = (maxcid >> 1) + 1;
+            ch.D = 2 * R2;
+            ch.rank_item.assign(R2, 0);
+            ch.node_of.assign(ch.D, -1);
+            const int32_t parent = pm.node_of[pr.mi];
+            uint32_t last_type = 0;
+            for (size_t k = q; k < q2; ++k) {
+                const FreqRec& fr = recs[k];
+                const uint32_t item = pm.rank_item[fr.slot >> 1];
+                const int32_t node = int32_t(nodes.size());
+                nodes.push_back(PNode{parent, item, fr.slot & 1u, fr.sup});
+                ch.rank_item[fr.cid >> 1] = item;
+                ch.node_of[fr.cid] = node;
+                ch.cap += fr.sup;
+                st.bytes_join_equiv += int64_t(12ull * fr.sup);
+                last_type = fr.slot & 1u;
+            }
+            const size_t nch = q2 - q;
+            if (nch > 0xFFFFu)
+                throw Error(FSM_ELIMIT, "SPADE: a prefix class has more than 65535 frequent children");
+            if (!(nch == 1 && last_type == kItm)) b.children.push_back(std::move(ch));
+            q = q2;
+        }
+        // groups of children that fit the frontier budget
+        b.groups.clear();
+        b.next_group = 0;
+        size_t gs = 0;
+        uint64_t acc = 0;
+        const uint64_t max_ent = uint64_t(1) << 31;
+        uint64_t acc_ent = 0;
+        for (size_t k = 0; k < b.children.size(); ++k) {
+            const uint64_t need = b.children[k].cap * entry_bytes() + uint64_t(b.children[k].D) * b.children[k].D * 4;
+            if (k > gs && (acc + need > budget || acc_ent + b.children[k].cap > max_ent)) {
+                b.groups.push_back({gs, k});
+                gs = k;
+                acc = 0;
+                acc_ent = 0;
+            }
+            acc += need;
+            acc_ent += b.children[k].cap;
+        }
+        if (gs < b.children.size()) b.groups.push_back({gs, b.children.size()});
+        if (ctx->opts.verbose)
+            std::fprintf(stderr, "[fsm] batch: classes=%zu entries=%llu freq=%llu children=%zu groups=%zu\n",
+                         b.cls.size(), (unsigned long long)tot_ent, (unsigned long long)nfreq,
+                         b.children.size(), b.groups.size());
+    }
+
+    // emit child rows of group g of batch b into a new batch
+    void emit(Batch& b, size_t g, Batch& nb) {
+        const auto [ga, gb] = b.groups[g];
+        nb.cls.resize(gb - ga);
+        std::vector<uint32_t> child_of(b.cbase_total, kNone);
+        std::vector<DChild> dch(gb - ga);
+        uint64_t total = 0;
+        for (size_t k = ga; k < gb; ++k) {
+            ChildInfo& ch = b.children[k];
+            ClassMeta& m = nb.cls[k - ga];
+            m.rank_item = std::move(ch.rank_item);
+            m.node_of = std::move(ch.node_of);
+            m.D = ch.D;
+            m.ebegin = uint32_t(total);
+            m.nent = uint32_t(ch.cap);
+            dch[k - ga] = DChild{uint32_t(total), uint32_t(ch.cap)};
+            child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
+            total += ch.cap;
+        }
+        nb.slab.alloc(total, W);
+        DevBuf d_child_of, d_ch, cursor((gb - ga) * 4 + 4);
+        upload(d_child_of, child_of);
+        upload(d_ch, dch);
+        FSM_HIP(hipMemsetAsync(cursor.p, 0, (gb - ga) * 4, s));
+        ctx->stats.bytes_streamed += int64_t(total * entry_bytes());
+        uint64_t tot_ent = 0;
+        for (auto& m : b.cls) tot_ent += m.nent;
+        ctx->stats.bytes_streamed += int64_t(tot_ent * entry_bytes());
+        if (b.nwork) {
+            auto ev = ev_pair();
+            FSM_HIP(hipEventRecord(ev.first, s));
+            const SlabPtrs sp = b.slab.ptrs();
+            const SlabPtrs op = nb.slab.ptrs();
+#define FSM_EMIT(WW)                                                                                           \
+    hipLaunchKernelGGL(k_emit<WW>, dim3(b.nwork), dim3(kBlock), 0, s, b.d_work.as<DWork>(), b.d_cls.as<DClass>(), \
+                       sp.mem, sp.lohi, sp.pos, sp.mask, b.cnt.as<uint32_t>(), d_child_of.as<uint32_t>(),       \
+                       d_ch.as<DChild>(), cursor.as<uint32_t>(), op)
+            switch (W) {
+                case 1: FSM_EMIT(1); break;
+                case 2: FSM_EMIT(2); break;
+                case 4: FSM_EMIT(4); break;
+                case 8: FSM_EMIT(8); break;
+                case 16: FSM_EMIT(16); break;
+                case 32: FSM_EMIT(32); break;
+                default: FSM_EMIT(64); break;
+            }
+#undef FSM_EMIT
+            FSM_HIP(hipGetLastError());
+            FSM_HIP(hipEventRecord(ev.second, s));
+            ev_emit.push_back(ev);
+        }
+        // the cursors must land exactly on the capacities (sum of child supports)
+        std::vector<uint32_t> cur(gb - ga);
+        FSM_HIP(hipMemcpyAsync(cur.data(), cursor.p, (gb - ga) * 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        for (size_t k = 0; k < gb - ga; ++k)
+            if (cur[k] != dch[k].cap)
+                throw Error(FSM_EDEVICE, "SPADE emit: child class " + std::to_string(k) + " wrote " +
+                                             std::to_string(cur[k]) + " entries, expected " + std::to_string(dch[k].cap));
+    }
+
+    void run_root(Batch& root, const std::vector<uint32_t>& freq_items, const std::vector<uint32_t>& f1) {
+        const int64_t R = db->R;
+        const uint64_t r0 = 0, r1 = uint64_t(R);
+        // rank map (dense item -> frequent rank)
+        std::vector<uint32_t> rank(size_t(db->U), kNone);
+        for (size_t r = 0; r < freq_items.size(); ++r) rank[freq_items[r]] = uint32_t(r);
+        DevBuf d_rank, rcnt((r1 - r0 + 1) * 4), roff((r1 - r0 + 1) * 8), flag(4);
+        upload(d_rank, rank);
+        FSM_HIP(hipMemsetAsync(flag.p, 0, 4, s));
+        const unsigned grid = unsigned((r1 - r0 + kBlock - 1) / kBlock);
+        if (r1 > r0) {
+            hipLaunchKernelGGL(k_root_count, dim3(grid), dim3(kBlock), 0, s, db->row_off.as<uint32_t>(),
+                               db->item.as<uint32_t>(), d_rank.as<uint32_t>(), r0, r1, rcnt.as<uint32_t>(),
+                               flag.as<uint32_t>());
+            FSM_HIP(hipGetLastError());
+        }
+        scan_exclusive(rcnt.as<uint32_t>(), roff.as<uint64_t>(), r1 - r0, s);
+        uint64_t E0 = 0;
+        uint32_t fl = 0;
+        FSM_HIP(hipMemcpyAsync(&E0, roff.as<uint64_t>() + (r1 - r0), 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(&fl, flag.p, 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        if (fl) throw Error(FSM_ELIMIT, "SPADE: a sequence has more than 65535 distinct frequent items");
+        if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
+        root.slab.alloc(E0, W);
+        if (r1 > r0) {
+            const SlabPtrs op = root.slab.ptrs();
+#define FSM_ROOTW(WW)                                                                                         \
+    hipLaunchKernelGGL(k_root_write<WW>, dim3(grid), dim3(kBlock), 0, s, db->row_off.as<uint32_t>(),           \
+                       db->item.as<uint32_t>(), db->mask.as<uint64_t>(), d_rank.as<uint32_t>(), r0, r1,       \
+                       roff.as<uint64_t>(), op)
+            switch (W) {
+                case 1: FSM_ROOTW(1); break;
+                case 2: FSM_ROOTW(2); break;
+                case 4: FSM_ROOTW(4); break;
+                case 8: FSM_ROOTW(8); break;
+                case 16: FSM_ROOTW(16); break;
+                case 32: FSM_ROOTW(32); break;
+                default: FSM_ROOTW(64); break;
+            }
+#undef FSM_ROOTW
+            FSM_HIP(hipGetLastError());
+        }
+        ClassMeta m;
+        const uint32_t F = uint32_t(freq_items.size());
+        m.D = 2 * F;
+        m.rank_item = freq_items;
+        m.node_of.assign(m.D, -1);
+        for (uint32_t r = 0; r < F; ++r) {
+            m.node_of[2 * r] = int32_t(nodes.size());
+            nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]]});
+        }
+        m.ebegin = 0;
+        m.nent = uint32_t(E0);
+        root.cls.push_back(std::move(m));
+        FSM_HIP(hipStreamSynchronize(s));
+    }
+
+    double elapsed(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
+        double tot = 0;
+        for (auto& p : v) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) tot += ms;
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+        v.clear();
+        return tot;
+    }
+};
+
+template <class T> void copy_out(T*& dst, const std::vector<T>& src) {
+    dst = static_cast<T*>(std::malloc(std::max<size_t>(src.size(), 1) * sizeof(T)));
+    if (!dst) throw Error(FSM_ENOMEM, "malloc failed");
+    if (!src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(T));
+}
+
+}  // namespace
+
+void spade_upload(fsm_ctx* ctx, fsm_db* db) {
+    const FlatSpade& f = db->spade;
+    auto* d = new SpadeDevDB();
+    try {
+        d->R = int64_t(f.row_off.size()) - 1;
+        d->E = int64_t(f.ent_item.size());
+        d->U = int64_t(f.item_val.size());
+        d->W = f.W;
+        d->row_off.alloc(f.row_off.size() * 4);
+        d->item.alloc(std::max<size_t>(f.ent_item.size(), 1) * 4);
+        d->mask.alloc(std::max<size_t>(f.ent_mask.size(), 1) * 8);
+        FSM_HIP(hipMemcpyAsync(d->row_off.p, f.row_off.data(), f.row_off.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        if (d->E) {
+            FSM_HIP(hipMemcpyAsync(d->item.p, f.ent_item.data(), f.ent_item.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+            FSM_HIP(hipMemcpyAsync(d->mask.p, f.ent_mask.data(), f.ent_mask.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+        }
+        FSM_HIP(hipStreamSynchronize(ctx->stream));
+    } catch (...) {
+        delete d;
+        throw;
+    }
+    db->spade_dev = d;
+}
+
+void spade_release(fsm_db* db) {
+    delete db->spade_dev;
+    db->spade_dev = nullptr;
+}
+
+void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
+    const double t0 = now_ms();
+    SpadeDevDB* d = db->spade_dev;
+    const int64_t total = db->spade.total;
+    Miner mn{ctx, d, ctx->stream, d->W, 1, 0, {}, {}, {}};
+    ctx->stats.mask_words = d->W;
+    // minsupp = Math.ceil(support * total) (SPADE.scala:113), >= 1 for the lattice
+    const double ms = std::ceil(support * double(total));
+    const bool none = !(ms == ms) || ms > double(INT32_MAX);
+    mn.minsup = none ? 0x7FFFFFFFu : (ms < 1.0 ? 1u : uint32_t(ms));
+    size_t free_b = 0, total_b = 0;
+    FSM_HIP(hipMemGetInfo(&free_b, &total_b));
+    mn.budget = ctx->opts.mem_budget > 0 ? uint64_t(ctx->opts.mem_budget) : uint64_t(free_b / 2);
+
+    // ---- F1 (K1)
+    std::vector<uint32_t> f1(size_t(d->U), 0);
+    {
+        DevBuf d_f1(std::max<int64_t>(d->U, 1) * 4);
+        FSM_HIP(hipMemsetAsync(d_f1.p, 0, size_t(d->U) * 4, ctx->stream));
+        if (d->E) {
+            const unsigned grid = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, 8192));
+            hipLaunchKernelGGL(k_f1, dim3(grid), dim3(kBlock), 0, ctx->stream, d->item.as<uint32_t>(), uint64_t(0),
+                               uint64_t(d->E), d_f1.as<uint32_t>());
+            FSM_HIP(hipGetLastError());
+        }
+        if (d->U) FSM_HIP(hipMemcpyAsync(f1.data(), d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));
+        FSM_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    std::vector<uint32_t> freq;
+    if (!none)
+        for (int64_t i = 0; i < d->U; ++i)
+            if (f1[size_t(i)] >= mn.minsup) freq.push_back(uint32_t(i));
+
+    std::vector<std::unique_ptr<Batch>> stack;
+    if (!freq.empty()) {
+        auto root = std::make_unique<Batch>();
+        mn.run_root(*root, freq, f1);
+        const double t1 = now_ms();
+        ctx->stats.ms_f1 = t1 - t0;
+        mn.count_and_freq(*root);
+        ctx->stats.ms_f2 = now_ms() - t1;
+        stack.push_back(std::move(root));
+    } else {
+        ctx->stats.ms_f1 = now_ms() - t0;
+    }
+    const double t2 = now_ms();
+    // ---- lattice: DFS over class batches (each group of children = one batch)
+    while (!stack.empty()) {
+        Batch& top = *stack.back();
+        if (top.next_group >= top.groups.size()) {
+            stack.pop_back();
+            continue;
+        }
+        const size_t g = top.next_group++;
+        auto nb = std::make_unique<Batch>();
+        mn.emit(top, g, *nb);
+        if (top.next_group >= top.groups.size()) {
+            // parent fully emitted: release it before descending
+            stack.pop_back();
+        }
+        mn.count_and_freq(*nb);
+        stack.push_back(std::move(nb));
+    }
+    FSM_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->stats.ms_lattice = now_ms() - t2;
+    ctx->stats.ms_count_kernel = mn.elapsed(mn.ev_count);
+    ctx->stats.ms_emit_kernel = mn.elapsed(mn.ev_emit);
+
+    // ---- output CSR in discovery order (the reference's order is discovery order too)
+    const auto& nodes = mn.nodes;
+    const int64_t n = int64_t(nodes.size());
+    std::vector<int32_t> sup(static_cast<size_t>(n));
+    std::vector<int64_t> pat_off(size_t(n) + 1, 0), set_off(1, 0);
+    std::vector<int32_t> items;
+    std::vector<uint32_t> path_item, path_type;
+    for (int64_t k = 0; k < n; ++k) {
+        path_item.clear();
+        path_type.clear();
+        for (int32_t q = int32_t(k); q >= 0; q = nodes[size_t(q)].parent) {
+            path_item.push_back(nodes[size_t(q)].item);
+            path_type.push_back(nodes[size_t(q)].type);
+        }
+        for (size_t t = path_item.size(); t-- > 0;) {
+            if (path_type[t] == kSeq && t != path_item.size() - 1) set_off.push_back(int64_t(items.size()));
+            items.push_back(db->spade.item_val[path_item[t]]);
+        }
+        set_off.push_back(int64_t(items.size()));
+        sup[size_t(k)] = int32_t(nodes[size_t(k)].support);
+        pat_off[size_t(k) + 1] = int64_t(set_off.size()) - 1;
+    }
+    auto* p = static_cast<fsm_patterns*>(std::calloc(1, sizeof(fsm_patterns)));
+    if (!p) throw Error(FSM_ENOMEM, "calloc failed");
+    p->n = n;
+    p->n_sets = int64_t(set_off.size()) - 1;
+    p->n_items = int64_t(items.size());
+    p->total = total;
+    p->minsup = int32_t(std::min<uint32_t>(mn.minsup, 0x7FFFFFFFu));
+    copy_out(p->support, sup);
+    copy_out(p->pat_off, pat_off);
+    copy_out(p->set_off, set_off);
+    copy_out(p->items, items);
+    ctx->stats.patterns = n;
+    ctx->stats.ms_mine = now_ms() - t0;
+    *out = p;
+}
+
+}  // namespace fsm

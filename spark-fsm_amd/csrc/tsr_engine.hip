@@ -1,0 +1,553 @@
+// tsr_engine.hip — Top-K Sequential Rules (TSR.scala:102-105, [EXT]
+// TSRAlgorithm) on MI355X.
+//
+// HBM layout (uploaded once by fsm_db_from_*):
+//   horizontal rows  row_off[N+1]; per entry item / first / last (u32), the
+//                    entries of a row sorted by item (binary-searchable)
+//   vertical lists   vert_off[U+1], vert_sid / vert_item: the sids of each
+//                    item (built on the GPU by k_vcount + scan + k_vscatter)
+//
+// The counts are computed on the GPU; the order-dependent top-k bookkeeping
+// (save / registerAsCandidate / popMaximum with the rising minsup) is replayed
+// on the host in exactly the reference's order, so the result is bit-identical
+// to the CPU restatement whatever the GPU scheduling:
+//   pair phase   k_pairs: for a block of items i, every s in sids(i) scans the
+//                tail of row s (items j > i) and counts i=>j (first_i < last_j)
+//                and j=>i (first_j < last_i) into a dense block x U matrix;
+//                k_pairs_compact (wave ballot) emits the pairs that can reach
+//                the block's starting minsup, in (i, j) order.
+//   expansions   k_expand: one thread per sid of the rarest item of the rule;
+//                binary-searches the rule's items in the row, derives firstX /
+//                lastY, and histograms the expandL (c before lastY) / expandR
+//                (c after firstX) candidates plus |sids(X u {c})|;
+//                k_expand_compact pulls the candidates with count >= minsup and
+//                re-zeroes the histograms.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <memory>
+#include <queue>
+
+#include "device_util.h"
+
+struct TsrDevDB {
+    fsm::DevBuf row_off, item, first, last;  // horizontal
+    fsm::DevBuf vert_off, vert_sid, vert_item;
+    int64_t N = 0, E = 0, U = 0;
+    std::vector<uint32_t> sup;  // |sids(item)|
+};
+
+namespace fsm {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxSide = 64;
+
+__global__ __launch_bounds__(kBlock) void k_vcount(const uint32_t* __restrict__ item, uint64_t E,
+                                                   uint32_t* __restrict__ cnt) {
+    for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += uint64_t(gridDim.x) * blockDim.x)
+        atomicAdd(&cnt[item[e]], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_vscatter(const uint32_t* __restrict__ row_off,
+                                                     const uint32_t* __restrict__ item, uint64_t N,
+                                                     const uint64_t* __restrict__ voff, uint32_t* __restrict__ cursor,
+                                                     uint32_t* __restrict__ vsid, uint32_t* __restrict__ vitem) {
+    const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (s >= N) return;
+    for (uint32_t e = row_off[s]; e < row_off[s + 1]; ++e) {
+        const uint32_t it = item[e];
+        const uint64_t d = voff[it] + atomicAdd(&cursor[it], 1u);
+        vsid[d] = uint32_t(s);
+        vitem[d] = it;
+    }
+}
+
+__device__ __forceinline__ uint32_t row_find(const uint32_t* __restrict__ item, uint32_t lo, uint32_t hi,
+                                             uint32_t key) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (item[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pairs(const uint32_t* __restrict__ vsid, const uint32_t* __restrict__ vitem,
+                                                  uint64_t v0, uint64_t v1, uint32_t a, uint32_t U, uint32_t t,
+                                                  const uint32_t* __restrict__ sup,
+                                                  const uint32_t* __restrict__ row_off,
+                                                  const uint32_t* __restrict__ item, const uint32_t* __restrict__ first,
+                                                  const uint32_t* __restrict__ last, uint32_t* __restrict__ scr) {
+    const uint64_t v = v0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (v >= v1) return;
+    const uint32_t i = vitem[v];
+    if (sup[i] < t) return;
+    const uint32_t s = vsid[v];
+    const uint32_t rb = row_off[s], re = row_off[s + 1];
+    const uint32_t k = row_find(item, rb, re, i);
+    const uint32_t fi = first[k], li = last[k];
+    uint32_t* row = scr + uint64_t(i - a) * U * 2;
+    for (uint32_t q = k + 1; q < re; ++q) {
+        const uint32_t j = item[q];
+        if (sup[j] < t) continue;
+        if (fi < last[q]) atomicAdd(row + 2 * j, 1u);       // i => j
+        if (first[q] < li) atomicAdd(row + 2 * j + 1, 1u);  // j => i
+    }
+}
+
+struct PairRec {
+    uint32_t i, j, ij, ji;
+};
+
+// one wave per item row of the block: count (out == nullptr) or write+zero
+__global__ __launch_bounds__(kBlock) void k_pairs_compact(uint32_t* __restrict__ scr, uint32_t a, uint32_t nb,
+                                                          uint32_t U, uint32_t t, uint32_t* __restrict__ rowcnt,
+                                                          const uint64_t* __restrict__ rowoff,
+                                                          PairRec* __restrict__ out) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (g >= nb) return;
+    const uint32_t i = a + g;
+    uint32_t* row = scr + uint64_t(g) * U * 2;
+    uint64_t o = out ? rowoff[g] : 0;
+    uint32_t n = 0;
+    for (uint32_t j0 = i + 1; j0 < U; j0 += 64) {
+        const uint32_t j = j0 + lane_id();
+        uint32_t ij = 0, ji = 0;
+        if (j < U) { ij = row[2 * j]; ji = row[2 * j + 1]; }
+        const bool keep = j < U && (ij >= t || ji >= t);
+        const uint64_t b = __ballot(keep);
+        if (out) {
+            if (keep) out[o + __popcll(b & lanemask_lt())] = PairRec{i, j, ij, ji};
+            if (j < U && (ij | ji)) { row[2 * j] = 0; row[2 * j + 1] = 0; }
+            o += uint64_t(__popcll(b));
+        } else {
+            n += uint32_t(__popcll(b));
+        }
+    }
+    if (!out && lane_id() == 0) rowcnt[g] = n;
+}
+
+struct Side {
+    uint32_t nx, ny, doL, doR;
+    uint32_t maxX, maxY, pad0, pad1;
+    uint32_t X[kMaxSide];
+    uint32_t Y[kMaxSide];
+};
+
+__device__ __forceinline__ bool in_sorted(const uint32_t* s, uint32_t n, uint32_t c) {
+    for (uint32_t k = 0; k < n; ++k) {
+        if (s[k] == c) return true;
+        if (s[k] > c) return false;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(kBlock) void k_expand(const Side side, const uint32_t* __restrict__ dsid, uint32_t nd,
+                                                   const uint32_t* __restrict__ row_off,
+                                                   const uint32_t* __restrict__ item,
+                                                   const uint32_t* __restrict__ first,
+                                                   const uint32_t* __restrict__ last, uint32_t* __restrict__ TL,
+                                                   uint32_t* __restrict__ DL, uint32_t* __restrict__ TR,
+                                                   uint32_t* __restrict__ nX) {
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nd) return;
+    const uint32_t s = dsid[v];
+    const uint32_t rb = row_off[s], re = row_off[s + 1];
+    uint32_t fX = 0;
+    for (uint32_t k = 0; k < side.nx; ++k) {
+        const uint32_t q = row_find(item, rb, re, side.X[k]);
+        if (q >= re || item[q] != side.X[k]) return;  // s not in sids(X)
+        fX = max(fX, first[q]);
+    }
+    atomicAdd(nX, 1u);
+    if (side.doL) {
+        // |sids(X u {c})| for candidate left extensions
+        const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
+        for (uint32_t q = q0; q < re; ++q)
+            if (!in_sorted(side.Y, side.ny, item[q])) atomicAdd(&DL[item[q]], 1u);
+    }
+    uint32_t lY = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < side.ny; ++k) {
+        const uint32_t q = row_find(item, rb, re, side.Y[k]);
+        if (q >= re || item[q] != side.Y[k]) return;  // s not in sids(Y)
+        lY = min(lY, last[q]);
+    }
+    if (fX >= lY) return;  // X => Y does not hold in s
+    if (side.doL) {        // expandL: c > max(X), c not in Y, c before lastY(s)
+        const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
+        for (uint32_t q = q0; q < re; ++q) {
+            const uint32_t c = item[q];
+            if (first[q] < lY && !in_sorted(side.Y, side.ny, c)) atomicAdd(&TL[c], 1u);
+        }
+    }
+    if (side.doR) {        // expandR: c > max(Y), c not in X, c after firstX(s)
+        const uint32_t q0 = row_find(item, rb, re, side.maxY + 1);
+        for (uint32_t q = q0; q < re; ++q) {
+            const uint32_t c = item[q];
+            if (last[q] > fX && !in_sorted(side.X, side.nx, c)) atomicAdd(&TR[c], 1u);
+        }
+    }
+}
+
+struct ExpRec {
+    uint32_t c, tl, dl, tr;
+};
+
+__global__ __launch_bounds__(kBlock) void k_expand_compact(uint32_t* __restrict__ TL, uint32_t* __restrict__ DL,
+                                                           uint32_t* __restrict__ TR, uint32_t U, uint32_t t,
+                                                           ExpRec* __restrict__ out, uint32_t* __restrict__ nout,
+                                                           uint32_t cap) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    bool keep = false;
+    uint32_t tl = 0, dl = 0, tr = 0;
+    if (c < U) {
+        tl = TL[c];
+        dl = DL[c];
+        tr = TR[c];
+        keep = tl >= t || tr >= t;
+        if (tl) TL[c] = 0;
+        if (dl) DL[c] = 0;
+        if (tr) TR[c] = 0;
+    }
+    const uint64_t b = __ballot(keep);
+    if (!b) return;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(nout, uint32_t(__popcll(b)));
+    base = __shfl(base, 0, 64);
+    const uint32_t idx = base + uint32_t(__popcll(b & lanemask_lt()));
+    if (keep && idx < cap) out[idx] = ExpRec{c, tl, dl, tr};
+}
+
+// ------------------------------------------------------------ host replay
+struct Rule {
+    std::vector<uint32_t> X, Y;  // dense ids, ascending
+    uint32_t sup = 0;
+    double conf = 0;
+    uint32_t nX = 0;             // |sids(X)|
+    bool expandLR = false;
+};
+
+// RuleG.compareTo [EXT, recalled; SURVEY A.3]
+int rule_cmp(const Rule* a, const Rule* b) {
+    if (a == b) return 0;
+    if (a->sup != b->sup) return a->sup < b->sup ? -1 : 1;
+    if (a->X.size() != b->X.size()) return a->X.size() < b->X.size() ? -1 : 1;
+    if (a->Y.size() != b->Y.size()) return a->Y.size() < b->Y.size() ? -1 : 1;
+    const int c4 = int(a->conf - b->conf);
+    if (c4) return c4;
+    for (size_t k = 0; k < a->X.size(); ++k)
+        if (a->X[k] != b->X[k]) return a->X[k] < b->X[k] ? -1 : 1;
+    for (size_t k = 0; k < a->Y.size(); ++k)
+        if (a->Y[k] != b->Y[k]) return a->Y[k] < b->Y[k] ? -1 : 1;
+    return 0;
+}
+struct MinFirst {  // std::priority_queue puts the "largest" on top
+    bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(a, b) > 0; }
+};
+struct MaxFirst {
+    bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(a, b) < 0; }
+};
+
+struct Replay {
+    int32_t k;
+    double minconf;
+    uint32_t minsup = 1;
+    std::priority_queue<Rule*, std::vector<Rule*>, MinFirst> krules;
+    std::priority_queue<Rule*, std::vector<Rule*>, MaxFirst> cand;
+    std::vector<std::unique_ptr<Rule>> all;
+
+    Rule* make() {
+        all.push_back(std::make_unique<Rule>());
+        return all.back().get();
+    }
+    // AlgoTopSeqRules.save
+    void save(Rule* r) {
+        krules.push(r);
+        if (int64_t(krules.size()) > k) {
+            if (r->sup > minsup) {
+                do {
+                    if (krules.empty()) break;
+                    krules.pop();
+                } while (int64_t(krules.size()) > k);
+            }
+            minsup = krules.top()->sup;
+        }
+    }
+    void reg(Rule* r, bool lr) {
+        r->expandLR = lr;
+        cand.push(r);
+    }
+};
+
+}  // namespace
+
+void tsr_upload(fsm_ctx* ctx, fsm_db* db) {
+    const FlatTsr& f = db->tsr;
+    hipStream_t s = ctx->stream;
+    auto d = std::make_unique<TsrDevDB>();
+    d->N = f.total;
+    d->E = int64_t(f.ent_item.size());
+    d->U = int64_t(f.item_val.size());
+    d->row_off.alloc(f.row_off.size() * 4);
+    d->item.alloc(size_t(std::max<int64_t>(d->E, 1)) * 4);
+    d->first.alloc(size_t(std::max<int64_t>(d->E, 1)) * 4);
+    d->last.alloc(size_t(std::max<int64_t>(d->E, 1)) * 4);
+    FSM_HIP(hipMemcpyAsync(d->row_off.p, f.row_off.data(), f.row_off.size() * 4, hipMemcpyHostToDevice, s));
+    if (d->E) {
+        FSM_HIP(hipMemcpyAsync(d->item.p, f.ent_item.data(), size_t(d->E) * 4, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipMemcpyAsync(d->first.p, f.ent_first.data(), size_t(d->E) * 4, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipMemcpyAsync(d->last.p, f.ent_last.data(), size_t(d->E) * 4, hipMemcpyHostToDevice, s));
+    }
+    // vertical transpose on the device (K0)
+    DevBuf cnt(size_t(std::max<int64_t>(d->U, 1)) * 4), cursor(size_t(std::max<int64_t>(d->U, 1)) * 4);
+    d->vert_off.alloc(size_t(d->U + 1) * 8);
+    d->vert_sid.alloc(size_t(std::max<int64_t>(d->E, 1)) * 4);
+    d->vert_item.alloc(size_t(std::max<int64_t>(d->E, 1)) * 4);
+    FSM_HIP(hipMemsetAsync(cnt.p, 0, size_t(d->U) * 4, s));
+    FSM_HIP(hipMemsetAsync(cursor.p, 0, size_t(d->U) * 4, s));
+    if (d->E) {
+        const unsigned g = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, 8192));
+        hipLaunchKernelGGL(k_vcount, dim3(g), dim3(kBlock), 0, s, d->item.as<uint32_t>(), uint64_t(d->E),
+                           cnt.as<uint32_t>());
+        FSM_HIP(hipGetLastError());
+    }
+    scan_exclusive(cnt.as<uint32_t>(), d->vert_off.as<uint64_t>(), size_t(d->U), s);
+    if (d->N) {
+        hipLaunchKernelGGL(k_vscatter, dim3(unsigned((d->N + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                           d->row_off.as<uint32_t>(), d->item.as<uint32_t>(), uint64_t(d->N),
+                           d->vert_off.as<uint64_t>(), cursor.as<uint32_t>(), d->vert_sid.as<uint32_t>(),
+                           d->vert_item.as<uint32_t>());
+        FSM_HIP(hipGetLastError());
+    }
+    d->sup.resize(size_t(d->U));
+    if (d->U) FSM_HIP(hipMemcpyAsync(d->sup.data(), cnt.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, s));
+    FSM_HIP(hipStreamSynchronize(s));
+    db->tsr_dev = d.release();
+}
+
+void tsr_release(fsm_db* db) {
+    delete db->tsr_dev;
+    db->tsr_dev = nullptr;
+}
+
+void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** out) {
+    const double t0 = now_ms();
+    TsrDevDB* d = db->tsr_dev;
+    hipStream_t s = ctx->stream;
+    const uint32_t U = uint32_t(d->U);
+    Replay rp{k, minconf};
+    std::vector<uint64_t> voff(size_t(U) + 1);
+    FSM_HIP(hipMemcpyAsync(voff.data(), d->vert_off.p, (size_t(U) + 1) * 8, hipMemcpyDeviceToHost, s));
+    DevBuf d_sup(size_t(std::max<uint32_t>(U, 1)) * 4);
+    FSM_HIP(hipMemcpyAsync(d_sup.p, d->sup.data(), size_t(U) * 4, hipMemcpyHostToDevice, s));
+    FSM_HIP(hipStreamSynchronize(s));
+    const std::vector<uint32_t>& sup = d->sup;
+
+    // ---------------- pair phase (i ascending, j > i; IJ then JI)
+    uint32_t nb_items = 16;
+    const uint64_t scr_cap_items = std::max<uint64_t>(1, (uint64_t(256) << 20) / (uint64_t(std::max<uint32_t>(U, 1)) * 8));
+    DevBuf scr;
+    uint64_t scr_items = 0;
+    std::vector<PairRec> recs;
+    for (uint32_t a = 0; a < U;) {
+        const uint32_t t = rp.minsup;
+        const uint32_t nb = uint32_t(std::min<uint64_t>({uint64_t(nb_items), uint64_t(U - a), scr_cap_items}));
+        const uint32_t b = a + nb;
+        if (scr_items < nb) {
+            scr.alloc(uint64_t(nb) * U * 8);
+            FSM_HIP(hipMemsetAsync(scr.p, 0, uint64_t(nb) * U * 8, s));
+            scr_items = nb;
+        }
+        const uint64_t v0 = voff[a], v1 = voff[b];
+        if (v1 > v0) {
+            hipLaunchKernelGGL(k_pairs, dim3(unsigned((v1 - v0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                               d->vert_sid.as<uint32_t>(), d->vert_item.as<uint32_t>(), v0, v1, a, U, t,
+                               d_sup.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
+                               d->first.as<uint32_t>(), d->last.as<uint32_t>(), scr.as<uint32_t>());
+            FSM_HIP(hipGetLastError());
+        }
+        DevBuf rowcnt(size_t(nb) * 4 + 4), rowoff((size_t(nb) + 1) * 8);
+        const unsigned grid = unsigned((uint64_t(nb) * 64 + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
+                           rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), (PairRec*)nullptr);
+        FSM_HIP(hipGetLastError());
+        scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nb, s);
+        std::vector<uint64_t> hoff(size_t(nb) + 1);
+        FSM_HIP(hipMemcpyAsync(hoff.data(), rowoff.p, (size_t(nb) + 1) * 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        const uint64_t nrec = hoff[nb];
+        DevBuf d_recs(std::max<uint64_t>(nrec, 1) * sizeof(PairRec));
+        hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
+                           rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>());
+        FSM_HIP(hipGetLastError());
+        recs.resize(nrec);
+        if (nrec) FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        for (uint32_t g = 0; g < nb; ++g) {
+            const uint32_t i = a + g;
+            if (sup[i] < rp.minsup) continue;
+            for (uint64_t q = hoff[g]; q < hoff[g + 1]; ++q) {
+                const PairRec& pr = recs[q];
+                const uint32_t j = pr.j;
+                if (sup[j] < rp.minsup) continue;
+                if (pr.ij >= rp.minsup) {
+                    Rule* r = rp.make();
+                    r->X = {i};
+                    r->Y = {j};
+                    r->sup = pr.ij;
+                    r->conf = double(pr.ij) / double(sup[i]);
+                    r->nX = sup[i];
+                    if (r->conf >= minconf) rp.save(r);
+                    rp.reg(r, true);
+                }
+                if (pr.ji >= rp.minsup) {
+                    Rule* r = rp.make();
+                    r->X = {j};
+                    r->Y = {i};
+                    r->sup = pr.ji;
+                    r->conf = double(pr.ji) / double(sup[j]);
+                    r->nX = sup[j];
+                    if (r->conf >= minconf) rp.save(r);
+                    rp.reg(r, true);
+                }
+            }
+        }
+        if (nrec < (1u << 20)) nb_items = std::min<uint32_t>(nb_items * 2, 4096);
+        else if (nrec > (4u << 20) && nb_items > 1) nb_items /= 2;
+        a = b;
+    }
+    scr.release();
+    const double t1 = now_ms();
+
+    // ---------------- expansions
+    DevBuf TL(size_t(std::max<uint32_t>(U, 1)) * 4), DL(size_t(std::max<uint32_t>(U, 1)) * 4),
+        TR(size_t(std::max<uint32_t>(U, 1)) * 4), nX(8), nout(8);
+    FSM_HIP(hipMemsetAsync(TL.p, 0, size_t(U) * 4, s));
+    FSM_HIP(hipMemsetAsync(DL.p, 0, size_t(U) * 4, s));
+    FSM_HIP(hipMemsetAsync(TR.p, 0, size_t(U) * 4, s));
+    uint32_t ecap = 1u << 16;
+    DevBuf d_exp(size_t(ecap) * sizeof(ExpRec));
+    std::vector<ExpRec> er;
+    int64_t expansions = 0;
+    while (!rp.cand.empty()) {
+        Rule* r = rp.cand.top();
+        rp.cand.pop();
+        if (r->sup < rp.minsup) break;
+        const bool doL = r->expandLR;
+        if (r->X.size() >= kMaxSide || r->Y.size() >= kMaxSide)
+            throw Error(FSM_ELIMIT, "TSR: rule side exceeds " + std::to_string(kMaxSide - 1) + " items");
+        Side sd{};
+        sd.nx = uint32_t(r->X.size());
+        sd.ny = uint32_t(r->Y.size());
+        sd.doL = doL;
+        sd.doR = 1;
+        sd.maxX = r->X.back();
+        sd.maxY = r->Y.back();
+        std::copy(r->X.begin(), r->X.end(), sd.X);
+        std::copy(r->Y.begin(), r->Y.end(), sd.Y);
+        // driver list: rarest item of X (expandL needs all of sids(X)), else of X u Y
+        uint32_t drv = r->X[0];
+        bool drv_in_x = true;
+        for (uint32_t x : r->X) if (sup[x] < sup[drv]) drv = x;
+        if (!doL)
+            for (uint32_t y : r->Y) if (sup[y] < sup[drv]) { drv = y; drv_in_x = false; }
+        const uint64_t nd = voff[drv + 1] - voff[drv];
+        const uint32_t t = rp.minsup;
+        FSM_HIP(hipMemsetAsync(nX.p, 0, 8, s));
+        FSM_HIP(hipMemsetAsync(nout.p, 0, 4, s));
+        if (nd) {
+            hipLaunchKernelGGL(k_expand, dim3(unsigned((nd + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sd,
+                               d->vert_sid.as<uint32_t>() + voff[drv], uint32_t(nd), d->row_off.as<uint32_t>(),
+                               d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
+                               TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), nX.as<uint32_t>());
+            FSM_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_expand_compact, dim3(unsigned((U + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                           TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), U, t, d_exp.as<ExpRec>(),
+                           nout.as<uint32_t>(), ecap);
+        FSM_HIP(hipGetLastError());
+        uint32_t hn[2] = {0, 0};
+        FSM_HIP(hipMemcpyAsync(&hn[0], nout.p, 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(&hn[1], nX.p, 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        if (hn[0] > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
+        er.resize(hn[0]);
+        if (hn[0]) {
+            FSM_HIP(hipMemcpyAsync(er.data(), d_exp.p, size_t(hn[0]) * sizeof(ExpRec), hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipStreamSynchronize(s));
+        }
+        if (drv_in_x && hn[1] != r->nX)
+            throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(hn[1]) + " vs " +
+                                         std::to_string(r->nX) + ")");
+        std::sort(er.begin(), er.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
+        expansions += doL ? 2 : 1;
+        if (doL) {  // expandL: X u {c} => Y
+            for (const ExpRec& e : er) {
+                if (e.tl == 0 || e.tl < rp.minsup) continue;
+                Rule* nr = rp.make();
+                nr->X = r->X;
+                nr->X.push_back(e.c);
+                nr->Y = r->Y;
+                nr->sup = e.tl;
+                nr->conf = double(e.tl) / double(e.dl);
+                nr->nX = e.dl;
+                if (nr->conf >= minconf) rp.save(nr);
+                rp.reg(nr, true);
+            }
+        }
+        for (const ExpRec& e : er) {  // expandR: X => Y u {c}
+            if (e.tr == 0 || e.tr < rp.minsup) continue;
+            Rule* nr = rp.make();
+            nr->X = r->X;
+            nr->Y = r->Y;
+            nr->Y.push_back(e.c);
+            nr->sup = e.tr;
+            nr->conf = double(e.tr) / double(r->nX);
+            nr->nX = r->nX;
+            if (nr->conf >= minconf) rp.save(nr);
+            rp.reg(nr, false);
+        }
+    }
+    // ---------------- result = kRules
+    std::vector<const Rule*> res;
+    while (!rp.krules.empty()) {
+        res.push_back(rp.krules.top());
+        rp.krules.pop();
+    }
+    auto* o = static_cast<fsm_rules*>(std::calloc(1, sizeof(fsm_rules)));
+    if (!o) throw Error(FSM_ENOMEM, "calloc failed");
+    const size_t n = res.size();
+    o->n = int64_t(n);
+    o->total = d->N;
+    o->final_minsup = int32_t(rp.minsup);
+    size_t na = 0, nc = 0;
+    for (const Rule* r : res) { na += r->X.size(); nc += r->Y.size(); }
+    o->support = static_cast<int32_t*>(std::malloc(std::max<size_t>(n, 1) * 4));
+    o->confidence = static_cast<double*>(std::malloc(std::max<size_t>(n, 1) * 8));
+    o->ante_off = static_cast<int64_t*>(std::malloc((n + 1) * 8));
+    o->cons_off = static_cast<int64_t*>(std::malloc((n + 1) * 8));
+    o->ante = static_cast<int32_t*>(std::malloc(std::max<size_t>(na, 1) * 4));
+    o->cons = static_cast<int32_t*>(std::malloc(std::max<size_t>(nc, 1) * 4));
+    if (!o->support || !o->confidence || !o->ante_off || !o->cons_off || !o->ante || !o->cons) {
+        fsm_rules_free(o);
+        throw Error(FSM_ENOMEM, "malloc failed");
+    }
+    o->ante_off[0] = o->cons_off[0] = 0;
+    for (size_t q = 0; q < n; ++q) {
+        const Rule* r = res[q];
+        o->support[q] = int32_t(r->sup);
+        o->confidence[q] = r->conf;
+        for (size_t x = 0; x < r->X.size(); ++x) o->ante[o->ante_off[q] + int64_t(x)] = db->tsr.item_val[r->X[x]];
+        for (size_t x = 0; x < r->Y.size(); ++x) o->cons[o->cons_off[q] + int64_t(x)] = db->tsr.item_val[r->Y[x]];
+        o->ante_off[q + 1] = o->ante_off[q] + int64_t(r->X.size());
+        o->cons_off[q + 1] = o->cons_off[q] + int64_t(r->Y.size());
+    }
+    ctx->stats.expansions = expansions;
+    ctx->stats.rules = int64_t(n);
+    ctx->stats.ms_f2 = t1 - t0;          // pair phase
+    ctx->stats.ms_lattice = now_ms() - t1;  // expansions
+    ctx->stats.ms_mine = now_ms() - t0;
+    *out = o;
+}
+
+}  // namespace fsm

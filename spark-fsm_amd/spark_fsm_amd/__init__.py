@@ -1,0 +1,9 @@
+"""spark_fsm_amd — MI355X engine for spark-fsm's hot path (SPADE + TSR).
+
+The product is libfsm.so (C ABI in include/fsm.h); this package is the host
+mirror of the reference's Scala API over it.
+"""
+from ._lib import FsmError, FsmParseError, MODE_SPADE, MODE_TSR, LIB_PATH  # noqa: F401
+from .engine import Engine, DB, default_engine  # noqa: F401
+from .api import (Pattern, Rule, extract_rdd_patterns, extract_rdd_rules,  # noqa: F401
+                  spade_actor_patterns, tsr_actor_rules)

@@ -1,0 +1,137 @@
+"""Engine: one fsm_ctx (HIP stream + device buffers) and its flattened DBs."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import MODE_SPADE, MODE_TSR, check
+
+
+class Engine:
+    """Owns a libfsm context on one gfx950 device."""
+
+    def __init__(self, device=0, verbose=False, mem_budget=0):
+        L = _lib.load()
+        opts = _lib.Opts()
+        opts.device = device
+        opts.nranks = 1
+        opts.rank = 0
+        opts.verbose = 1 if verbose else 0
+        opts.mem_budget = int(mem_budget)
+        self._ctx = ctypes.c_void_p()
+        check(L.fsm_ctx_create(ctypes.byref(opts), ctypes.byref(self._ctx)), None)
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.fsm_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------ DBs
+    def db_from_spmf(self, records, mode):
+        """records: sequence of (sid, spmf_line) — the RDD[(Int,String)]."""
+        n = len(records)
+        sids = (ctypes.c_int32 * max(n, 1))(*[int(s) for s, _ in records])
+        enc = [l.encode("utf-8") if isinstance(l, str) else bytes(l) for _, l in records]
+        lines = (ctypes.c_char_p * max(n, 1))(*enc)
+        lens = (ctypes.c_int64 * max(n, 1))(*[len(b) for b in enc])
+        db = ctypes.c_void_p()
+        check(self._L.fsm_db_from_spmf(self._ctx, mode, sids, lines, lens, n, ctypes.byref(db)), self._ctx)
+        return DB(self, db, mode)
+
+    def db_from_tokens(self, sids, seq_off, tokens, mode):
+        sids = np.ascontiguousarray(sids, dtype=np.int32)
+        seq_off = np.ascontiguousarray(seq_off, dtype=np.int64)
+        tokens = np.ascontiguousarray(tokens, dtype=np.int64)
+        n = len(sids)
+        db = ctypes.c_void_p()
+        P = ctypes.POINTER
+        check(self._L.fsm_db_from_tokens(
+            self._ctx, mode, sids.ctypes.data_as(P(ctypes.c_int32)), seq_off.ctypes.data_as(P(ctypes.c_int64)),
+            tokens.ctypes.data_as(P(ctypes.c_int64)), n, ctypes.byref(db)), self._ctx)
+        return DB(self, db, mode)
+
+    # ------------------------------------------------------------ mining
+    def spade(self, db, support, dfs=True):
+        """-> (patterns: list[(itemsets tuple-of-tuples, support)], meta dict)."""
+        out = ctypes.POINTER(_lib.Patterns)()
+        check(self._L.fsm_spade_mine(self._ctx, db.handle, float(support), 1 if dfs else 0,
+                                     ctypes.byref(out)), self._ctx)
+        try:
+            p = out.contents
+            n = p.n
+            sup = np.ctypeslib.as_array(p.support, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0, np.int32)
+            po = np.ctypeslib.as_array(p.pat_off, shape=(n + 1,)).copy()
+            so = np.ctypeslib.as_array(p.set_off, shape=(p.n_sets + 1,)).copy()
+            it = np.ctypeslib.as_array(p.items, shape=(max(p.n_items, 1),))[:p.n_items].copy()
+            meta = {"total": p.total, "minsup": p.minsup}
+        finally:
+            self._L.fsm_patterns_free(out)
+        itl = it.tolist()
+        sol = so.tolist()
+        pats = []
+        for i in range(n):
+            sets = tuple(tuple(itl[sol[s]:sol[s + 1]]) for s in range(po[i], po[i + 1]))
+            pats.append((sets, int(sup[i])))
+        return pats, meta
+
+    def tsr(self, db, k, minconf):
+        """-> (rules: list[(antecedent, consequent, support, confidence)], meta)."""
+        out = ctypes.POINTER(_lib.Rules)()
+        check(self._L.fsm_tsr_mine(self._ctx, db.handle, int(k), float(minconf), ctypes.byref(out)), self._ctx)
+        try:
+            r = out.contents
+            rules = []
+            for i in range(r.n):
+                x = tuple(r.ante[q] for q in range(r.ante_off[i], r.ante_off[i + 1]))
+                y = tuple(r.cons[q] for q in range(r.cons_off[i], r.cons_off[i + 1]))
+                rules.append((x, y, r.support[i], r.confidence[i]))
+            meta = {"total": r.total, "final_minsup": r.final_minsup}
+        finally:
+            self._L.fsm_rules_free(out)
+        return rules, meta
+
+    def stats(self):
+        st = _lib.Stats()
+        check(self._L.fsm_get_stats(self._ctx, ctypes.byref(st)), self._ctx)
+        return st.as_dict()
+
+
+class DB:
+    def __init__(self, engine, handle, mode):
+        self.engine = engine
+        self.handle = handle
+        self.mode = mode
+
+    def free(self):
+        if self.handle:
+            self.engine._L.fsm_db_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+_default = None
+
+
+def default_engine():
+    global _default
+    if _default is None:
+        _default = Engine(0)
+    return _default

@@ -1,0 +1,132 @@
+"""CPU tests: the CPU restatement (oracle/) against the committed golden
+fixtures and against the independent brute-force enumerator.  No GPU."""
+import json
+import os
+import random
+
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from oracle import brute, oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def canon_patterns(pats):
+    return [(tuple(tuple(s) for s in p), sup) for p, sup in pats]
+
+
+@pytest.mark.parametrize("case", load("spade_cases.json"), ids=lambda c: c["name"])
+def test_oracle_spade_golden(case):
+    recs = [tuple(r) for r in case["records"]]
+    o = oracle.spade(recs, case["support"])
+    assert o["patterns"] == canon_patterns(case["patterns"])
+    assert o["minsup"] == case["minsup"]
+    assert o["joins"] == case["joins"]
+
+
+@pytest.mark.parametrize("case", load("tsr_cases.json"), ids=lambda c: c["name"])
+def test_oracle_tsr_golden(case):
+    recs = [tuple(r) for r in case["records"]]
+    o = oracle.tsr(recs, case["k"], case["minconf"])
+    exp = [(tuple(x), tuple(y), s, c) for x, y, s, c in case["rules"]]
+    assert o["rules"] == exp
+    assert o["final_minsup"] == case["final_minsup"]
+    brute.check_tsr(o["rules"], brute.brute_tsr_valid(recs, case["minconf"]), case["k"])
+
+
+ERR = load("error_cases.json")
+
+
+@pytest.mark.parametrize("case", ERR["spade"], ids=lambda c: c["name"])
+def test_oracle_spade_errors(case):
+    with pytest.raises(oracle.OracleError):
+        oracle.spade([tuple(r) for r in case["records"]], 0.5)
+
+
+@pytest.mark.parametrize("case", ERR["tsr"], ids=lambda c: c["name"])
+def test_oracle_tsr_errors(case):
+    with pytest.raises(oracle.OracleError):
+        oracle.tsr([tuple(r) for r in case["records"]], 3, 0.5)
+
+
+def test_java_split_semantics():
+    assert brute.java_split_space("") == [""]
+    assert brute.java_split_space(" ") == []
+    assert brute.java_split_space("1 -1  ") == ["1", "-1"]
+    assert brute.java_split_space(" 1") == ["", "1"]
+    # trailing spaces are legal for the reference, a leading one is not
+    assert oracle.spade([(0, "1 -1 2 -1   ")], 1.0)["patterns"] == [(((1,),), 1), (((1,), (2,)), 1), (((2,),), 1)]
+
+
+def test_threshold_is_ceil_of_support_times_total():
+    recs = [(i, "1 -1") for i in range(3)] + [(3, "2 -1")]
+    # ceil(0.5 * 4) = 2 ; ceil(0.26 * 4) = ceil(1.04) = 2 ; ceil(0.25*4) = 1
+    assert oracle.spade(recs, 0.26)["minsup"] == 2
+    assert oracle.spade(recs, 0.25)["minsup"] == 1
+    assert [p for p, _ in oracle.spade(recs, 0.26)["patterns"]] == [((1,),)]
+
+
+def _db(draw_items, rng, ts):
+    pass
+
+
+records_st = st.lists(
+    st.lists(st.lists(st.integers(1, 4), min_size=1, max_size=3), min_size=0, max_size=4),
+    min_size=1, max_size=7)
+
+
+def _render(db, ts_every=0):
+    out = []
+    for s, seq in enumerate(db):
+        toks = []
+        for k, iset in enumerate(seq):
+            if ts_every and k % ts_every == 1:
+                toks.append("<%d>" % (k * 2 % 5))
+            toks += [str(i) for i in iset] + ["-1"]
+        out.append((s, " ".join(toks + ["-2"])))
+    return out
+
+
+@settings(max_examples=60, deadline=None)
+@given(records_st, st.sampled_from([0.0, 0.2, 0.34, 0.5, 0.75, 1.0]), st.integers(0, 3))
+def test_oracle_spade_matches_brute(db, support, ts_every):
+    recs = _render(db, ts_every)
+    assert oracle.spade(recs, support)["patterns"] == brute.brute_spade(recs, support)
+
+
+@settings(max_examples=60, deadline=None)
+@given(records_st, st.integers(1, 6), st.sampled_from([0.0, 0.25, 0.5, 0.9]))
+def test_oracle_tsr_invariants(db, k, minconf):
+    recs = _render(db)
+    if not any(db):
+        with pytest.raises(oracle.OracleError):
+            oracle.tsr(recs, k, minconf)
+        return
+    o = oracle.tsr(recs, k, minconf)
+    brute.check_tsr(o["rules"], brute.brute_tsr_valid(recs, minconf), k)
+
+
+def test_oracle_deterministic_on_quest_sample():
+    from tools import gen
+    ds = gen.quest(2000, seed=3)
+    recs = ds.records()
+    a = oracle.spade(recs, 0.01)
+    b = oracle.spade(list(reversed(recs)), 0.01)  # record order must not matter
+    assert a["patterns"] == b["patterns"] and a["joins"] == b["joins"]
+    assert len(a["patterns"]) > 50
+
+
+def test_tsr_random_orders_are_definitional():
+    rng = random.Random(5)
+    for _ in range(20):
+        db = [[[rng.randint(1, 5)] for _ in range(rng.randint(1, 6))] for _ in range(rng.randint(2, 8))]
+        recs = _render(db)
+        k = rng.randint(1, 10)
+        mc = rng.choice([0.0, 0.5])
+        brute.check_tsr(oracle.tsr(recs, k, mc)["rules"], brute.brute_tsr_valid(recs, mc), k)

@@ -1,0 +1,275 @@
+"""GPU parity: libfsm (HIP, gfx950) vs the CPU restatement / golden fixtures.
+
+Bit-exact for everything (integer supports, pattern sets, rule sets and the
+double confidences, which are the same IEEE division on both sides).  Small
+and medium cases compare full outputs with the oracle; full-size configs use
+size-independent properties (definitional re-count of sampled outputs,
+threshold / top-k invariants)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def fsm():
+    import spark_fsm_amd
+    return spark_fsm_amd
+
+
+@pytest.fixture(scope="module")
+def eng(fsm):
+    e = fsm.Engine(0)
+    yield e
+    e.close()
+
+
+def gpu_spade(eng, recs, support, tokens=None):
+    from spark_fsm_amd import MODE_SPADE
+    if tokens is not None:
+        db = eng.db_from_tokens(tokens.sids, tokens.seq_off, tokens.tokens, MODE_SPADE)
+    else:
+        db = eng.db_from_spmf(recs, MODE_SPADE)
+    try:
+        pats, meta = eng.spade(db, support)
+    finally:
+        db.free()
+    return sorted(pats), meta, eng.stats()
+
+
+def gpu_tsr(eng, recs, k, minconf, tokens=None):
+    from spark_fsm_amd import MODE_TSR
+    if tokens is not None:
+        db = eng.db_from_tokens(tokens.sids, tokens.seq_off, tokens.tokens, MODE_TSR)
+    else:
+        db = eng.db_from_spmf(recs, MODE_TSR)
+    try:
+        rules, meta = eng.tsr(db, k, minconf)
+    finally:
+        db.free()
+    rules.sort(key=lambda t: (-t[2], t[0], t[1]))
+    return rules, meta, eng.stats()
+
+
+def canon(pats):
+    return [(tuple(tuple(s) for s in p), sup) for p, sup in pats]
+
+
+# ------------------------------------------------------------------ golden
+@pytest.mark.parametrize("case", load("spade_cases.json"), ids=lambda c: c["name"])
+def test_spade_golden(eng, case):
+    recs = [tuple(r) for r in case["records"]]
+    pats, meta, st = gpu_spade(eng, recs, case["support"])
+    assert pats == canon(case["patterns"])
+    assert meta["minsup"] == case["minsup"] or not case["patterns"]
+    assert st["joins"] == case["joins"]
+
+
+@pytest.mark.parametrize("case", load("tsr_cases.json"), ids=lambda c: c["name"])
+def test_tsr_golden(eng, case):
+    recs = [tuple(r) for r in case["records"]]
+    rules, meta, _ = gpu_tsr(eng, recs, case["k"], case["minconf"])
+    assert rules == [(tuple(x), tuple(y), s, c) for x, y, s, c in case["rules"]]
+    assert meta["final_minsup"] == case["final_minsup"]
+
+
+ERR = load("error_cases.json")
+
+
+@pytest.mark.parametrize("case", ERR["spade"], ids=lambda c: c["name"])
+def test_spade_errors(eng, fsm, case):
+    with pytest.raises(fsm.FsmParseError):
+        gpu_spade(eng, [tuple(r) for r in case["records"]], 0.5)
+
+
+@pytest.mark.parametrize("case", ERR["tsr"], ids=lambda c: c["name"])
+def test_tsr_errors(eng, fsm, case):
+    with pytest.raises(fsm.FsmParseError):
+        gpu_tsr(eng, [tuple(r) for r in case["records"]], 3, 0.5)
+
+
+def test_tsr_k_zero_rejected(eng, fsm):
+    with pytest.raises(fsm.FsmError):
+        gpu_tsr(eng, [(0, "1 -1 2 -1")], 0, 0.5)
+
+
+# ------------------------------------------------------- random vs oracle
+def rand_records(rng, nseq, nitems, maxsets, maxset, ts):
+    recs = []
+    for s in range(nseq):
+        toks = []
+        for _ in range(rng.randint(0, maxsets)):
+            if ts and rng.random() < 0.3:
+                toks.append("<%d>" % rng.randint(0, 9))
+            toks += [str(rng.randint(1, nitems)) for _ in range(rng.randint(1, maxset))]
+            toks.append("-1")
+        recs.append((s, " ".join(toks + ["-2"])))
+    return recs
+
+
+def test_spade_random_vs_oracle(eng):
+    from oracle import oracle
+    rng = random.Random(11)
+    for it in range(60):
+        recs = rand_records(rng, rng.randint(1, 60), rng.randint(2, 12), 8, 4, ts=it % 2 == 0)
+        sup = rng.choice([0.02, 0.05, 0.1, 0.2, 0.4])
+        o = oracle.spade(recs, sup)
+        pats, _, st = gpu_spade(eng, recs, sup)
+        assert pats == o["patterns"], (it, recs, sup)
+        assert st["joins"] == o["joins"]
+
+
+def test_tsr_random_vs_oracle(eng):
+    from oracle import oracle
+    rng = random.Random(12)
+    for it in range(60):
+        recs = rand_records(rng, rng.randint(2, 60), rng.randint(2, 12), 8, 3, ts=False)
+        if not any(t not in ("-1", "-2") for _, l in recs for t in l.split(" ")):
+            continue
+        k, mc = rng.randint(1, 40), rng.choice([0.0, 0.2, 0.5, 0.9])
+        o = oracle.tsr(recs, k, mc)
+        rules, meta, _ = gpu_tsr(eng, recs, k, mc)
+        assert rules == o["rules"], (it, recs, k, mc)
+        assert meta["final_minsup"] == o["final_minsup"]
+
+
+def test_long_sequences_multiword_masks(eng):
+    """> 64 distinct timestamps per sequence (W = 2 and W = 4 masks)."""
+    from oracle import oracle
+    rng = random.Random(3)
+    for nsets in (70, 150):
+        recs = []
+        for s in range(12):
+            toks = []
+            for _ in range(nsets):
+                toks += [str(rng.randint(1, 6)), "-1"]
+            recs.append((s, " ".join(toks)))
+        o = oracle.spade(recs, 1.0)
+        pats, _, st = gpu_spade(eng, recs, 1.0)
+        assert pats == o["patterns"] and st["joins"] == o["joins"]
+
+
+def test_small_memory_budget_splits_groups(fsm):
+    """Force the frontier into many small class groups: same answer."""
+    from oracle import oracle
+    from tools import gen
+    ds = gen.quest(3000, seed=2)
+    recs = ds.records()
+    o = oracle.spade(recs, 0.008)
+    with fsm.Engine(0, mem_budget=64 << 10) as e:
+        pats, _, st = gpu_spade(e, recs, 0.008)
+    assert pats == o["patterns"] and st["joins"] == o["joins"]
+    assert st["batches"] > 3
+
+
+# ------------------------------------------------------ dataset shapes
+@pytest.mark.parametrize("D,sup", [(10000, 0.005), (10000, 0.01), (20000, 0.004)])
+def test_spade_quest_vs_oracle(eng, D, sup):
+    from oracle import oracle
+    from tools import gen
+    ds = gen.quest(D, seed=1)
+    o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
+    pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
+    assert meta["minsup"] == o["minsup"]
+    assert pats == o["patterns"]
+    assert st["joins"] == o["joins"]
+
+
+def test_spade_text_and_token_paths_agree(eng):
+    from tools import gen
+    ds = gen.quest(3000, seed=5)
+    a, _, _ = gpu_spade(eng, ds.records(), 0.01)
+    b, _, _ = gpu_spade(eng, None, 0.01, tokens=ds)
+    assert a == b and len(a) > 10
+
+
+@pytest.mark.parametrize("shape,n,sup", [("bible", 2000, 0.03), ("sign", 730, 0.35)])
+def test_spade_long_sequence_shapes_vs_oracle(eng, shape, n, sup):
+    from oracle import oracle
+    from tools import gen
+    ds = getattr(gen, shape)(seed=1).head(n)
+    o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
+    pats, _, st = gpu_spade(eng, None, sup, tokens=ds)
+    assert pats == o["patterns"] and st["joins"] == o["joins"]
+    assert len(pats) > 20
+
+
+@pytest.mark.parametrize("n,k,mc", [(5000, 50, 0.5), (20000, 200, 0.5), (3000, 100, 0.1)])
+def test_tsr_kosarak_shape_vs_oracle(eng, n, k, mc):
+    from oracle import oracle
+    from tools import gen
+    ds = gen.kosarak(D=n, seed=1)
+    recs = ds.records()
+    o = oracle.tsr(recs, k, mc)
+    rules, meta, _ = gpu_tsr(eng, None, k, mc, tokens=ds)
+    assert rules == o["rules"]
+    assert meta["final_minsup"] == o["final_minsup"]
+
+
+def test_tsr_bible_shape_vs_oracle(eng):
+    from oracle import oracle
+    from tools import gen
+    ds = gen.bible(seed=2).head(1500)
+    o = oracle.tsr(ds.records(), 100, 0.3)
+    rules, meta, _ = gpu_tsr(eng, None, 100, 0.3, tokens=ds)
+    assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
+
+
+# ---------------------------------------------- full-size properties
+def test_spade_quest_d1m_properties(eng):
+    """BASELINE config 3 size (D1M, minsup 0.1%): definitional re-count of a
+    sample of the output, exact F1, threshold, prefix anti-monotonicity."""
+    from oracle import oracle
+    from tools import gen
+    ds = gen.quest(1000000, seed=1)
+    pats, meta, st = gpu_spade(eng, None, 0.001, tokens=ds)
+    assert meta["minsup"] == 1000 and meta["total"] == 1000000
+    sup = dict(pats)
+    assert min(sup.values()) >= 1000
+    # F1: exact distinct-sid supports
+    tk, so = ds.tokens, ds.seq_off
+    sid = np.repeat(np.arange(len(ds)), np.diff(so))
+    m = tk >= 0
+    u = np.unique(sid[m].astype(np.int64) * (1 << 32) + tk[m])
+    items, counts = np.unique(u & 0xFFFFFFFF, return_counts=True)
+    f1 = {((int(i),),): int(c) for i, c in zip(items, counts) if c >= 1000}
+    assert {p: s for p, s in sup.items() if len(p) == 1 and len(p[0]) == 1} == f1
+    # every pattern's prefix (drop last item) is frequent with >= support
+    for p, s in pats:
+        if sum(len(x) for x in p) == 1:
+            continue
+        last = p[-1]
+        par = p[:-1] + ((last[:-1],) if len(last) > 1 else ())
+        assert sup[par] >= s
+    # definitional re-count of a random sample of multi-item patterns
+    rng = random.Random(0)
+    multi = [x for x in pats if sum(len(s) for s in x[0]) >= 2]
+    assert len(multi) > 100
+    for p, s in rng.sample(multi, 25):
+        assert oracle.pattern_support(so, tk, p) == s, p
+    assert st["joins"] > 4.0e7
+
+
+def test_tsr_kosarak_full_properties(eng):
+    """BASELINE config 4 size: 990,002 sequences, k = 1000, minconf 0.5."""
+    from oracle import oracle
+    from tools import gen
+    ds = gen.kosarak(seed=1)
+    rules, meta, _ = gpu_tsr(eng, None, 1000, 0.5, tokens=ds)
+    assert len(rules) >= 1000
+    assert min(r[2] for r in rules) == meta["final_minsup"]
+    rng = random.Random(0)
+    for x, y, s, c in rng.sample(rules, 20):
+        sup, nx = oracle.rule_support(ds.seq_off, ds.tokens, list(x), list(y))
+        assert sup == s and c == sup / nx and c >= 0.5
