@@ -96,7 +96,7 @@ def zipf(D, nitems, zipf_s, mean_len, sigma, max_len, p_succ, distinct, seed, na
 
 
 def kosarak(D=990002, seed=1):
-    return zipf(D, 41270, 1.0, 8.1, 1.1, 2500, 0.3, True, seed, "kosarak-shaped-D%d" % D)
+    return zipf(D, 41270, 1.0, 8.1, 1.1, 2500, 0.6, True, seed, "kosarak-shaped-D%d" % D)
 
 
 def bible(D=36369, seed=1):
