@@ -62,18 +62,29 @@ template <int W> __device__ __forceinline__ void store_mask(uint64_t* __restrict
     }
 }
 
-// first / last set bit (mask known non-zero)
+// first / last set bit (mask known non-zero).  Branch-free (selects only): an
+// earlier early-return form was lowered into divergent branches whose register
+// shuffling lost mask words in k_emit<4> (hipcc 7.2, gfx950).
 template <int W> __device__ __forceinline__ uint32_t mask_lo(const uint64_t (&m)[W]) {
+    uint32_t lo = 0;
 #pragma unroll
-    for (int k = 0; k < W; ++k)
-        if (m[k]) return uint32_t(k * 64 + __builtin_ctzll(m[k]));
-    return 0;
+    for (int k = W - 1; k >= 0; --k) lo = m[k] ? uint32_t(k * 64 + __builtin_ctzll(m[k])) : lo;
+    return lo;
 }
 template <int W> __device__ __forceinline__ uint32_t mask_hi(const uint64_t (&m)[W]) {
+    uint32_t hi = 0;
 #pragma unroll
-    for (int k = W - 1; k >= 0; --k)
-        if (m[k]) return uint32_t(k * 64 + 63 - __builtin_clzll(m[k]));
-    return 0;
+    for (int k = 0; k < W; ++k) hi = m[k] ? uint32_t(k * 64 + 63 - __builtin_clzll(m[k])) : hi;
+    return hi;
+}
+// clear every eid <= lo (temporal join: bits strictly after the first bit of L(i))
+template <int W> __device__ __forceinline__ void mask_clear_upto(uint64_t (&m)[W], uint32_t lo) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const int sh = int(lo) + 1 - k * 64;  // bits [0, sh) of word k are cleared
+        const uint64_t keep = sh <= 0 ? ~0ull : (sh >= 64 ? 0ull : (~0ull << sh));
+        m[k] &= keep;
+    }
 }
 
 // ---------------------------------------------------------------- scans

@@ -1,5 +1,7 @@
 // device_util.hip — three-phase exclusive scan (tile scan -> scan of tile sums
 // -> add), 2048 elements per 256-thread tile, wave64 shuffles + LDS.
+#include <cstdlib>
+
 #include "device_util.h"
 
 namespace fsm {
@@ -57,16 +59,16 @@ template <class T> void scan_impl(const T* in, uint64_t* out, size_t n, hipStrea
     const size_t nt = (n + kScanTile - 1) / kScanTile;
     if (nt == 1) {
         hipLaunchKernelGGL(k_scan_tile<T>, dim3(1), dim3(kScanT), 0, s, in, out, out + n, n);
-        FSM_HIP(hipGetLastError());
+        FSM_LAUNCHED("k_scan_tile", s);
         return;
     }
     DevBuf sums((nt) * sizeof(uint64_t));
     DevBuf offs((nt + 1) * sizeof(uint64_t));
     hipLaunchKernelGGL(k_scan_tile<T>, dim3(unsigned(nt)), dim3(kScanT), 0, s, in, out, sums.as<uint64_t>(), n);
-    FSM_HIP(hipGetLastError());
+    FSM_LAUNCHED("k_scan_tile", s);
     scan_impl<uint64_t>(sums.as<uint64_t>(), offs.as<uint64_t>(), nt, s);
     hipLaunchKernelGGL(k_scan_add, dim3(unsigned(nt)), dim3(kScanT), 0, s, out, offs.as<uint64_t>(), n);
-    FSM_HIP(hipGetLastError());
+    FSM_LAUNCHED("k_scan_add", s);
     FSM_HIP(hipMemcpyAsync(out + n, offs.as<uint64_t>() + nt, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     FSM_HIP(hipStreamSynchronize(s));  // sums/offs are released on return
 }
@@ -75,5 +77,24 @@ template <class T> void scan_impl(const T* in, uint64_t* out, size_t n, hipStrea
 
 void scan_exclusive(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint32_t>(in, out, n, s); }
 void scan_exclusive(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint64_t>(in, out, n, s); }
+
+bool debug_sync() {
+    static const bool on = [] {
+        const char* v = std::getenv("FSM_DEBUG_SYNC");
+        return v && v[0] == '1';
+    }();
+    return on;
+}
+
+void check_launch(const char* what, hipStream_t s, const char* file, int line) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && debug_sync()) {
+        e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipGetLastError();
+    }
+    if (e != hipSuccess)
+        throw Error(FSM_EDEVICE, std::string("kernel ") + what + ": " + hipGetErrorString(e) + " (" + file + ":" +
+                                     std::to_string(line) + ")");
+}
 
 }  // namespace fsm

@@ -278,6 +278,7 @@ void flatten_spade(const Source& src, FlatSpade& out) {
     std::vector<std::vector<uint32_t>> row_len(static_cast<size_t>(T2));
     std::vector<std::vector<uint8_t>> row_words(static_cast<size_t>(T2));
     std::vector<int> maxE(size_t(T2), 0);
+    std::vector<int64_t> maxOcc(size_t(T2), 0);
     parallel_chunks(R, T2, [&](int t, int64_t a, int64_t b) {
         std::vector<uint64_t> buf;
         std::vector<std::pair<int32_t, int32_t>> ie;  // (item, eid)
@@ -304,6 +305,7 @@ void flatten_spade(const Source& src, FlatSpade& out) {
                 ie.push_back({int32_t(uint32_t(buf[q])), e});
             }
             maxE[size_t(t)] = std::max(maxE[size_t(t)], e + 1);
+            maxOcc[size_t(t)] = std::max<int64_t>(maxOcc[size_t(t)], int64_t(ie.size()));
             const int wr = std::max(1, std::min(64, (e + 1 + 63) / 64));
             std::sort(ie.begin(), ie.end());
             uint32_t len = 0;
@@ -325,6 +327,7 @@ void flatten_spade(const Source& src, FlatSpade& out) {
     });
     int mE = 0;
     for (int v : maxE) mE = std::max(mE, v);
+    for (int64_t v : maxOcc) out.max_occ = std::max(out.max_occ, v);
     if (mE > 4096)
         throw Error(FSM_ELIMIT, "SPADE: a sequence has " + std::to_string(mE) +
                                     " distinct timestamps; the engine supports up to 4096");

@@ -27,6 +27,12 @@ struct Error : std::runtime_error {
                                                 " (" __FILE__ ":" + std::to_string(__LINE__) + ")"); \
     } while (0)
 
+// After every kernel launch: report launch errors with the kernel's name; with
+// FSM_DEBUG_SYNC=1 in the environment also synchronize to localize device faults.
+bool debug_sync();
+void check_launch(const char* what, hipStream_t s, const char* file, int line);
+#define FSM_LAUNCHED(name, stream) ::fsm::check_launch(name, stream, __FILE__, __LINE__)
+
 inline double now_ms() {
     using namespace std::chrono;
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
@@ -73,6 +79,7 @@ struct DevBuf {
 struct FlatSpade {
     int64_t total = 0;                 // input records = sequences.count()
     int W = 1;                         // u64 words per eid mask (power of two)
+    int64_t max_occ = 0;               // max (item, eid) occurrences in one row = longest pattern
     std::vector<int32_t> item_val;     // dense item id -> item value (ascending)
     std::vector<uint32_t> row_off;     // [rows+1]
     std::vector<uint32_t> ent_item;    // dense item id

@@ -244,7 +244,6 @@ __global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work,
         if (n == 0) continue;
         const uint32_t base = ch[cc].ebegin + atomicAdd(&cursor[cc], n);
         uint32_t k = 0;
-        const uint32_t lw = lo_i >> 6, lb = lo_i & 63u;
         for (uint32_t q = 0; q < rl; ++q) {
             const uint32_t f = rb + q;
             const uint32_t mj = mem[f];
@@ -255,11 +254,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work,
                 if (cid != kNone) {
                     uint64_t m[W];
                     load_mask<W>(mask + size_t(f) * W, m);
-#pragma unroll
-                    for (int x = 0; x < W; ++x) {
-                        if (uint32_t(x) < lw) m[x] = 0;
-                        else if (uint32_t(x) == lw) m[x] = lb == 63u ? 0ull : (m[x] & (~0ull << (lb + 1u)));
-                    }
+                    mask_clear_upto<W>(m, lo_i);
                     const uint32_t d = base + k;
                     o.mem[d] = cid;
                     o.lohi[d] = mask_lo<W>(m) | (hj << 16);
@@ -340,6 +335,7 @@ struct Batch {
     std::vector<ChildInfo> children;
     std::vector<std::pair<size_t, size_t>> groups;
     size_t next_group = 0;
+    int64_t depth = 1;  // items per member pattern of this batch's classes
 };
 
 struct Miner {
@@ -404,8 +400,34 @@ struct Miner {
         st.classes += 1;
     }
 
+    // FSM_DEBUG_DUMP=1: print every class row entry of small batches (debugging aid)
+    void dump(Batch& b) {
+        static const bool on = [] { const char* v = std::getenv("FSM_DEBUG_DUMP"); return v && v[0] == '1'; }();
+        uint64_t n = 0;
+        for (auto& m : b.cls) n += m.nent;
+        if (!on || n > 4096) return;
+        std::vector<uint32_t> mem(n), lohi(n), pos(n);
+        std::vector<uint64_t> mk(n * uint64_t(W));
+        FSM_HIP(hipMemcpyAsync(mem.data(), b.slab.mem.p, n * 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(lohi.data(), b.slab.lohi.p, n * 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(pos.data(), b.slab.pos.p, n * 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(mk.data(), b.slab.mask.p, n * 8 * W, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        std::fprintf(stderr, "[dump] depth=%lld classes=%zu\n", (long long)b.depth, b.cls.size());
+        for (size_t c = 0; c < b.cls.size(); ++c) {
+            std::fprintf(stderr, "  class %zu D=%u nent=%u\n", c, b.cls[c].D, b.cls[c].nent);
+            for (uint32_t e = b.cls[c].ebegin; e < b.cls[c].ebegin + b.cls[c].nent; ++e) {
+                std::fprintf(stderr, "    e=%u mem=%u lo=%u hi=%u off=%u len=%u mask=", e, mem[e], lohi[e] & 0xFFFF,
+                             lohi[e] >> 16, pos[e] >> 16, pos[e] & 0xFFFF);
+                for (int w = 0; w < W; ++w) std::fprintf(stderr, "%016llx ", (unsigned long long)mk[e * W + w]);
+                std::fprintf(stderr, "\n");
+            }
+        }
+    }
+
     // count kernel + frequent-candidate extraction; fills b.children / b.groups
     void count_and_freq(Batch& b) {
+        dump(b);
         prepare(b);
         for (auto& m : b.cls) stats_for_class(m);
         fsm_stats& st = ctx->stats;
@@ -434,7 +456,7 @@ struct Miner {
                 default: FSM_COUNT(64); break;
             }
 #undef FSM_COUNT
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_count", s);
             FSM_HIP(hipEventRecord(ev.second, s));
             ev_count.push_back(ev);
             st.count_launches += 1;
@@ -451,7 +473,7 @@ struct Miner {
         if (nrows) {
             hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
                                b.d_cls.as<DClass>(), b.cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_freq_count", s);
         }
         scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
         uint64_t nfreq = 0;
@@ -463,7 +485,7 @@ struct Miner {
             hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
                                b.d_cls.as<DClass>(), b.cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(),
                                d_recs.as<FreqRec>());
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_freq_write", s);
             FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nfreq * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
             FSM_HIP(hipStreamSynchronize(s));
         }
@@ -574,7 +596,7 @@ struct Miner {
                 default: FSM_EMIT(64); break;
             }
 #undef FSM_EMIT
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_emit", s);
             FSM_HIP(hipEventRecord(ev.second, s));
             ev_emit.push_back(ev);
         }
@@ -602,7 +624,7 @@ struct Miner {
             hipLaunchKernelGGL(k_root_count, dim3(grid), dim3(kBlock), 0, s, db->row_off.as<uint32_t>(),
                                db->item.as<uint32_t>(), d_rank.as<uint32_t>(), r0, r1, rcnt.as<uint32_t>(),
                                flag.as<uint32_t>());
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_root_count", s);
         }
         scan_exclusive(rcnt.as<uint32_t>(), roff.as<uint64_t>(), r1 - r0, s);
         uint64_t E0 = 0;
@@ -629,7 +651,7 @@ struct Miner {
                 default: FSM_ROOTW(64); break;
             }
 #undef FSM_ROOTW
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_root_write", s);
         }
         ClassMeta m;
         const uint32_t F = uint32_t(freq_items.size());
@@ -719,7 +741,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             const unsigned grid = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, 8192));
             hipLaunchKernelGGL(k_f1, dim3(grid), dim3(kBlock), 0, ctx->stream, d->item.as<uint32_t>(), uint64_t(0),
                                uint64_t(d->E), d_f1.as<uint32_t>());
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_f1", ctx->stream);
         }
         if (d->U) FSM_HIP(hipMemcpyAsync(f1.data(), d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));
         FSM_HIP(hipStreamSynchronize(ctx->stream));
@@ -751,6 +773,11 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         }
         const size_t g = top.next_group++;
         auto nb = std::make_unique<Batch>();
+        nb->depth = top.depth + 1;
+        // a pattern cannot hold more items than the longest sequence has (item, eid) occurrences
+        if (nb->depth > db->spade.max_occ)
+            throw Error(FSM_EDEVICE, "SPADE internal error: lattice depth " + std::to_string(nb->depth) +
+                                         " exceeds the longest sequence (" + std::to_string(db->spade.max_occ) + ")");
         mn.emit(top, g, *nb);
         if (top.next_group >= top.groups.size()) {
             // parent fully emitted: release it before descending

@@ -309,7 +309,7 @@ void tsr_upload(fsm_ctx* ctx, fsm_db* db) {
         const unsigned g = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, 8192));
         hipLaunchKernelGGL(k_vcount, dim3(g), dim3(kBlock), 0, s, d->item.as<uint32_t>(), uint64_t(d->E),
                            cnt.as<uint32_t>());
-        FSM_HIP(hipGetLastError());
+        FSM_LAUNCHED("k_vcount", s);
     }
     scan_exclusive(cnt.as<uint32_t>(), d->vert_off.as<uint64_t>(), size_t(d->U), s);
     if (d->N) {
@@ -317,7 +317,7 @@ void tsr_upload(fsm_ctx* ctx, fsm_db* db) {
                            d->row_off.as<uint32_t>(), d->item.as<uint32_t>(), uint64_t(d->N),
                            d->vert_off.as<uint64_t>(), cursor.as<uint32_t>(), d->vert_sid.as<uint32_t>(),
                            d->vert_item.as<uint32_t>());
-        FSM_HIP(hipGetLastError());
+        FSM_LAUNCHED("k_vscatter", s);
     }
     d->sup.resize(size_t(d->U));
     if (d->U) FSM_HIP(hipMemcpyAsync(d->sup.data(), cnt.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, s));
@@ -364,13 +364,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                d->vert_sid.as<uint32_t>(), d->vert_item.as<uint32_t>(), v0, v1, a, U, t,
                                d_sup.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
                                d->first.as<uint32_t>(), d->last.as<uint32_t>(), scr.as<uint32_t>());
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_pairs", s);
         }
         DevBuf rowcnt(size_t(nb) * 4 + 4), rowoff((size_t(nb) + 1) * 8);
         const unsigned grid = unsigned((uint64_t(nb) * 64 + kBlock - 1) / kBlock);
         hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
                            rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), (PairRec*)nullptr);
-        FSM_HIP(hipGetLastError());
+        FSM_LAUNCHED("k_pairs_compact", s);
         scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nb, s);
         std::vector<uint64_t> hoff(size_t(nb) + 1);
         FSM_HIP(hipMemcpyAsync(hoff.data(), rowoff.p, (size_t(nb) + 1) * 8, hipMemcpyDeviceToHost, s));
@@ -379,7 +379,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         DevBuf d_recs(std::max<uint64_t>(nrec, 1) * sizeof(PairRec));
         hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
                            rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>());
-        FSM_HIP(hipGetLastError());
+        FSM_LAUNCHED("k_pairs_compact", s);
         recs.resize(nrec);
         if (nrec) FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
         FSM_HIP(hipStreamSynchronize(s));
@@ -460,12 +460,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                d->vert_sid.as<uint32_t>() + voff[drv], uint32_t(nd), d->row_off.as<uint32_t>(),
                                d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
                                TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), nX.as<uint32_t>());
-            FSM_HIP(hipGetLastError());
+            FSM_LAUNCHED("k_expand", s);
         }
         hipLaunchKernelGGL(k_expand_compact, dim3(unsigned((U + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                            TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), U, t, d_exp.as<ExpRec>(),
                            nout.as<uint32_t>(), ecap);
-        FSM_HIP(hipGetLastError());
+        FSM_LAUNCHED("k_expand_compact", s);
         uint32_t hn[2] = {0, 0};
         FSM_HIP(hipMemcpyAsync(&hn[0], nout.p, 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(&hn[1], nX.p, 4, hipMemcpyDeviceToHost, s));
