@@ -72,13 +72,13 @@ def main():
     prep = eng.stats()
 
     for _ in range(args.warmup):
-        eng.spade(db, args.support)
+        eng.spade_csr(db, args.support)
 
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        pats, meta = eng.spade(db, args.support)
+        csr, meta = eng.spade_csr(db, args.support)
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -122,7 +122,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_count (class pair-count)",
                      "kernel_ms_per_step": count_ms, "kernel_bytes_per_step": st["bytes_count_alg"]},
-        "extra": {"mine_ms": ms, "joins": joins_all, "patterns": len(pats), "minsup": meta["minsup"],
+        "extra": {"mine_ms": ms, "joins": joins_all, "patterns": meta["n"], "minsup": meta["minsup"],
                   "classes": st["classes"], "batches": st["batches"], "entries": st["entries"],
                   "ms_f1": st["ms_f1"], "ms_f2_root": st["ms_f2"], "ms_lattice": st["ms_lattice"],
                   "ms_emit_kernel": st["ms_emit_kernel"], "ms_flatten": prep["ms_flatten"],

@@ -1,6 +1,8 @@
 // device_util.hip — three-phase exclusive scan (tile scan -> scan of tile sums
 // -> add), 2048 elements per 256-thread tile, wave64 shuffles + LDS.
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "device_util.h"
 
@@ -77,6 +79,56 @@ template <class T> void scan_impl(const T* in, uint64_t* out, size_t n, hipStrea
 
 void scan_exclusive(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint32_t>(in, out, n, s); }
 void scan_exclusive(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint64_t>(in, out, n, s); }
+
+namespace {
+std::mutex g_pool_mu;
+std::multimap<size_t, void*>& pool_map() {
+    static auto* m = new std::multimap<size_t, void*>();  // leaked on exit on purpose
+    return *m;
+}
+}  // namespace
+
+void* pool_alloc(size_t bytes, size_t* granted) {
+    // size classes: powers of two up to 1 MiB, then sz/16 steps
+    size_t sz = 4096;
+    while (sz < bytes) sz <<= 1;
+    if (sz > (size_t(1) << 20)) {
+        const size_t step = sz >> 4;  // sz/2 < bytes <= sz: round bytes up to sz/16 steps
+        sz = (bytes + step - 1) / step * step;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        auto& m = pool_map();
+        auto it = m.lower_bound(sz);  // smallest cached block that fits, at most 2x larger
+        if (it != m.end() && it->first <= 2 * sz) {
+            void* p = it->second;
+            *granted = it->first;
+            m.erase(it);
+            return p;
+        }
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, sz);
+    if (e != hipSuccess) {
+        pool_trim();  // give cached blocks back and retry once
+        e = hipMalloc(&p, sz);
+        if (e != hipSuccess)
+            throw Error(FSM_ENOMEM, "hipMalloc(" + std::to_string(sz) + " bytes) failed: " + hipGetErrorString(e));
+    }
+    *granted = sz;
+    return p;
+}
+
+void pool_free(void* p, size_t granted) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    pool_map().emplace(granted, p);
+}
+
+void pool_trim() {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    for (auto& kv : pool_map()) (void)hipFree(kv.second);
+    pool_map().clear();
+}
 
 bool debug_sync() {
     static const bool on = [] {

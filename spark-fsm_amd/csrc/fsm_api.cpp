@@ -107,6 +107,8 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
 
 void fsm_ctx_destroy(fsm_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    fsm::pool_trim();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -38,7 +38,14 @@ inline double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-// Owning device allocation (hipMalloc) with RAII.
+// Device memory pool: hipMalloc/hipFree synchronize and cost milliseconds for
+// the multi-hundred-MB frontier slabs, so freed blocks are cached per size
+// class (power of two >= 4 KiB) and reused by later batches and later calls.
+void* pool_alloc(size_t bytes, size_t* granted);
+void pool_free(void* p, size_t granted);
+void pool_trim();  // hipFree every cached block (fsm_ctx_destroy)
+
+// Owning device allocation from the pool, RAII.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -54,17 +61,10 @@ struct DevBuf {
     ~DevBuf() { release(); }
     void alloc(size_t n) {
         release();
-        if (n == 0) n = 16;
-        hipError_t e = hipMalloc(&p, n);
-        if (e != hipSuccess) {
-            p = nullptr;
-            throw Error(FSM_ENOMEM, "hipMalloc(" + std::to_string(n) + " bytes) failed: " +
-                                        hipGetErrorString(e));
-        }
-        bytes = n;
+        p = pool_alloc(n ? n : 16, &bytes);
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) pool_free(p, bytes);
         p = nullptr;
         bytes = 0;
     }

@@ -6,29 +6,35 @@
 // member m of [P] (m = P->x or P x) present in that sequence:
 //     mem  u32  member id = rank(x) << 1 | type   (type 0 = sequence-ext, 1 = itemset-ext)
 //     lohi u32  first | last set eid of the entry's mask (16 bits each)
-//     pos  u32  offset-in-row << 16 | row length  (rows are contiguous runs)
+//     pos  u32  offset-in-row << 16 | row length  (rows are contiguous runs,
+//               sorted by member id)
 //     mask u64[W] eid bitmask (the id-list entry (sid, eids) of member m)
 // The entries of member m across all rows of the class ARE its id-list L(m).
 //
 // Kernels (one launch each per class batch; a batch = hundreds..thousands of
 // classes of one DFS frontier):
-//   k_count   every (entry i, entry j) pair of a row evaluates the temporal /
-//             equality join predicate of SURVEY A.2 and bumps the pair's
-//             support counter: ALL n^2 candidate joins of a class in a single
-//             streaming pass over its entries (vs n^2 separate list merges).
-//   k_freq_*  one wave per member row of the counter matrix: ballot the
-//             frequent candidates (support >= minsup), give them child member
-//             ids (wave prefix popcount), compact them for the host.
-//   k_emit    writes the child classes' rows (the joined id-lists of the
-//             frequent candidates) straight into the next frontier slab.
+//   k_count        every (entry i, entry j) pair of a row evaluates the temporal /
+//                  equality join predicate of SURVEY A.2 and bumps the pair's
+//                  support counter: ALL n^2 candidate joins of a class in one
+//                  streaming pass over its entries (vs n^2 separate list merges).
+//   k_rootpair_*   the root class (the F2 pair matrix, by far the largest) counts
+//                  without per-pair global atomics: pairs become 15-bit bucket
+//                  keys (LDS histogram of bucket sizes per block, scatter as u16
+//                  keys), then one LDS histogram of 32768 counters per bucket.
+//   k_freq_*       one wave per member row of the counter matrix: ballot the
+//                  frequent candidates (support >= minsup), give them child member
+//                  ids (wave prefix popcount), compact them for the host.
+//   k_emit         for each entry, walk its member's frequent children, binary-
+//                  search the partner entry in the (member-sorted) row, write the
+//                  joined id-list entries of the child classes into the next slab.
 // The root class is the flattened DB restricted to frequent items (F1 = k_f1,
-// row filter = k_root_*); its pair-count matrix is the F2 matrix (K2).
+// row filter = k_root_*).
 #include <algorithm>
-#include <cstdio>
-#include <numeric>
-#include <memory>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <memory>
+#include <numeric>
 
 #include "device_util.h"
 
@@ -44,12 +50,19 @@ namespace fsm {
 namespace {
 
 constexpr uint32_t kSeq = 0, kItm = 1;
-constexpr uint32_t kChunk = 2048;  // class entries per workgroup work item
+constexpr uint32_t kChunk = 2048;        // class entries per workgroup work item
+constexpr uint32_t kRootChunk = 16384;   // root entries per block in the bucketed pair count
+constexpr int kBucketBits = 15;          // 32768 counters (128 KiB LDS) per bucket
+constexpr uint32_t kMaxBuckets = 16384;  // LDS bucket histogram of the scatter pass (64 KiB)
 constexpr int kBlock = 256;
 
 struct DClass {
-    uint32_t ebegin, nent, D, cbase;
-    uint64_t cnt_off;
+    uint64_t cnt_off;     // counter matrix of the class
+    uint32_t ebegin, nent;
+    uint32_t D;           // member id space (2 * ranks)
+    uint32_t cbase;       // offset of the class's members in per-member arrays
+    uint32_t mshift;      // counter row of member mi = mi >> mshift (root: 1, only SEQ members)
+    uint32_t pad;
 };
 struct DWork {
     uint32_t cls, e0, e1, pad;
@@ -74,12 +87,25 @@ struct SlabPtrs {
 // ------------------------------------------------------------------ kernels
 
 // K1: F1 histogram = distinct-sid support per item (entries are distinct per
-// (row, item)).  SPADE.scala:113-126 `idList.getSupport()`.
+// (row, item)); LDS-privatized per block when the item dictionary fits.
+// SPADE.scala:113-126 `idList.getSupport()`.
 __global__ __launch_bounds__(kBlock) void k_f1(const uint32_t* __restrict__ item, uint64_t e0, uint64_t e1,
-                                               uint32_t* __restrict__ f1) {
+                                               uint32_t* __restrict__ f1, uint32_t U, int use_lds) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
+    if (use_lds) {
+        for (uint32_t u = threadIdx.x; u < U; u += blockDim.x) h[u] = 0;
+        __syncthreads();
+    }
     for (uint64_t e = e0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < e1;
-         e += uint64_t(gridDim.x) * blockDim.x)
-        atomicAdd(&f1[item[e]], 1u);
+         e += uint64_t(gridDim.x) * blockDim.x) {
+        if (use_lds) atomicAdd(&h[item[e]], 1u);
+        else atomicAdd(&f1[item[e]], 1u);
+    }
+    if (use_lds) {
+        __syncthreads();
+        for (uint32_t u = threadIdx.x; u < U; u += blockDim.x)
+            if (h[u]) atomicAdd(&f1[u], h[u]);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_root_count(const uint32_t* __restrict__ row_off,
@@ -94,28 +120,35 @@ __global__ __launch_bounds__(kBlock) void k_root_count(const uint32_t* __restric
     if (c > 0xFFFFu) atomicOr(flag, 1u);
 }
 
+// one wave per DB row: ballot the frequent items, write them compacted
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_root_write(const uint32_t* __restrict__ row_off,
                                                        const uint32_t* __restrict__ item,
                                                        const uint64_t* __restrict__ mask,
                                                        const uint32_t* __restrict__ rank, uint64_t r0, uint64_t r1,
                                                        const uint64_t* __restrict__ off, SlabPtrs o) {
-    const uint64_t r = r0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t r = r0 + ((uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
     if (r >= r1) return;
     const uint64_t ob = off[r - r0];
     const uint32_t len = uint32_t(off[r - r0 + 1] - ob);
+    const uint32_t e1 = row_off[r + 1];
     uint32_t k = 0;
-    for (uint32_t e = row_off[r]; e < row_off[r + 1]; ++e) {
-        const uint32_t rk = rank[item[e]];
-        if (rk == kNone) continue;
-        uint64_t m[W];
-        load_mask<W>(mask + size_t(e) * W, m);
-        const uint64_t d = ob + k;
-        o.mem[d] = rk << 1 | kSeq;
-        o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
-        o.pos[d] = (k << 16) | len;
-        store_mask<W>(o.mask + size_t(d) * W, m);
-        ++k;
+    for (uint32_t b = row_off[r]; b < e1; b += 64) {
+        const uint32_t e = b + lane_id();
+        const uint32_t rk = e < e1 ? rank[item[e]] : kNone;
+        const bool fr = rk != kNone;
+        const uint64_t bal = __ballot(fr);
+        if (fr) {
+            const uint32_t p = k + uint32_t(__popcll(bal & lanemask_lt()));
+            uint64_t m[W];
+            load_mask<W>(mask + size_t(e) * W, m);
+            const uint64_t d = ob + p;
+            o.mem[d] = rk << 1 | kSeq;
+            o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+            o.pos[d] = (p << 16) | len;
+            store_mask<W>(o.mask + size_t(d) * W, m);
+        }
+        k += uint32_t(__popcll(bal));
     }
 }
 
@@ -143,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void k_count(const DWork* __restrict__ work
         const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
         uint64_t mk[W];
         load_mask<W>(mask + size_t(e) * W, mk);
-        uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi) * c.D;
+        uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi >> c.mshift) * c.D;
         for (uint32_t q = 0; q < rl; ++q) {
             const uint32_t f = rb + q;
             const uint32_t mj = mem[f];
@@ -162,6 +195,88 @@ __global__ __launch_bounds__(kBlock) void k_count(const DWork* __restrict__ work
     }
 }
 
+// Root pair enumeration shared by the two bucket passes: calls f(key) for every
+// frequent-item pair (i, j) of the row whose join is non-empty, key = rank_i * D + slot.
+template <int W, class F>
+__device__ __forceinline__ void root_pairs(uint32_t e, const uint32_t* __restrict__ mem,
+                                           const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                           const uint64_t* __restrict__ mask, uint32_t D, F&& f) {
+    const uint32_t ri = mem[e] >> 1, p = pos[e];
+    const uint32_t lo_i = lohi[e] & 0xFFFFu;
+    const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
+    uint64_t mk[W];
+    load_mask<W>(mask + size_t(e) * W, mk);
+    const uint32_t base = ri * D;
+    for (uint32_t q = 0; q < rl; ++q) {
+        const uint32_t g = rb + q;
+        const uint32_t rj = mem[g] >> 1;
+        if ((lohi[g] >> 16) > lo_i) f(base + (rj << 1));                                   // x -> y
+        if (rj > ri && and_nonzero<W>(mk, mask + size_t(g) * W)) f(base + (rj << 1 | 1u));  // (x y)
+    }
+}
+
+// pass 1: per-block LDS histogram of bucket sizes -> blkhist[block][bucket], totals
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_rootpair_hist(uint32_t E0, const uint32_t* __restrict__ mem,
+                                                          const uint32_t* __restrict__ lohi,
+                                                          const uint32_t* __restrict__ pos,
+                                                          const uint64_t* __restrict__ mask, uint32_t D, uint32_t nb,
+                                                          uint32_t* __restrict__ blkhist,
+                                                          uint32_t* __restrict__ total) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    const uint32_t e0 = blockIdx.x * kRootChunk, e1 = min(E0, e0 + kRootChunk);
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
+        root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { atomicAdd(&h[key >> kBucketBits], 1u); });
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+        const uint32_t v = h[b];
+        blkhist[uint64_t(blockIdx.x) * nb + b] = v;
+        if (v) atomicAdd(&total[b], v);
+    }
+}
+
+// pass 2: reserve each block's share of every bucket, scatter the 15-bit keys
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_rootpair_scatter(uint32_t E0, const uint32_t* __restrict__ mem,
+                                                             const uint32_t* __restrict__ lohi,
+                                                             const uint32_t* __restrict__ pos,
+                                                             const uint64_t* __restrict__ mask, uint32_t D,
+                                                             uint32_t nb, const uint32_t* __restrict__ blkhist,
+                                                             const uint64_t* __restrict__ boff,
+                                                             uint32_t* __restrict__ gcur,
+                                                             uint16_t* __restrict__ keys) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+        const uint32_t v = blkhist[uint64_t(blockIdx.x) * nb + b];
+        cur[b] = v ? atomicAdd(&gcur[b], v) : 0u;
+    }
+    __syncthreads();
+    const uint32_t e0 = blockIdx.x * kRootChunk, e1 = min(E0, e0 + kRootChunk);
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
+        root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) {
+            const uint32_t b = key >> kBucketBits;
+            const uint32_t p = atomicAdd(&cur[b], 1u);
+            keys[boff[b] + p] = uint16_t(key & ((1u << kBucketBits) - 1u));
+        });
+}
+
+// pass 3: one block per bucket, 32768 LDS counters, dense write of the bucket's counters
+__global__ __launch_bounds__(1024) void k_bucket_count(const uint16_t* __restrict__ keys,
+                                                       const uint64_t* __restrict__ boff, uint64_t K,
+                                                       uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[1u << kBucketBits];
+    for (uint32_t t = threadIdx.x; t < (1u << kBucketBits); t += blockDim.x) h[t] = 0;
+    __syncthreads();
+    const uint64_t k0 = boff[blockIdx.x], k1 = boff[blockIdx.x + 1];
+    for (uint64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) atomicAdd(&h[keys[k]], 1u);
+    __syncthreads();
+    const uint64_t base = uint64_t(blockIdx.x) << kBucketBits;
+    for (uint32_t t = threadIdx.x; t < (1u << kBucketBits); t += blockDim.x)
+        if (base + t < K) cnt[base + t] = h[t];
+}
+
 __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ rows, uint32_t nrows,
                                                        const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
                                                        uint32_t minsup, uint32_t* __restrict__ rowcnt) {
@@ -169,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ 
     if (g >= nrows) return;
     const DRow r = rows[g];
     const DClass c = cls[r.cls];
-    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi) * c.D;
+    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
     uint32_t n = 0;
     for (uint32_t s = 0; s < c.D; s += 64) {
         const uint32_t slot = s + lane_id();
@@ -180,14 +295,14 @@ __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ 
 }
 
 __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ rows, uint32_t nrows,
-                                                       const DClass* __restrict__ cls, uint32_t* __restrict__ cnt,
+                                                       const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
                                                        uint32_t minsup, const uint64_t* __restrict__ rowoff,
                                                        FreqRec* __restrict__ out) {
     const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (g >= nrows) return;
     const DRow r = rows[g];
     const DClass c = cls[r.cls];
-    uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi) * c.D;
+    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
     uint64_t o = rowoff[g];
     uint32_t nrank = 0;
     const unsigned lane = lane_id();
@@ -199,20 +314,33 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
         const bool partner = __shfl_xor(int(fr), 1, 64) != 0;
         const uint64_t lead = __ballot((fr || partner) && !(lane & 1u));
         const uint32_t crank = nrank + uint32_t(__popcll(lead & lead_lt));
-        const uint32_t cid = fr ? (crank << 1 | (slot & 1u)) : kNone;
-        if (slot < c.D) base[slot] = cid;
         const uint64_t fb = __ballot(fr);
-        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{g, slot, v, cid};
+        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{g, slot, v, crank << 1 | (slot & 1u)};
         o += uint64_t(__popcll(fb));
         nrank += uint32_t(__popcll(lead));
     }
 }
 
+__device__ __forceinline__ uint32_t find_member(const uint32_t* __restrict__ mem, uint32_t lo, uint32_t hi,
+                                                uint32_t key) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (mem[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// Child rows: for entry i of member mi, walk mi's frequent children (kids,
+// sorted by slot = child member order) and binary-search the partner entry j
+// in the member-sorted row.  Emitted rows are again sorted by member id.
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work, const DClass* __restrict__ cls,
                                                  const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
                                                  const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
-                                                 const uint32_t* __restrict__ ids, const uint32_t* __restrict__ child_of,
+                                                 const uint32_t* __restrict__ kid_off,
+                                                 const uint32_t* __restrict__ kid_slot,
+                                                 const uint32_t* __restrict__ kid_cid,
+                                                 const uint32_t* __restrict__ child_of,
                                                  const DChild* __restrict__ ch, uint32_t* __restrict__ cursor,
                                                  SlabPtrs o) {
     const DWork w = work[blockIdx.x];
@@ -221,74 +349,73 @@ __global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work,
         const uint32_t mi = mem[e];
         const uint32_t cc = child_of[c.cbase + mi];
         if (cc == kNone) continue;
+        const uint32_t k0 = kid_off[c.cbase + mi], k1 = kid_off[c.cbase + mi + 1];
         const uint32_t p = pos[e];
         const uint32_t lo_i = lohi[e] & 0xFFFFu;
-        const uint32_t ti = mi & 1u, ri = mi >> 1;
-        const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
+        const uint32_t ti = mi & 1u;
+        const uint32_t rb = e - (p >> 16), re = rb + (p & 0xFFFFu);
         uint64_t mk[W];
         load_mask<W>(mask + size_t(e) * W, mk);
-        const uint32_t* rid = ids + c.cnt_off + uint64_t(mi) * c.D;
         uint32_t n = 0;
-        for (uint32_t q = 0; q < rl; ++q) {
-            const uint32_t f = rb + q;
-            const uint32_t mj = mem[f];
-            const uint32_t tj = mj & 1u, rj = mj >> 1;
-            if (tj == kSeq) {
-                if ((lohi[f] >> 16) > lo_i && rid[rj << 1] != kNone) ++n;
-                if (ti == kSeq && rj > ri && rid[rj << 1 | 1u] != kNone && and_nonzero<W>(mk, mask + size_t(f) * W)) ++n;
-            } else if (ti == kItm && rj > ri && rid[rj << 1 | 1u] != kNone &&
-                       and_nonzero<W>(mk, mask + size_t(f) * W)) {
-                ++n;
-            }
+        for (uint32_t q = k0; q < k1; ++q) {
+            const uint32_t slot = kid_slot[q];
+            const uint32_t ct = slot & 1u;
+            const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : ti);  // partner member id
+            const uint32_t f = find_member(mem, rb, re, target);
+            if (f >= re || mem[f] != target) continue;
+            if (ct == kSeq) n += (lohi[f] >> 16) > lo_i;
+            else n += and_nonzero<W>(mk, mask + size_t(f) * W);
         }
         if (n == 0) continue;
         const uint32_t base = ch[cc].ebegin + atomicAdd(&cursor[cc], n);
         uint32_t k = 0;
-        for (uint32_t q = 0; q < rl; ++q) {
-            const uint32_t f = rb + q;
-            const uint32_t mj = mem[f];
-            const uint32_t tj = mj & 1u, rj = mj >> 1;
-            const uint32_t hj = lohi[f] >> 16;
-            if (tj == kSeq && hj > lo_i) {
-                const uint32_t cid = rid[rj << 1];
-                if (cid != kNone) {
-                    uint64_t m[W];
-                    load_mask<W>(mask + size_t(f) * W, m);
-                    mask_clear_upto<W>(m, lo_i);
-                    const uint32_t d = base + k;
-                    o.mem[d] = cid;
-                    o.lohi[d] = mask_lo<W>(m) | (hj << 16);
-                    o.pos[d] = (k << 16) | n;
-                    store_mask<W>(o.mask + size_t(d) * W, m);
-                    ++k;
-                }
-            }
-            if (rj > ri && ti == tj) {
-                const uint32_t cid = rid[rj << 1 | 1u];
-                if (cid != kNone) {
-                    uint64_t m[W];
-                    load_mask<W>(mask + size_t(f) * W, m);
-                    uint64_t acc = 0;
+        for (uint32_t q = k0; q < k1; ++q) {
+            const uint32_t slot = kid_slot[q];
+            const uint32_t ct = slot & 1u;
+            const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : ti);
+            const uint32_t f = find_member(mem, rb, re, target);
+            if (f >= re || mem[f] != target) continue;
+            uint64_t m[W];
+            load_mask<W>(mask + size_t(f) * W, m);
+            uint32_t lo, hi;
+            if (ct == kSeq) {
+                hi = lohi[f] >> 16;
+                if (hi <= lo_i) continue;
+                mask_clear_upto<W>(m, lo_i);
+                lo = mask_lo<W>(m);
+            } else {
+                uint64_t acc = 0;
 #pragma unroll
-                    for (int x = 0; x < W; ++x) {
-                        m[x] &= mk[x];
-                        acc |= m[x];
-                    }
-                    if (acc) {
-                        const uint32_t d = base + k;
-                        o.mem[d] = cid;
-                        o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
-                        o.pos[d] = (k << 16) | n;
-                        store_mask<W>(o.mask + size_t(d) * W, m);
-                        ++k;
-                    }
+                for (int x = 0; x < W; ++x) {
+                    m[x] &= mk[x];
+                    acc |= m[x];
                 }
+                if (!acc) continue;
+                lo = mask_lo<W>(m);
+                hi = mask_hi<W>(m);
             }
+            const uint32_t d = base + k;
+            o.mem[d] = kid_cid[q];
+            o.lohi[d] = lo | (hi << 16);
+            o.pos[d] = (k << 16) | n;
+            store_mask<W>(o.mask + size_t(d) * W, m);
+            ++k;
         }
     }
 }
 
 // ------------------------------------------------------------- host side
+
+#define FSM_W_DISPATCH(W_, MACRO) \
+    switch (W_) {                 \
+        case 1: MACRO(1); break;  \
+        case 2: MACRO(2); break;  \
+        case 4: MACRO(4); break;  \
+        case 8: MACRO(8); break;  \
+        case 16: MACRO(16); break; \
+        case 32: MACRO(32); break; \
+        default: MACRO(64); break; \
+    }
 
 struct Slab {
     DevBuf mem, lohi, pos, mask;
@@ -307,6 +434,7 @@ struct ClassMeta {
     std::vector<uint32_t> rank_item;  // rank -> dense item id
     std::vector<int32_t> node_of;     // member id -> pattern node (-1: absent)
     uint32_t D = 0;
+    uint32_t mshift = 0;
     uint64_t cnt_off = 0;
     uint32_t ebegin = 0, nent = 0, cbase = 0;
 };
@@ -329,13 +457,17 @@ struct PNode {
 struct Batch {
     Slab slab;
     std::vector<ClassMeta> cls;
-    DevBuf d_cls, d_work, cnt;
+    std::vector<DClass> h_cls;
+    std::vector<DWork> h_work;
+    DevBuf d_cls, d_work;
+    DevBuf kid_off, kid_slot, kid_cid;  // frequent children of every member (CSR over cbase + mi)
     uint32_t nwork = 0;
     uint64_t n_cnt = 0, cbase_total = 0;
     std::vector<ChildInfo> children;
     std::vector<std::pair<size_t, size_t>> groups;
     size_t next_group = 0;
     int64_t depth = 1;  // items per member pattern of this batch's classes
+    bool root = false;
 };
 
 struct Miner {
@@ -350,6 +482,8 @@ struct Miner {
 
     uint64_t entry_bytes() const { return 12ull + 8ull * uint64_t(W); }
 
+    // pageable H2D copies are staged before hipMemcpyAsync returns; callers keep
+    // the host vectors alive until the next synchronization anyway.
     template <class T> void upload(DevBuf& d, const std::vector<T>& h) {
         d.alloc(h.size() * sizeof(T));
         if (!h.empty()) FSM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
@@ -364,25 +498,25 @@ struct Miner {
 
     // work items + class descriptors for a batch whose classes have ebegin/nent set
     void prepare(Batch& b) {
-        std::vector<DClass> dc(b.cls.size());
-        std::vector<DWork> wk;
+        b.h_cls.resize(b.cls.size());
+        b.h_work.clear();
         uint64_t off = 0, cb = 0;
         for (size_t c = 0; c < b.cls.size(); ++c) {
             ClassMeta& m = b.cls[c];
             m.cnt_off = off;
             m.cbase = uint32_t(cb);
-            off += uint64_t(m.D) * m.D;
+            off += uint64_t(m.D >> m.mshift) * m.D;
             cb += m.D;
-            dc[c] = DClass{m.ebegin, m.nent, m.D, m.cbase, m.cnt_off};
+            b.h_cls[c] = DClass{m.cnt_off, m.ebegin, m.nent, m.D, m.cbase, m.mshift, 0};
             for (uint32_t e = 0; e < m.nent; e += kChunk)
-                wk.push_back(DWork{uint32_t(c), m.ebegin + e, m.ebegin + std::min(m.nent, e + kChunk), 0});
+                b.h_work.push_back(DWork{uint32_t(c), m.ebegin + e, m.ebegin + std::min(m.nent, e + kChunk), 0});
         }
         if (cb >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
         b.n_cnt = off;
         b.cbase_total = cb;
-        b.nwork = uint32_t(wk.size());
-        upload(b.d_cls, dc);
-        upload(b.d_work, wk);
+        b.nwork = uint32_t(b.h_work.size());
+        upload(b.d_cls, b.h_cls);
+        upload(b.d_work, b.h_work);
     }
 
     void stats_for_class(const ClassMeta& m) {
@@ -425,7 +559,48 @@ struct Miner {
         }
     }
 
-    // count kernel + frequent-candidate extraction; fills b.children / b.groups
+    // Root counters without per-pair global atomics (3 passes, see file header).
+    // Returns false if the key space is too large for the bucket histogram.
+    bool root_bucket_count(Batch& b, uint32_t* cnt) {
+        const ClassMeta& m = b.cls[0];
+        const uint64_t K = uint64_t(m.D >> m.mshift) * m.D;
+        const uint64_t nb64 = (K + (1u << kBucketBits) - 1) >> kBucketBits;
+        if (nb64 > kMaxBuckets || K >= (uint64_t(1) << 32) || m.nent == 0) return false;
+        const uint32_t nb = uint32_t(nb64);
+        const uint32_t E0 = m.nent;
+        const uint32_t nblk = (E0 + kRootChunk - 1) / kRootChunk;
+        DevBuf blkhist(uint64_t(nblk) * nb * 4), total(uint64_t(nb) * 4 + 4), boff((uint64_t(nb) + 1) * 8),
+            gcur(uint64_t(nb) * 4 + 4);
+        FSM_HIP(hipMemsetAsync(total.p, 0, uint64_t(nb) * 4, s));
+        FSM_HIP(hipMemsetAsync(gcur.p, 0, uint64_t(nb) * 4, s));
+        const SlabPtrs sp = b.slab.ptrs();
+        const size_t lds = size_t(nb) * 4;
+#define FSM_RP_HIST(WW)                                                                                    \
+    hipLaunchKernelGGL(k_rootpair_hist<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
+                       sp.mask, m.D, nb, blkhist.as<uint32_t>(), total.as<uint32_t>())
+        FSM_W_DISPATCH(W, FSM_RP_HIST)
+#undef FSM_RP_HIST
+        FSM_LAUNCHED("k_rootpair_hist", s);
+        scan_exclusive(total.as<uint32_t>(), boff.as<uint64_t>(), nb, s);
+        uint64_t npairs = 0;
+        FSM_HIP(hipMemcpyAsync(&npairs, boff.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        DevBuf keys(std::max<uint64_t>(npairs, 1) * 2);
+#define FSM_RP_SCAT(WW)                                                                                        \
+    hipLaunchKernelGGL(k_rootpair_scatter<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
+                       sp.mask, m.D, nb, blkhist.as<uint32_t>(), boff.as<uint64_t>(), gcur.as<uint32_t>(),    \
+                       keys.as<uint16_t>())
+        FSM_W_DISPATCH(W, FSM_RP_SCAT)
+#undef FSM_RP_SCAT
+        FSM_LAUNCHED("k_rootpair_scatter", s);
+        hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(1024), 0, s, keys.as<uint16_t>(), boff.as<uint64_t>(), K,
+                           cnt);
+        FSM_LAUNCHED("k_bucket_count", s);
+        FSM_HIP(hipStreamSynchronize(s));  // keys / blkhist released on return
+        return true;
+    }
+
+    // count kernel + frequent-candidate extraction; fills b.children / b.groups / kids
     void count_and_freq(Batch& b) {
         dump(b);
         prepare(b);
@@ -437,26 +612,20 @@ struct Miner {
         st.entries += int64_t(tot_ent);
         st.bytes_streamed += int64_t(tot_ent * entry_bytes());
         st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
-        b.cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
-        FSM_HIP(hipMemsetAsync(b.cnt.p, 0, b.n_cnt * 4, s));
+        DevBuf cnt(std::max<uint64_t>(b.n_cnt, 1) * 4);
         if (b.nwork) {
             auto ev = ev_pair();
             FSM_HIP(hipEventRecord(ev.first, s));
-            const SlabPtrs sp = b.slab.ptrs();
+            if (!(b.root && root_bucket_count(b, cnt.as<uint32_t>()))) {
+                FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
+                const SlabPtrs sp = b.slab.ptrs();
 #define FSM_COUNT(WW)                                                                                   \
     hipLaunchKernelGGL(k_count<WW>, dim3(b.nwork), dim3(kBlock), 0, s, b.d_work.as<DWork>(),           \
-                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.cnt.as<uint32_t>())
-            switch (W) {
-                case 1: FSM_COUNT(1); break;
-                case 2: FSM_COUNT(2); break;
-                case 4: FSM_COUNT(4); break;
-                case 8: FSM_COUNT(8); break;
-                case 16: FSM_COUNT(16); break;
-                case 32: FSM_COUNT(32); break;
-                default: FSM_COUNT(64); break;
-            }
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, cnt.as<uint32_t>())
+                FSM_W_DISPATCH(W, FSM_COUNT)
 #undef FSM_COUNT
-            FSM_LAUNCHED("k_count", s);
+                FSM_LAUNCHED("k_count", s);
+            }
             FSM_HIP(hipEventRecord(ev.second, s));
             ev_count.push_back(ev);
             st.count_launches += 1;
@@ -472,7 +641,7 @@ struct Miner {
         const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
         if (nrows) {
             hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
-                               b.d_cls.as<DClass>(), b.cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
+                               b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
             FSM_LAUNCHED("k_freq_count", s);
         }
         scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
@@ -483,12 +652,24 @@ struct Miner {
         if (nfreq) {
             DevBuf d_recs(nfreq * sizeof(FreqRec));
             hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
-                               b.d_cls.as<DClass>(), b.cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(),
+                               b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(),
                                d_recs.as<FreqRec>());
             FSM_LAUNCHED("k_freq_write", s);
             FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nfreq * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
             FSM_HIP(hipStreamSynchronize(s));
         }
+        cnt.release();
+        // kids CSR over (cbase + mi): the frequent children of every member, by slot
+        std::vector<uint32_t> koff(b.cbase_total + 1, 0), kslot(nfreq), kcid(nfreq);
+        for (const FreqRec& fr : recs) koff[b.cls[rows[fr.row].cls].cbase + rows[fr.row].mi + 1] += 1;
+        for (uint64_t x = 0; x < b.cbase_total; ++x) koff[x + 1] += koff[x];
+        for (uint64_t q = 0; q < nfreq; ++q) {  // recs are ordered by (row, slot) = CSR order
+            kslot[q] = recs[q].slot;
+            kcid[q] = recs[q].cid;
+        }
+        upload(b.kid_off, koff);
+        upload(b.kid_slot, kslot);
+        upload(b.kid_cid, kcid);
         // children (new pattern nodes) in deterministic (row, slot) order
         b.children.clear();
         for (size_t q = 0; q < recs.size();) {
@@ -584,17 +765,10 @@ struct Miner {
             const SlabPtrs op = nb.slab.ptrs();
 #define FSM_EMIT(WW)                                                                                           \
     hipLaunchKernelGGL(k_emit<WW>, dim3(b.nwork), dim3(kBlock), 0, s, b.d_work.as<DWork>(), b.d_cls.as<DClass>(), \
-                       sp.mem, sp.lohi, sp.pos, sp.mask, b.cnt.as<uint32_t>(), d_child_of.as<uint32_t>(),       \
-                       d_ch.as<DChild>(), cursor.as<uint32_t>(), op)
-            switch (W) {
-                case 1: FSM_EMIT(1); break;
-                case 2: FSM_EMIT(2); break;
-                case 4: FSM_EMIT(4); break;
-                case 8: FSM_EMIT(8); break;
-                case 16: FSM_EMIT(16); break;
-                case 32: FSM_EMIT(32); break;
-                default: FSM_EMIT(64); break;
-            }
+                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),   \
+                       b.kid_cid.as<uint32_t>(), d_child_of.as<uint32_t>(), d_ch.as<DChild>(),                \
+                       cursor.as<uint32_t>(), op)
+            FSM_W_DISPATCH(W, FSM_EMIT)
 #undef FSM_EMIT
             FSM_LAUNCHED("k_emit", s);
             FSM_HIP(hipEventRecord(ev.second, s));
@@ -619,11 +793,10 @@ struct Miner {
         DevBuf d_rank, rcnt((r1 - r0 + 1) * 4), roff((r1 - r0 + 1) * 8), flag(4);
         upload(d_rank, rank);
         FSM_HIP(hipMemsetAsync(flag.p, 0, 4, s));
-        const unsigned grid = unsigned((r1 - r0 + kBlock - 1) / kBlock);
         if (r1 > r0) {
-            hipLaunchKernelGGL(k_root_count, dim3(grid), dim3(kBlock), 0, s, db->row_off.as<uint32_t>(),
-                               db->item.as<uint32_t>(), d_rank.as<uint32_t>(), r0, r1, rcnt.as<uint32_t>(),
-                               flag.as<uint32_t>());
+            hipLaunchKernelGGL(k_root_count, dim3(unsigned((r1 - r0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                               db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), d_rank.as<uint32_t>(), r0, r1,
+                               rcnt.as<uint32_t>(), flag.as<uint32_t>());
             FSM_LAUNCHED("k_root_count", s);
         }
         scan_exclusive(rcnt.as<uint32_t>(), roff.as<uint64_t>(), r1 - r0, s);
@@ -637,25 +810,19 @@ struct Miner {
         root.slab.alloc(E0, W);
         if (r1 > r0) {
             const SlabPtrs op = root.slab.ptrs();
+            const unsigned grid = unsigned(((r1 - r0) * 64 + kBlock - 1) / kBlock);
 #define FSM_ROOTW(WW)                                                                                         \
     hipLaunchKernelGGL(k_root_write<WW>, dim3(grid), dim3(kBlock), 0, s, db->row_off.as<uint32_t>(),           \
                        db->item.as<uint32_t>(), db->mask.as<uint64_t>(), d_rank.as<uint32_t>(), r0, r1,       \
                        roff.as<uint64_t>(), op)
-            switch (W) {
-                case 1: FSM_ROOTW(1); break;
-                case 2: FSM_ROOTW(2); break;
-                case 4: FSM_ROOTW(4); break;
-                case 8: FSM_ROOTW(8); break;
-                case 16: FSM_ROOTW(16); break;
-                case 32: FSM_ROOTW(32); break;
-                default: FSM_ROOTW(64); break;
-            }
+            FSM_W_DISPATCH(W, FSM_ROOTW)
 #undef FSM_ROOTW
             FSM_LAUNCHED("k_root_write", s);
         }
         ClassMeta m;
         const uint32_t F = uint32_t(freq_items.size());
         m.D = 2 * F;
+        m.mshift = 1;  // root members are all sequence-extensions: counter rows by rank
         m.rank_item = freq_items;
         m.node_of.assign(m.D, -1);
         for (uint32_t r = 0; r < F; ++r) {
@@ -665,6 +832,7 @@ struct Miner {
         m.ebegin = 0;
         m.nent = uint32_t(E0);
         root.cls.push_back(std::move(m));
+        root.root = true;
         FSM_HIP(hipStreamSynchronize(s));
     }
 
@@ -738,9 +906,11 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         DevBuf d_f1(std::max<int64_t>(d->U, 1) * 4);
         FSM_HIP(hipMemsetAsync(d_f1.p, 0, size_t(d->U) * 4, ctx->stream));
         if (d->E) {
-            const unsigned grid = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, 8192));
-            hipLaunchKernelGGL(k_f1, dim3(grid), dim3(kBlock), 0, ctx->stream, d->item.as<uint32_t>(), uint64_t(0),
-                               uint64_t(d->E), d_f1.as<uint32_t>());
+            const int use_lds = d->U <= 16384;
+            const unsigned grid = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, use_lds ? 1024 : 8192));
+            hipLaunchKernelGGL(k_f1, dim3(grid), dim3(kBlock), use_lds ? size_t(d->U) * 4 : 0, ctx->stream,
+                               d->item.as<uint32_t>(), uint64_t(0), uint64_t(d->E), d_f1.as<uint32_t>(),
+                               uint32_t(d->U), use_lds);
             FSM_LAUNCHED("k_f1", ctx->stream);
         }
         if (d->U) FSM_HIP(hipMemcpyAsync(f1.data(), d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));

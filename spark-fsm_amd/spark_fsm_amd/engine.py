@@ -64,8 +64,8 @@ class Engine:
         return DB(self, db, mode)
 
     # ------------------------------------------------------------ mining
-    def spade(self, db, support, dfs=True):
-        """-> (patterns: list[(itemsets tuple-of-tuples, support)], meta dict)."""
+    def spade_csr(self, db, support, dfs=True):
+        """fsm_spade_mine -> CSR numpy arrays (support, pat_off, set_off, items), meta."""
         out = ctypes.POINTER(_lib.Patterns)()
         check(self._L.fsm_spade_mine(self._ctx, db.handle, float(support), 1 if dfs else 0,
                                      ctypes.byref(out)), self._ctx)
@@ -76,9 +76,15 @@ class Engine:
             po = np.ctypeslib.as_array(p.pat_off, shape=(n + 1,)).copy()
             so = np.ctypeslib.as_array(p.set_off, shape=(p.n_sets + 1,)).copy()
             it = np.ctypeslib.as_array(p.items, shape=(max(p.n_items, 1),))[:p.n_items].copy()
-            meta = {"total": p.total, "minsup": p.minsup}
+            meta = {"total": p.total, "minsup": p.minsup, "n": n}
         finally:
             self._L.fsm_patterns_free(out)
+        return (sup, po, so, it), meta
+
+    def spade(self, db, support, dfs=True):
+        """-> (patterns: list[(itemsets tuple-of-tuples, support)], meta dict)."""
+        (sup, po, so, it), meta = self.spade_csr(db, support, dfs)
+        n = meta["n"]
         itl = it.tolist()
         sol = so.tolist()
         pats = []
