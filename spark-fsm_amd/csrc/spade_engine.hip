@@ -56,28 +56,23 @@ constexpr int kBucketBits = 15;          // 32768 counters (128 KiB LDS) per buc
 constexpr uint32_t kMaxBuckets = 16384;  // LDS bucket histogram of the scatter pass (64 KiB)
 constexpr int kBlock = 256;
 
+
 struct DClass {
     uint64_t cnt_off;     // counter matrix of the class
-    uint32_t ebegin, nent;
     uint32_t D;           // member id space (2 * ranks)
     uint32_t cbase;       // offset of the class's members in per-member arrays
     uint32_t mshift;      // counter row of member mi = mi >> mshift (root: 1, only SEQ members)
-    uint32_t pad;
-};
-struct DWork {
-    uint32_t cls, e0, e1, pad;
+    uint32_t pad[3];
 };
 struct DRow {
     uint32_t cls, mi;
-};
-struct DChild {
-    uint32_t ebegin, cap;
 };
 struct FreqRec {
     uint32_t row, slot, sup, cid;
 };
 
 struct SlabPtrs {
+    uint32_t* cid;  // class of the entry (index into the batch's class table)
     uint32_t* mem;
     uint32_t* lohi;
     uint32_t* pos;
@@ -163,13 +158,14 @@ template <int W> __device__ __forceinline__ bool and_nonzero(const uint64_t (&a)
 
 // K2/K3/K4: all candidate joins of every class of the batch, one pass.
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_count(const DWork* __restrict__ work, const DClass* __restrict__ cls,
+__global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __restrict__ cid,
+                                                  const DClass* __restrict__ cls,
                                                   const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
                                                   const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
                                                   uint32_t* __restrict__ cnt) {
-    const DWork w = work[blockIdx.x];
-    const DClass c = cls[w.cls];
-    for (uint32_t e = w.e0 + threadIdx.x; e < w.e1; e += blockDim.x) {
+    const uint32_t e1 = min(E, (blockIdx.x + 1) * kChunk);
+    for (uint32_t e = blockIdx.x * kChunk + threadIdx.x; e < e1; e += blockDim.x) {
+        const DClass c = cls[cid[e]];
         const uint32_t mi = mem[e], p = pos[e];
         const uint32_t lo_i = lohi[e] & 0xFFFFu;
         const uint32_t ti = mi & 1u, ri = mi >> 1;
@@ -221,12 +217,12 @@ __global__ __launch_bounds__(kBlock) void k_rootpair_hist(uint32_t E0, const uin
                                                           const uint32_t* __restrict__ lohi,
                                                           const uint32_t* __restrict__ pos,
                                                           const uint64_t* __restrict__ mask, uint32_t D, uint32_t nb,
-                                                          uint32_t* __restrict__ blkhist,
+                                                          uint32_t chunk, uint32_t* __restrict__ blkhist,
                                                           uint32_t* __restrict__ total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
     __syncthreads();
-    const uint32_t e0 = blockIdx.x * kRootChunk, e1 = min(E0, e0 + kRootChunk);
+    const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
         root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { atomicAdd(&h[key >> kBucketBits], 1u); });
     __syncthreads();
@@ -243,22 +239,22 @@ __global__ __launch_bounds__(kBlock) void k_rootpair_scatter(uint32_t E0, const 
                                                              const uint32_t* __restrict__ lohi,
                                                              const uint32_t* __restrict__ pos,
                                                              const uint64_t* __restrict__ mask, uint32_t D,
-                                                             uint32_t nb, const uint32_t* __restrict__ blkhist,
+                                                             uint32_t nb, uint32_t chunk,
+                                                             const uint32_t* __restrict__ blkhist,
                                                              const uint64_t* __restrict__ boff,
                                                              uint32_t* __restrict__ gcur,
                                                              uint16_t* __restrict__ keys) {
+    // cur[b] = absolute key index of this block's next slot in bucket b (< 2^32, host-checked)
     extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
         const uint32_t v = blkhist[uint64_t(blockIdx.x) * nb + b];
-        cur[b] = v ? atomicAdd(&gcur[b], v) : 0u;
+        cur[b] = v ? uint32_t(boff[b]) + atomicAdd(&gcur[b], v) : 0u;
     }
     __syncthreads();
-    const uint32_t e0 = blockIdx.x * kRootChunk, e1 = min(E0, e0 + kRootChunk);
+    const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
         root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) {
-            const uint32_t b = key >> kBucketBits;
-            const uint32_t p = atomicAdd(&cur[b], 1u);
-            keys[boff[b] + p] = uint16_t(key & ((1u << kBucketBits) - 1u));
+            keys[atomicAdd(&cur[key >> kBucketBits], 1u)] = uint16_t(key & ((1u << kBucketBits) - 1u));
         });
 }
 
@@ -330,25 +326,37 @@ __device__ __forceinline__ uint32_t find_member(const uint32_t* __restrict__ mem
     return lo;
 }
 
-// Child rows: for entry i of member mi, walk mi's frequent children (kids,
-// sorted by slot = child member order) and binary-search the partner entry j
-// in the member-sorted row.  Emitted rows are again sorted by member id.
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work, const DClass* __restrict__ cls,
-                                                 const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
-                                                 const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
+// Child rows.  Entry i (member mi, class c, sequence s) produces the whole
+// run of sequence s in the child class [c, mi]: one entry per frequent child of
+// mi whose join with i is non-empty (partner j found by binary search in the
+// member-sorted run), in child member order.  Runs are written in parent entry
+// order at exclusive-scan offsets, so every block writes one contiguous,
+// coalesced stretch (no per-class cursors, no partial-line scatter).
+template <int W, bool kWrite>
+__global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __restrict__ cid,
+                                                 const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                 const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                                 const uint64_t* __restrict__ mask,
                                                  const uint32_t* __restrict__ kid_off,
                                                  const uint32_t* __restrict__ kid_slot,
                                                  const uint32_t* __restrict__ kid_cid,
-                                                 const uint32_t* __restrict__ child_of,
-                                                 const DChild* __restrict__ ch, uint32_t* __restrict__ cursor,
-                                                 SlabPtrs o) {
-    const DWork w = work[blockIdx.x];
-    const DClass c = cls[w.cls];
-    for (uint32_t e = w.e0 + threadIdx.x; e < w.e1; e += blockDim.x) {
+                                                 const uint32_t* __restrict__ child_of, uint32_t* __restrict__ ncnt,
+                                                 const uint64_t* __restrict__ off, SlabPtrs o) {
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+        uint32_t n = 0;
+        uint64_t base = 0;
+        if constexpr (kWrite) {
+            base = off[e];
+            n = uint32_t(off[e + 1] - base);
+            if (n == 0) continue;
+        }
+        const DClass c = cls[cid[e]];
         const uint32_t mi = mem[e];
         const uint32_t cc = child_of[c.cbase + mi];
-        if (cc == kNone) continue;
+        if (cc == kNone) {
+            if constexpr (!kWrite) ncnt[e] = 0;
+            continue;
+        }
         const uint32_t k0 = kid_off[c.cbase + mi], k1 = kid_off[c.cbase + mi + 1];
         const uint32_t p = pos[e];
         const uint32_t lo_i = lohi[e] & 0xFFFFu;
@@ -356,51 +364,46 @@ __global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work,
         const uint32_t rb = e - (p >> 16), re = rb + (p & 0xFFFFu);
         uint64_t mk[W];
         load_mask<W>(mask + size_t(e) * W, mk);
-        uint32_t n = 0;
+        uint32_t k = 0;
         for (uint32_t q = k0; q < k1; ++q) {
             const uint32_t slot = kid_slot[q];
             const uint32_t ct = slot & 1u;
             const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : ti);  // partner member id
             const uint32_t f = find_member(mem, rb, re, target);
             if (f >= re || mem[f] != target) continue;
-            if (ct == kSeq) n += (lohi[f] >> 16) > lo_i;
-            else n += and_nonzero<W>(mk, mask + size_t(f) * W);
-        }
-        if (n == 0) continue;
-        const uint32_t base = ch[cc].ebegin + atomicAdd(&cursor[cc], n);
-        uint32_t k = 0;
-        for (uint32_t q = k0; q < k1; ++q) {
-            const uint32_t slot = kid_slot[q];
-            const uint32_t ct = slot & 1u;
-            const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : ti);
-            const uint32_t f = find_member(mem, rb, re, target);
-            if (f >= re || mem[f] != target) continue;
-            uint64_t m[W];
-            load_mask<W>(mask + size_t(f) * W, m);
-            uint32_t lo, hi;
-            if (ct == kSeq) {
-                hi = lohi[f] >> 16;
-                if (hi <= lo_i) continue;
-                mask_clear_upto<W>(m, lo_i);
-                lo = mask_lo<W>(m);
+            if constexpr (!kWrite) {
+                if (ct == kSeq) k += (lohi[f] >> 16) > lo_i;
+                else k += and_nonzero<W>(mk, mask + size_t(f) * W);
             } else {
-                uint64_t acc = 0;
+                uint64_t m[W];
+                load_mask<W>(mask + size_t(f) * W, m);
+                uint32_t lo, hi;
+                if (ct == kSeq) {
+                    hi = lohi[f] >> 16;
+                    if (hi <= lo_i) continue;
+                    mask_clear_upto<W>(m, lo_i);
+                    lo = mask_lo<W>(m);
+                } else {
+                    uint64_t acc = 0;
 #pragma unroll
-                for (int x = 0; x < W; ++x) {
-                    m[x] &= mk[x];
-                    acc |= m[x];
+                    for (int x = 0; x < W; ++x) {
+                        m[x] &= mk[x];
+                        acc |= m[x];
+                    }
+                    if (!acc) continue;
+                    lo = mask_lo<W>(m);
+                    hi = mask_hi<W>(m);
                 }
-                if (!acc) continue;
-                lo = mask_lo<W>(m);
-                hi = mask_hi<W>(m);
+                const uint64_t d = base + k;
+                o.cid[d] = cc;
+                o.mem[d] = kid_cid[q];
+                o.lohi[d] = lo | (hi << 16);
+                o.pos[d] = (k << 16) | n;
+                store_mask<W>(o.mask + d * W, m);
+                ++k;
             }
-            const uint32_t d = base + k;
-            o.mem[d] = kid_cid[q];
-            o.lohi[d] = lo | (hi << 16);
-            o.pos[d] = (k << 16) | n;
-            store_mask<W>(o.mask + size_t(d) * W, m);
-            ++k;
         }
+        if constexpr (!kWrite) ncnt[e] = k;
     }
 }
 
@@ -418,16 +421,20 @@ __global__ __launch_bounds__(kBlock) void k_emit(const DWork* __restrict__ work,
     }
 
 struct Slab {
-    DevBuf mem, lohi, pos, mask;
+    DevBuf cid, mem, lohi, pos, mask;
     uint64_t cap = 0;
     void alloc(uint64_t n, int W) {
+        cid.alloc(n * 4);
         mem.alloc(n * 4);
         lohi.alloc(n * 4);
         pos.alloc(n * 4);
         mask.alloc(n * 8 * uint64_t(W));
         cap = n;
     }
-    SlabPtrs ptrs() const { return SlabPtrs{mem.as<uint32_t>(), lohi.as<uint32_t>(), pos.as<uint32_t>(), mask.as<uint64_t>()}; }
+    SlabPtrs ptrs() const {
+        return SlabPtrs{cid.as<uint32_t>(), mem.as<uint32_t>(), lohi.as<uint32_t>(), pos.as<uint32_t>(),
+                        mask.as<uint64_t>()};
+    }
 };
 
 struct ClassMeta {
@@ -436,7 +443,7 @@ struct ClassMeta {
     uint32_t D = 0;
     uint32_t mshift = 0;
     uint64_t cnt_off = 0;
-    uint32_t ebegin = 0, nent = 0, cbase = 0;
+    uint32_t nent = 0, cbase = 0;  // entries of the class in the batch slab (= sum of member supports)
 };
 
 struct ChildInfo {
@@ -458,10 +465,9 @@ struct Batch {
     Slab slab;
     std::vector<ClassMeta> cls;
     std::vector<DClass> h_cls;
-    std::vector<DWork> h_work;
-    DevBuf d_cls, d_work;
+    DevBuf d_cls;
     DevBuf kid_off, kid_slot, kid_cid;  // frequent children of every member (CSR over cbase + mi)
-    uint32_t nwork = 0;
+    uint64_t E = 0;                     // entries in the slab (runs of all classes, any order)
     uint64_t n_cnt = 0, cbase_total = 0;
     std::vector<ChildInfo> children;
     std::vector<std::pair<size_t, size_t>> groups;
@@ -496,10 +502,9 @@ struct Miner {
         return {a, b};
     }
 
-    // work items + class descriptors for a batch whose classes have ebegin/nent set
+    // class descriptors (counter matrix offsets, member bases) of a batch
     void prepare(Batch& b) {
         b.h_cls.resize(b.cls.size());
-        b.h_work.clear();
         uint64_t off = 0, cb = 0;
         for (size_t c = 0; c < b.cls.size(); ++c) {
             ClassMeta& m = b.cls[c];
@@ -507,16 +512,12 @@ struct Miner {
             m.cbase = uint32_t(cb);
             off += uint64_t(m.D >> m.mshift) * m.D;
             cb += m.D;
-            b.h_cls[c] = DClass{m.cnt_off, m.ebegin, m.nent, m.D, m.cbase, m.mshift, 0};
-            for (uint32_t e = 0; e < m.nent; e += kChunk)
-                b.h_work.push_back(DWork{uint32_t(c), m.ebegin + e, m.ebegin + std::min(m.nent, e + kChunk), 0});
+            b.h_cls[c] = DClass{m.cnt_off, m.D, m.cbase, m.mshift, {0, 0, 0}};
         }
         if (cb >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
         b.n_cnt = off;
         b.cbase_total = cb;
-        b.nwork = uint32_t(b.h_work.size());
         upload(b.d_cls, b.h_cls);
-        upload(b.d_work, b.h_work);
     }
 
     void stats_for_class(const ClassMeta& m) {
@@ -537,26 +538,34 @@ struct Miner {
     // FSM_DEBUG_DUMP=1: print every class row entry of small batches (debugging aid)
     void dump(Batch& b) {
         static const bool on = [] { const char* v = std::getenv("FSM_DEBUG_DUMP"); return v && v[0] == '1'; }();
-        uint64_t n = 0;
-        for (auto& m : b.cls) n += m.nent;
+        const uint64_t n = b.E;
         if (!on || n > 4096) return;
-        std::vector<uint32_t> mem(n), lohi(n), pos(n);
+        std::vector<uint32_t> cid(n), mem(n), lohi(n), pos(n);
         std::vector<uint64_t> mk(n * uint64_t(W));
+        FSM_HIP(hipMemcpyAsync(cid.data(), b.slab.cid.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(mem.data(), b.slab.mem.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(lohi.data(), b.slab.lohi.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(pos.data(), b.slab.pos.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(mk.data(), b.slab.mask.p, n * 8 * W, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipStreamSynchronize(s));
         std::fprintf(stderr, "[dump] depth=%lld classes=%zu\n", (long long)b.depth, b.cls.size());
-        for (size_t c = 0; c < b.cls.size(); ++c) {
-            std::fprintf(stderr, "  class %zu D=%u nent=%u\n", c, b.cls[c].D, b.cls[c].nent);
-            for (uint32_t e = b.cls[c].ebegin; e < b.cls[c].ebegin + b.cls[c].nent; ++e) {
-                std::fprintf(stderr, "    e=%u mem=%u lo=%u hi=%u off=%u len=%u mask=", e, mem[e], lohi[e] & 0xFFFF,
-                             lohi[e] >> 16, pos[e] >> 16, pos[e] & 0xFFFF);
-                for (int w = 0; w < W; ++w) std::fprintf(stderr, "%016llx ", (unsigned long long)mk[e * W + w]);
-                std::fprintf(stderr, "\n");
-            }
+        for (uint64_t e = 0; e < n; ++e) {
+            std::fprintf(stderr, "    e=%llu cls=%u mem=%u lo=%u hi=%u off=%u len=%u mask=", (unsigned long long)e,
+                         cid[e], mem[e], lohi[e] & 0xFFFF, lohi[e] >> 16, pos[e] >> 16, pos[e] & 0xFFFF);
+            for (int w = 0; w < W; ++w) std::fprintf(stderr, "%016llx ", (unsigned long long)mk[e * W + w]);
+            std::fprintf(stderr, "\n");
         }
+    }
+
+    // FSM_ROOT_PATH=atomic forces the global-atomic root F2 path (tests, profiling).
+    static bool root_atomic() {
+        const char* v = std::getenv("FSM_ROOT_PATH");
+        return v && !std::strcmp(v, "atomic");
+    }
+    // root entries per block of the bucketed passes (FSM_ROOT_CHUNK overrides, for tuning)
+    static uint32_t root_chunk() {
+        const char* v = std::getenv("FSM_ROOT_CHUNK");
+        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kRootChunk;
     }
 
     // Root counters without per-pair global atomics (3 passes, see file header).
@@ -568,7 +577,8 @@ struct Miner {
         if (nb64 > kMaxBuckets || K >= (uint64_t(1) << 32) || m.nent == 0) return false;
         const uint32_t nb = uint32_t(nb64);
         const uint32_t E0 = m.nent;
-        const uint32_t nblk = (E0 + kRootChunk - 1) / kRootChunk;
+        const uint32_t chunk = root_chunk();
+        const uint32_t nblk = (E0 + chunk - 1) / chunk;
         DevBuf blkhist(uint64_t(nblk) * nb * 4), total(uint64_t(nb) * 4 + 4), boff((uint64_t(nb) + 1) * 8),
             gcur(uint64_t(nb) * 4 + 4);
         FSM_HIP(hipMemsetAsync(total.p, 0, uint64_t(nb) * 4, s));
@@ -577,7 +587,7 @@ struct Miner {
         const size_t lds = size_t(nb) * 4;
 #define FSM_RP_HIST(WW)                                                                                    \
     hipLaunchKernelGGL(k_rootpair_hist<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
-                       sp.mask, m.D, nb, blkhist.as<uint32_t>(), total.as<uint32_t>())
+                       sp.mask, m.D, nb, chunk, blkhist.as<uint32_t>(), total.as<uint32_t>())
         FSM_W_DISPATCH(W, FSM_RP_HIST)
 #undef FSM_RP_HIST
         FSM_LAUNCHED("k_rootpair_hist", s);
@@ -585,10 +595,11 @@ struct Miner {
         uint64_t npairs = 0;
         FSM_HIP(hipMemcpyAsync(&npairs, boff.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipStreamSynchronize(s));
+        if (npairs >= (uint64_t(1) << 32)) return false;  // scatter keeps absolute key indices in u32
         DevBuf keys(std::max<uint64_t>(npairs, 1) * 2);
 #define FSM_RP_SCAT(WW)                                                                                        \
     hipLaunchKernelGGL(k_rootpair_scatter<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
-                       sp.mask, m.D, nb, blkhist.as<uint32_t>(), boff.as<uint64_t>(), gcur.as<uint32_t>(),    \
+                       sp.mask, m.D, nb, chunk, blkhist.as<uint32_t>(), boff.as<uint64_t>(), gcur.as<uint32_t>(), \
                        keys.as<uint16_t>())
         FSM_W_DISPATCH(W, FSM_RP_SCAT)
 #undef FSM_RP_SCAT
@@ -607,21 +618,22 @@ struct Miner {
         for (auto& m : b.cls) stats_for_class(m);
         fsm_stats& st = ctx->stats;
         st.batches += 1;
-        uint64_t tot_ent = 0;
-        for (auto& m : b.cls) tot_ent += m.nent;
+        const uint64_t tot_ent = b.E;
         st.entries += int64_t(tot_ent);
         st.bytes_streamed += int64_t(tot_ent * entry_bytes());
         st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
         DevBuf cnt(std::max<uint64_t>(b.n_cnt, 1) * 4);
-        if (b.nwork) {
+        if (b.E) {
             auto ev = ev_pair();
             FSM_HIP(hipEventRecord(ev.first, s));
-            if (!(b.root && root_bucket_count(b, cnt.as<uint32_t>()))) {
+            const bool done = b.root && !root_atomic() && root_bucket_count(b, cnt.as<uint32_t>());
+            if (!done) {
                 FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
                 const SlabPtrs sp = b.slab.ptrs();
 #define FSM_COUNT(WW)                                                                                   \
-    hipLaunchKernelGGL(k_count<WW>, dim3(b.nwork), dim3(kBlock), 0, s, b.d_work.as<DWork>(),           \
-                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, cnt.as<uint32_t>())
+    hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + kChunk - 1) / kChunk)), dim3(kBlock), 0, s,   \
+                       uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
+                       cnt.as<uint32_t>())
                 FSM_W_DISPATCH(W, FSM_COUNT)
 #undef FSM_COUNT
                 FSM_LAUNCHED("k_count", s);
@@ -730,12 +742,12 @@ struct Miner {
                          b.children.size(), b.groups.size());
     }
 
-    // emit child rows of group g of batch b into a new batch
+    // emit child rows of group g of batch b into a new batch: count pass,
+    // exclusive scan of the per-entry run lengths, write pass
     void emit(Batch& b, size_t g, Batch& nb) {
         const auto [ga, gb] = b.groups[g];
         nb.cls.resize(gb - ga);
         std::vector<uint32_t> child_of(b.cbase_total, kNone);
-        std::vector<DChild> dch(gb - ga);
         uint64_t total = 0;
         for (size_t k = ga; k < gb; ++k) {
             ChildInfo& ch = b.children[k];
@@ -743,45 +755,47 @@ struct Miner {
             m.rank_item = std::move(ch.rank_item);
             m.node_of = std::move(ch.node_of);
             m.D = ch.D;
-            m.ebegin = uint32_t(total);
             m.nent = uint32_t(ch.cap);
-            dch[k - ga] = DChild{uint32_t(total), uint32_t(ch.cap)};
             child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
             total += ch.cap;
         }
+        if (total >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch exceeds 2^32 entries");
         nb.slab.alloc(total, W);
-        DevBuf d_child_of, d_ch, cursor((gb - ga) * 4 + 4);
+        nb.E = total;
+        DevBuf d_child_of, ncnt(std::max<uint64_t>(b.E, 1) * 4), off((b.E + 1) * 8);
         upload(d_child_of, child_of);
-        upload(d_ch, dch);
-        FSM_HIP(hipMemsetAsync(cursor.p, 0, (gb - ga) * 4, s));
-        ctx->stats.bytes_streamed += int64_t(total * entry_bytes());
-        uint64_t tot_ent = 0;
-        for (auto& m : b.cls) tot_ent += m.nent;
-        ctx->stats.bytes_streamed += int64_t(tot_ent * entry_bytes());
-        if (b.nwork) {
+        ctx->stats.bytes_streamed += int64_t((total + 2 * b.E) * entry_bytes());
+        uint64_t written = 0;
+        if (b.E) {
             auto ev = ev_pair();
             FSM_HIP(hipEventRecord(ev.first, s));
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
-#define FSM_EMIT(WW)                                                                                           \
-    hipLaunchKernelGGL(k_emit<WW>, dim3(b.nwork), dim3(kBlock), 0, s, b.d_work.as<DWork>(), b.d_cls.as<DClass>(), \
-                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),   \
-                       b.kid_cid.as<uint32_t>(), d_child_of.as<uint32_t>(), d_ch.as<DChild>(),                \
-                       cursor.as<uint32_t>(), op)
-            FSM_W_DISPATCH(W, FSM_EMIT)
+            const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 1u << 20));
+#define FSM_EMIT(WW, WR)                                                                                            \
+    hipLaunchKernelGGL((k_emit<WW, WR>), dim3(grid), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
+                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),        \
+                       b.kid_cid.as<uint32_t>(), d_child_of.as<uint32_t>(), ncnt.as<uint32_t>(),                   \
+                       off.as<uint64_t>(), op)
+#define FSM_EMIT_COUNT(WW) FSM_EMIT(WW, false)
+#define FSM_EMIT_WRITE(WW) FSM_EMIT(WW, true)
+            FSM_W_DISPATCH(W, FSM_EMIT_COUNT)
+            FSM_LAUNCHED("k_emit<count>", s);
+            scan_exclusive(ncnt.as<uint32_t>(), off.as<uint64_t>(), b.E, s);
+            FSM_W_DISPATCH(W, FSM_EMIT_WRITE)
+            FSM_LAUNCHED("k_emit<write>", s);
+#undef FSM_EMIT_WRITE
+#undef FSM_EMIT_COUNT
 #undef FSM_EMIT
-            FSM_LAUNCHED("k_emit", s);
             FSM_HIP(hipEventRecord(ev.second, s));
             ev_emit.push_back(ev);
+            FSM_HIP(hipMemcpyAsync(&written, off.as<uint64_t>() + b.E, 8, hipMemcpyDeviceToHost, s));
         }
-        // the cursors must land exactly on the capacities (sum of child supports)
-        std::vector<uint32_t> cur(gb - ga);
-        FSM_HIP(hipMemcpyAsync(cur.data(), cursor.p, (gb - ga) * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipStreamSynchronize(s));
-        for (size_t k = 0; k < gb - ga; ++k)
-            if (cur[k] != dch[k].cap)
-                throw Error(FSM_EDEVICE, "SPADE emit: child class " + std::to_string(k) + " wrote " +
-                                             std::to_string(cur[k]) + " entries, expected " + std::to_string(dch[k].cap));
+        // the runs must add up exactly to the capacities (sum of child supports)
+        if (written != total)
+            throw Error(FSM_EDEVICE, "SPADE emit: wrote " + std::to_string(written) + " child entries, expected " +
+                                         std::to_string(total));
     }
 
     void run_root(Batch& root, const std::vector<uint32_t>& freq_items, const std::vector<uint32_t>& f1) {
@@ -808,6 +822,8 @@ struct Miner {
         if (fl) throw Error(FSM_ELIMIT, "SPADE: a sequence has more than 65535 distinct frequent items");
         if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
         root.slab.alloc(E0, W);
+        root.E = E0;
+        FSM_HIP(hipMemsetAsync(root.slab.cid.p, 0, E0 * 4, s));
         if (r1 > r0) {
             const SlabPtrs op = root.slab.ptrs();
             const unsigned grid = unsigned(((r1 - r0) * 64 + kBlock - 1) / kBlock);
@@ -829,7 +845,6 @@ struct Miner {
             m.node_of[2 * r] = int32_t(nodes.size());
             nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]]});
         }
-        m.ebegin = 0;
         m.nent = uint32_t(E0);
         root.cls.push_back(std::move(m));
         root.root = true;
