@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FSM_ABI_VERSION 1
+#define FSM_ABI_VERSION 2
 
 /* status codes */
 #define FSM_OK 0
@@ -52,13 +52,26 @@ typedef struct fsm_db fsm_db;
 
 typedef enum { FSM_MODE_SPADE = 0, FSM_MODE_TSR = 1 } fsm_mode;
 
+/* Host-side collectives, an alternative to RCCL for nranks > 1 (several ranks
+ * on one GPU, or any host transport).  Both are called collectively by every
+ * rank with the same sizes and return 0 on success.  Buffers are host memory.
+ *   allreduce_u32: buf[0..n) <- element-wise sum over ranks (in place)
+ *   allgather:     recv[r*bytes .. (r+1)*bytes) <- rank r's send[0..bytes)   */
+typedef struct {
+    void* user;
+    int (*allreduce_u32)(void* user, uint32_t* buf, int64_t n);
+    int (*allgather)(void* user, const void* send, void* recv, int64_t bytes);
+} fsm_host_comm;
+
 typedef struct {
     int32_t device;          /* local HIP device ordinal */
-    int32_t nranks;          /* 1: single GPU; >1: SPADE prefix classes sharded over ranks */
+    int32_t nranks;          /* 1: single GPU; >1: SPADE sharded over ranks (one process per GPU) */
     int32_t rank;            /* this process's rank in [0, nranks) */
     int32_t verbose;         /* 1: per-level trace on stderr */
     uint8_t unique_id[128];  /* RCCL unique id (fsm_comm_unique_id on rank 0), nranks > 1 */
     int64_t mem_budget;      /* device bytes for lattice frontier slabs; 0 = 1/2 of free HBM */
+    const fsm_host_comm* host_comm; /* nranks > 1: NULL = RCCL over unique_id, else these callbacks
+                                       (must outlive the context) */
 } fsm_opts;
 
 /* SPADE result: the patterns of List[Pattern] in CSR form.  Pattern p has
@@ -116,7 +129,16 @@ typedef struct {
 } fsm_stats;
 
 int fsm_abi_version(void);
+/* RCCL unique id for fsm_opts.unique_id (call on rank 0, broadcast the bytes). */
 int fsm_comm_unique_id(uint8_t out[128]);
+/* Multi-GPU work plan (pure host, deterministic): largest-first assignment of
+ * n work units with estimated volumes to the least-loaded of nranks ranks.
+ * The engine shards SPADE's first-level prefix classes with it. */
+int fsm_shard_plan(const uint64_t* volume, int64_t n, int32_t nranks, int32_t* owner);
+/* Collective self-test of the nranks > 1 plumbing (all-reduce, all-gather of
+ * ragged blobs) on the context-free transport of opts; no GPU compute when
+ * opts->host_comm is set.  0 = every rank saw the expected data. */
+int fsm_comm_selftest(const fsm_opts* opts);
 
 int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out);
 void fsm_ctx_destroy(fsm_ctx* ctx);

@@ -1,0 +1,191 @@
+// comm.cpp — the two collectives the sharded SPADE path needs:
+// an in-place u32 sum all-reduce (F1 histogram, statistics) and an all-gather
+// of equal-sized byte blocks (frequent-pair records, pattern CSRs).
+//
+//   RcclComm  one rank per GPU over RCCL (xGMI inside a node).  librccl is
+//             dlopen'ed on first use, so that libfsm loads and runs single-GPU
+//             without it, and binds to the librccl.so.1 a host process (PyTorch)
+//             has already loaded instead of a second copy.
+//   HostComm  host callbacks supplied by the caller (fsm_host_comm): used to
+//             run several ranks on one GPU (tests) or over any host transport.
+//             Device buffers are staged through host memory around the callback.
+#include <dlfcn.h>
+
+#include <mutex>
+
+#include <rccl/rccl.h>
+
+#include "comm.h"
+
+namespace fsm {
+namespace {
+
+struct RcclApi {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+const RcclApi& rccl() {
+    static RcclApi api;
+    static std::once_flag once;
+    static std::string err;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            err = std::string("cannot load librccl.so.1: ") + dlerror();
+            return;
+        }
+        api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        api.all_reduce = reinterpret_cast<decltype(api.all_reduce)>(dlsym(h, "ncclAllReduce"));
+        api.all_gather = reinterpret_cast<decltype(api.all_gather)>(dlsym(h, "ncclAllGather"));
+        api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(h, "ncclGetErrorString"));
+        if (!api.get_unique_id || !api.comm_init_rank || !api.comm_destroy || !api.all_reduce || !api.all_gather ||
+            !api.error_string) {
+            err = "librccl.so.1 lacks an expected symbol";
+            api = RcclApi{};
+        }
+    });
+    if (!api.all_reduce) throw Error(FSM_ECOMM, err.empty() ? "RCCL unavailable" : err);
+    return api;
+}
+
+void nccl_check(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw Error(FSM_ECOMM, std::string(what) + ": " + rccl().error_string(r));
+}
+
+class RcclComm final : public Comm {
+  public:
+    RcclComm(int nranks, int rank, const uint8_t id[128]) : Comm(nranks, rank) {
+        ncclUniqueId uid;
+        std::memcpy(uid.internal, id, sizeof(uid.internal));
+        nccl_check(rccl().comm_init_rank(&comm_, nranks, uid, rank), "ncclCommInitRank");
+    }
+    ~RcclComm() override {
+        if (comm_) (void)rccl().comm_destroy(comm_);
+    }
+    void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
+        if (n) nccl_check(rccl().all_reduce(dev, dev, n, ncclUint32, ncclSum, comm_, s), "ncclAllReduce");
+    }
+    void allgather(const void* dev_send, void* dev_recv, size_t bytes, hipStream_t s) override {
+        if (bytes) nccl_check(rccl().all_gather(dev_send, dev_recv, bytes, ncclUint8, comm_, s), "ncclAllGather");
+    }
+
+  private:
+    ncclComm_t comm_ = nullptr;
+};
+
+class HostComm final : public Comm {
+  public:
+    HostComm(int nranks, int rank, const fsm_host_comm& cb) : Comm(nranks, rank), cb_(cb) {
+        if (!cb_.allreduce_u32 || !cb_.allgather) throw Error(FSM_EINVAL, "fsm_host_comm: missing callback");
+    }
+    void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
+        std::vector<uint32_t> h(n);
+        if (n) FSM_HIP(hipMemcpyAsync(h.data(), dev, n * 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        if (cb_.allreduce_u32(cb_.user, h.data(), int64_t(n)) != 0)
+            throw Error(FSM_ECOMM, "host all-reduce callback failed");
+        if (n) FSM_HIP(hipMemcpyAsync(dev, h.data(), n * 4, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipStreamSynchronize(s));
+    }
+    void allgather(const void* dev_send, void* dev_recv, size_t bytes, hipStream_t s) override {
+        std::vector<uint8_t> snd(bytes), rcv(bytes * size_t(nranks()));
+        if (bytes) FSM_HIP(hipMemcpyAsync(snd.data(), dev_send, bytes, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        if (cb_.allgather(cb_.user, snd.data(), rcv.data(), int64_t(bytes)) != 0)
+            throw Error(FSM_ECOMM, "host all-gather callback failed");
+        if (bytes) FSM_HIP(hipMemcpyAsync(dev_recv, rcv.data(), rcv.size(), hipMemcpyHostToDevice, s));
+        FSM_HIP(hipStreamSynchronize(s));
+    }
+    void host_allreduce_u32(uint32_t* h, size_t n, hipStream_t) override {
+        if (cb_.allreduce_u32(cb_.user, h, int64_t(n)) != 0) throw Error(FSM_ECOMM, "host all-reduce callback failed");
+    }
+    void host_allgather(const void* send, void* recv, size_t bytes, hipStream_t) override {
+        if (cb_.allgather(cb_.user, send, recv, int64_t(bytes)) != 0)
+            throw Error(FSM_ECOMM, "host all-gather callback failed");
+    }
+
+  private:
+    fsm_host_comm cb_;
+};
+
+}  // namespace
+
+void Comm::host_allreduce_u32(uint32_t* h, size_t n, hipStream_t s) {
+    DevBuf d(std::max<size_t>(n, 1) * 4);
+    if (n) FSM_HIP(hipMemcpyAsync(d.p, h, n * 4, hipMemcpyHostToDevice, s));
+    allreduce_u32(d.as<uint32_t>(), n, s);
+    if (n) FSM_HIP(hipMemcpyAsync(h, d.p, n * 4, hipMemcpyDeviceToHost, s));
+    FSM_HIP(hipStreamSynchronize(s));
+}
+
+void Comm::host_allgather(const void* send, void* recv, size_t bytes, hipStream_t s) {
+    DevBuf ds(std::max<size_t>(bytes, 1)), dr(std::max<size_t>(bytes * size_t(nranks()), 1));
+    if (bytes) FSM_HIP(hipMemcpyAsync(ds.p, send, bytes, hipMemcpyHostToDevice, s));
+    allgather(ds.p, dr.p, bytes, s);
+    if (bytes) FSM_HIP(hipMemcpyAsync(recv, dr.p, bytes * size_t(nranks()), hipMemcpyDeviceToHost, s));
+    FSM_HIP(hipStreamSynchronize(s));
+}
+
+std::vector<uint8_t> Comm::gather_blobs(const std::vector<uint8_t>& mine, std::vector<size_t>& sizes, hipStream_t s) {
+    const int N = nranks();
+    std::vector<uint32_t> sz(size_t(N) * 2, 0);  // (lo, hi) u32 halves of each rank's size
+    sz[size_t(rank()) * 2] = uint32_t(mine.size() & 0xFFFFFFFFu);
+    sz[size_t(rank()) * 2 + 1] = uint32_t(uint64_t(mine.size()) >> 32);
+    host_allreduce_u32(sz.data(), sz.size(), s);
+    sizes.assign(size_t(N), 0);
+    size_t mx = 0;
+    for (int r = 0; r < N; ++r) {
+        sizes[size_t(r)] = size_t(sz[size_t(r) * 2]) | (size_t(sz[size_t(r) * 2 + 1]) << 32);
+        mx = std::max(mx, sizes[size_t(r)]);
+    }
+    mx = (mx + 7) & ~size_t(7);
+    std::vector<uint8_t> snd(mx, 0), all(mx * size_t(N));
+    if (!mine.empty()) std::memcpy(snd.data(), mine.data(), mine.size());
+    host_allgather(snd.data(), all.data(), mx, s);
+    std::vector<uint8_t> out;
+    for (int r = 0; r < N; ++r)
+        out.insert(out.end(), all.begin() + ptrdiff_t(size_t(r) * mx), all.begin() + ptrdiff_t(size_t(r) * mx + sizes[size_t(r)]));
+    return out;
+}
+
+void rccl_unique_id(uint8_t out[128]) {
+    ncclUniqueId uid;
+    nccl_check(rccl().get_unique_id(&uid), "ncclGetUniqueId");
+    std::memcpy(out, uid.internal, 128);
+}
+
+std::unique_ptr<Comm> make_comm(const fsm_opts& o) {
+    if (o.nranks <= 1) return nullptr;
+    if (o.rank < 0 || o.rank >= o.nranks) throw Error(FSM_EINVAL, "rank out of range");
+    if (o.host_comm) return std::make_unique<HostComm>(o.nranks, o.rank, *o.host_comm);
+    return std::make_unique<RcclComm>(o.nranks, o.rank, o.unique_id);
+}
+
+}  // namespace fsm
+
+namespace fsm {
+
+void shard_plan(const uint64_t* volume, int64_t n, int32_t nranks, int32_t* owner) {
+    std::vector<int64_t> idx(size_t(std::max<int64_t>(n, 0)));
+    for (int64_t i = 0; i < n; ++i) idx[size_t(i)] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return volume[a] > volume[b]; });
+    std::vector<uint64_t> load(size_t(nranks), 0);
+    for (int64_t i : idx) {
+        int32_t best = 0;
+        for (int32_t r = 1; r < nranks; ++r)
+            if (load[size_t(r)] < load[size_t(best)]) best = r;
+        owner[i] = best;
+        load[size_t(best)] += volume[i];
+    }
+}
+
+}  // namespace fsm

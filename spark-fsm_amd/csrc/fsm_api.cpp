@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <new>
 
+#include "comm.h"
 #include "fsm_internal.h"
 
 using fsm::Error;
@@ -71,7 +72,38 @@ int fsm_abi_version(void) { return FSM_ABI_VERSION; }
 int fsm_comm_unique_id(uint8_t out[128]) {
     if (!out) return FSM_EINVAL;
     std::memset(out, 0, 128);
-    return fail(nullptr, FSM_ECOMM, "multi-rank SPADE is not built into this library yet");
+    return guarded(nullptr, [&] { fsm::rccl_unique_id(out); });
+}
+
+int fsm_shard_plan(const uint64_t* volume, int64_t n, int32_t nranks, int32_t* owner) {
+    if (n < 0 || nranks < 1 || (n > 0 && (!volume || !owner))) return fail(nullptr, FSM_EINVAL, "bad shard plan arguments");
+    return guarded(nullptr, [&] { fsm::shard_plan(volume, n, nranks, owner); });
+}
+
+int fsm_comm_selftest(const fsm_opts* opts) {
+    if (!opts || opts->nranks < 2) return fail(nullptr, FSM_EINVAL, "selftest needs nranks >= 2");
+    return guarded(nullptr, [&] {
+        if (!opts->host_comm) FSM_HIP(hipSetDevice(opts->device));
+        auto comm = fsm::make_comm(*opts);
+        const uint32_t N = uint32_t(opts->nranks), r = uint32_t(opts->rank);
+        std::vector<uint32_t> v(1000);
+        for (uint32_t i = 0; i < v.size(); ++i) v[i] = r + i;
+        comm->host_allreduce_u32(v.data(), v.size(), nullptr);
+        for (uint32_t i = 0; i < v.size(); ++i)
+            if (v[i] != N * i + N * (N - 1) / 2) throw Error(FSM_ECOMM, "selftest: all-reduce mismatch");
+        std::vector<uint8_t> mine(size_t(r) * 3 + 1);
+        for (size_t j = 0; j < mine.size(); ++j) mine[j] = uint8_t(r * 7 + j);
+        std::vector<size_t> sizes;
+        const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, nullptr);
+        size_t at = 0;
+        for (uint32_t q = 0; q < N; ++q) {
+            if (sizes[q] != size_t(q) * 3 + 1) throw Error(FSM_ECOMM, "selftest: gather size mismatch");
+            for (size_t j = 0; j < sizes[q]; ++j)
+                if (all[at + j] != uint8_t(q * 7 + j)) throw Error(FSM_ECOMM, "selftest: gather data mismatch");
+            at += sizes[q];
+        }
+        if (at != all.size()) throw Error(FSM_ECOMM, "selftest: gather length mismatch");
+    });
 }
 
 int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
@@ -82,8 +114,6 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
     if (opts) ctx->opts = *opts;
     if (ctx->opts.nranks <= 0) ctx->opts.nranks = 1;
     const int rc = guarded(ctx, [&] {
-        if (ctx->opts.nranks != 1)
-            throw Error(FSM_ECOMM, "multi-rank SPADE is not built into this library yet");
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
             throw Error(FSM_EDEVICE, "no HIP device available (libfsm requires an MI355X / gfx950 GPU)");
@@ -95,6 +125,7 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
         if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             throw Error(FSM_EDEVICE, std::string("libfsm is built for gfx950; device is ") + prop.gcnArchName);
         FSM_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->comm = fsm::make_comm(ctx->opts).release();
     });
     if (rc != FSM_OK) {
         g_err = ctx->err;
@@ -108,6 +139,7 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
 void fsm_ctx_destroy(fsm_ctx* ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    delete ctx->comm;
     fsm::pool_trim();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

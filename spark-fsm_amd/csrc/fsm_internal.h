@@ -114,6 +114,9 @@ void flatten_tsr(const Source& src, FlatTsr& out);
 
 struct SpadeDevDB;
 struct TsrDevDB;
+namespace fsm {
+class Comm;
+}
 
 struct fsm_ctx {
     fsm_opts opts{};
@@ -121,7 +124,7 @@ struct fsm_ctx {
     fsm_stats stats{};
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    void* comm = nullptr;  // ncclComm_t when nranks > 1
+    fsm::Comm* comm = nullptr;  // nranks > 1 (owned)
 };
 
 struct fsm_db {

@@ -36,6 +36,7 @@
 #include <memory>
 #include <numeric>
 
+#include "comm.h"
 #include "device_util.h"
 
 struct SpadeDevDB {
@@ -162,11 +163,12 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
                                                   const DClass* __restrict__ cls,
                                                   const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
                                                   const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
-                                                  uint32_t* __restrict__ cnt) {
+                                                  uint32_t mlo, uint32_t mhi, uint32_t* __restrict__ cnt) {
     const uint32_t e1 = min(E, (blockIdx.x + 1) * kChunk);
     for (uint32_t e = blockIdx.x * kChunk + threadIdx.x; e < e1; e += blockDim.x) {
-        const DClass c = cls[cid[e]];
         const uint32_t mi = mem[e], p = pos[e];
+        if (mi - mlo >= mhi - mlo) continue;  // member rows of another rank (sharded root)
+        const DClass c = cls[cid[e]];
         const uint32_t lo_i = lohi[e] & 0xFFFFu;
         const uint32_t ti = mi & 1u, ri = mi >> 1;
         const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
@@ -217,14 +219,16 @@ __global__ __launch_bounds__(kBlock) void k_rootpair_hist(uint32_t E0, const uin
                                                           const uint32_t* __restrict__ lohi,
                                                           const uint32_t* __restrict__ pos,
                                                           const uint64_t* __restrict__ mask, uint32_t D, uint32_t nb,
-                                                          uint32_t chunk, uint32_t* __restrict__ blkhist,
+                                                          uint32_t chunk, uint32_t mlo, uint32_t mhi,
+                                                          uint32_t* __restrict__ blkhist,
                                                           uint32_t* __restrict__ total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
     __syncthreads();
     const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
-        root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { atomicAdd(&h[key >> kBucketBits], 1u); });
+        if (mem[e] - mlo < mhi - mlo)
+            root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { atomicAdd(&h[key >> kBucketBits], 1u); });
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
         const uint32_t v = h[b];
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(kBlock) void k_rootpair_scatter(uint32_t E0, const 
                                                              const uint32_t* __restrict__ lohi,
                                                              const uint32_t* __restrict__ pos,
                                                              const uint64_t* __restrict__ mask, uint32_t D,
-                                                             uint32_t nb, uint32_t chunk,
+                                                             uint32_t nb, uint32_t chunk, uint32_t mlo, uint32_t mhi,
                                                              const uint32_t* __restrict__ blkhist,
                                                              const uint64_t* __restrict__ boff,
                                                              uint32_t* __restrict__ gcur,
@@ -253,7 +257,8 @@ __global__ __launch_bounds__(kBlock) void k_rootpair_scatter(uint32_t E0, const 
     __syncthreads();
     const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
-        root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) {
+        if (mem[e] - mlo < mhi - mlo)
+            root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) {
             keys[atomicAdd(&cur[key >> kBucketBits], 1u)] = uint16_t(key & ((1u << kBucketBits) - 1u));
         });
 }
@@ -293,7 +298,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ 
 __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ rows, uint32_t nrows,
                                                        const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
                                                        uint32_t minsup, const uint64_t* __restrict__ rowoff,
-                                                       FreqRec* __restrict__ out) {
+                                                       uint32_t row_base, FreqRec* __restrict__ out) {
     const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (g >= nrows) return;
     const DRow r = rows[g];
@@ -311,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
         const uint64_t lead = __ballot((fr || partner) && !(lane & 1u));
         const uint32_t crank = nrank + uint32_t(__popcll(lead & lead_lt));
         const uint64_t fb = __ballot(fr);
-        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{g, slot, v, crank << 1 | (slot & 1u)};
+        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{row_base + g, slot, v, crank << 1 | (slot & 1u)};
         o += uint64_t(__popcll(fb));
         nrank += uint32_t(__popcll(lead));
     }
@@ -485,6 +490,11 @@ struct Miner {
     uint64_t budget;
     std::vector<PNode> nodes;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_count, ev_emit;
+    // sharded mining (nranks > 1): this rank counts the root rows of ranks
+    // [slice_lo, slice_hi) and mines the first-level classes shard_plan gives it
+    Comm* comm = nullptr;
+    uint32_t slice_lo = 0, slice_hi = kNone;
+    size_t n_shared = 0;  // pattern nodes every rank holds (root + its frequent children)
 
     uint64_t entry_bytes() const { return 12ull + 8ull * uint64_t(W); }
 
@@ -557,6 +567,10 @@ struct Miner {
         }
     }
 
+    // member ids whose counter rows this rank computes (all but the sharded root)
+    uint32_t member_lo(const Batch& b) const { return comm && b.root ? 2 * slice_lo : 0u; }
+    uint32_t member_hi(const Batch& b) const { return comm && b.root ? 2 * slice_hi : kNone; }
+
     // FSM_ROOT_PATH=atomic forces the global-atomic root F2 path (tests, profiling).
     static bool root_atomic() {
         const char* v = std::getenv("FSM_ROOT_PATH");
@@ -577,6 +591,7 @@ struct Miner {
         if (nb64 > kMaxBuckets || K >= (uint64_t(1) << 32) || m.nent == 0) return false;
         const uint32_t nb = uint32_t(nb64);
         const uint32_t E0 = m.nent;
+        const uint32_t mlo = member_lo(b), mhi = member_hi(b);
         const uint32_t chunk = root_chunk();
         const uint32_t nblk = (E0 + chunk - 1) / chunk;
         DevBuf blkhist(uint64_t(nblk) * nb * 4), total(uint64_t(nb) * 4 + 4), boff((uint64_t(nb) + 1) * 8),
@@ -587,7 +602,7 @@ struct Miner {
         const size_t lds = size_t(nb) * 4;
 #define FSM_RP_HIST(WW)                                                                                    \
     hipLaunchKernelGGL(k_rootpair_hist<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
-                       sp.mask, m.D, nb, chunk, blkhist.as<uint32_t>(), total.as<uint32_t>())
+                       sp.mask, m.D, nb, chunk, mlo, mhi, blkhist.as<uint32_t>(), total.as<uint32_t>())
         FSM_W_DISPATCH(W, FSM_RP_HIST)
 #undef FSM_RP_HIST
         FSM_LAUNCHED("k_rootpair_hist", s);
@@ -599,7 +614,8 @@ struct Miner {
         DevBuf keys(std::max<uint64_t>(npairs, 1) * 2);
 #define FSM_RP_SCAT(WW)                                                                                        \
     hipLaunchKernelGGL(k_rootpair_scatter<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
-                       sp.mask, m.D, nb, chunk, blkhist.as<uint32_t>(), boff.as<uint64_t>(), gcur.as<uint32_t>(), \
+                       sp.mask, m.D, nb, chunk, mlo, mhi, blkhist.as<uint32_t>(), boff.as<uint64_t>(),            \
+                       gcur.as<uint32_t>(), \
                        keys.as<uint16_t>())
         FSM_W_DISPATCH(W, FSM_RP_SCAT)
 #undef FSM_RP_SCAT
@@ -615,7 +631,9 @@ struct Miner {
     void count_and_freq(Batch& b) {
         dump(b);
         prepare(b);
-        for (auto& m : b.cls) stats_for_class(m);
+        const bool shard = comm && b.root;  // root rows split over ranks, frequent pairs all-gathered
+        if (!shard || comm->rank() == 0)
+            for (auto& m : b.cls) stats_for_class(m);
         fsm_stats& st = ctx->stats;
         st.batches += 1;
         const uint64_t tot_ent = b.E;
@@ -633,7 +651,7 @@ struct Miner {
 #define FSM_COUNT(WW)                                                                                   \
     hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + kChunk - 1) / kChunk)), dim3(kBlock), 0, s,   \
                        uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
-                       cnt.as<uint32_t>())
+                       member_lo(b), member_hi(b), cnt.as<uint32_t>())
                 FSM_W_DISPATCH(W, FSM_COUNT)
 #undef FSM_COUNT
                 FSM_LAUNCHED("k_count", s);
@@ -647,9 +665,12 @@ struct Miner {
         for (size_t c = 0; c < b.cls.size(); ++c)
             for (uint32_t mi = 0; mi < b.cls[c].D; ++mi)
                 if (b.cls[c].node_of[mi] >= 0) rows.push_back(DRow{uint32_t(c), mi});
-        const uint32_t nrows = uint32_t(rows.size());
+        // root rows are rows[r] = rank r: a shard extracts its own slice of them
+        const uint32_t rlo = shard ? std::min<uint32_t>(slice_lo, uint32_t(rows.size())) : 0u;
+        const uint32_t rhi = shard ? std::min<uint32_t>(slice_hi, uint32_t(rows.size())) : uint32_t(rows.size());
+        const uint32_t nrows = rhi - rlo;
         DevBuf d_rows, rowcnt((size_t(nrows) + 1) * 4), rowoff((size_t(nrows) + 1) * 8);
-        upload(d_rows, rows);
+        upload(d_rows, std::vector<DRow>(rows.begin() + rlo, rows.begin() + rhi));
         const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
         if (nrows) {
             hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
@@ -664,13 +685,22 @@ struct Miner {
         if (nfreq) {
             DevBuf d_recs(nfreq * sizeof(FreqRec));
             hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
-                               b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(),
+                               b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
                                d_recs.as<FreqRec>());
             FSM_LAUNCHED("k_freq_write", s);
             FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nfreq * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
             FSM_HIP(hipStreamSynchronize(s));
         }
         cnt.release();
+        if (shard) {  // every rank gets every frequent pair, in row order (slices ascend with the rank)
+            std::vector<uint8_t> mine(recs.size() * sizeof(FreqRec));
+            if (!recs.empty()) std::memcpy(mine.data(), recs.data(), mine.size());
+            std::vector<size_t> sizes;
+            const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s);
+            nfreq = all.size() / sizeof(FreqRec);
+            recs.resize(nfreq);
+            if (nfreq) std::memcpy(recs.data(), all.data(), all.size());
+        }
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
         std::vector<uint32_t> koff(b.cbase_total + 1, 0), kslot(nfreq), kcid(nfreq);
         for (const FreqRec& fr : recs) koff[b.cls[rows[fr.row].cls].cbase + rows[fr.row].mi + 1] += 1;
@@ -716,6 +746,19 @@ struct Miner {
                 throw Error(FSM_ELIMIT, "SPADE: a prefix class has more than 65535 frequent children");
             if (!(nch == 1 && last_type == kItm)) b.children.push_back(std::move(ch));
             q = q2;
+        }
+        if (shard) {
+            // first-level classes: largest-first by estimated id-list volume (the
+            // class's entries), same plan on every rank; keep this rank's share
+            n_shared = nodes.size();
+            std::vector<uint64_t> vol(b.children.size());
+            std::vector<int32_t> owner(b.children.size());
+            for (size_t k = 0; k < vol.size(); ++k) vol[k] = b.children[k].cap;
+            shard_plan(vol.data(), int64_t(vol.size()), comm->nranks(), owner.data());
+            std::vector<ChildInfo> kept;
+            for (size_t k = 0; k < vol.size(); ++k)
+                if (owner[k] == comm->rank()) kept.push_back(std::move(b.children[k]));
+            b.children = std::move(kept);
         }
         // groups of children that fit the frontier budget
         b.groups.clear();
@@ -870,6 +913,62 @@ template <class T> void copy_out(T*& dst, const std::vector<T>& src) {
     if (!src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(T));
 }
 
+// every rank's pattern CSR, concatenated in rank order, on every rank
+void gather_patterns(Comm* comm, hipStream_t s, std::vector<int32_t>& sup, std::vector<int64_t>& pat_off,
+                     std::vector<int64_t>& set_off, std::vector<int32_t>& items) {
+    // blob (int32): n, n_sets, n_items, sup[n], sets-per-pattern[n], set sizes[n_sets], items[n_items]
+    const size_t n = sup.size(), ns = set_off.size() - 1, ni = items.size();
+    if (n > size_t(INT32_MAX) || ns > size_t(INT32_MAX) || ni > size_t(INT32_MAX))
+        throw Error(FSM_ELIMIT, "SPADE: pattern output of one rank exceeds 2^31 entries");
+    std::vector<int32_t> b;
+    b.reserve(3 + 2 * n + ns + ni);
+    b.push_back(int32_t(n));
+    b.push_back(int32_t(ns));
+    b.push_back(int32_t(ni));
+    b.insert(b.end(), sup.begin(), sup.end());
+    for (size_t k = 0; k < n; ++k) b.push_back(int32_t(pat_off[k + 1] - pat_off[k]));
+    for (size_t k = 0; k < ns; ++k) b.push_back(int32_t(set_off[k + 1] - set_off[k]));
+    b.insert(b.end(), items.begin(), items.end());
+    std::vector<uint8_t> mine(b.size() * 4);
+    std::memcpy(mine.data(), b.data(), mine.size());
+    std::vector<size_t> sizes;
+    const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s);
+    sup.clear();
+    items.clear();
+    pat_off.assign(1, 0);
+    set_off.assign(1, 0);
+    size_t at = 0;
+    for (size_t r = 0; r < sizes.size(); ++r) {
+        std::vector<int32_t> v(sizes[r] / 4);
+        if (!v.empty()) std::memcpy(v.data(), all.data() + at, sizes[r]);
+        at += sizes[r];
+        const size_t rn = size_t(v[0]), rs = size_t(v[1]), ri = size_t(v[2]);
+        const int32_t* p = v.data() + 3;
+        sup.insert(sup.end(), p, p + rn);
+        for (size_t k = 0; k < rn; ++k) pat_off.push_back(pat_off.back() + p[rn + k]);
+        for (size_t k = 0; k < rs; ++k) set_off.push_back(set_off.back() + p[2 * rn + k]);
+        items.insert(items.end(), p + 2 * rn + rs, p + 2 * rn + rs + ri);
+    }
+}
+
+// sum the work counters of all ranks (joins etc. are counted where the work ran)
+void gather_stats(Comm* comm, hipStream_t s, fsm_stats& st) {
+    int64_t* f[] = {&st.joins, &st.classes, &st.batches, &st.entries, &st.bytes_join_equiv,
+                    &st.bytes_streamed, &st.bytes_count_alg, &st.count_launches};
+    constexpr size_t K = sizeof(f) / sizeof(f[0]);
+    std::vector<uint8_t> mine(K * 8);
+    for (size_t k = 0; k < K; ++k) std::memcpy(mine.data() + 8 * k, f[k], 8);
+    std::vector<size_t> sizes;
+    const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s);
+    for (size_t k = 0; k < K; ++k) *f[k] = 0;
+    for (size_t r = 0; r < sizes.size(); ++r)
+        for (size_t k = 0; k < K; ++k) {
+            int64_t v;
+            std::memcpy(&v, all.data() + r * K * 8 + 8 * k, 8);
+            *f[k] += v;
+        }
+}
+
 }  // namespace
 
 void spade_upload(fsm_ctx* ctx, fsm_db* db) {
@@ -906,6 +1005,8 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     SpadeDevDB* d = db->spade_dev;
     const int64_t total = db->spade.total;
     Miner mn{ctx, d, ctx->stream, d->W, 1, 0, {}, {}, {}};
+    mn.comm = ctx->comm;
+    Comm* comm = ctx->comm;
     ctx->stats.mask_words = d->W;
     // minsupp = Math.ceil(support * total) (SPADE.scala:113), >= 1 for the lattice
     const double ms = std::ceil(support * double(total));
@@ -920,14 +1021,17 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     {
         DevBuf d_f1(std::max<int64_t>(d->U, 1) * 4);
         FSM_HIP(hipMemsetAsync(d_f1.p, 0, size_t(d->U) * 4, ctx->stream));
-        if (d->E) {
+        // sharded: each rank histograms its slice of the entries, then one all-reduce
+        const uint64_t e0 = comm ? uint64_t(d->E) * uint64_t(comm->rank()) / uint64_t(comm->nranks()) : 0;
+        const uint64_t e1 = comm ? uint64_t(d->E) * uint64_t(comm->rank() + 1) / uint64_t(comm->nranks()) : uint64_t(d->E);
+        if (e1 > e0) {
             const int use_lds = d->U <= 16384;
-            const unsigned grid = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, use_lds ? 1024 : 8192));
+            const unsigned grid = unsigned(std::min<uint64_t>((e1 - e0 + kBlock - 1) / kBlock, use_lds ? 1024 : 8192));
             hipLaunchKernelGGL(k_f1, dim3(grid), dim3(kBlock), use_lds ? size_t(d->U) * 4 : 0, ctx->stream,
-                               d->item.as<uint32_t>(), uint64_t(0), uint64_t(d->E), d_f1.as<uint32_t>(),
-                               uint32_t(d->U), use_lds);
+                               d->item.as<uint32_t>(), e0, e1, d_f1.as<uint32_t>(), uint32_t(d->U), use_lds);
             FSM_LAUNCHED("k_f1", ctx->stream);
         }
+        if (comm) comm->allreduce_u32(d_f1.as<uint32_t>(), size_t(d->U), ctx->stream);
         if (d->U) FSM_HIP(hipMemcpyAsync(f1.data(), d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));
         FSM_HIP(hipStreamSynchronize(ctx->stream));
     }
@@ -936,6 +1040,19 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         for (int64_t i = 0; i < d->U; ++i)
             if (f1[size_t(i)] >= mn.minsup) freq.push_back(uint32_t(i));
 
+    if (comm && !freq.empty()) {
+        // root counter rows: contiguous rank slices of about equal entry counts
+        uint64_t tot = 0, acc = 0;
+        for (uint32_t it : freq) tot += f1[it];
+        const uint64_t N = uint64_t(comm->nranks()), r = uint64_t(comm->rank());
+        mn.slice_lo = mn.slice_hi = uint32_t(freq.size());
+        for (size_t k = 0; k < freq.size(); ++k) {
+            if (mn.slice_lo == freq.size() && acc * N >= tot * r) mn.slice_lo = uint32_t(k);
+            if (acc * N >= tot * (r + 1)) { mn.slice_hi = uint32_t(k); break; }
+            acc += f1[freq[k]];
+        }
+        if (mn.slice_hi < mn.slice_lo) mn.slice_hi = mn.slice_lo;
+    }
     std::vector<std::unique_ptr<Batch>> stack;
     if (!freq.empty()) {
         auto root = std::make_unique<Batch>();
@@ -976,14 +1093,16 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     ctx->stats.ms_count_kernel = mn.elapsed(mn.ev_count);
     ctx->stats.ms_emit_kernel = mn.elapsed(mn.ev_emit);
 
-    // ---- output CSR in discovery order (the reference's order is discovery order too)
+    // ---- output CSR in discovery order (the reference's order is discovery order too);
+    // sharded: rank 0 holds the shared root levels, every rank its own classes
     const auto& nodes = mn.nodes;
-    const int64_t n = int64_t(nodes.size());
+    const int64_t first = (comm && comm->rank() != 0) ? int64_t(mn.n_shared) : 0;
+    int64_t n = int64_t(nodes.size()) - first;
     std::vector<int32_t> sup(static_cast<size_t>(n));
     std::vector<int64_t> pat_off(size_t(n) + 1, 0), set_off(1, 0);
     std::vector<int32_t> items;
     std::vector<uint32_t> path_item, path_type;
-    for (int64_t k = 0; k < n; ++k) {
+    for (int64_t k = first; k < int64_t(nodes.size()); ++k) {
         path_item.clear();
         path_type.clear();
         for (int32_t q = int32_t(k); q >= 0; q = nodes[size_t(q)].parent) {
@@ -995,8 +1114,13 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             items.push_back(db->spade.item_val[path_item[t]]);
         }
         set_off.push_back(int64_t(items.size()));
-        sup[size_t(k)] = int32_t(nodes[size_t(k)].support);
-        pat_off[size_t(k) + 1] = int64_t(set_off.size()) - 1;
+        sup[size_t(k - first)] = int32_t(nodes[size_t(k)].support);
+        pat_off[size_t(k - first) + 1] = int64_t(set_off.size()) - 1;
+    }
+    if (comm) {
+        gather_patterns(comm, ctx->stream, sup, pat_off, set_off, items);
+        n = int64_t(sup.size());
+        gather_stats(comm, ctx->stream, ctx->stats);
     }
     auto* p = static_cast<fsm_patterns*>(std::calloc(1, sizeof(fsm_patterns)));
     if (!p) throw Error(FSM_ENOMEM, "calloc failed");

@@ -5,5 +5,6 @@ mirror of the reference's Scala API over it.
 """
 from ._lib import FsmError, FsmParseError, MODE_SPADE, MODE_TSR, LIB_PATH  # noqa: F401
 from .engine import Engine, DB, default_engine  # noqa: F401
+from .dist import comm_unique_id, shard_plan, TorchHostComm  # noqa: F401
 from .api import (Pattern, Rule, extract_rdd_patterns, extract_rdd_rules,  # noqa: F401
                   spade_actor_patterns, tsr_actor_rules)

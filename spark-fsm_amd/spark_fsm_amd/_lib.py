@@ -28,6 +28,18 @@ class FsmParseError(FsmError):
     """Input the reference itself would throw on (-> TrainActor FAILURE)."""
 
 
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int64)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+
+
+class HostComm(ctypes.Structure):
+    _fields_ = [
+        ("user", ctypes.c_void_p),
+        ("allreduce_u32", ALLREDUCE_FN),
+        ("allgather", ALLGATHER_FN),
+    ]
+
+
 class Opts(ctypes.Structure):
     _fields_ = [
         ("device", ctypes.c_int32),
@@ -36,6 +48,7 @@ class Opts(ctypes.Structure):
         ("verbose", ctypes.c_int32),
         ("unique_id", ctypes.c_uint8 * 128),
         ("mem_budget", ctypes.c_int64),
+        ("host_comm", ctypes.POINTER(HostComm)),
     ]
 
 
@@ -81,7 +94,7 @@ class Stats(ctypes.Structure):
 
 # Every symbol declared in include/fsm.h (checked by tests/test_abi.py).
 EXPORTS = [
-    "fsm_abi_version", "fsm_comm_unique_id", "fsm_ctx_create", "fsm_ctx_destroy",
+    "fsm_abi_version", "fsm_comm_unique_id", "fsm_shard_plan", "fsm_comm_selftest", "fsm_ctx_create", "fsm_ctx_destroy",
     "fsm_last_error", "fsm_get_stats", "fsm_db_from_spmf", "fsm_db_from_tokens",
     "fsm_db_free", "fsm_spade_mine", "fsm_patterns_free", "fsm_tsr_mine", "fsm_rules_free",
 ]
@@ -104,6 +117,8 @@ def load():
     vp = ctypes.c_void_p
     L.fsm_abi_version.restype = ctypes.c_int
     L.fsm_comm_unique_id.argtypes = [P(ctypes.c_uint8)]
+    L.fsm_shard_plan.argtypes = [P(ctypes.c_uint64), ctypes.c_int64, ctypes.c_int32, P(ctypes.c_int32)]
+    L.fsm_comm_selftest.argtypes = [P(Opts)]
     L.fsm_ctx_create.argtypes = [P(Opts), P(vp)]
     L.fsm_ctx_destroy.argtypes = [vp]
     L.fsm_ctx_destroy.restype = None

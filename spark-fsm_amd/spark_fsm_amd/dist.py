@@ -1,0 +1,86 @@
+"""Multi-rank plumbing for libfsm's sharded SPADE.
+
+libfsm runs one rank per GPU.  Its collectives go either over RCCL (the
+production path: rank 0 calls `comm_unique_id()`, the bytes are broadcast by
+any channel, every rank passes them to `Engine(..., unique_id=...)`) or over
+host callbacks (`TorchHostComm`: any torch.distributed process group, e.g.
+gloo).  The host form runs several ranks on one GPU, which is how the sharded
+path is tested on a one-GPU box, and drives the CPU tests of the plumbing.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def comm_unique_id():
+    """RCCL unique id (128 bytes) for Engine(unique_id=...), on rank 0."""
+    L = _lib.load()
+    buf = (ctypes.c_uint8 * 128)()
+    _lib.check(L.fsm_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def shard_plan(volumes, nranks):
+    """fsm_shard_plan: owner rank of each work unit (largest first, least loaded)."""
+    L = _lib.load()
+    v = np.ascontiguousarray(volumes, dtype=np.uint64)
+    owner = np.zeros(len(v), dtype=np.int32)
+    P = ctypes.POINTER
+    _lib.check(L.fsm_shard_plan(v.ctypes.data_as(P(ctypes.c_uint64)), len(v), int(nranks),
+                                owner.ctypes.data_as(P(ctypes.c_int32))))
+    return owner
+
+
+class TorchHostComm:
+    """fsm_host_comm over a torch.distributed process group (CPU tensors)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self._dist = dist
+        self._group = group
+        self._ar = _lib.ALLREDUCE_FN(self._allreduce)
+        self._ag = _lib.ALLGATHER_FN(self._allgather)
+        self.struct = _lib.HostComm(None, self._ar, self._ag)
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def _allreduce(self, user, buf, n):
+        try:
+            import torch
+            if n > 0:
+                a = np.ctypeslib.as_array(buf, shape=(n,)).view(np.int32)  # u32 sums mod 2^32 == i32 bits
+                t = torch.from_numpy(a)  # shares the C buffer: reduced in place
+                self._dist.all_reduce(t, group=self._group)
+            return 0
+        except Exception:  # noqa: BLE001 - must not unwind through C
+            return 1
+
+    def _allgather(self, user, send, recv, nbytes):
+        try:
+            import torch
+            if nbytes > 0:
+                s = torch.from_numpy(np.ctypeslib.as_array(ctypes.cast(send, ctypes.POINTER(ctypes.c_uint8)),
+                                                           shape=(nbytes,)).copy())
+                out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+                self._dist.all_gather(out, s, group=self._group)
+                r = np.ctypeslib.as_array(ctypes.cast(recv, ctypes.POINTER(ctypes.c_uint8)),
+                                          shape=(nbytes * self.world,))
+                for k, t in enumerate(out):
+                    r[k * nbytes:(k + 1) * nbytes] = t.numpy()
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+
+def selftest(nranks, rank, host_comm=None, unique_id=None, device=0):
+    """fsm_comm_selftest: all-reduce + ragged all-gather across the ranks."""
+    L = _lib.load()
+    o = _lib.Opts()
+    o.device, o.nranks, o.rank = device, nranks, rank
+    if unique_id is not None:
+        ctypes.memmove(o.unique_id, unique_id, 128)
+    if host_comm is not None:
+        o.host_comm = ctypes.pointer(host_comm.struct)
+    _lib.check(L.fsm_comm_selftest(ctypes.byref(o)))

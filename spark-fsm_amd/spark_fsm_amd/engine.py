@@ -10,14 +10,22 @@ from ._lib import MODE_SPADE, MODE_TSR, check
 class Engine:
     """Owns a libfsm context on one gfx950 device."""
 
-    def __init__(self, device=0, verbose=False, mem_budget=0):
+    def __init__(self, device=0, verbose=False, mem_budget=0, nranks=1, rank=0, unique_id=None, host_comm=None):
+        """nranks > 1: sharded SPADE, one Engine per rank, collectives over RCCL
+        (unique_id from dist.comm_unique_id() on rank 0) or over host_comm
+        (a dist.TorchHostComm; kept alive by this Engine)."""
         L = _lib.load()
         opts = _lib.Opts()
         opts.device = device
-        opts.nranks = 1
-        opts.rank = 0
+        opts.nranks = int(nranks)
+        opts.rank = int(rank)
         opts.verbose = 1 if verbose else 0
         opts.mem_budget = int(mem_budget)
+        if unique_id is not None:
+            ctypes.memmove(opts.unique_id, bytes(unique_id), 128)
+        self._host_comm = host_comm
+        if host_comm is not None:
+            opts.host_comm = ctypes.pointer(host_comm.struct)
         self._ctx = ctypes.c_void_p()
         check(L.fsm_ctx_create(ctypes.byref(opts), ctypes.byref(self._ctx)), None)
         self._L = L

@@ -1,0 +1,47 @@
+"""One rank of a multi-process libfsm run (launched by tests/test_dist.py and
+tests/test_parity_gpu.py as a plain child process).
+
+  python tests/dist_worker.py <mode> <out.json> [args...]
+  mode selftest       : fsm_comm_selftest over a gloo TorchHostComm (no GPU)
+  mode spade D sup    : sharded SPADE on cuda:0 over a gloo TorchHostComm
+Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (torch.distributed, gloo).
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "spark-fsm_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def main():
+    mode, out = sys.argv[1], sys.argv[2]
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    import spark_fsm_amd as fsm
+    from spark_fsm_amd import dist as fdist
+    hc = fdist.TorchHostComm()
+    res = {"rank": rank, "world": world}
+    if mode == "selftest":
+        fdist.selftest(world, rank, host_comm=hc)
+        res["ok"] = True
+    elif mode == "spade":
+        from tools import gen
+        D, sup = int(sys.argv[3]), float(sys.argv[4])
+        ds = gen.quest(D, seed=int(sys.argv[5]) if len(sys.argv) > 5 else 1)
+        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc) as eng:
+            db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+            pats, meta = eng.spade(db, sup)
+            st = eng.stats()
+            db.free()
+        res.update(patterns=sorted(pats), minsup=meta["minsup"], joins=st["joins"], classes=st["classes"])
+    with open(out, "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

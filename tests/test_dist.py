@@ -1,0 +1,83 @@
+"""N > 1 plumbing on the CPU: the shard plan the engine uses for first-level
+prefix classes, and the host-callback collectives (all-reduce, ragged
+all-gather) between world_size-2 gloo processes through libfsm's own
+fsm_comm_selftest.  The sharded mining itself runs on the GPU in
+tests/test_parity_gpu.py::test_sharded_spade_two_ranks."""
+import json
+import os
+import random
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "dist_worker.py")
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(world, args, tmp_path, timeout=300):
+    """Start `world` worker processes (gloo rendezvous on 127.0.0.1); return their JSON results."""
+    port = free_port()
+    procs, outs = [], []
+    for r in range(world):
+        out = str(tmp_path / ("rank%d.json" % r))
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, WORKER] + [args[0], out] + list(args[1:]), env=env))
+        outs.append(out)
+    try:
+        codes = [p.wait(timeout=timeout) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert codes == [0] * world, codes
+    res = []
+    for o in outs:
+        with open(o) as f:
+            res.append(json.load(f))
+    return res
+
+
+def test_shard_plan_is_a_balanced_partition():
+    from spark_fsm_amd import shard_plan
+    rng = random.Random(5)
+    for _ in range(50):
+        n = rng.randint(0, 300)
+        vol = [rng.choice([1, 10, 100, 5000]) * rng.randint(1, 9) for _ in range(n)]
+        for N in (1, 2, 3, 8):
+            own = shard_plan(vol, N)
+            assert len(own) == n and all(0 <= o < N for o in own)
+            assert (own == shard_plan(vol, N)).all()  # deterministic: every rank computes the same plan
+            load = np.bincount(own, weights=np.array(vol, dtype=float), minlength=N) if n else np.zeros(N)
+            if n:
+                # LPT: the heaviest rank carries at most the mean plus one unit
+                assert load.max() <= sum(vol) / N + max(vol) + 1e-9
+
+
+def test_shard_plan_largest_first():
+    from spark_fsm_amd import shard_plan
+    assert list(shard_plan([5, 3, 9, 1, 1, 7], 3)) == [2, 2, 0, 1, 1, 1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_comm_collectives_gloo(world, tmp_path):
+    res = run_ranks(world, ["selftest"], tmp_path, timeout=180)
+    assert [r["rank"] for r in res] == list(range(world)) and all(r["ok"] for r in res)
+
+
+def test_selftest_rejects_single_rank():
+    import ctypes
+    from spark_fsm_amd import _lib
+    L = _lib.load()
+    o = _lib.Opts()
+    o.nranks = 1
+    assert L.fsm_comm_selftest(ctypes.byref(o)) == _lib.FSM_EINVAL

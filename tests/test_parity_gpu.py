@@ -280,3 +280,28 @@ def test_root_f2_paths_agree(eng, path, monkeypatch):
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
     pats, meta, st = gpu_spade(eng, None, 0.003, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
+
+
+# ------------------------------------------------------ sharded (N > 1)
+@pytest.mark.parametrize("world,D,sup,ref", [(2, 20000, 0.003, "oracle"), (3, 20000, 0.003, "oracle"),
+                                             (2, 200000, 0.002, "gpu1")])
+def test_sharded_spade_two_ranks(eng, world, D, sup, ref, tmp_path):
+    """The sharded SPADE path (F1 all-reduce, root rows split over ranks,
+    frequent pairs all-gathered, first-level classes by shard plan, patterns
+    all-gathered) with `world` ranks on this one GPU over gloo host
+    collectives: every rank returns the complete, single-rank result."""
+    from test_dist import run_ranks
+    from tools import gen
+    res = run_ranks(world, ["spade", str(D), str(sup), "1"], tmp_path, timeout=110)
+    ds = gen.quest(D, seed=1)
+    if ref == "oracle":
+        from oracle import oracle
+        o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
+        exp, joins = o["patterns"], o["joins"]
+    else:
+        pats, _, st = gpu_spade(eng, None, sup, tokens=ds)
+        exp, joins = pats, st["joins"]
+    for r in res:
+        assert canon(r["patterns"]) == exp
+        assert r["joins"] == joins
+    assert sum(1 for _ in exp) > 100
