@@ -81,3 +81,13 @@ def test_selftest_rejects_single_rank():
     o = _lib.Opts()
     o.nranks = 1
     assert L.fsm_comm_selftest(ctypes.byref(o)) == _lib.FSM_EINVAL
+
+
+def test_rccl_unique_id():
+    """librccl is dlopen'ed lazily; ncclGetUniqueId needs no GPU."""
+    from spark_fsm_amd import FsmError, comm_unique_id
+    try:
+        uid = comm_unique_id()
+    except FsmError as e:  # pragma: no cover - image without librccl
+        pytest.skip(str(e))
+    assert isinstance(uid, bytes) and len(uid) == 128 and any(uid)
