@@ -24,6 +24,20 @@ for p in (ROOT, os.path.join(ROOT, "spark-fsm_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
+PMC_FILE = "profiles/pmc_latest.json"  # tools/pmc_summary.py output of the committed rocprofv3 --pmc passes
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per step of `kernel` from the committed PMC summary:
+    2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: on gfx950 FETCH_SIZE counts
+    half the bytes of wide reads), summed over the kernel's launches in one step."""
+    try:
+        with open(os.path.join(ROOT, PMC_FILE)) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+        return 2 * k["FETCH_SIZE_bytes_per_step"] + k["WRITE_SIZE_bytes_per_step"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_model():
@@ -108,8 +122,12 @@ def main():
         return
 
     value = joins_all / (ms / 1000.0)  # joins of all ranks (libfsm sums them) / slowest rank
-    count_ms = st["ms_count_kernel"]
-    achieved = (st["bytes_count_alg"] / 1e9) / (count_ms / 1000.0) if count_ms > 0 else 0.0
+    # roofline of the dominant kernel: algorithmic bytes / its device time (HIP
+    # events on libfsm's stream, summed over the launches of the last step)
+    ks = eng.kernel_stats()
+    dom = max(ks, key=lambda k: k["ms"])
+    achieved = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
+    traffic = pmc_traffic(dom["name"])
     line = {
         "metric": "id-list joins/sec + end-to-end SPADE mine time, Quest D1M minsup 0.1%",
         "value": value,
@@ -127,15 +145,18 @@ def main():
             args.sequences, args.seed, args.support), "parallelism": "single GPU" if world == 1 else
             "prefix classes sharded over %d GPUs" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_count (class pair-count)",
-                     "kernel_ms_per_step": count_ms, "kernel_bytes_per_step": st["bytes_count_alg"]},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": dom["name"], "launches_per_step": dom["launches"],
+                     "kernel_ms_per_step": dom["ms"], "alg_bytes_per_step": dom["alg_bytes"],
+                     "traffic_source": PMC_FILE if traffic is not None else None},
         "extra": {"mine_ms": ms, "joins": joins_all, "patterns": meta["n"], "minsup": meta["minsup"],
                   "classes": st["classes"], "batches": st["batches"], "entries": st["entries"],
                   "ms_f1": st["ms_f1"], "ms_f2_root": st["ms_f2"], "ms_lattice": st["ms_lattice"],
-                  "ms_emit_kernel": st["ms_emit_kernel"], "ms_flatten": prep["ms_flatten"],
-                  "ms_upload": prep["ms_upload"],
-                  "join_equiv_GBps": (st["bytes_join_equiv"] / 1e9) / (ms / 1000.0)},
+                  "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
+                  "join_equiv_GBps": (st["bytes_join_equiv"] / 1e9) / (ms / 1000.0),
+                  "kernels": sorted(({"name": k["name"], "launches": k["launches"], "ms": round(k["ms"], 4),
+                                      "GBps": round((k["alg_bytes"] / 1e9) / (k["ms"] / 1000.0), 1) if k["ms"] else 0}
+                                     for k in ks), key=lambda k: -k["ms"])},
     }
     if not args.no_cpu_baseline and world == 1:
         from oracle import oracle

@@ -128,6 +128,16 @@ typedef struct {
     int64_t bytes_count_alg;    /* count kernel algorithmic bytes: entries * (12 + 8W) */
 } fsm_stats;
 
+/* Per-kernel device time of the last fsm_*_mine call (HIP events on the
+ * context's stream) with the kernel's algorithmic bytes: the
+ * numbers bench.py's roofline is computed from. */
+typedef struct {
+    char name[40];
+    int64_t launches;
+    int64_t alg_bytes;          /* algorithmic HBM bytes over all launches */
+    double ms;                  /* summed device time over all launches */
+} fsm_kernel_stat;
+
 int fsm_abi_version(void);
 /* RCCL unique id for fsm_opts.unique_id (call on rank 0, broadcast the bytes). */
 int fsm_comm_unique_id(uint8_t out[128]);
@@ -144,6 +154,8 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out);
 void fsm_ctx_destroy(fsm_ctx* ctx);
 const char* fsm_last_error(const fsm_ctx* ctx);
 int fsm_get_stats(const fsm_ctx* ctx, fsm_stats* out);
+/* Copies up to max entries; *n = number available. */
+int fsm_get_kernel_stats(const fsm_ctx* ctx, fsm_kernel_stat* out, int32_t max, int32_t* n);
 
 /* Flatten an SPMF-format dataset (one line per sequence id, as produced by
  * SPMFHandler.sequence2SPMF) once and upload it to HBM.  mode selects the

@@ -4,6 +4,8 @@
 #include <map>
 #include <mutex>
 
+#include <cstdio>
+
 #include "device_util.h"
 
 namespace fsm {
@@ -147,6 +149,53 @@ void check_launch(const char* what, hipStream_t s, const char* file, int line) {
     if (e != hipSuccess)
         throw Error(FSM_EDEVICE, std::string("kernel ") + what + ": " + hipGetErrorString(e) + " (" + file + ":" +
                                      std::to_string(line) + ")");
+}
+
+size_t KernelClock::begin(const char* name) {
+    size_t idx = recs.size();
+    for (size_t k = 0; k < recs.size(); ++k)
+        if (recs[k].name == name) idx = k;
+    if (idx == recs.size()) recs.push_back(Rec{name, {}, 0});
+    hipEvent_t a, b;
+    FSM_HIP(hipEventCreate(&a));
+    if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        throw Error(FSM_EDEVICE, "hipEventCreate failed");
+    }
+    recs[idx].ev.push_back({a, b});
+    FSM_HIP(hipEventRecord(a, s));
+    return idx;
+}
+
+void KernelClock::end(size_t idx, int64_t alg_bytes) {
+    FSM_HIP(hipEventRecord(recs[idx].ev.back().second, s));
+    recs[idx].bytes += alg_bytes;
+}
+
+void KernelClock::finish(std::vector<fsm_kernel_stat>& out) {
+    FSM_HIP(hipStreamSynchronize(s));
+    out.clear();
+    for (auto& r : recs) {
+        fsm_kernel_stat k{};
+        std::snprintf(k.name, sizeof(k.name), "%s", r.name.c_str());
+        k.launches = int64_t(r.ev.size());
+        k.alg_bytes = r.bytes;
+        for (auto& e : r.ev) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) k.ms += ms;
+        }
+        out.push_back(k);
+    }
+    release();
+}
+
+void KernelClock::release() {
+    for (auto& r : recs)
+        for (auto& e : r.ev) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+    recs.clear();
 }
 
 }  // namespace fsm

@@ -145,6 +145,13 @@ void fsm_ctx_destroy(fsm_ctx* ctx) {
     delete ctx;
 }
 
+int fsm_get_kernel_stats(const fsm_ctx* ctx, fsm_kernel_stat* out, int32_t max, int32_t* n) {
+    if (!ctx || !n || max < 0 || (max > 0 && !out)) return FSM_EINVAL;
+    *n = int32_t(ctx->kstats.size());
+    for (int32_t k = 0; k < max && k < *n; ++k) out[k] = ctx->kstats[size_t(k)];
+    return FSM_OK;
+}
+
 const char* fsm_last_error(const fsm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 int fsm_get_stats(const fsm_ctx* ctx, fsm_stats* out) {

@@ -38,6 +38,27 @@ inline double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
+// Per-kernel timing with HIP events on one stream: begin() before a launch,
+// end() after it with the launch's algorithmic bytes; finish() folds the
+// events into fsm_kernel_stat rows (summed per kernel name).
+struct KernelClock {
+    struct Rec {
+        std::string name;
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+        int64_t bytes = 0;
+    };
+    hipStream_t s = nullptr;
+    std::vector<Rec> recs;
+    explicit KernelClock(hipStream_t st) : s(st) {}
+    KernelClock(const KernelClock&) = delete;
+    KernelClock& operator=(const KernelClock&) = delete;
+    ~KernelClock() { release(); }
+    size_t begin(const char* name);
+    void end(size_t idx, int64_t alg_bytes);
+    void finish(std::vector<fsm_kernel_stat>& out);
+    void release();
+};
+
 // Device memory pool: hipMalloc/hipFree synchronize and cost milliseconds for
 // the multi-hundred-MB frontier slabs, so freed blocks are cached per size
 // class (power of two >= 4 KiB) and reused by later batches and later calls.
@@ -125,6 +146,7 @@ struct fsm_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     fsm::Comm* comm = nullptr;  // nranks > 1 (owned)
+    std::vector<fsm_kernel_stat> kstats;  // of the last mine call
 };
 
 struct fsm_db {

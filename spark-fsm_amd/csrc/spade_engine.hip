@@ -489,14 +489,14 @@ struct Miner {
     uint32_t minsup;
     uint64_t budget;
     std::vector<PNode> nodes;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_count, ev_emit;
+    KernelClock* clk = nullptr;
     // sharded mining (nranks > 1): this rank counts the root rows of ranks
     // [slice_lo, slice_hi) and mines the first-level classes shard_plan gives it
     Comm* comm = nullptr;
     uint32_t slice_lo = 0, slice_hi = kNone;
     size_t n_shared = 0;  // pattern nodes every rank holds (root + its frequent children)
 
-    uint64_t entry_bytes() const { return 12ull + 8ull * uint64_t(W); }
+    uint64_t entry_bytes() const { return 16ull + 8ull * uint64_t(W); }  // cid, mem, lohi, pos, mask
 
     // pageable H2D copies are staged before hipMemcpyAsync returns; callers keep
     // the host vectors alive until the next synchronization anyway.
@@ -505,12 +505,6 @@ struct Miner {
         if (!h.empty()) FSM_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
     }
 
-    std::pair<hipEvent_t, hipEvent_t> ev_pair() {
-        hipEvent_t a, b;
-        FSM_HIP(hipEventCreate(&a));
-        FSM_HIP(hipEventCreate(&b));
-        return {a, b};
-    }
 
     // class descriptors (counter matrix offsets, member bases) of a batch
     void prepare(Batch& b) {
@@ -603,9 +597,12 @@ struct Miner {
 #define FSM_RP_HIST(WW)                                                                                    \
     hipLaunchKernelGGL(k_rootpair_hist<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
                        sp.mask, m.D, nb, chunk, mlo, mhi, blkhist.as<uint32_t>(), total.as<uint32_t>())
+        const int64_t slab_bytes = int64_t(E0) * int64_t(16 + 8 * W);
+        size_t tk = clk->begin("k_rootpair_hist");
         FSM_W_DISPATCH(W, FSM_RP_HIST)
 #undef FSM_RP_HIST
         FSM_LAUNCHED("k_rootpair_hist", s);
+        clk->end(tk, slab_bytes);
         scan_exclusive(total.as<uint32_t>(), boff.as<uint64_t>(), nb, s);
         uint64_t npairs = 0;
         FSM_HIP(hipMemcpyAsync(&npairs, boff.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
@@ -617,12 +614,16 @@ struct Miner {
                        sp.mask, m.D, nb, chunk, mlo, mhi, blkhist.as<uint32_t>(), boff.as<uint64_t>(),            \
                        gcur.as<uint32_t>(), \
                        keys.as<uint16_t>())
+        tk = clk->begin("k_rootpair_scatter");
         FSM_W_DISPATCH(W, FSM_RP_SCAT)
 #undef FSM_RP_SCAT
         FSM_LAUNCHED("k_rootpair_scatter", s);
+        clk->end(tk, slab_bytes + int64_t(npairs) * 2);
+        tk = clk->begin("k_bucket_count");
         hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(1024), 0, s, keys.as<uint16_t>(), boff.as<uint64_t>(), K,
                            cnt);
         FSM_LAUNCHED("k_bucket_count", s);
+        clk->end(tk, int64_t(npairs) * 2 + int64_t(K) * 4);
         FSM_HIP(hipStreamSynchronize(s));  // keys / blkhist released on return
         return true;
     }
@@ -642,8 +643,6 @@ struct Miner {
         st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
         DevBuf cnt(std::max<uint64_t>(b.n_cnt, 1) * 4);
         if (b.E) {
-            auto ev = ev_pair();
-            FSM_HIP(hipEventRecord(ev.first, s));
             const bool done = b.root && !root_atomic() && root_bucket_count(b, cnt.as<uint32_t>());
             if (!done) {
                 FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
@@ -652,12 +651,12 @@ struct Miner {
     hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + kChunk - 1) / kChunk)), dim3(kBlock), 0, s,   \
                        uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
                        member_lo(b), member_hi(b), cnt.as<uint32_t>())
+                const size_t tk = clk->begin("k_count");
                 FSM_W_DISPATCH(W, FSM_COUNT)
 #undef FSM_COUNT
                 FSM_LAUNCHED("k_count", s);
+                clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));
             }
-            FSM_HIP(hipEventRecord(ev.second, s));
-            ev_count.push_back(ev);
             st.count_launches += 1;
         }
         // member rows of the counter matrix
@@ -673,9 +672,11 @@ struct Miner {
         upload(d_rows, std::vector<DRow>(rows.begin() + rlo, rows.begin() + rhi));
         const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
         if (nrows) {
+            const size_t tk = clk->begin("k_freq_count");
             hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
                                b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
             FSM_LAUNCHED("k_freq_count", s);
+            clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4));
         }
         scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
         uint64_t nfreq = 0;
@@ -684,10 +685,13 @@ struct Miner {
         std::vector<FreqRec> recs(nfreq);
         if (nfreq) {
             DevBuf d_recs(nfreq * sizeof(FreqRec));
+            const size_t tk = clk->begin("k_freq_write");
             hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
                                b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
                                d_recs.as<FreqRec>());
             FSM_LAUNCHED("k_freq_write", s);
+            clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
+                                 nfreq * sizeof(FreqRec)));
             FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nfreq * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
             FSM_HIP(hipStreamSynchronize(s));
         }
@@ -810,8 +814,6 @@ struct Miner {
         ctx->stats.bytes_streamed += int64_t((total + 2 * b.E) * entry_bytes());
         uint64_t written = 0;
         if (b.E) {
-            auto ev = ev_pair();
-            FSM_HIP(hipEventRecord(ev.first, s));
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
             const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 1u << 20));
@@ -822,16 +824,18 @@ struct Miner {
                        off.as<uint64_t>(), op)
 #define FSM_EMIT_COUNT(WW) FSM_EMIT(WW, false)
 #define FSM_EMIT_WRITE(WW) FSM_EMIT(WW, true)
+            size_t tk = clk->begin("k_emit<count>");
             FSM_W_DISPATCH(W, FSM_EMIT_COUNT)
             FSM_LAUNCHED("k_emit<count>", s);
+            clk->end(tk, int64_t(b.E * (entry_bytes() + 4)));
             scan_exclusive(ncnt.as<uint32_t>(), off.as<uint64_t>(), b.E, s);
+            tk = clk->begin("k_emit<write>");
             FSM_W_DISPATCH(W, FSM_EMIT_WRITE)
             FSM_LAUNCHED("k_emit<write>", s);
+            clk->end(tk, int64_t(b.E * (entry_bytes() + 8) + total * entry_bytes()));
 #undef FSM_EMIT_WRITE
 #undef FSM_EMIT_COUNT
 #undef FSM_EMIT
-            FSM_HIP(hipEventRecord(ev.second, s));
-            ev_emit.push_back(ev);
             FSM_HIP(hipMemcpyAsync(&written, off.as<uint64_t>() + b.E, 8, hipMemcpyDeviceToHost, s));
         }
         FSM_HIP(hipStreamSynchronize(s));
@@ -851,10 +855,12 @@ struct Miner {
         upload(d_rank, rank);
         FSM_HIP(hipMemsetAsync(flag.p, 0, 4, s));
         if (r1 > r0) {
+            const size_t tk = clk->begin("k_root_count");
             hipLaunchKernelGGL(k_root_count, dim3(unsigned((r1 - r0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                                db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), d_rank.as<uint32_t>(), r0, r1,
                                rcnt.as<uint32_t>(), flag.as<uint32_t>());
             FSM_LAUNCHED("k_root_count", s);
+            clk->end(tk, int64_t((r1 - r0) * 12 + uint64_t(db->E) * 8));
         }
         scan_exclusive(rcnt.as<uint32_t>(), roff.as<uint64_t>(), r1 - r0, s);
         uint64_t E0 = 0;
@@ -870,6 +876,7 @@ struct Miner {
         if (r1 > r0) {
             const SlabPtrs op = root.slab.ptrs();
             const unsigned grid = unsigned(((r1 - r0) * 64 + kBlock - 1) / kBlock);
+            const size_t tk = clk->begin("k_root_write");
 #define FSM_ROOTW(WW)                                                                                         \
     hipLaunchKernelGGL(k_root_write<WW>, dim3(grid), dim3(kBlock), 0, s, db->row_off.as<uint32_t>(),           \
                        db->item.as<uint32_t>(), db->mask.as<uint64_t>(), d_rank.as<uint32_t>(), r0, r1,       \
@@ -877,6 +884,7 @@ struct Miner {
             FSM_W_DISPATCH(W, FSM_ROOTW)
 #undef FSM_ROOTW
             FSM_LAUNCHED("k_root_write", s);
+            clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W)) + E0 * (16 + 8 * uint64_t(W))));
         }
         ClassMeta m;
         const uint32_t F = uint32_t(freq_items.size());
@@ -894,17 +902,6 @@ struct Miner {
         FSM_HIP(hipStreamSynchronize(s));
     }
 
-    double elapsed(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
-        double tot = 0;
-        for (auto& p : v) {
-            float ms = 0;
-            if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) tot += ms;
-            (void)hipEventDestroy(p.first);
-            (void)hipEventDestroy(p.second);
-        }
-        v.clear();
-        return tot;
-    }
 };
 
 template <class T> void copy_out(T*& dst, const std::vector<T>& src) {
@@ -1004,7 +1001,9 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     const double t0 = now_ms();
     SpadeDevDB* d = db->spade_dev;
     const int64_t total = db->spade.total;
-    Miner mn{ctx, d, ctx->stream, d->W, 1, 0, {}, {}, {}};
+    Miner mn{ctx, d, ctx->stream, d->W, 1, 0, {}};
+    KernelClock clock(ctx->stream);
+    mn.clk = &clock;
     mn.comm = ctx->comm;
     Comm* comm = ctx->comm;
     ctx->stats.mask_words = d->W;
@@ -1027,9 +1026,11 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         if (e1 > e0) {
             const int use_lds = d->U <= 16384;
             const unsigned grid = unsigned(std::min<uint64_t>((e1 - e0 + kBlock - 1) / kBlock, use_lds ? 1024 : 8192));
+            const size_t tk = clock.begin("k_f1");
             hipLaunchKernelGGL(k_f1, dim3(grid), dim3(kBlock), use_lds ? size_t(d->U) * 4 : 0, ctx->stream,
                                d->item.as<uint32_t>(), e0, e1, d_f1.as<uint32_t>(), uint32_t(d->U), use_lds);
             FSM_LAUNCHED("k_f1", ctx->stream);
+            clock.end(tk, int64_t((e1 - e0) * 4 + uint64_t(d->U) * 4));
         }
         if (comm) comm->allreduce_u32(d_f1.as<uint32_t>(), size_t(d->U), ctx->stream);
         if (d->U) FSM_HIP(hipMemcpyAsync(f1.data(), d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -1090,8 +1091,12 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     }
     FSM_HIP(hipStreamSynchronize(ctx->stream));
     ctx->stats.ms_lattice = now_ms() - t2;
-    ctx->stats.ms_count_kernel = mn.elapsed(mn.ev_count);
-    ctx->stats.ms_emit_kernel = mn.elapsed(mn.ev_emit);
+    clock.finish(ctx->kstats);
+    for (const fsm_kernel_stat& k : ctx->kstats) {
+        const std::string nm = k.name;
+        if (nm == "k_count" || nm.rfind("k_rootpair", 0) == 0 || nm == "k_bucket_count") ctx->stats.ms_count_kernel += k.ms;
+        if (nm.rfind("k_emit", 0) == 0) ctx->stats.ms_emit_kernel += k.ms;
+    }
 
     // ---- output CSR in discovery order (the reference's order is discovery order too);
     // sharded: rank 0 holds the shared root levels, every rank its own classes

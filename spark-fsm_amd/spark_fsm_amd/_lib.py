@@ -80,6 +80,11 @@ class Rules(ctypes.Structure):
     ]
 
 
+class KernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 40), ("launches", ctypes.c_int64), ("alg_bytes", ctypes.c_int64),
+                ("ms", ctypes.c_double)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "joins", "patterns", "classes", "batches", "entries", "bytes_join_equiv",
@@ -95,7 +100,7 @@ class Stats(ctypes.Structure):
 # Every symbol declared in include/fsm.h (checked by tests/test_abi.py).
 EXPORTS = [
     "fsm_abi_version", "fsm_comm_unique_id", "fsm_shard_plan", "fsm_comm_selftest", "fsm_ctx_create", "fsm_ctx_destroy",
-    "fsm_last_error", "fsm_get_stats", "fsm_db_from_spmf", "fsm_db_from_tokens",
+    "fsm_last_error", "fsm_get_stats", "fsm_get_kernel_stats", "fsm_db_from_spmf", "fsm_db_from_tokens",
     "fsm_db_free", "fsm_spade_mine", "fsm_patterns_free", "fsm_tsr_mine", "fsm_rules_free",
 ]
 
@@ -125,6 +130,7 @@ def load():
     L.fsm_last_error.argtypes = [vp]
     L.fsm_last_error.restype = ctypes.c_char_p
     L.fsm_get_stats.argtypes = [vp, P(Stats)]
+    L.fsm_get_kernel_stats.argtypes = [vp, P(KernelStat), ctypes.c_int32, P(ctypes.c_int32)]
     L.fsm_db_from_spmf.argtypes = [vp, ctypes.c_int32, P(ctypes.c_int32), P(ctypes.c_char_p),
                                    P(ctypes.c_int64), ctypes.c_int64, P(vp)]
     L.fsm_db_from_tokens.argtypes = [vp, ctypes.c_int32, P(ctypes.c_int32), P(ctypes.c_int64),

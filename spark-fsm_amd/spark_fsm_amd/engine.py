@@ -117,6 +117,15 @@ class Engine:
             self._L.fsm_rules_free(out)
         return rules, meta
 
+    def kernel_stats(self):
+        """[{name, launches, alg_bytes, ms}] of the last mine call (device time, HIP events)."""
+        n = ctypes.c_int32()
+        check(self._L.fsm_get_kernel_stats(self._ctx, None, 0, ctypes.byref(n)), self._ctx)
+        arr = (_lib.KernelStat * max(n.value, 1))()
+        check(self._L.fsm_get_kernel_stats(self._ctx, arr, n.value, ctypes.byref(n)), self._ctx)
+        return [{"name": k.name.decode(), "launches": k.launches, "alg_bytes": k.alg_bytes, "ms": k.ms}
+                for k in arr[:n.value]]
+
     def stats(self):
         st = _lib.Stats()
         check(self._L.fsm_get_stats(self._ctx, ctypes.byref(st)), self._ctx)

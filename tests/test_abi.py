@@ -93,13 +93,14 @@ def test_struct_layout_matches_c_compiler(tmp_path):
     """sizeof / offsetof of every ABI struct as gcc sees include/fsm.h == the ctypes mirror."""
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "fsm.h"\nint main(void){\n'
-                   'printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(fsm_opts), sizeof(fsm_patterns),'
-                   ' sizeof(fsm_rules), sizeof(fsm_stats), sizeof(fsm_host_comm),'
+                   'printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(fsm_opts), sizeof(fsm_patterns),'
+                   ' sizeof(fsm_rules), sizeof(fsm_stats), sizeof(fsm_host_comm), sizeof(fsm_kernel_stat),'
                    ' offsetof(fsm_opts, host_comm), offsetof(fsm_stats, bytes_count_alg));\nreturn 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     exp = [ctypes.sizeof(_lib.Opts), ctypes.sizeof(_lib.Patterns), ctypes.sizeof(_lib.Rules),
-           ctypes.sizeof(_lib.Stats), ctypes.sizeof(_lib.HostComm), _lib.Opts.host_comm.offset,
+           ctypes.sizeof(_lib.Stats), ctypes.sizeof(_lib.HostComm), ctypes.sizeof(_lib.KernelStat),
+           _lib.Opts.host_comm.offset,
            _lib.Stats.bytes_count_alg.offset]
     assert got == exp

@@ -1,0 +1,62 @@
+"""Fold rocprofv3 --pmc CSV passes into profiles/pmc_latest.json.
+
+Usage (each pass is its own rocprofv3 run of ONE bench step, see tools/profile.sh):
+    python tools/pmc_summary.py OUT.json DIR_FETCH DIR_WRITE [more dirs...]
+
+For every kernel (named as libfsm's fsm_get_kernel_stats names it) the JSON has
+the counter totals over the step's dispatches, in bytes (rocprofv3 reports
+FETCH_SIZE / WRITE_SIZE in KiB), plus the dispatch count.  bench.py reads it
+for `roofline.traffic` = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md,
+HBM [CDNA4]: gfx950 FETCH_SIZE counts half of the bytes of wide reads).
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+
+def kernel_name(demangled):
+    m = re.search(r"\b(k_\w+)(<([^>]*)>)?", demangled)
+    if not m:
+        return demangled.split("(")[0][:40]
+    base, targs = m.group(1), m.group(3) or ""
+    if base == "k_emit":
+        return "k_emit<write>" if "true" in targs else "k_emit<count>"
+    return base
+
+
+def read_dir(d):
+    rows = []
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        with open(path) as f:
+            rows.extend(csv.DictReader(f))
+    return rows
+
+
+def main():
+    out, dirs = sys.argv[1], sys.argv[2:]
+    kernels = {}
+    for d in dirs:
+        for r in read_dir(d):
+            name = kernel_name(r.get("Kernel_Name", ""))
+            ctr = r.get("Counter_Name", "")
+            val = float(r.get("Counter_Value", 0) or 0)
+            k = kernels.setdefault(name, {"dispatches": {}})
+            if ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+                k[ctr + "_bytes_per_step"] = k.get(ctr + "_bytes_per_step", 0) + int(val * 1024)
+            else:
+                k[ctr] = k.get(ctr, 0) + val
+            k["dispatches"][r.get("Dispatch_Id", "")] = 1
+    for k in kernels.values():
+        k["dispatches"] = len(k["dispatches"])
+    with open(out, "w") as f:
+        json.dump({"source": "rocprofv3 --pmc, one bench.py step per pass: " + " ".join(dirs),
+                   "note": "bytes summed over the step's dispatches; FETCH_SIZE uncorrected here",
+                   "kernels": kernels}, f, indent=1, sort_keys=True)
+    print(json.dumps({n: {c: v for c, v in k.items() if c != "dispatches"} for n, k in kernels.items()})[:2000])
+
+
+if __name__ == "__main__":
+    main()
