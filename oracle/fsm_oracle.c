@@ -827,7 +827,16 @@ static void tsr_expand_right(tsr_ctx* c, rule* r) {
 
 int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
                int32_t k, double minconf, oracle_rules** out, char* err, int errlen) {
+    return oracle_tsr_timed(sids, lines, lens, n, k, minconf, 0.0, out, err, errlen);
+}
+
+/* time_limit_s > 0 stops after that many seconds of mining (bounded CPU
+ * baseline): the result is then partial, complete = 0. */
+int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
+                     int32_t k, double minconf, double time_limit_s, oracle_rules** out, char* err, int errlen) {
     *out = NULL;
+    int complete = 1;
+    double t_start = 0.0;
     if (k < 1) {
         set_err(err, errlen, "TSR: k must be >= 1 (got %d)", k);
         return -1;
@@ -944,7 +953,11 @@ int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* len
         c.tids_of = calloc((size_t)(nu ? nu : 1), sizeof(i32vec));
 
         /* Pair phase: i ascending, j > i; IJ then JI. */
-        for (int64_t i = 0; i < nu; i++) {
+        t_start = mono_s();
+        const double deadline = time_limit_s > 0 ? t_start + time_limit_s : 0.0;
+        int64_t pairs = 0;
+        for (int64_t i = 0; i < nu && complete; i++) {
+            if (deadline > 0 && mono_s() > deadline) { complete = 0; break; }
             const tidpos* fi = c.first[i];
             const tidpos* li = c.last[i];
             if (fi->n < c.minsup) continue;
@@ -952,6 +965,7 @@ int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* len
                 const tidpos* fj = c.first[j];
                 const tidpos* lj = c.last[j];
                 if (fj->n < c.minsup) continue;
+                pairs++;
                 int64_t a = 0, b = 0, nij = 0, nji = 0;
                 int32_t* tij = malloc((size_t)(fi->n < fj->n ? fi->n : fj->n) * sizeof(int32_t) + 4);
                 int32_t* tji = malloc((size_t)(fi->n < fj->n ? fi->n : fj->n) * sizeof(int32_t) + 4);
@@ -991,7 +1005,8 @@ int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* len
             }
         }
         /* Expansion loop */
-        while (c.cand.n > 0) {
+        while (complete && c.cand.n > 0) {
+            if (deadline > 0 && mono_s() > deadline) { complete = 0; break; }
             rule* r = heap_pop(&c.cand);
             r->in_cand = 0;
             if (r->sup < c.minsup) break;
@@ -1010,6 +1025,9 @@ int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* len
         o->total = n;
         o->expansions = c.expansions;
         o->final_minsup = c.minsup;
+        o->complete = complete;
+        o->seconds = mono_s() - t_start;
+        o->pairs = pairs;
         o->support = malloc((size_t)(nr ? nr : 1) * sizeof(int32_t));
         o->confidence = malloc((size_t)(nr ? nr : 1) * sizeof(double));
         o->ante_off = malloc((size_t)(nr + 1) * sizeof(int64_t));

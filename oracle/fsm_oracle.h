@@ -54,6 +54,9 @@ typedef struct {
     int64_t  total;      /* number of input sequences */
     int64_t  expansions; /* expandL/expandR calls */
     int32_t  final_minsup;
+    int32_t  complete;   /* 0 if a time limit stopped the mining early */
+    double   seconds;    /* wall time of the pair phase + expansions (after parse and Vertical build) */
+    int64_t  pairs;      /* item pairs (i < j, both >= minsup) evaluated in the pair phase */
 } oracle_rules;
 
 /* Returns 0 on success; on failure returns nonzero and writes a message to err. */
@@ -65,6 +68,8 @@ int oracle_spade_tokens(const int64_t* seq_off, const int64_t* tokens, int64_t n
 
 int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
                int32_t k, double minconf, oracle_rules** out, char* err, int errlen);
+int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
+                     int32_t k, double minconf, double time_limit_s, oracle_rules** out, char* err, int errlen);
 void oracle_rules_free(oracle_rules* r);
 
 /* Definitional point checks over a token stream (-1 / -2 separators). */

@@ -50,6 +50,9 @@ class _Rules(ctypes.Structure):
         ("total", ctypes.c_int64),
         ("expansions", ctypes.c_int64),
         ("final_minsup", ctypes.c_int32),
+        ("complete", ctypes.c_int32),
+        ("seconds", ctypes.c_double),
+        ("pairs", ctypes.c_int64),
     ]
 
 
@@ -88,6 +91,11 @@ def lib():
             ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
             ctypes.POINTER(ctypes.POINTER(_Rules)), ctypes.c_char_p, ctypes.c_int]
         L.oracle_tsr.restype = ctypes.c_int
+        L.oracle_tsr_timed.argtypes = [
+            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_char_p),
+            ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+            ctypes.POINTER(ctypes.POINTER(_Rules)), ctypes.c_char_p, ctypes.c_int]
+        L.oracle_tsr_timed.restype = ctypes.c_int
         L.oracle_rules_free.argtypes = [ctypes.POINTER(_Rules)]
         _lib = L
     return _lib
@@ -181,13 +189,15 @@ def spade(records, support):
     return res
 
 
-def tsr(records, k, minconf):
-    """TSR.extractRDDRules restated: records = [(sid, spmf_line)], sids = 0..N-1."""
+def tsr(records, k, minconf, time_limit_s=0.0):
+    """TSR.extractRDDRules restated: records = [(sid, spmf_line)], sids = 0..N-1.
+    time_limit_s > 0 bounds the mining time (CPU baseline): complete = False then."""
     L = lib()
     n, sids, lines, lens, _keep = _marshal(records)
     out = ctypes.POINTER(_Rules)()
     err = ctypes.create_string_buffer(512)
-    rc = L.oracle_tsr(sids, lines, lens, n, int(k), float(minconf), ctypes.byref(out), err, 512)
+    rc = L.oracle_tsr_timed(sids, lines, lens, n, int(k), float(minconf), float(time_limit_s), ctypes.byref(out),
+                            err, 512)
     if rc != 0:
         raise OracleError(err.value.decode())
     r = out.contents
@@ -198,6 +208,6 @@ def tsr(records, k, minconf):
         rules.append((x, y, r.support[i], r.confidence[i]))
     rules.sort(key=lambda t: (-t[2], t[0], t[1]))
     res = {"rules": rules, "total": r.total, "expansions": r.expansions,
-           "final_minsup": r.final_minsup}
+           "final_minsup": r.final_minsup, "complete": bool(r.complete), "seconds": r.seconds, "pairs": r.pairs}
     L.oracle_rules_free(out)
     return res

@@ -1,0 +1,134 @@
+"""Every BASELINE.json config on one GPU, next to the CPU restatement on the
+same host (the BASELINE.md table).  bench.py is the driver's one-line contract
+(config 3); this is the per-config sweep, run on the GPU box:
+
+    python tools/bench_configs.py [--only c2,c4] [--cpu-seconds 20] > gpurun_out/configs.jsonl
+
+One JSON line per config.  GPU: median of 3 timed fsm_*_mine calls after one
+warmup, DB resident in HBM.  CPU: oracle/fsm_oracle.c, 1 thread, same DB and
+parameters, bounded to --cpu-seconds (SPADE: joins/s over the completed part;
+TSR: a full run on the largest sequence prefix that completes in the bound,
+with the GPU timed on that same prefix as well).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "spark-fsm_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+CONFIGS = {
+    "c1": ("spade", "quest", dict(D=10000), 0.005),
+    "c2": ("spade", "quest", dict(D=100000), 0.005),
+    "c3": ("spade", "quest", dict(D=1000000), 0.001),
+    "c4": ("tsr", "kosarak", dict(D=990002), (1000, 0.5)),
+    "c5-bible": ("spade", "bible", dict(), 0.004),
+    "c5-sign": ("spade", "sign", dict(), 0.015),
+}
+
+
+def dataset(shape, kw):
+    from tools import gen
+    if shape == "quest":
+        return gen.quest(kw["D"], seed=1)
+    if shape == "kosarak":
+        return gen.kosarak(D=kw["D"], seed=1)
+    return getattr(gen, shape)(seed=1)
+
+
+def log(msg):
+    print("[configs %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+
+
+def time_gpu(fn, reps=3):
+    fn()  # warmup
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append((time.perf_counter() - t0) * 1000.0)
+    return statistics.median(ts), out
+
+
+def run_spade(eng, fsm, name, ds, sup, cpu_s):
+    from oracle import oracle
+    db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+    prep = eng.stats()
+    ms, (csr, meta) = time_gpu(lambda: eng.spade_csr(db, sup))
+    st = eng.stats()
+    ks = sorted(eng.kernel_stats(), key=lambda k: -k["ms"])[:4]
+    db.free()
+    log("%s: GPU %.2f ms; CPU restatement (bound %.0f s)" % (name, ms, cpu_s))
+    r = oracle.spade_tokens(ds.seq_off, ds.tokens, sup, time_limit_s=cpu_s, want_patterns=False)
+    return {"config": name, "algo": "SPADE", "dataset": ds.name, "sequences": len(ds), "minsup": sup,
+            "minsup_abs": meta["minsup"], "gpu_mine_ms": ms, "patterns": meta["n"], "joins": st["joins"],
+            "gpu_joins_per_s": st["joins"] / (ms / 1000.0), "mask_words": st["mask_words"],
+            "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
+            "top_kernels": [{"name": k["name"], "ms": round(k["ms"], 3),
+                             "GBps": round(k["alg_bytes"] / 1e9 / (k["ms"] / 1e3), 1) if k["ms"] else 0}
+                            for k in ks],
+            "cpu_1thr_joins_per_s": r["joins"] / r["seconds"], "cpu_complete": r["complete"],
+            "cpu_seconds": r["seconds"], "cpu_joins": r["joins"],
+            "speedup_joins_per_s": (st["joins"] / (ms / 1000.0)) / (r["joins"] / r["seconds"])}
+
+
+def run_tsr(eng, fsm, name, ds, params, cpu_s):
+    from oracle import oracle
+    k, mc = params
+    db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
+    prep = eng.stats()
+    ms, (rules, meta) = time_gpu(lambda: eng.tsr(db, k, mc), reps=3)
+    st = eng.stats()
+    ks = sorted(eng.kernel_stats(), key=lambda q: -q["ms"])[:4]
+    db.free()
+    # CPU: the largest prefix (halving from 200K) whose full run fits the bound
+    n = min(len(ds), 200000)
+    cpu = None
+    log("%s: GPU %.2f ms; CPU restatement on prefixes (bound %.0f s each)" % (name, ms, cpu_s))
+    while n >= 1000:
+        log("%s: CPU prefix %d" % (name, n))
+        sub = ds.head(n)
+        r = oracle.tsr(sub.records(), k, mc, time_limit_s=cpu_s)
+        if r["complete"]:
+            dbs = eng.db_from_tokens(sub.sids, sub.seq_off, sub.tokens, fsm.MODE_TSR)
+            gms, (grules, _) = time_gpu(lambda: eng.tsr(dbs, k, mc), reps=3)
+            dbs.free()
+            grules.sort(key=lambda t: (-t[2], t[0], t[1]))
+            cpu = {"cpu_prefix_sequences": n, "cpu_seconds": r["seconds"], "cpu_expansions": r["expansions"],
+                   "gpu_ms_on_prefix": gms, "prefix_rules_identical": grules == r["rules"],
+                   "speedup_on_prefix": r["seconds"] * 1000.0 / gms}
+            break
+        n //= 2
+    out = {"config": name, "algo": "TSR", "dataset": ds.name, "sequences": len(ds), "k": k, "minconf": mc,
+           "gpu_mine_ms": ms, "rules": len(rules), "final_minsup": meta["final_minsup"],
+           "expansions": st["expansions"], "ms_pair_phase": st["ms_f2"], "ms_expansions": st["ms_lattice"],
+           "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
+           "top_kernels": [{"name": q["name"], "ms": round(q["ms"], 3)} for q in ks]}
+    out.update(cpu or {"cpu": "no prefix >= 1000 sequences completed within the bound"})
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    args = ap.parse_args()
+    import torch  # noqa: F401  (one HIP runtime per process, see _lib.py)
+    import spark_fsm_amd as fsm
+    want = [c for c in args.only.split(",") if c] or list(CONFIGS)
+    with fsm.Engine(0) as eng:
+        for name in want:
+            algo, shape, kw, par = CONFIGS[name]
+            log("%s: generating %s" % (name, shape))
+            ds = dataset(shape, kw)
+            res = (run_spade if algo == "spade" else run_tsr)(eng, fsm, name, ds, par, args.cpu_seconds)
+            print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
