@@ -66,6 +66,24 @@ void* pool_alloc(size_t bytes, size_t* granted);
 void pool_free(void* p, size_t granted);
 void pool_trim();  // hipFree every cached block (fsm_ctx_destroy)
 
+// Mapped pinned host memory (kernels write results straight into it; the host
+// reads them after a stream sync, with no copy launch).
+struct PinnedBuf {
+    void* host = nullptr;
+    void* dev = nullptr;
+    explicit PinnedBuf(size_t bytes) {
+        if (hipHostMalloc(&host, bytes ? bytes : 16, hipHostMallocMapped) != hipSuccess)
+            throw Error(FSM_ENOMEM, "hipHostMalloc failed");
+        if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess) {
+            (void)hipHostFree(host);
+            throw Error(FSM_EDEVICE, "hipHostGetDevicePointer failed");
+        }
+    }
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { (void)hipHostFree(host); }
+};
+
 // Owning device allocation from the pool, RAII.
 struct DevBuf {
     void* p = nullptr;

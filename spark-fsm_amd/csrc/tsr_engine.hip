@@ -42,6 +42,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kMaxSide = 64;
+constexpr int kCollectBlocks = 32;
 
 __global__ __launch_bounds__(kBlock) void k_vcount(const uint32_t* __restrict__ item, uint64_t E,
                                                    uint32_t* __restrict__ cnt) {
@@ -142,49 +143,88 @@ __device__ __forceinline__ bool in_sorted(const uint32_t* s, uint32_t n, uint32_
     return false;
 }
 
+// expansion control block (device memory), reset by k_expand_collect
+struct ExpCtl {
+    uint32_t nx;     // |sids(X)| seen by this expansion
+    uint32_t nlist;  // items touched (list entries)
+    uint32_t nout;   // candidates kept
+    uint32_t done;   // collect blocks finished
+};
+
+// histogram bump (no returned value: the lanes' atomics stay in flight) that
+// also records the item the first time it is touched in this expansion, so the
+// collect pass visits only touched items
+__device__ __forceinline__ void bump(uint32_t* __restrict__ h, uint32_t c, uint32_t* __restrict__ seen,
+                                     uint32_t* __restrict__ list, ExpCtl* __restrict__ ctl) {
+    atomicAdd(&h[c], 1u);
+    if (__hip_atomic_load(&seen[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+        atomicExch(&seen[c], 1u) == 0u)
+        list[atomicAdd(&ctl->nlist, 1u)] = c;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), d, 64)));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = min(v, uint32_t(__shfl_xor(int(v), d, 64)));
+    return v;
+}
+
+// One wave per sid of the driver item (rows are up to thousands of items long
+// on Kosarak-shaped data: the lanes split the binary searches and the row
+// scans, so one long row does not serialize a thread).
 __global__ __launch_bounds__(kBlock) void k_expand(const Side side, const uint32_t* __restrict__ dsid, uint32_t nd,
                                                    const uint32_t* __restrict__ row_off,
                                                    const uint32_t* __restrict__ item,
                                                    const uint32_t* __restrict__ first,
                                                    const uint32_t* __restrict__ last, uint32_t* __restrict__ TL,
                                                    uint32_t* __restrict__ DL, uint32_t* __restrict__ TR,
-                                                   uint32_t* __restrict__ nX) {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+                                                   uint32_t* __restrict__ seen, uint32_t* __restrict__ list,
+                                                   ExpCtl* __restrict__ ctl) {
+    const uint32_t v = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (v >= nd) return;
+    const uint32_t lane = lane_id();
     const uint32_t s = dsid[v];
     const uint32_t rb = row_off[s], re = row_off[s + 1];
+    bool ok = true;
     uint32_t fX = 0;
-    for (uint32_t k = 0; k < side.nx; ++k) {
+    for (uint32_t k = lane; k < side.nx; k += 64) {
         const uint32_t q = row_find(item, rb, re, side.X[k]);
-        if (q >= re || item[q] != side.X[k]) return;  // s not in sids(X)
-        fX = max(fX, first[q]);
+        if (q >= re || item[q] != side.X[k]) ok = false;
+        else fX = max(fX, first[q]);
     }
-    atomicAdd(nX, 1u);
-    if (side.doL) {
-        // |sids(X u {c})| for candidate left extensions
+    if (__ballot(!ok)) return;  // s not in sids(X)
+    fX = wave_max(fX);
+    if (lane == 0) atomicAdd(&ctl->nx, 1u);
+    if (side.doL) {  // |sids(X u {c})| for candidate left extensions
         const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
-        for (uint32_t q = q0; q < re; ++q)
-            if (!in_sorted(side.Y, side.ny, item[q])) atomicAdd(&DL[item[q]], 1u);
+        for (uint32_t q = q0 + lane; q < re; q += 64)
+            if (!in_sorted(side.Y, side.ny, item[q])) bump(DL, item[q], seen, list, ctl);
     }
     uint32_t lY = 0xFFFFFFFFu;
-    for (uint32_t k = 0; k < side.ny; ++k) {
+    for (uint32_t k = lane; k < side.ny; k += 64) {
         const uint32_t q = row_find(item, rb, re, side.Y[k]);
-        if (q >= re || item[q] != side.Y[k]) return;  // s not in sids(Y)
-        lY = min(lY, last[q]);
+        if (q >= re || item[q] != side.Y[k]) ok = false;
+        else lY = min(lY, last[q]);
     }
+    if (__ballot(!ok)) return;  // s not in sids(Y)
+    lY = wave_min(lY);
     if (fX >= lY) return;  // X => Y does not hold in s
     if (side.doL) {        // expandL: c > max(X), c not in Y, c before lastY(s)
         const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
-        for (uint32_t q = q0; q < re; ++q) {
+        for (uint32_t q = q0 + lane; q < re; q += 64) {
             const uint32_t c = item[q];
-            if (first[q] < lY && !in_sorted(side.Y, side.ny, c)) atomicAdd(&TL[c], 1u);
+            if (first[q] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
         }
     }
     if (side.doR) {        // expandR: c > max(Y), c not in X, c after firstX(s)
         const uint32_t q0 = row_find(item, rb, re, side.maxY + 1);
-        for (uint32_t q = q0; q < re; ++q) {
+        for (uint32_t q = q0 + lane; q < re; q += 64) {
             const uint32_t c = item[q];
-            if (last[q] > fX && !in_sorted(side.X, side.nx, c)) atomicAdd(&TR[c], 1u);
+            if (last[q] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
         }
     }
 }
@@ -192,30 +232,46 @@ __global__ __launch_bounds__(kBlock) void k_expand(const Side side, const uint32
 struct ExpRec {
     uint32_t c, tl, dl, tr;
 };
+struct ExpHdr {
+    uint32_t nout, nx, pad0, pad1;
+};
 
-__global__ __launch_bounds__(kBlock) void k_expand_compact(uint32_t* __restrict__ TL, uint32_t* __restrict__ DL,
-                                                           uint32_t* __restrict__ TR, uint32_t U, uint32_t t,
-                                                           ExpRec* __restrict__ out, uint32_t* __restrict__ nout,
-                                                           uint32_t cap) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    bool keep = false;
-    uint32_t tl = 0, dl = 0, tr = 0;
-    if (c < U) {
-        tl = TL[c];
-        dl = DL[c];
-        tr = TR[c];
-        keep = tl >= t || tr >= t;
-        if (tl) TL[c] = 0;
-        if (dl) DL[c] = 0;
-        if (tr) TR[c] = 0;
+// Visit the touched items of this expansion: keep the candidates with count
+// >= t (records go to mapped pinned host memory, any order; the host sorts
+// them by item), re-zero their counters and flags; the last block to finish
+// publishes the header and resets the control block for the next expansion.
+__global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict__ TL, uint32_t* __restrict__ DL,
+                                                           uint32_t* __restrict__ TR, uint32_t* __restrict__ seen,
+                                                           const uint32_t* __restrict__ list, ExpCtl* __restrict__ ctl,
+                                                           uint32_t t, ExpRec* __restrict__ out,
+                                                           ExpHdr* __restrict__ hdr, uint32_t cap) {
+    const uint32_t n = ctl->nlist;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t c = list[i];
+        const uint32_t tl = TL[c], dl = DL[c], tr = TR[c];
+        TL[c] = 0;
+        DL[c] = 0;
+        TR[c] = 0;
+        seen[c] = 0;
+        if (tl >= t || tr >= t) {
+            const uint32_t idx = atomicAdd(&ctl->nout, 1u);
+            if (idx < cap) out[idx] = ExpRec{c, tl, dl, tr};
+        }
     }
-    const uint64_t b = __ballot(keep);
-    if (!b) return;
-    uint32_t base = 0;
-    if (lane_id() == 0) base = atomicAdd(nout, uint32_t(__popcll(b)));
-    base = __shfl(base, 0, 64);
-    const uint32_t idx = base + uint32_t(__popcll(b & lanemask_lt()));
-    if (keep && idx < cap) out[idx] = ExpRec{c, tl, dl, tr};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&ctl->done, 1u) == gridDim.x - 1) {
+            __threadfence();
+            hdr->nout = atomicAdd(&ctl->nout, 0u);
+            hdr->nx = atomicAdd(&ctl->nx, 0u);
+            ctl->nx = 0;
+            ctl->nlist = 0;
+            ctl->nout = 0;
+            ctl->done = 0;
+            __threadfence_system();
+        }
+    }
 }
 
 // ------------------------------------------------------------ host replay
@@ -418,17 +474,29 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     }
     scr.release();
     const double t1 = now_ms();
+    if (ctx->opts.verbose)
+        std::fprintf(stderr, "[fsm tsr] pair phase %.0f ms: minsup %u, candidates %zu, rules %zu\n", t1 - t0,
+                     rp.minsup, rp.cand.size(), rp.krules.size());
 
     // ---------------- expansions
     DevBuf TL(size_t(std::max<uint32_t>(U, 1)) * 4), DL(size_t(std::max<uint32_t>(U, 1)) * 4),
-        TR(size_t(std::max<uint32_t>(U, 1)) * 4), nX(8), nout(8);
+        TR(size_t(std::max<uint32_t>(U, 1)) * 4), seen(size_t(std::max<uint32_t>(U, 1)) * 4),
+        list(size_t(std::max<uint32_t>(U, 1)) * 4), ctl(sizeof(ExpCtl));
     FSM_HIP(hipMemsetAsync(TL.p, 0, size_t(U) * 4, s));
     FSM_HIP(hipMemsetAsync(DL.p, 0, size_t(U) * 4, s));
     FSM_HIP(hipMemsetAsync(TR.p, 0, size_t(U) * 4, s));
-    uint32_t ecap = 1u << 16;
-    DevBuf d_exp(size_t(ecap) * sizeof(ExpRec));
+    FSM_HIP(hipMemsetAsync(seen.p, 0, size_t(U) * 4, s));
+    FSM_HIP(hipMemsetAsync(ctl.p, 0, sizeof(ExpCtl), s));
+    // expansion results land in mapped pinned host memory (at most one record per item)
+    const uint32_t ecap = std::max<uint32_t>(U, 1);
+    PinnedBuf pin(sizeof(ExpHdr) + size_t(ecap) * sizeof(ExpRec));
+    ExpHdr* h_hdr = static_cast<ExpHdr*>(pin.host);
+    ExpRec* h_rec = reinterpret_cast<ExpRec*>(h_hdr + 1);
+    ExpHdr* d_hdr = static_cast<ExpHdr*>(pin.dev);
+    ExpRec* d_rec = reinterpret_cast<ExpRec*>(d_hdr + 1);
     std::vector<ExpRec> er;
     int64_t expansions = 0;
+    double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     while (!rp.cand.empty()) {
         Rule* r = rp.cand.top();
         rp.cand.pop();
@@ -453,34 +521,32 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             for (uint32_t y : r->Y) if (sup[y] < sup[drv]) { drv = y; drv_in_x = false; }
         const uint64_t nd = voff[drv + 1] - voff[drv];
         const uint32_t t = rp.minsup;
-        FSM_HIP(hipMemsetAsync(nX.p, 0, 8, s));
-        FSM_HIP(hipMemsetAsync(nout.p, 0, 4, s));
         if (nd) {
-            hipLaunchKernelGGL(k_expand, dim3(unsigned((nd + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sd,
+            hipLaunchKernelGGL(k_expand, dim3(unsigned((uint64_t(nd) * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sd,
                                d->vert_sid.as<uint32_t>() + voff[drv], uint32_t(nd), d->row_off.as<uint32_t>(),
                                d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
-                               TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), nX.as<uint32_t>());
+                               TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(),
+                               list.as<uint32_t>(), ctl.as<ExpCtl>());
             FSM_LAUNCHED("k_expand", s);
         }
-        hipLaunchKernelGGL(k_expand_compact, dim3(unsigned((U + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                           TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), U, t, d_exp.as<ExpRec>(),
-                           nout.as<uint32_t>(), ecap);
-        FSM_LAUNCHED("k_expand_compact", s);
-        uint32_t hn[2] = {0, 0};
-        FSM_HIP(hipMemcpyAsync(&hn[0], nout.p, 4, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipMemcpyAsync(&hn[1], nX.p, 4, hipMemcpyDeviceToHost, s));
+        hipLaunchKernelGGL(k_expand_collect, dim3(kCollectBlocks), dim3(kBlock), 0, s, TL.as<uint32_t>(),
+                           DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
+                           ctl.as<ExpCtl>(), t, d_rec, d_hdr, ecap);
+        FSM_LAUNCHED("k_expand_collect", s);
+        const double tw0 = now_ms();
         FSM_HIP(hipStreamSynchronize(s));
+        wait_ms += now_ms() - tw0;
+        const uint32_t hn[2] = {h_hdr->nout, h_hdr->nx};
         if (hn[0] > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
-        er.resize(hn[0]);
-        if (hn[0]) {
-            FSM_HIP(hipMemcpyAsync(er.data(), d_exp.p, size_t(hn[0]) * sizeof(ExpRec), hipMemcpyDeviceToHost, s));
-            FSM_HIP(hipStreamSynchronize(s));
-        }
+        er.assign(h_rec, h_rec + hn[0]);
+        std::sort(er.begin(), er.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
         if (drv_in_x && hn[1] != r->nX)
             throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(hn[1]) + " vs " +
                                          std::to_string(r->nX) + ")");
-        std::sort(er.begin(), er.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
         expansions += doL ? 2 : 1;
+        if (ctx->opts.verbose && (expansions & 1023) < 2)
+            std::fprintf(stderr, "[fsm tsr] %lld expansions, minsup %u, candidates %zu, rules %zu, %.0f ms\n",
+                         (long long)expansions, rp.minsup, rp.cand.size(), rp.krules.size(), now_ms() - t0);
         if (doL) {  // expandL: X u {c} => Y
             for (const ExpRec& e : er) {
                 if (e.tl == 0 || e.tl < rp.minsup) continue;
@@ -546,6 +612,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     ctx->stats.rules = int64_t(n);
     ctx->stats.ms_f2 = t1 - t0;          // pair phase
     ctx->stats.ms_lattice = now_ms() - t1;  // expansions
+    ctx->stats.ms_count_kernel = wait_ms;   // of which: waiting for the expansion kernels
+    if (ctx->opts.verbose)
+        std::fprintf(stderr, "[fsm tsr] expansions: %lld, %.0f ms, %.0f ms waiting on the GPU\n",
+                     (long long)expansions, ctx->stats.ms_lattice, wait_ms);
     ctx->stats.ms_mine = now_ms() - t0;
     *out = o;
 }
