@@ -52,9 +52,9 @@ namespace {
 
 constexpr uint32_t kSeq = 0, kItm = 1;
 constexpr uint32_t kChunk = 2048;        // class entries per workgroup work item
-constexpr uint32_t kRootChunk = 16384;   // root entries per block in the bucketed pair count
-constexpr int kBucketBits = 15;          // 32768 counters (128 KiB LDS) per bucket
-constexpr uint32_t kMaxBuckets = 16384;  // LDS bucket histogram of the scatter pass (64 KiB)
+constexpr uint32_t kRootChunk = 16384;     // root entries per block of the group histogram / scatter
+constexpr uint32_t kGroupCounters = 32768;  // root F2: u32 LDS counters of one rank group (128 KiB)
+constexpr uint32_t kMaxGroups = 16384;      // LDS histogram of k_group_hist (64 KiB)
 constexpr int kBlock = 256;
 
 
@@ -213,69 +213,97 @@ __device__ __forceinline__ void root_pairs(uint32_t e, const uint32_t* __restric
     }
 }
 
-// pass 1: per-block LDS histogram of bucket sizes -> blkhist[block][bucket], totals
+// Root F2 (the F x 2F counter matrix, 220 MB at D1M: far beyond LDS, and
+// global atomics into it run at the memory side).  Every key of a root entry
+// lies in the counter row of its own rank, so the matrix is cut into rank
+// groups of `per` ranks whose per*D counters fit 128 KiB of LDS, and:
+//   k_root_ub       upper bound of the keys of each entry (temporal: row length;
+//                   equality: partners of higher rank); exclusive scan -> koff
+//   k_root_keys     THE one partner enumeration (horizontal, coalesced row reads):
+//                   entry e writes its keys, local to its group (u16), at
+//                   koff[e]: a wave's writes form one contiguous stretch
+//   k_group_hist    entries per (group, block); exclusive scan -> order
+//   k_group_scatter run descriptors (koff, nkeys) in group order, row order inside
+//   k_group_count   one block per group: stream its runs into LDS counters, write
+//                   the group's slice of the matrix once (coalesced)
+__global__ __launch_bounds__(kBlock) void k_root_ub(uint32_t E0, const uint32_t* __restrict__ mem,
+                                                    const uint32_t* __restrict__ pos, uint32_t mlo, uint32_t mhi,
+                                                    uint32_t* __restrict__ ub) {
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E0; e += gridDim.x * blockDim.x) {
+        const uint32_t p = pos[e], rl = p & 0xFFFFu, off = p >> 16;
+        ub[e] = (mem[e] - mlo < mhi - mlo) ? 2 * rl - 1 - off : 0u;
+    }
+}
+
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_rootpair_hist(uint32_t E0, const uint32_t* __restrict__ mem,
-                                                          const uint32_t* __restrict__ lohi,
-                                                          const uint32_t* __restrict__ pos,
-                                                          const uint64_t* __restrict__ mask, uint32_t D, uint32_t nb,
-                                                          uint32_t chunk, uint32_t mlo, uint32_t mhi,
-                                                          uint32_t* __restrict__ blkhist,
-                                                          uint32_t* __restrict__ total) {
+__global__ __launch_bounds__(kBlock) void k_root_keys(uint32_t E0, const uint32_t* __restrict__ mem,
+                                                      const uint32_t* __restrict__ lohi,
+                                                      const uint32_t* __restrict__ pos,
+                                                      const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
+                                                      uint32_t mlo, uint32_t mhi, const uint64_t* __restrict__ koff,
+                                                      uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey) {
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E0; e += gridDim.x * blockDim.x) {
+        const uint32_t mi = mem[e];
+        uint32_t n = 0;
+        if (mi - mlo < mhi - mlo) {
+            const uint32_t gbase = ((mi >> 1) / per) * per * D;
+            uint16_t* out = keys + koff[e];
+            root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { out[n++] = uint16_t(key - gbase); });
+        }
+        nkey[e] = uint16_t(n);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_group_hist(uint32_t E0, const uint32_t* __restrict__ mem, uint32_t per,
+                                                       uint32_t G, uint32_t nblk, uint32_t chunk, uint32_t mlo,
+                                                       uint32_t mhi, uint32_t* __restrict__ ghist) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
     __syncthreads();
     const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
-    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
-        if (mem[e] - mlo < mhi - mlo)
-            root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { atomicAdd(&h[key >> kBucketBits], 1u); });
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-        const uint32_t v = h[b];
-        blkhist[uint64_t(blockIdx.x) * nb + b] = v;
-        if (v) atomicAdd(&total[b], v);
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const uint32_t mi = mem[e];
+        if (mi - mlo < mhi - mlo) atomicAdd(&h[(mi >> 1) / per], 1u);
     }
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) ghist[uint64_t(g) * nblk + blockIdx.x] = h[g];
 }
 
-// pass 2: reserve each block's share of every bucket, scatter the 15-bit keys
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_rootpair_scatter(uint32_t E0, const uint32_t* __restrict__ mem,
-                                                             const uint32_t* __restrict__ lohi,
-                                                             const uint32_t* __restrict__ pos,
-                                                             const uint64_t* __restrict__ mask, uint32_t D,
-                                                             uint32_t nb, uint32_t chunk, uint32_t mlo, uint32_t mhi,
-                                                             const uint32_t* __restrict__ blkhist,
-                                                             const uint64_t* __restrict__ boff,
-                                                             uint32_t* __restrict__ gcur,
-                                                             uint16_t* __restrict__ keys) {
-    // cur[b] = absolute key index of this block's next slot in bucket b (< 2^32, host-checked)
+__global__ __launch_bounds__(kBlock) void k_group_scatter(uint32_t E0, const uint32_t* __restrict__ mem, uint32_t per,
+                                                          uint32_t G, uint32_t nblk, uint32_t chunk, uint32_t mlo,
+                                                          uint32_t mhi, const uint64_t* __restrict__ goff,
+                                                          const uint64_t* __restrict__ koff,
+                                                          const uint16_t* __restrict__ nkey,
+                                                          uint2* __restrict__ runs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-        const uint32_t v = blkhist[uint64_t(blockIdx.x) * nb + b];
-        cur[b] = v ? uint32_t(boff[b]) + atomicAdd(&gcur[b], v) : 0u;
-    }
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(goff[uint64_t(g) * nblk + blockIdx.x]);
     __syncthreads();
     const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
-    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
-        if (mem[e] - mlo < mhi - mlo)
-            root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) {
-            keys[atomicAdd(&cur[key >> kBucketBits], 1u)] = uint16_t(key & ((1u << kBucketBits) - 1u));
-        });
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const uint32_t mi = mem[e];
+        if (mi - mlo < mhi - mlo)
+            runs[atomicAdd(&cur[(mi >> 1) / per], 1u)] = make_uint2(uint32_t(koff[e]), nkey[e]);
+    }
 }
 
-// pass 3: one block per bucket, 32768 LDS counters, dense write of the bucket's counters
-__global__ __launch_bounds__(1024) void k_bucket_count(const uint16_t* __restrict__ keys,
-                                                       const uint64_t* __restrict__ boff, uint64_t K,
-                                                       uint32_t* __restrict__ cnt) {
-    __shared__ uint32_t h[1u << kBucketBits];
-    for (uint32_t t = threadIdx.x; t < (1u << kBucketBits); t += blockDim.x) h[t] = 0;
+__global__ __launch_bounds__(1024) void k_group_count(const uint64_t* __restrict__ goff, uint32_t nblk,
+                                                      const uint2* __restrict__ runs,
+                                                      const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
+                                                      uint32_t F, uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[kGroupCounters];
+    const uint32_t g = blockIdx.x;
+    const uint32_t l0 = uint32_t(goff[uint64_t(g) * nblk]), l1 = uint32_t(goff[uint64_t(g + 1) * nblk]);
+    if (l0 == l1) return;  // no entries of this group here (another rank's slice)
+    for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x) h[t] = 0;
     __syncthreads();
-    const uint64_t k0 = boff[blockIdx.x], k1 = boff[blockIdx.x + 1];
-    for (uint64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) atomicAdd(&h[keys[k]], 1u);
+    for (uint32_t i = l0 + threadIdx.x; i < l1; i += blockDim.x) {
+        const uint2 r = runs[i];
+        const uint16_t* k = keys + r.x;
+        for (uint32_t j = 0; j < r.y; ++j) atomicAdd(&h[k[j]], 1u);
+    }
     __syncthreads();
-    const uint64_t base = uint64_t(blockIdx.x) << kBucketBits;
-    for (uint32_t t = threadIdx.x; t < (1u << kBucketBits); t += blockDim.x)
-        if (base + t < K) cnt[base + t] = h[t];
+    const uint32_t base = g * per * D, n = (min(F, (g + 1) * per) - g * per) * D;
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) cnt[base + t] = h[t];
 }
 
 __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ rows, uint32_t nrows,
@@ -576,55 +604,67 @@ struct Miner {
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kRootChunk;
     }
 
-    // Root counters without per-pair global atomics (3 passes, see file header).
-    // Returns false if the key space is too large for the bucket histogram.
-    bool root_bucket_count(Batch& b, uint32_t* cnt) {
+    // Root counters by rank groups (see k_root_keys).  Returns false when a
+    // counter row does not fit the LDS group tile or the groups are too many.
+    bool root_group_count(Batch& b, uint32_t* cnt) {
         const ClassMeta& m = b.cls[0];
-        const uint64_t K = uint64_t(m.D >> m.mshift) * m.D;
-        const uint64_t nb64 = (K + (1u << kBucketBits) - 1) >> kBucketBits;
-        if (nb64 > kMaxBuckets || K >= (uint64_t(1) << 32) || m.nent == 0) return false;
-        const uint32_t nb = uint32_t(nb64);
+        const uint32_t D = m.D, F = m.D / 2;
+        const uint64_t K = uint64_t(F) * D;
+        if (m.nent == 0 || D > kGroupCounters || K >= (uint64_t(1) << 32)) return false;
+        const uint32_t per = kGroupCounters / D;
+        const uint32_t G = (F + per - 1) / per;
+        if (G > kMaxGroups) return false;
         const uint32_t E0 = m.nent;
         const uint32_t mlo = member_lo(b), mhi = member_hi(b);
+        const SlabPtrs sp = b.slab.ptrs();
+        const int64_t slab_bytes = int64_t(E0) * int64_t(16 + 8 * W);
+        const unsigned grid = unsigned(std::min<uint64_t>((E0 + kBlock - 1) / kBlock, 1u << 16));
+        // key-run upper bounds -> offsets
+        DevBuf ub(uint64_t(E0) * 4), koff((uint64_t(E0) + 1) * 8);
+        size_t tk = clk->begin("k_root_ub");
+        hipLaunchKernelGGL(k_root_ub, dim3(grid), dim3(kBlock), 0, s, E0, sp.mem, sp.pos, mlo, mhi, ub.as<uint32_t>());
+        FSM_LAUNCHED("k_root_ub", s);
+        clk->end(tk, int64_t(E0) * 12);
+        scan_exclusive(ub.as<uint32_t>(), koff.as<uint64_t>(), E0, s);
+        ub.release();
+        uint64_t nslots = 0;
+        FSM_HIP(hipMemcpyAsync(&nslots, koff.as<uint64_t>() + E0, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        if (nslots >= (uint64_t(1) << 32)) return false;  // run offsets are kept in u32
+        // the one enumeration
+        DevBuf keys(std::max<uint64_t>(nslots, 1) * 2), nkey(uint64_t(E0) * 2);
+        tk = clk->begin("k_root_keys");
+#define FSM_RK(WW)                                                                                             \
+    hipLaunchKernelGGL(k_root_keys<WW>, dim3(grid), dim3(kBlock), 0, s, E0, sp.mem, sp.lohi, sp.pos, sp.mask, \
+                       D, per, mlo, mhi, koff.as<uint64_t>(), keys.as<uint16_t>(), nkey.as<uint16_t>())
+        FSM_W_DISPATCH(W, FSM_RK)
+#undef FSM_RK
+        FSM_LAUNCHED("k_root_keys", s);
+        clk->end(tk, slab_bytes + int64_t(E0) * 10 + int64_t(nslots) * 2);
+        // runs in group order
         const uint32_t chunk = root_chunk();
         const uint32_t nblk = (E0 + chunk - 1) / chunk;
-        DevBuf blkhist(uint64_t(nblk) * nb * 4), total(uint64_t(nb) * 4 + 4), boff((uint64_t(nb) + 1) * 8),
-            gcur(uint64_t(nb) * 4 + 4);
-        FSM_HIP(hipMemsetAsync(total.p, 0, uint64_t(nb) * 4, s));
-        FSM_HIP(hipMemsetAsync(gcur.p, 0, uint64_t(nb) * 4, s));
-        const SlabPtrs sp = b.slab.ptrs();
-        const size_t lds = size_t(nb) * 4;
-#define FSM_RP_HIST(WW)                                                                                    \
-    hipLaunchKernelGGL(k_rootpair_hist<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
-                       sp.mask, m.D, nb, chunk, mlo, mhi, blkhist.as<uint32_t>(), total.as<uint32_t>())
-        const int64_t slab_bytes = int64_t(E0) * int64_t(16 + 8 * W);
-        size_t tk = clk->begin("k_rootpair_hist");
-        FSM_W_DISPATCH(W, FSM_RP_HIST)
-#undef FSM_RP_HIST
-        FSM_LAUNCHED("k_rootpair_hist", s);
-        clk->end(tk, slab_bytes);
-        scan_exclusive(total.as<uint32_t>(), boff.as<uint64_t>(), nb, s);
-        uint64_t npairs = 0;
-        FSM_HIP(hipMemcpyAsync(&npairs, boff.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipStreamSynchronize(s));
-        if (npairs >= (uint64_t(1) << 32)) return false;  // scatter keeps absolute key indices in u32
-        DevBuf keys(std::max<uint64_t>(npairs, 1) * 2);
-#define FSM_RP_SCAT(WW)                                                                                        \
-    hipLaunchKernelGGL(k_rootpair_scatter<WW>, dim3(nblk), dim3(kBlock), lds, s, E0, sp.mem, sp.lohi, sp.pos, \
-                       sp.mask, m.D, nb, chunk, mlo, mhi, blkhist.as<uint32_t>(), boff.as<uint64_t>(),            \
-                       gcur.as<uint32_t>(), \
-                       keys.as<uint16_t>())
-        tk = clk->begin("k_rootpair_scatter");
-        FSM_W_DISPATCH(W, FSM_RP_SCAT)
-#undef FSM_RP_SCAT
-        FSM_LAUNCHED("k_rootpair_scatter", s);
-        clk->end(tk, slab_bytes + int64_t(npairs) * 2);
-        tk = clk->begin("k_bucket_count");
-        hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(1024), 0, s, keys.as<uint16_t>(), boff.as<uint64_t>(), K,
-                           cnt);
-        FSM_LAUNCHED("k_bucket_count", s);
-        clk->end(tk, int64_t(npairs) * 2 + int64_t(K) * 4);
-        FSM_HIP(hipStreamSynchronize(s));  // keys / blkhist released on return
+        const uint64_t nh = uint64_t(G) * nblk;
+        DevBuf ghist(nh * 4), goff((nh + 1) * 8), runs(uint64_t(E0) * 8);
+        tk = clk->begin("k_group_hist");
+        hipLaunchKernelGGL(k_group_hist, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, E0, sp.mem, per, G, nblk, chunk,
+                           mlo, mhi, ghist.as<uint32_t>());
+        FSM_LAUNCHED("k_group_hist", s);
+        clk->end(tk, int64_t(E0) * 4 + int64_t(nh) * 4);
+        scan_exclusive(ghist.as<uint32_t>(), goff.as<uint64_t>(), nh, s);
+        tk = clk->begin("k_group_scatter");
+        hipLaunchKernelGGL(k_group_scatter, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, E0, sp.mem, per, G, nblk,
+                           chunk, mlo, mhi, goff.as<uint64_t>(), koff.as<uint64_t>(), nkey.as<uint16_t>(),
+                           runs.as<uint2>());
+        FSM_LAUNCHED("k_group_scatter", s);
+        clk->end(tk, int64_t(E0) * (4 + 8 + 2 + 8));
+        // one block per group
+        tk = clk->begin("k_group_count");
+        hipLaunchKernelGGL(k_group_count, dim3(G), dim3(1024), 0, s, goff.as<uint64_t>(), nblk, runs.as<uint2>(),
+                           keys.as<uint16_t>(), D, per, F, cnt);
+        FSM_LAUNCHED("k_group_count", s);
+        clk->end(tk, int64_t(E0) * 8 + int64_t(nslots) * 2 + int64_t(K) * 4);
+        FSM_HIP(hipStreamSynchronize(s));  // temporaries released on return
         return true;
     }
 
@@ -643,7 +683,7 @@ struct Miner {
         st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
         DevBuf cnt(std::max<uint64_t>(b.n_cnt, 1) * 4);
         if (b.E) {
-            const bool done = b.root && !root_atomic() && root_bucket_count(b, cnt.as<uint32_t>());
+            const bool done = b.root && !root_atomic() && root_group_count(b, cnt.as<uint32_t>());
             if (!done) {
                 FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
                 const SlabPtrs sp = b.slab.ptrs();

@@ -266,15 +266,16 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["bucket", "bucket-small-chunk", "atomic"])
+@pytest.mark.parametrize("path", ["group", "group-small-chunk", "atomic"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
-    """The root F2 implementations (bucketed keys, at the default and at a
-    small block chunk; global atomics) give the oracle's patterns and joins."""
+    """The root F2 implementations (key runs counted per rank group, at the
+    default and at a small block chunk; global atomics) give the oracle's
+    patterns and joins."""
     from oracle import oracle
     from tools import gen
     if path == "atomic":
         monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
-    if path == "bucket-small-chunk":
+    if path == "group-small-chunk":
         monkeypatch.setenv("FSM_ROOT_CHUNK", "300")
     ds = gen.quest(20000, seed=4)
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
