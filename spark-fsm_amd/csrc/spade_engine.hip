@@ -350,21 +350,24 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
     }
 }
 
-__device__ __forceinline__ uint32_t find_member(const uint32_t* __restrict__ mem, uint32_t lo, uint32_t hi,
-                                                uint32_t key) {
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (mem[mid] < key) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
 // Child rows.  Entry i (member mi, class c, sequence s) produces the whole
 // run of sequence s in the child class [c, mi]: one entry per frequent child of
 // mi whose join with i is non-empty (partner j found by binary search in the
 // member-sorted run), in child member order.  Runs are written in parent entry
 // order at exclusive-scan offsets, so every block writes one contiguous,
 // coalesced stretch (no per-class cursors, no partial-line scatter).
+//
+// Work is flattened to (entry, kid) pairs per wave: the 64 entries of a wave
+// expose their kid counts, a wave prefix sum numbers the pairs, and each lane
+// takes one pair per step (owner found by a 6-step shuffle search).  Kid counts
+// are heavily skewed (popular members have dozens of frequent children), so a
+// thread-per-entry loop would leave most lanes idle behind the longest list.
+__device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bits [a, b), 0 <= a <= b <= 64
+    const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
+    const uint64_t lo = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
+    return hi & ~lo;
+}
+
 template <int W, bool kWrite>
 __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __restrict__ cid,
                                                  const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
@@ -375,68 +378,113 @@ __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __r
                                                  const uint32_t* __restrict__ kid_cid,
                                                  const uint32_t* __restrict__ child_of, uint32_t* __restrict__ ncnt,
                                                  const uint64_t* __restrict__ off, SlabPtrs o) {
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
-        uint32_t n = 0;
+    const uint32_t lane = lane_id();
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wstride = gridDim.x * wpb * 64;
+    for (uint32_t w0 = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 64; w0 < E; w0 += wstride) {
+        const uint32_t e = w0 + lane;
+        // this lane's entry: its frequent children kid_slot[k0 .. k0 + nk)
+        uint32_t k0 = 0, nk = 0, cc = kNone, rb = 0, re = 0, lt = 0, n_run = 0;
         uint64_t base = 0;
-        if constexpr (kWrite) {
-            base = off[e];
-            n = uint32_t(off[e + 1] - base);
-            if (n == 0) continue;
-        }
-        const DClass c = cls[cid[e]];
-        const uint32_t mi = mem[e];
-        const uint32_t cc = child_of[c.cbase + mi];
-        if (cc == kNone) {
-            if constexpr (!kWrite) ncnt[e] = 0;
-            continue;
-        }
-        const uint32_t k0 = kid_off[c.cbase + mi], k1 = kid_off[c.cbase + mi + 1];
-        const uint32_t p = pos[e];
-        const uint32_t lo_i = lohi[e] & 0xFFFFu;
-        const uint32_t ti = mi & 1u;
-        const uint32_t rb = e - (p >> 16), re = rb + (p & 0xFFFFu);
-        uint64_t mk[W];
-        load_mask<W>(mask + size_t(e) * W, mk);
-        uint32_t k = 0;
-        for (uint32_t q = k0; q < k1; ++q) {
-            const uint32_t slot = kid_slot[q];
-            const uint32_t ct = slot & 1u;
-            const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : ti);  // partner member id
-            const uint32_t f = find_member(mem, rb, re, target);
-            if (f >= re || mem[f] != target) continue;
-            if constexpr (!kWrite) {
-                if (ct == kSeq) k += (lohi[f] >> 16) > lo_i;
-                else k += and_nonzero<W>(mk, mask + size_t(f) * W);
-            } else {
-                uint64_t m[W];
-                load_mask<W>(mask + size_t(f) * W, m);
-                uint32_t lo, hi;
-                if (ct == kSeq) {
-                    hi = lohi[f] >> 16;
-                    if (hi <= lo_i) continue;
-                    mask_clear_upto<W>(m, lo_i);
-                    lo = mask_lo<W>(m);
-                } else {
-                    uint64_t acc = 0;
-#pragma unroll
-                    for (int x = 0; x < W; ++x) {
-                        m[x] &= mk[x];
-                        acc |= m[x];
-                    }
-                    if (!acc) continue;
-                    lo = mask_lo<W>(m);
-                    hi = mask_hi<W>(m);
-                }
-                const uint64_t d = base + k;
-                o.cid[d] = cc;
-                o.mem[d] = kid_cid[q];
-                o.lohi[d] = lo | (hi << 16);
-                o.pos[d] = (k << 16) | n;
-                store_mask<W>(o.mask + d * W, m);
-                ++k;
+        if (e < E) {
+            const DClass c = cls[cid[e]];
+            const uint32_t mi = mem[e];
+            cc = child_of[c.cbase + mi];
+            if (cc != kNone) {
+                k0 = kid_off[c.cbase + mi];
+                nk = kid_off[c.cbase + mi + 1] - k0;
+                const uint32_t p = pos[e];
+                rb = e - (p >> 16);
+                re = rb + (p & 0xFFFFu);
+                lt = (lohi[e] & 0xFFFFu) | ((mi & 1u) << 16);  // lo | type << 16
+            }
+            if constexpr (kWrite) {
+                base = off[e];
+                n_run = uint32_t(off[e + 1] - base);
+                if (n_run == 0) nk = 0;
             }
         }
-        if constexpr (!kWrite) ncnt[e] = k;
+        const uint32_t incl = wave_incl_scan(nk), excl = incl - nk;
+        const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
+        uint32_t done = 0;  // this lane's (as owner) non-empty joins so far
+        for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+            const uint32_t pp = p0 + lane;
+            // owner: the largest lane whose first pair index <= pp
+            uint32_t ow = 0;
+#pragma unroll
+            for (uint32_t step = 32; step > 0; step >>= 1) {
+                const uint32_t cand = ow + step;
+                if (uint32_t(__shfl(int(excl), int(cand), 64)) <= pp) ow = cand;
+            }
+            const uint32_t o_k0 = uint32_t(__shfl(int(k0), int(ow), 64));
+            const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
+            const uint32_t o_rb = uint32_t(__shfl(int(rb), int(ow), 64));
+            const uint32_t o_re = uint32_t(__shfl(int(re), int(ow), 64));
+            const uint32_t o_lt = uint32_t(__shfl(int(lt), int(ow), 64));
+            const uint32_t o_done = uint32_t(__shfl(int(done), int(ow), 64));
+            const uint32_t o_e = w0 + ow;
+            bool ok = false;
+            uint32_t q = 0, f = 0, slot = 0;
+            if (pp < total) {
+                q = o_k0 + (pp - o_ex);
+                slot = kid_slot[q];
+                const uint32_t ct = slot & 1u;
+                const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : (o_lt >> 16));  // partner member id
+                uint32_t lo = o_rb, hi = o_re;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (mem[mid] < target) lo = mid + 1; else hi = mid;
+                }
+                f = lo;
+                if (f < o_re && mem[f] == target) {
+                    if (ct == kSeq) {
+                        ok = (lohi[f] >> 16) > (o_lt & 0xFFFFu);
+                    } else {
+                        uint64_t mk[W];
+                        load_mask<W>(mask + size_t(o_e) * W, mk);
+                        ok = and_nonzero<W>(mk, mask + size_t(f) * W);
+                    }
+                }
+            }
+            const uint64_t succ = __ballot(ok);
+            if constexpr (kWrite) {
+                // shuffles stay outside the branch: a source lane must be active
+                const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
+                const uint64_t o_base = __shfl(base, int(ow), 64);
+                const uint32_t o_cc = uint32_t(__shfl(int(cc), int(ow), 64));
+                if (ok) {
+                    const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
+                    const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
+                    uint64_t m[W];
+                    load_mask<W>(mask + size_t(f) * W, m);
+                    uint32_t lo2, hi2;
+                    if ((slot & 1u) == kSeq) {
+                        hi2 = lohi[f] >> 16;
+                        mask_clear_upto<W>(m, o_lt & 0xFFFFu);
+                        lo2 = mask_lo<W>(m);
+                    } else {
+                        uint64_t mk[W];
+                        load_mask<W>(mask + size_t(o_e) * W, mk);
+#pragma unroll
+                        for (int x = 0; x < W; ++x) m[x] &= mk[x];
+                        lo2 = mask_lo<W>(m);
+                        hi2 = mask_hi<W>(m);
+                    }
+                    const uint64_t d = o_base + k;
+                    o.cid[d] = o_cc;
+                    o.mem[d] = kid_cid[q];
+                    o.lohi[d] = lo2 | (hi2 << 16);
+                    o.pos[d] = (k << 16) | o_n;
+                    store_mask<W>(o.mask + d * W, m);
+                }
+            }
+            // each lane, as owner, adds its joins of this step
+            const uint32_t a = (excl > p0 ? excl : p0), bnd = (incl < p0 + 64 ? incl : p0 + 64);
+            if (bnd > a) done += uint32_t(__popcll(succ & lane_range(a - p0, bnd - p0)));
+        }
+        if constexpr (!kWrite) {
+            if (e < E) ncnt[e] = done;
+        }
     }
 }
 
@@ -856,7 +904,7 @@ struct Miner {
         if (b.E) {
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
-            const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 1u << 20));
+            const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 1u << 16));
 #define FSM_EMIT(WW, WR)                                                                                            \
     hipLaunchKernelGGL((k_emit<WW, WR>), dim3(grid), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
                        sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),        \
