@@ -27,6 +27,8 @@
 #include <cstdio>
 #include <memory>
 #include <queue>
+#include <set>
+#include <unordered_map>
 
 #include "device_util.h"
 
@@ -42,7 +44,8 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kMaxSide = 64;
-constexpr int kCollectBlocks = 32;
+constexpr int kCollectBlocks = 8;   // collect blocks per rule slot
+constexpr int kExpBatch = 32;       // rules expanded per launch (speculative, committed in order)
 
 __global__ __launch_bounds__(kBlock) void k_vcount(const uint32_t* __restrict__ item, uint64_t E,
                                                    uint32_t* __restrict__ cnt) {
@@ -176,18 +179,35 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 // One wave per sid of the driver item (rows are up to thousands of items long
 // on Kosarak-shaped data: the lanes split the binary searches and the row
 // scans, so one long row does not serialize a thread).
-__global__ __launch_bounds__(kBlock) void k_expand(const Side side, const uint32_t* __restrict__ dsid, uint32_t nd,
+// A batch of up to kExpBatch rules (slot b: rule side, driver sid range,
+// histograms / touched list / control at slot offsets) in one launch; waves
+// are numbered across slots by the prefix wave_off.
+__global__ __launch_bounds__(kBlock) void k_expand(const Side* __restrict__ sides,
+                                                   const uint64_t* __restrict__ drv_off,
+                                                   const uint64_t* __restrict__ wave_off, uint32_t nslot,
+                                                   const uint32_t* __restrict__ vert_sid,
                                                    const uint32_t* __restrict__ row_off,
                                                    const uint32_t* __restrict__ item,
                                                    const uint32_t* __restrict__ first,
-                                                   const uint32_t* __restrict__ last, uint32_t* __restrict__ TL,
-                                                   uint32_t* __restrict__ DL, uint32_t* __restrict__ TR,
-                                                   uint32_t* __restrict__ seen, uint32_t* __restrict__ list,
-                                                   ExpCtl* __restrict__ ctl) {
-    const uint32_t v = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (v >= nd) return;
+                                                   const uint32_t* __restrict__ last, uint32_t U,
+                                                   uint32_t* __restrict__ TLb, uint32_t* __restrict__ DLb,
+                                                   uint32_t* __restrict__ TRb, uint32_t* __restrict__ seenb,
+                                                   uint32_t* __restrict__ listb, ExpCtl* __restrict__ ctlb) {
+    const uint64_t w = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    if (w >= wave_off[nslot]) return;
+    uint32_t b = 0;  // slot of this wave: the last b with wave_off[b] <= w
+    for (uint32_t step = kExpBatch / 2; step > 0; step >>= 1)
+        if (b + step < nslot && wave_off[b + step] <= w) b += step;
+    const Side& side = sides[b];
+    const uint64_t U64 = U;
+    uint32_t* TL = TLb + b * U64;
+    uint32_t* DL = DLb + b * U64;
+    uint32_t* TR = TRb + b * U64;
+    uint32_t* seen = seenb + b * U64;
+    uint32_t* list = listb + b * U64;
+    ExpCtl* ctl = ctlb + b;
     const uint32_t lane = lane_id();
-    const uint32_t s = dsid[v];
+    const uint32_t s = vert_sid[drv_off[b] + (w - wave_off[b])];
     const uint32_t rb = row_off[s], re = row_off[s + 1];
     bool ok = true;
     uint32_t fX = 0;
@@ -240,11 +260,21 @@ struct ExpHdr {
 // >= t (records go to mapped pinned host memory, any order; the host sorts
 // them by item), re-zero their counters and flags; the last block to finish
 // publishes the header and resets the control block for the next expansion.
-__global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict__ TL, uint32_t* __restrict__ DL,
-                                                           uint32_t* __restrict__ TR, uint32_t* __restrict__ seen,
-                                                           const uint32_t* __restrict__ list, ExpCtl* __restrict__ ctl,
-                                                           uint32_t t, ExpRec* __restrict__ out,
-                                                           ExpHdr* __restrict__ hdr, uint32_t cap) {
+__global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict__ TLb, uint32_t* __restrict__ DLb,
+                                                           uint32_t* __restrict__ TRb, uint32_t* __restrict__ seenb,
+                                                           const uint32_t* __restrict__ listb,
+                                                           ExpCtl* __restrict__ ctlb, uint32_t U, uint32_t t,
+                                                           ExpRec* __restrict__ outb, ExpHdr* __restrict__ hdrb,
+                                                           uint32_t cap) {
+    const uint64_t b = blockIdx.y, U64 = U;
+    uint32_t* TL = TLb + b * U64;
+    uint32_t* DL = DLb + b * U64;
+    uint32_t* TR = TRb + b * U64;
+    uint32_t* seen = seenb + b * U64;
+    const uint32_t* list = listb + b * U64;
+    ExpCtl* ctl = ctlb + b;
+    ExpRec* out = outb + b * uint64_t(cap);
+    ExpHdr* hdr = hdrb + b;
     const uint32_t n = ctl->nlist;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t c = list[i];
@@ -302,6 +332,9 @@ struct MinFirst {  // std::priority_queue puts the "largest" on top
 };
 struct MaxFirst {
     bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(a, b) < 0; }
+};
+struct PendingOrder {  // largest first (the heap's pop order)
+    bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(a, b) > 0; }
 };
 
 struct Replay {
@@ -479,75 +512,104 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      rp.minsup, rp.cand.size(), rp.krules.size());
 
     // ---------------- expansions
-    DevBuf TL(size_t(std::max<uint32_t>(U, 1)) * 4), DL(size_t(std::max<uint32_t>(U, 1)) * 4),
-        TR(size_t(std::max<uint32_t>(U, 1)) * 4), seen(size_t(std::max<uint32_t>(U, 1)) * 4),
-        list(size_t(std::max<uint32_t>(U, 1)) * 4), ctl(sizeof(ExpCtl));
-    FSM_HIP(hipMemsetAsync(TL.p, 0, size_t(U) * 4, s));
-    FSM_HIP(hipMemsetAsync(DL.p, 0, size_t(U) * 4, s));
-    FSM_HIP(hipMemsetAsync(TR.p, 0, size_t(U) * 4, s));
-    FSM_HIP(hipMemsetAsync(seen.p, 0, size_t(U) * 4, s));
-    FSM_HIP(hipMemsetAsync(ctl.p, 0, sizeof(ExpCtl), s));
-    // expansion results land in mapped pinned host memory (at most one record per item)
+    // Batched speculation, committed in the exact sequential order: the next
+    // kExpBatch candidates (in heap order) are expanded together on the GPU;
+    // they are committed one by one while each is still the heap maximum; when
+    // a newly registered rule outranks the next one, the rest go back to the
+    // heap with their results cached (results are minsup-independent supersets,
+    // re-filtered against the current minsup at commit), so no expansion is
+    // computed twice and the outcome equals the one-at-a-time replay.
+    const uint64_t SU = uint64_t(kExpBatch) * std::max<uint32_t>(U, 1);
+    DevBuf TL(SU * 4), DL(SU * 4), TR(SU * 4), seen(SU * 4), list(SU * 4), ctl(kExpBatch * sizeof(ExpCtl));
+    FSM_HIP(hipMemsetAsync(TL.p, 0, SU * 4, s));
+    FSM_HIP(hipMemsetAsync(DL.p, 0, SU * 4, s));
+    FSM_HIP(hipMemsetAsync(TR.p, 0, SU * 4, s));
+    FSM_HIP(hipMemsetAsync(seen.p, 0, SU * 4, s));
+    FSM_HIP(hipMemsetAsync(ctl.p, 0, kExpBatch * sizeof(ExpCtl), s));
+    DevBuf d_sides(kExpBatch * sizeof(Side)), d_drv((kExpBatch + 1) * 8), d_wave((kExpBatch + 1) * 8);
+    // expansion results land in mapped pinned host memory (at most one record per item per slot)
     const uint32_t ecap = std::max<uint32_t>(U, 1);
-    PinnedBuf pin(sizeof(ExpHdr) + size_t(ecap) * sizeof(ExpRec));
+    PinnedBuf pin(kExpBatch * sizeof(ExpHdr) + kExpBatch * size_t(ecap) * sizeof(ExpRec));
     ExpHdr* h_hdr = static_cast<ExpHdr*>(pin.host);
-    ExpRec* h_rec = reinterpret_cast<ExpRec*>(h_hdr + 1);
+    ExpRec* h_rec = reinterpret_cast<ExpRec*>(h_hdr + kExpBatch);
     ExpHdr* d_hdr = static_cast<ExpHdr*>(pin.dev);
-    ExpRec* d_rec = reinterpret_cast<ExpRec*>(d_hdr + 1);
-    std::vector<ExpRec> er;
-    int64_t expansions = 0;
+    ExpRec* d_rec = reinterpret_cast<ExpRec*>(d_hdr + kExpBatch);
+    struct ExpResult {
+        std::vector<ExpRec> recs;
+    };
+    std::unordered_map<Rule*, ExpResult> cache;
+    int64_t expansions = 0, launches = 0, spec_pushback = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
-    while (!rp.cand.empty()) {
-        Rule* r = rp.cand.top();
-        rp.cand.pop();
-        if (r->sup < rp.minsup) break;
-        const bool doL = r->expandLR;
-        if (r->X.size() >= kMaxSide || r->Y.size() >= kMaxSide)
-            throw Error(FSM_ELIMIT, "TSR: rule side exceeds " + std::to_string(kMaxSide - 1) + " items");
-        Side sd{};
-        sd.nx = uint32_t(r->X.size());
-        sd.ny = uint32_t(r->Y.size());
-        sd.doL = doL;
-        sd.doR = 1;
-        sd.maxX = r->X.back();
-        sd.maxY = r->Y.back();
-        std::copy(r->X.begin(), r->X.end(), sd.X);
-        std::copy(r->Y.begin(), r->Y.end(), sd.Y);
-        // driver list: rarest item of X (expandL needs all of sids(X)), else of X u Y
-        uint32_t drv = r->X[0];
-        bool drv_in_x = true;
-        for (uint32_t x : r->X) if (sup[x] < sup[drv]) drv = x;
-        if (!doL)
-            for (uint32_t y : r->Y) if (sup[y] < sup[drv]) { drv = y; drv_in_x = false; }
-        const uint64_t nd = voff[drv + 1] - voff[drv];
-        const uint32_t t = rp.minsup;
-        if (nd) {
-            hipLaunchKernelGGL(k_expand, dim3(unsigned((uint64_t(nd) * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sd,
-                               d->vert_sid.as<uint32_t>() + voff[drv], uint32_t(nd), d->row_off.as<uint32_t>(),
-                               d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
-                               TL.as<uint32_t>(), DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(),
-                               list.as<uint32_t>(), ctl.as<ExpCtl>());
+    std::vector<Side> sides;
+    std::vector<uint64_t> drv_off, wave_off;
+
+    auto launch = [&](const std::vector<Rule*>& batch) {
+        const uint32_t nb = uint32_t(batch.size());
+        sides.assign(nb, Side{});
+        drv_off.assign(nb + 1, 0);
+        wave_off.assign(nb + 1, 0);
+        std::vector<char> drv_in_x(nb, 1);
+        for (uint32_t k = 0; k < nb; ++k) {
+            const Rule* r = batch[k];
+            if (r->X.size() >= kMaxSide || r->Y.size() >= kMaxSide)
+                throw Error(FSM_ELIMIT, "TSR: rule side exceeds " + std::to_string(kMaxSide - 1) + " items");
+            Side& sd = sides[k];
+            sd.nx = uint32_t(r->X.size());
+            sd.ny = uint32_t(r->Y.size());
+            sd.doL = r->expandLR;
+            sd.doR = 1;
+            sd.maxX = r->X.back();
+            sd.maxY = r->Y.back();
+            std::copy(r->X.begin(), r->X.end(), sd.X);
+            std::copy(r->Y.begin(), r->Y.end(), sd.Y);
+            // driver list: rarest item of X (expandL needs all of sids(X)), else of X u Y
+            uint32_t drv = r->X[0];
+            for (uint32_t x : r->X) if (sup[x] < sup[drv]) drv = x;
+            if (!r->expandLR)
+                for (uint32_t y : r->Y) if (sup[y] < sup[drv]) { drv = y; drv_in_x[k] = 0; }
+            drv_off[k] = voff[drv];
+            wave_off[k + 1] = wave_off[k] + (voff[drv + 1] - voff[drv]);
+        }
+        FSM_HIP(hipMemcpyAsync(d_sides.p, sides.data(), nb * sizeof(Side), hipMemcpyHostToDevice, s));
+        FSM_HIP(hipMemcpyAsync(d_drv.p, drv_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipMemcpyAsync(d_wave.p, wave_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
+        const uint64_t waves = wave_off[nb];
+        if (waves) {
+            hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                               d_sides.as<Side>(), d_drv.as<uint64_t>(), d_wave.as<uint64_t>(), nb,
+                               d->vert_sid.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
+                               d->first.as<uint32_t>(), d->last.as<uint32_t>(), U, TL.as<uint32_t>(),
+                               DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
+                               ctl.as<ExpCtl>());
             FSM_LAUNCHED("k_expand", s);
         }
-        hipLaunchKernelGGL(k_expand_collect, dim3(kCollectBlocks), dim3(kBlock), 0, s, TL.as<uint32_t>(),
+        hipLaunchKernelGGL(k_expand_collect, dim3(kCollectBlocks, nb), dim3(kBlock), 0, s, TL.as<uint32_t>(),
                            DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
-                           ctl.as<ExpCtl>(), t, d_rec, d_hdr, ecap);
+                           ctl.as<ExpCtl>(), U, rp.minsup, d_rec, d_hdr, ecap);
         FSM_LAUNCHED("k_expand_collect", s);
         const double tw0 = now_ms();
         FSM_HIP(hipStreamSynchronize(s));
         wait_ms += now_ms() - tw0;
-        const uint32_t hn[2] = {h_hdr->nout, h_hdr->nx};
-        if (hn[0] > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
-        er.assign(h_rec, h_rec + hn[0]);
-        std::sort(er.begin(), er.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
-        if (drv_in_x && hn[1] != r->nX)
-            throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(hn[1]) + " vs " +
-                                         std::to_string(r->nX) + ")");
-        expansions += doL ? 2 : 1;
-        if (ctx->opts.verbose && (expansions & 1023) < 2)
+        ++launches;
+        for (uint32_t k = 0; k < nb; ++k) {
+            const ExpHdr h = h_hdr[k];
+            if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
+            if (drv_in_x[k] && h.nx != batch[k]->nX)
+                throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(h.nx) + " vs " +
+                                             std::to_string(batch[k]->nX) + ")");
+            ExpResult& res = cache[batch[k]];
+            const ExpRec* rec = h_rec + size_t(k) * ecap;
+            res.recs.assign(rec, rec + h.nout);
+            std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
+        }
+    };
+
+    auto commit = [&](Rule* r, const std::vector<ExpRec>& er) {
+        expansions += r->expandLR ? 2 : 1;
+        if (ctx->opts.verbose && (expansions & 0xFFFF) < 2)
             std::fprintf(stderr, "[fsm tsr] %lld expansions, minsup %u, candidates %zu, rules %zu, %.0f ms\n",
                          (long long)expansions, rp.minsup, rp.cand.size(), rp.krules.size(), now_ms() - t0);
-        if (doL) {  // expandL: X u {c} => Y
+        if (r->expandLR) {  // expandL: X u {c} => Y
             for (const ExpRec& e : er) {
                 if (e.tl == 0 || e.tl < rp.minsup) continue;
                 Rule* nr = rp.make();
@@ -573,7 +635,40 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (nr->conf >= minconf) rp.save(nr);
             rp.reg(nr, false);
         }
+    };
+
+    // Speculated rules wait in `pending` (ordered like the heap, results
+    // cached) instead of going back to the heap: the next rule to commit is
+    // always the larger of the heap top and the pending front, which is
+    // exactly the one-at-a-time order; new rules only ever enter the heap.
+    std::set<Rule*, PendingOrder> pending;
+    std::vector<Rule*> batch;
+    for (;;) {
+        const bool have_h = !rp.cand.empty(), have_p = !pending.empty();
+        if (!have_h && !have_p) break;
+        const bool from_p = have_p && (!have_h || rule_cmp(*pending.begin(), rp.cand.top()) > 0);
+        Rule* r = from_p ? *pending.begin() : rp.cand.top();
+        if (r->sup < rp.minsup) break;
+        if (from_p) {
+            pending.erase(pending.begin());
+            auto ci = cache.find(r);
+            commit(r, ci->second.recs);
+            cache.erase(ci);
+            continue;
+        }
+        // r (uncached) and the next heap rules are expanded together
+        batch.clear();
+        while (batch.size() < size_t(kExpBatch) && !rp.cand.empty() && rp.cand.top()->sup >= rp.minsup) {
+            batch.push_back(rp.cand.top());
+            rp.cand.pop();
+        }
+        launch(batch);
+        spec_pushback += int64_t(batch.size()) - 1;
+        for (Rule* c : batch) pending.insert(c);
     }
+    if (ctx->opts.verbose)
+        std::fprintf(stderr, "[fsm tsr] expansions %lld in %lld launches (%lld pushed back), %.0f ms waiting on the GPU\n",
+                     (long long)expansions, (long long)launches, (long long)spec_pushback, wait_ms);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {
@@ -613,9 +708,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     ctx->stats.ms_f2 = t1 - t0;          // pair phase
     ctx->stats.ms_lattice = now_ms() - t1;  // expansions
     ctx->stats.ms_count_kernel = wait_ms;   // of which: waiting for the expansion kernels
-    if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] expansions: %lld, %.0f ms, %.0f ms waiting on the GPU\n",
-                     (long long)expansions, ctx->stats.ms_lattice, wait_ms);
+    ctx->stats.count_launches = launches;
     ctx->stats.ms_mine = now_ms() - t0;
     *out = o;
 }
