@@ -35,7 +35,9 @@
 struct TsrDevDB {
     fsm::DevBuf row_off, item, first, last;  // horizontal
     fsm::DevBuf vert_off, vert_sid, vert_item;
+    fsm::DevBuf bm;                          // sid bitmaps: U x NW u32 (empty when over budget)
     int64_t N = 0, E = 0, U = 0;
+    uint32_t NW = 0;                         // u32 words per item bitmap = ceil(N / 32)
     std::vector<uint32_t> sup;  // |sids(item)|
 };
 
@@ -46,6 +48,8 @@ constexpr int kBlock = 256;
 constexpr int kMaxSide = 64;
 constexpr int kCollectBlocks = 8;   // collect blocks per rule slot
 constexpr int kExpBatch = 32;       // rules expanded per launch (speculative, committed in order)
+constexpr int kExpandBlocks = 128;  // bitmap path: expansion blocks per rule slot
+constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 
 __global__ __launch_bounds__(kBlock) void k_vcount(const uint32_t* __restrict__ item, uint64_t E,
                                                    uint32_t* __restrict__ cnt) {
@@ -152,6 +156,8 @@ struct ExpCtl {
     uint32_t nlist;  // items touched (list entries)
     uint32_t nout;   // candidates kept
     uint32_t done;   // collect blocks finished
+    uint32_t nsid;   // bitmap path: sids containing X u Y (slot list length)
+    uint32_t pad[3];
 };
 
 // histogram bump (no returned value: the lanes' atomics stay in flight) that
@@ -265,7 +271,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
                                                            const uint32_t* __restrict__ listb,
                                                            ExpCtl* __restrict__ ctlb, uint32_t U, uint32_t t,
                                                            ExpRec* __restrict__ outb, ExpHdr* __restrict__ hdrb,
-                                                           uint32_t cap) {
+                                                           uint32_t cap, uint4* __restrict__ dlw,
+                                                           uint32_t* __restrict__ ndlw) {
     const uint64_t b = blockIdx.y, U64 = U;
     uint32_t* TL = TLb + b * U64;
     uint32_t* DL = DLb + b * U64;
@@ -285,7 +292,11 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
         seen[c] = 0;
         if (tl >= t || tr >= t) {
             const uint32_t idx = atomicAdd(&ctl->nout, 1u);
-            if (idx < cap) out[idx] = ExpRec{c, tl, dl, tr};
+            if (idx < cap) {
+                out[idx] = ExpRec{c, tl, dl, tr};
+                // bitmap path: |sids(X u {c})| of a left extension comes from k_dl
+                if (dlw && tl >= t) dlw[atomicAdd(ndlw, 1u)] = make_uint4(uint32_t(b), c, idx, 0u);
+            }
         }
     }
     __syncthreads();
@@ -299,8 +310,132 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
             ctl->nlist = 0;
             ctl->nout = 0;
             ctl->done = 0;
+            ctl->nsid = 0;
             __threadfence_system();
         }
+    }
+}
+
+// ---- sid bitmaps: one bit per sequence per item.  They replace
+// the driver item's sid list as the expansion domain: the sids holding every
+// item of X u Y come from one AND over |X|+|Y| bitmaps, and |sids(X u {c})|
+// of the left-extension candidates that survive from AND + popcount, so no
+// expansion walks the rows of all sids(X) any more.
+__global__ __launch_bounds__(kBlock) void k_bitmap_build(const uint32_t* __restrict__ vsid,
+                                                         const uint32_t* __restrict__ vitem, uint64_t E,
+                                                         uint32_t NW, uint32_t* __restrict__ bm) {
+    for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += uint64_t(gridDim.x) * blockDim.x) {
+        const uint32_t sid = vsid[e];
+        atomicOr(&bm[uint64_t(vitem[e]) * NW + (sid >> 5)], 1u << (sid & 31u));
+    }
+}
+
+// slot b (blockIdx.y): the sids holding every item of X u Y -> slot sid list
+__global__ __launch_bounds__(kBlock) void k_rule_sids(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
+                                                      uint32_t NW, uint32_t N, uint32_t* __restrict__ sidsb,
+                                                      ExpCtl* __restrict__ ctlb) {
+    const uint32_t b = blockIdx.y;
+    const Side& side = sides[b];
+    uint32_t* out = sidsb + uint64_t(b) * N;
+    ExpCtl* ctl = ctlb + b;
+    const uint32_t lane = lane_id();
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t w0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); w0 < NW; w0 += stride) {
+        const uint32_t w = w0 + lane;
+        uint32_t v = 0;
+        if (w < NW) {
+            v = ~0u;
+            for (uint32_t k = 0; k < side.nx; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
+            for (uint32_t k = 0; k < side.ny; ++k) v &= bm[uint64_t(side.Y[k]) * NW + w];
+        }
+        const uint32_t cnt = uint32_t(__popc(v));
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t tot = uint32_t(__shfl(int(incl), 63, 64));
+        uint32_t base = 0;
+        if (lane == 63 && tot) base = atomicAdd(&ctl->nsid, tot);
+        base = uint32_t(__shfl(int(base), 63, 64));
+        uint32_t p = base + incl - cnt;
+        while (v) {
+            const uint32_t bit = uint32_t(__builtin_ctz(v));
+            out[p++] = w * 32u + bit;
+            v &= v - 1u;
+        }
+    }
+}
+
+// expansion over the slot's sid list (one wave per sid): TL / TR only
+__global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides,
+                                                      const uint32_t* __restrict__ sidsb, uint32_t N,
+                                                      const uint32_t* __restrict__ row_off,
+                                                      const uint32_t* __restrict__ item,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ last, uint32_t U,
+                                                      uint32_t* __restrict__ TLb, uint32_t* __restrict__ TRb,
+                                                      uint32_t* __restrict__ seenb, uint32_t* __restrict__ listb,
+                                                      ExpCtl* __restrict__ ctlb) {
+    const uint64_t b = blockIdx.y, U64 = U;
+    const Side& side = sides[b];
+    const uint32_t* sids = sidsb + b * N;
+    uint32_t* TL = TLb + b * U64;
+    uint32_t* TR = TRb + b * U64;
+    uint32_t* seen = seenb + b * U64;
+    uint32_t* list = listb + b * U64;
+    ExpCtl* ctl = ctlb + b;
+    const uint32_t nsid = ctl->nsid;
+    const uint32_t lane = lane_id();
+    const uint32_t wpb = blockDim.x >> 6;
+    for (uint32_t v = blockIdx.x * wpb + (threadIdx.x >> 6); v < nsid; v += gridDim.x * wpb) {
+        const uint32_t s = sids[v];
+        const uint32_t rb = row_off[s], re = row_off[s + 1];
+        uint32_t fX = 0, lY = 0xFFFFFFFFu;
+        for (uint32_t k = lane; k < side.nx; k += 64) fX = max(fX, first[row_find(item, rb, re, side.X[k])]);
+        for (uint32_t k = lane; k < side.ny; k += 64) lY = min(lY, last[row_find(item, rb, re, side.Y[k])]);
+        fX = wave_max(fX);
+        lY = wave_min(lY);
+        if (fX >= lY) continue;  // X => Y does not hold in s
+        if (side.doL) {          // expandL: c > max(X), c not in Y, c before lastY(s)
+            const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
+            for (uint32_t q = q0 + lane; q < re; q += 64) {
+                const uint32_t c = item[q];
+                if (first[q] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
+            }
+        }
+        if (side.doR) {          // expandR: c > max(Y), c not in X, c after firstX(s)
+            const uint32_t q0 = row_find(item, rb, re, side.maxY + 1);
+            for (uint32_t q = q0 + lane; q < re; q += 64) {
+                const uint32_t c = item[q];
+                if (last[q] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
+            }
+        }
+    }
+}
+
+// |sids(X u {c})| for the kept left-extension candidates: AND + popcount
+__global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
+                                               uint32_t NW, const uint4* __restrict__ dlw,
+                                               const uint32_t* __restrict__ ndlw, ExpRec* __restrict__ outb,
+                                               uint32_t cap) {
+    __shared__ uint32_t red[kBlock / 64];
+    const uint32_t n = *ndlw;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint4 wk = dlw[i];
+        const Side& side = sides[wk.x];
+        uint32_t acc = 0;
+        for (uint32_t w = threadIdx.x; w < NW; w += blockDim.x) {
+            uint32_t v = bm[uint64_t(wk.y) * NW + w];
+            for (uint32_t k = 0; k < side.nx; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
+            acc += uint32_t(__popc(v));
+        }
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) acc += uint32_t(__shfl_xor(int(acc), d, 64));
+        if (lane_id() == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (uint32_t k = 0; k < blockDim.x / 64; ++k) tot += red[k];
+            outb[uint64_t(wk.x) * cap + wk.z].dl = tot;
+        }
+        __syncthreads();
     }
 }
 
@@ -407,6 +542,21 @@ void tsr_upload(fsm_ctx* ctx, fsm_db* db) {
                            d->vert_off.as<uint64_t>(), cursor.as<uint32_t>(), d->vert_sid.as<uint32_t>(),
                            d->vert_item.as<uint32_t>());
         FSM_LAUNCHED("k_vscatter", s);
+    }
+    // sid bitmaps for the expansion domain (skipped when they would take more
+    // than a quarter of the free HBM; FSM_TSR_BITMAP=0 forces the list path)
+    d->NW = uint32_t((d->N + 31) / 32);
+    const uint64_t bm_bytes = uint64_t(d->U) * d->NW * 4;
+    size_t free_b = 0, total_b = 0;
+    FSM_HIP(hipMemGetInfo(&free_b, &total_b));
+    const char* bm_env = std::getenv("FSM_TSR_BITMAP");
+    if (d->E && bm_bytes <= free_b / 4 && !(bm_env && bm_env[0] == '0')) {
+        d->bm.alloc(bm_bytes);
+        FSM_HIP(hipMemsetAsync(d->bm.p, 0, bm_bytes, s));
+        const unsigned g = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, 8192));
+        hipLaunchKernelGGL(k_bitmap_build, dim3(g), dim3(kBlock), 0, s, d->vert_sid.as<uint32_t>(),
+                           d->vert_item.as<uint32_t>(), uint64_t(d->E), d->NW, d->bm.as<uint32_t>());
+        FSM_LAUNCHED("k_bitmap_build", s);
     }
     d->sup.resize(size_t(d->U));
     if (d->U) FSM_HIP(hipMemcpyAsync(d->sup.data(), cnt.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, s));
@@ -527,6 +677,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     FSM_HIP(hipMemsetAsync(seen.p, 0, SU * 4, s));
     FSM_HIP(hipMemsetAsync(ctl.p, 0, kExpBatch * sizeof(ExpCtl), s));
     DevBuf d_sides(kExpBatch * sizeof(Side)), d_drv((kExpBatch + 1) * 8), d_wave((kExpBatch + 1) * 8);
+    const bool use_bm = d->bm.p != nullptr;
+    DevBuf d_sids, d_dlw, d_ndlw(16);
+    if (use_bm) {
+        d_sids.alloc(uint64_t(kExpBatch) * std::max<int64_t>(d->N, 1) * 4);
+        d_dlw.alloc(SU * sizeof(uint4));
+    }
     // expansion results land in mapped pinned host memory (at most one record per item per slot)
     const uint32_t ecap = std::max<uint32_t>(U, 1);
     PinnedBuf pin(kExpBatch * sizeof(ExpHdr) + kExpBatch * size_t(ecap) * sizeof(ExpRec));
@@ -573,7 +729,20 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         FSM_HIP(hipMemcpyAsync(d_sides.p, sides.data(), nb * sizeof(Side), hipMemcpyHostToDevice, s));
         FSM_HIP(hipMemcpyAsync(d_drv.p, drv_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
         FSM_HIP(hipMemcpyAsync(d_wave.p, wave_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
-        const uint64_t waves = wave_off[nb];
+        const uint64_t waves = use_bm ? 0 : wave_off[nb];
+        if (use_bm) {
+            FSM_HIP(hipMemsetAsync(d_ndlw.p, 0, 4, s));
+            const unsigned gx = unsigned(std::min<uint64_t>((uint64_t(d->NW) + kBlock - 1) / kBlock, 64));
+            hipLaunchKernelGGL(k_rule_sids, dim3(std::max(gx, 1u), nb), dim3(kBlock), 0, s, d_sides.as<Side>(),
+                               d->bm.as<uint32_t>(), d->NW, uint32_t(d->N), d_sids.as<uint32_t>(), ctl.as<ExpCtl>());
+            FSM_LAUNCHED("k_rule_sids", s);
+            hipLaunchKernelGGL(k_expand_bm, dim3(kExpandBlocks, nb), dim3(kBlock), 0, s, d_sides.as<Side>(),
+                               d_sids.as<uint32_t>(), uint32_t(d->N), d->row_off.as<uint32_t>(),
+                               d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(), U,
+                               TL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
+                               ctl.as<ExpCtl>());
+            FSM_LAUNCHED("k_expand_bm", s);
+        }
         if (waves) {
             hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                                d_sides.as<Side>(), d_drv.as<uint64_t>(), d_wave.as<uint64_t>(), nb,
@@ -585,8 +754,14 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
         hipLaunchKernelGGL(k_expand_collect, dim3(kCollectBlocks, nb), dim3(kBlock), 0, s, TL.as<uint32_t>(),
                            DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
-                           ctl.as<ExpCtl>(), U, rp.minsup, d_rec, d_hdr, ecap);
+                           ctl.as<ExpCtl>(), U, rp.minsup, d_rec, d_hdr, ecap,
+                           use_bm ? d_dlw.as<uint4>() : nullptr, d_ndlw.as<uint32_t>());
         FSM_LAUNCHED("k_expand_collect", s);
+        if (use_bm) {
+            hipLaunchKernelGGL(k_dl, dim3(kDlBlocks), dim3(kBlock), 0, s, d_sides.as<Side>(), d->bm.as<uint32_t>(),
+                               d->NW, d_dlw.as<uint4>(), d_ndlw.as<uint32_t>(), d_rec, ecap);
+            FSM_LAUNCHED("k_dl", s);
+        }
         const double tw0 = now_ms();
         FSM_HIP(hipStreamSynchronize(s));
         wait_ms += now_ms() - tw0;
@@ -594,7 +769,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         for (uint32_t k = 0; k < nb; ++k) {
             const ExpHdr h = h_hdr[k];
             if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
-            if (drv_in_x[k] && h.nx != batch[k]->nX)
+            if (!use_bm && drv_in_x[k] && h.nx != batch[k]->nX)
                 throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(h.nx) + " vs " +
                                              std::to_string(batch[k]->nX) + ")");
             ExpResult& res = cache[batch[k]];

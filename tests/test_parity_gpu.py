@@ -306,3 +306,22 @@ def test_sharded_spade_two_ranks(eng, world, D, sup, ref, tmp_path):
         assert canon(r["patterns"]) == exp
         assert r["joins"] == joins
     assert sum(1 for _ in exp) > 100
+
+
+@pytest.mark.parametrize("bitmap", ["1", "0"])
+def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
+    """TSR expansions over sid bitmaps (default) and over the driver item's
+    sid list (FSM_TSR_BITMAP=0, the over-budget fallback) give the oracle's rules."""
+    from oracle import oracle
+    from tools import gen
+    from spark_fsm_amd import MODE_TSR
+    monkeypatch.setenv("FSM_TSR_BITMAP", bitmap)
+    ds = gen.kosarak(D=6000, seed=3)
+    o = oracle.tsr(ds.records(), 300, 0.4)
+    db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)  # bitmaps are built at upload
+    try:
+        rules, meta = eng.tsr(db, 300, 0.4)
+    finally:
+        db.free()
+    rules.sort(key=lambda t: (-t[2], t[0], t[1]))
+    assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
