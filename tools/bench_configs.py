@@ -30,6 +30,8 @@ CONFIGS = {
     "c5-bible": ("spade", "bible", dict(), 0.004),
     "c5-sign": ("spade", "sign", dict(), 0.015),
 }
+# CPU prefix search for TSR starts here (the restatement needs minutes beyond ~20K sequences at k = 1000)
+TSR_CPU_PREFIX = 40000
 
 
 def dataset(shape, kw):
@@ -45,8 +47,9 @@ def log(msg):
     print("[configs %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
 
 
-def time_gpu(fn, reps=3):
-    fn()  # warmup
+def time_gpu(fn, reps=3, warmup=True):
+    if warmup:
+        fn()
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -82,12 +85,12 @@ def run_tsr(eng, fsm, name, ds, params, cpu_s):
     k, mc = params
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
     prep = eng.stats()
-    ms, (rules, meta) = time_gpu(lambda: eng.tsr(db, k, mc), reps=3)
+    ms, (rules, meta) = time_gpu(lambda: eng.tsr(db, k, mc), reps=1, warmup=False)  # a full run is tens of s
     st = eng.stats()
     ks = sorted(eng.kernel_stats(), key=lambda q: -q["ms"])[:4]
     db.free()
-    # CPU: the largest prefix (halving from 200K) whose full run fits the bound
-    n = min(len(ds), 200000)
+    # CPU: the largest prefix (halving from TSR_CPU_PREFIX) whose full run fits the bound
+    n = min(len(ds), TSR_CPU_PREFIX)
     cpu = None
     log("%s: GPU %.2f ms; CPU restatement on prefixes (bound %.0f s each)" % (name, ms, cpu_s))
     while n >= 1000:
