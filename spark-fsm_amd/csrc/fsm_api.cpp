@@ -201,6 +201,7 @@ int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_pa
         ctx->stats = fsm_stats{};
         ctx->stats.ms_flatten = fl;
         ctx->stats.ms_upload = up;
+        ctx->kstats.clear();
         fsm::spade_mine(ctx, db, support, out);
     });
 }
@@ -217,6 +218,7 @@ int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules*
         ctx->stats = fsm_stats{};
         ctx->stats.ms_flatten = fl;
         ctx->stats.ms_upload = up;
+        ctx->kstats.clear();
         fsm::tsr_mine(ctx, db, k, minconf, out);
     });
 }

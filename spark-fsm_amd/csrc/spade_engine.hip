@@ -1,34 +1,33 @@
 // spade_engine.hip — SPADE frequent-sequence mining on MI355X (SURVEY §8a rows
 // a2-a5; the [EXT] SpadeAlgorithm of SPADE.scala:132-135).
 //
-// Layout.  Every prefix equivalence class [P] lives in HBM as a horizontal
-// "class-row" set: one row per sequence containing P, holding one entry per
-// member m of [P] (m = P->x or P x) present in that sequence:
+// Layout.  A batch of prefix equivalence classes [P] lives in HBM as runs: one
+// run per (class, sequence containing P), holding one entry per member m of [P]
+// (m = P->x or P x) present in that sequence, sorted by member id:
+//     cid  u32  class of the entry (index into the batch's class table)
 //     mem  u32  member id = rank(x) << 1 | type   (type 0 = sequence-ext, 1 = itemset-ext)
 //     lohi u32  first | last set eid of the entry's mask (16 bits each)
-//     pos  u32  offset-in-row << 16 | row length  (rows are contiguous runs,
-//               sorted by member id)
+//     pos  u32  offset-in-run << 16 | run length
 //     mask u64[W] eid bitmask (the id-list entry (sid, eids) of member m)
-// The entries of member m across all rows of the class ARE its id-list L(m).
+// The entries of member m across all runs of its class ARE its id-list L(m).
+// Runs are laid out in parent-entry order (see k_emit).
 //
-// Kernels (one launch each per class batch; a batch = hundreds..thousands of
-// classes of one DFS frontier):
-//   k_count        every (entry i, entry j) pair of a row evaluates the temporal /
+// Kernels (one launch each per class batch):
+//   k_count        every (entry i, entry j) pair of a run evaluates the temporal /
 //                  equality join predicate of SURVEY A.2 and bumps the pair's
 //                  support counter: ALL n^2 candidate joins of a class in one
 //                  streaming pass over its entries (vs n^2 separate list merges).
-//   k_rootpair_*   the root class (the F2 pair matrix, by far the largest) counts
-//                  without per-pair global atomics: pairs become 15-bit bucket
-//                  keys (LDS histogram of bucket sizes per block, scatter as u16
-//                  keys), then one LDS histogram of 32768 counters per bucket.
+//   root F2        the root class (the F x 2F pair matrix, by far the largest):
+//                  one enumeration writes every entry's keys as a run, runs are
+//                  indexed by rank group and counted in LDS (k_root_* / k_group_*).
 //   k_freq_*       one wave per member row of the counter matrix: ballot the
 //                  frequent candidates (support >= minsup), give them child member
 //                  ids (wave prefix popcount), compact them for the host.
-//   k_emit         for each entry, walk its member's frequent children, binary-
-//                  search the partner entry in the (member-sorted) row, write the
-//                  joined id-list entries of the child classes into the next slab.
+//   k_emit         (entry, frequent child) pairs flattened across the lanes:
+//                  binary-search the partner entry in the (member-sorted) run,
+//                  write the child runs at scan offsets into the next slab.
 // The root class is the flattened DB restricted to frequent items (F1 = k_f1,
-// row filter = k_root_*).
+// row filter = k_root_count / k_root_write).
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -193,6 +192,12 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
     }
 }
 
+__device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bits [a, b), 0 <= a <= b <= 64
+    const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
+    const uint64_t lo = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
+    return hi & ~lo;
+}
+
 // Root pair enumeration shared by the two bucket passes: calls f(key) for every
 // frequent-item pair (i, j) of the row whose join is non-empty, key = rank_i * D + slot.
 template <int W, class F>
@@ -241,8 +246,10 @@ __global__ __launch_bounds__(kBlock) void k_root_keys(uint32_t E0, const uint32_
                                                       const uint32_t* __restrict__ pos,
                                                       const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
                                                       uint32_t mlo, uint32_t mhi, const uint64_t* __restrict__ koff,
-                                                      uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey) {
+                                                      uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey,
+                                                      uint32_t min_rl) {
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E0; e += gridDim.x * blockDim.x) {
+        if ((pos[e] & 0xFFFFu) <= min_rl) continue;  // row handled by k_root_keys_row
         const uint32_t mi = mem[e];
         uint32_t n = 0;
         if (mi - mlo < mhi - mlo) {
@@ -251,6 +258,82 @@ __global__ __launch_bounds__(kBlock) void k_root_keys(uint32_t E0, const uint32_
             root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { out[n++] = uint16_t(key - gbase); });
         }
         nkey[e] = uint16_t(n);
+    }
+}
+
+// The same enumeration, one wave per root row of <= 64 entries (the
+// per-entry kernel above takes the longer rows): lane l holds entry rb + l in
+// registers; the rl^2 (i, q) pairs are spread over the lanes 64 at a time and
+// read both entries by shuffles, so each row is loaded once, coalesced, and no
+// lane idles behind a long row.  Entry i's keys are compacted into its run by
+// ballot prefixes over the lanes that carry its pairs in the step.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_root_keys_row(uint32_t R, const uint64_t* __restrict__ roff,
+                                                          const uint32_t* __restrict__ mem,
+                                                          const uint32_t* __restrict__ lohi,
+                                                          const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
+                                                          uint32_t mlo, uint32_t mhi,
+                                                          const uint64_t* __restrict__ koff,
+                                                          uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey) {
+    const uint32_t lane = lane_id();
+    const uint32_t wstride = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < R; r += wstride) {
+        const uint32_t rb = uint32_t(roff[r]), rl = uint32_t(roff[r + 1]) - rb;
+        if (rl == 0 || rl > 64) continue;  // wave-uniform
+        uint32_t me = 0, mlh = 0, act = 0;
+        uint64_t mm[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) mm[k] = 0;
+        uint64_t kb = 0;
+        if (lane < rl) {
+            me = mem[rb + lane];
+            mlh = lohi[rb + lane];
+            load_mask<W>(mask + size_t(rb + lane) * W, mm);
+            kb = koff[rb + lane];
+            act = (me - mlo < mhi - mlo) ? 1u : 0u;
+        }
+        uint32_t cnt = 0;  // keys of entry `lane` written so far
+        const uint32_t npairs = rl * rl;
+        for (uint32_t p0 = 0; p0 < npairs; p0 += 64) {
+            const uint32_t p = p0 + lane;
+            const bool valid = p < npairs;
+            const uint32_t i = valid ? p / rl : 0u;
+            const uint32_t q = valid ? p - i * rl : 0u;
+            const uint32_t mi = uint32_t(__shfl(int(me), int(i), 64));
+            const uint32_t li = uint32_t(__shfl(int(mlh), int(i), 64));
+            const uint32_t ai = uint32_t(__shfl(int(act), int(i), 64));
+            const uint64_t kbi = __shfl(kb, int(i), 64);
+            const uint32_t ci = uint32_t(__shfl(int(cnt), int(i), 64));
+            const uint32_t mq = uint32_t(__shfl(int(me), int(q), 64));
+            const uint32_t lq = uint32_t(__shfl(int(mlh), int(q), 64));
+            bool inter = false;
+#pragma unroll
+            for (int k = 0; k < W; ++k) inter |= (__shfl(mm[k], int(i), 64) & __shfl(mm[k], int(q), 64)) != 0ull;
+            const uint32_t ri = mi >> 1, rq = mq >> 1;
+            const bool t_ok = valid && ai && (lq >> 16) > (li & 0xFFFFu);
+            const bool e_ok = valid && ai && rq > ri && inter;
+            const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
+            // lanes of entry i in this step: [a, b)
+            const uint32_t a = (i * rl > p0 ? i * rl - p0 : 0u);
+            const uint32_t b = ((i + 1) * rl - p0 < 64u ? (i + 1) * rl - p0 : 64u);
+            const uint64_t below = lane_range(a, lane), mine = lane_range(a, b);
+            const uint32_t gbase = (ri / per) * per * D;
+            const uint32_t kbase = ri * D - gbase + (rq << 1);
+            if (t_ok) keys[kbi + ci + uint32_t(__popcll(tb & below))] = uint16_t(kbase);
+            if (e_ok)
+                keys[kbi + ci + uint32_t(__popcll(tb & mine)) + uint32_t(__popcll(eb & below))] = uint16_t(kbase | 1u);
+            // every lane, as entry `lane`, adds the keys its pairs produced in this step
+            if (lane < rl) {
+                const uint32_t a2 = (lane * rl > p0 ? lane * rl - p0 : 0u);
+                const uint32_t e2 = (lane + 1) * rl;
+                if (e2 > p0 && a2 < 64u) {
+                    const uint32_t b2 = (e2 - p0 < 64u ? e2 - p0 : 64u);
+                    const uint64_t m2 = lane_range(a2, b2);
+                    cnt += uint32_t(__popcll(tb & m2)) + uint32_t(__popcll(eb & m2));
+                }
+            }
+        }
+        if (lane < rl) nkey[rb + lane] = uint16_t(cnt);
     }
 }
 
@@ -362,11 +445,6 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
 // takes one pair per step (owner found by a 6-step shuffle search).  Kid counts
 // are heavily skewed (popular members have dozens of frequent children), so a
 // thread-per-entry loop would leave most lanes idle behind the longest list.
-__device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bits [a, b), 0 <= a <= b <= 64
-    const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
-    const uint64_t lo = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
-    return hi & ~lo;
-}
 
 template <int W, bool kWrite>
 __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __restrict__ cid,
@@ -555,6 +633,8 @@ struct Batch {
     size_t next_group = 0;
     int64_t depth = 1;  // items per member pattern of this batch's classes
     bool root = false;
+    DevBuf root_rows;   // root batch: u64 [R+1] slab offset of every DB row's run
+    uint64_t R = 0;
 };
 
 struct Miner {
@@ -681,14 +761,30 @@ struct Miner {
         if (nslots >= (uint64_t(1) << 32)) return false;  // run offsets are kept in u32
         // the one enumeration
         DevBuf keys(std::max<uint64_t>(nslots, 1) * 2), nkey(uint64_t(E0) * 2);
+        // rows of <= 64 entries: one wave per row; longer rows (and a root
+        // without row offsets): the per-entry kernel
+        const bool rows = b.root_rows.p != nullptr && b.R > 0;
+        const uint32_t min_rl = rows ? 64u : 0u;
+        if (rows) {
+            tk = clk->begin("k_root_keys_row");
+            const unsigned rgrid = unsigned(std::min<uint64_t>((b.R * 64 + kBlock - 1) / kBlock, 1u << 16));
+#define FSM_RKR(WW)                                                                                                 \
+    hipLaunchKernelGGL(k_root_keys_row<WW>, dim3(rgrid), dim3(kBlock), 0, s, uint32_t(b.R),                       \
+                       b.root_rows.as<uint64_t>(), sp.mem, sp.lohi, sp.mask, D, per, mlo, mhi, koff.as<uint64_t>(), \
+                       keys.as<uint16_t>(), nkey.as<uint16_t>())
+            FSM_W_DISPATCH(W, FSM_RKR)
+#undef FSM_RKR
+            FSM_LAUNCHED("k_root_keys_row", s);
+            clk->end(tk, slab_bytes + int64_t(E0) * 10 + int64_t(nslots) * 2);
+        }
         tk = clk->begin("k_root_keys");
 #define FSM_RK(WW)                                                                                             \
     hipLaunchKernelGGL(k_root_keys<WW>, dim3(grid), dim3(kBlock), 0, s, E0, sp.mem, sp.lohi, sp.pos, sp.mask, \
-                       D, per, mlo, mhi, koff.as<uint64_t>(), keys.as<uint16_t>(), nkey.as<uint16_t>())
+                       D, per, mlo, mhi, koff.as<uint64_t>(), keys.as<uint16_t>(), nkey.as<uint16_t>(), min_rl)
         FSM_W_DISPATCH(W, FSM_RK)
 #undef FSM_RK
         FSM_LAUNCHED("k_root_keys", s);
-        clk->end(tk, slab_bytes + int64_t(E0) * 10 + int64_t(nslots) * 2);
+        clk->end(tk, rows ? int64_t(E0) * 4 : slab_bytes + int64_t(E0) * 10 + int64_t(nslots) * 2);
         // runs in group order
         const uint32_t chunk = root_chunk();
         const uint32_t nblk = (E0 + chunk - 1) / chunk;
@@ -987,6 +1083,8 @@ struct Miner {
         m.nent = uint32_t(E0);
         root.cls.push_back(std::move(m));
         root.root = true;
+        root.root_rows = std::move(roff);
+        root.R = r1 - r0;
         FSM_HIP(hipStreamSynchronize(s));
     }
 
