@@ -1,5 +1,5 @@
-// device_util.hip — three-phase exclusive scan (tile scan -> scan of tile sums
-// -> add), 2048 elements per 256-thread tile, wave64 shuffles + LDS.
+// device_util.hip — single-pass exclusive scan (decoupled look-back), the
+// device memory pool and kernel timing.
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -11,48 +11,88 @@
 namespace fsm {
 namespace {
 
+// One launch per scan: tiles of 4096 elements are claimed in order through a
+// ticket, each wave scans 16 coalesced 64-element chunks of its 1024, the
+// block combines its 4 waves in LDS, then thread 0 publishes the tile's
+// aggregate and walks back over its predecessors' status words until it meets
+// an inclusive prefix (flag and value packed in one u64, so relaxed agent-scope
+// atomics are enough).  Ticket order means every tile a block waits on has
+// already started, so the walk always ends.  No tile-sum buffers and no host
+// synchronisation: the only scratch is the per-stream status array, cleared
+// by one memset per scan.
 constexpr int kScanT = 256;
-constexpr int kScanV = 8;
+constexpr int kScanV = 16;
 constexpr int kScanTile = kScanT * kScanV;
+constexpr uint64_t kStAgg = uint64_t(1) << 62, kStPre = uint64_t(2) << 62, kStVal = kStAgg - 1;
 
 template <class T>
-__global__ __launch_bounds__(kScanT) void k_scan_tile(const T* __restrict__ in, uint64_t* __restrict__ out,
-                                                      uint64_t* __restrict__ tile_sum, size_t n) {
+__global__ __launch_bounds__(kScanT) void k_scan(const T* __restrict__ in, uint64_t* __restrict__ out, size_t n,
+                                                 uint32_t* __restrict__ ticket, uint64_t* __restrict__ state) {
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_excl;
     __shared__ uint64_t wsum[kScanT / 64];
-    const size_t base = size_t(blockIdx.x) * kScanTile + size_t(threadIdx.x) * kScanV;
-    uint64_t v[kScanV];
-    uint64_t s = 0;
-#pragma unroll
-    for (int k = 0; k < kScanV; ++k) {
-        const size_t i = base + size_t(k);
-        v[k] = i < n ? uint64_t(in[i]) : 0ull;
-        s += v[k];
-    }
-    const uint64_t incl = wave_incl_scan(s);
-    const unsigned wave = threadIdx.x >> 6;
-    if (lane_id() == 63) wsum[wave] = incl;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
-    uint64_t woff = 0;
-    for (unsigned w = 0; w < wave; ++w) woff += wsum[w];
-    uint64_t run = woff + incl - s;
+    const uint32_t tile = s_tile;
+    const unsigned lane = lane_id(), wave = threadIdx.x >> 6;
+    const size_t wbase = size_t(tile) * kScanTile + size_t(wave) * 64 * kScanV;
+    uint64_t r[kScanV];
+    uint64_t run = 0;
 #pragma unroll
     for (int k = 0; k < kScanV; ++k) {
-        const size_t i = base + size_t(k);
-        if (i < n) out[i] = run;
-        run += v[k];
+        const size_t i = wbase + size_t(k) * 64 + lane;
+        const uint64_t x = i < n ? uint64_t(in[i]) : 0ull;
+        const uint64_t inc = wave_incl_scan(x);
+        r[k] = run + inc - x;
+        run += __shfl(inc, 63, 64);
     }
-    if (threadIdx.x == kScanT - 1) tile_sum[blockIdx.x] = woff + incl;
+    if (lane == 0) wsum[wave] = run;
+    __syncthreads();
+    uint64_t woff = 0, tot = 0;
+#pragma unroll
+    for (unsigned w = 0; w < kScanT / 64; ++w) {
+        woff += w < wave ? wsum[w] : 0ull;
+        tot += wsum[w];
+    }
+    if (threadIdx.x == 0) {
+        uint64_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(&state[0], kStPre | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&state[tile], kStAgg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = int64_t(tile) - 1;
+            for (;;) {
+                const uint64_t st = __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (st == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += st & kStVal;
+                if (st & kStPre) break;
+                --j;
+            }
+            __hip_atomic_store(&state[tile], kStPre | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_excl = excl;
+        if ((size_t(tile) + 1) * kScanTile >= n) out[n] = excl + tot;  // the last tile writes the total
+    }
+    __syncthreads();
+    const uint64_t base = s_excl + woff;
+#pragma unroll
+    for (int k = 0; k < kScanV; ++k) {
+        const size_t i = wbase + size_t(k) * 64 + lane;
+        if (i < n) out[i] = base + r[k];
+    }
 }
 
-__global__ __launch_bounds__(kScanT) void k_scan_add(uint64_t* __restrict__ out, const uint64_t* __restrict__ tile_off,
-                                                     size_t n) {
-    const uint64_t add = tile_off[blockIdx.x];
-    const size_t base = size_t(blockIdx.x) * kScanTile + size_t(threadIdx.x) * kScanV;
-#pragma unroll
-    for (int k = 0; k < kScanV; ++k) {
-        const size_t i = base + size_t(k);
-        if (i < n) out[i] += add;
-    }
+struct ScanScratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_scan_mu;
+std::map<hipStream_t, ScanScratch>& scan_scratch() {
+    static auto* m = new std::map<hipStream_t, ScanScratch>();  // leaked on exit on purpose
+    return *m;
 }
 
 template <class T> void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s) {
@@ -61,20 +101,29 @@ template <class T> void scan_impl(const T* in, uint64_t* out, size_t n, hipStrea
         return;
     }
     const size_t nt = (n + kScanTile - 1) / kScanTile;
-    if (nt == 1) {
-        hipLaunchKernelGGL(k_scan_tile<T>, dim3(1), dim3(kScanT), 0, s, in, out, out + n, n);
-        FSM_LAUNCHED("k_scan_tile", s);
-        return;
+    if (nt >= (size_t(1) << 31)) throw Error(FSM_ELIMIT, "scan: too many elements");
+    const size_t need = (nt + 1) * sizeof(uint64_t);  // [ticket | state[nt]]
+    void* scr;
+    {
+        std::lock_guard<std::mutex> g(g_scan_mu);
+        ScanScratch& sc = scan_scratch()[s];
+        if (sc.bytes < need) {
+            if (sc.p) {
+                FSM_HIP(hipStreamSynchronize(s));
+                FSM_HIP(hipFree(sc.p));
+                sc.p = nullptr;
+                sc.bytes = 0;
+            }
+            const size_t want = std::max<size_t>(need, size_t(1) << 16);
+            FSM_HIP(hipMalloc(&sc.p, want));
+            sc.bytes = want;
+        }
+        scr = sc.p;
     }
-    DevBuf sums((nt) * sizeof(uint64_t));
-    DevBuf offs((nt + 1) * sizeof(uint64_t));
-    hipLaunchKernelGGL(k_scan_tile<T>, dim3(unsigned(nt)), dim3(kScanT), 0, s, in, out, sums.as<uint64_t>(), n);
-    FSM_LAUNCHED("k_scan_tile", s);
-    scan_impl<uint64_t>(sums.as<uint64_t>(), offs.as<uint64_t>(), nt, s);
-    hipLaunchKernelGGL(k_scan_add, dim3(unsigned(nt)), dim3(kScanT), 0, s, out, offs.as<uint64_t>(), n);
-    FSM_LAUNCHED("k_scan_add", s);
-    FSM_HIP(hipMemcpyAsync(out + n, offs.as<uint64_t>() + nt, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
-    FSM_HIP(hipStreamSynchronize(s));  // sums/offs are released on return
+    FSM_HIP(hipMemsetAsync(scr, 0, need, s));
+    hipLaunchKernelGGL(k_scan<T>, dim3(unsigned(nt)), dim3(kScanT), 0, s, in, out, n, static_cast<uint32_t*>(scr),
+                       static_cast<uint64_t*>(scr) + 1);
+    FSM_LAUNCHED("k_scan", s);
 }
 
 }  // namespace
