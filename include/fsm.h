@@ -126,6 +126,8 @@ typedef struct {
     int64_t count_launches;
     int64_t mask_words;         /* W: u64 words per eid mask of this DB */
     int64_t bytes_count_alg;    /* count kernel algorithmic bytes: entries * (12 + 8W) */
+    double ms_gpu_wait;         /* SPADE: host time blocked on the stream during F1/F2/lattice */
+    double ms_output;           /* SPADE: host build of the pattern CSR */
 } fsm_stats;
 
 /* Per-kernel device time of the last fsm_*_mine call (HIP events on the

@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <memory>
 #include <numeric>
+#include <thread>
 
 #include "comm.h"
 #include "device_util.h"
@@ -652,6 +653,13 @@ struct Miner {
     uint32_t slice_lo = 0, slice_hi = kNone;
     size_t n_shared = 0;  // pattern nodes every rank holds (root + its frequent children)
 
+    double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
+    void sync() {
+        const double t = now_ms();
+        FSM_HIP(hipStreamSynchronize(s));
+        wait_ms += now_ms() - t;
+    }
+
     uint64_t entry_bytes() const { return 16ull + 8ull * uint64_t(W); }  // cid, mem, lohi, pos, mask
 
     // pageable H2D copies are staged before hipMemcpyAsync returns; callers keep
@@ -707,7 +715,7 @@ struct Miner {
         FSM_HIP(hipMemcpyAsync(lohi.data(), b.slab.lohi.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(pos.data(), b.slab.pos.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(mk.data(), b.slab.mask.p, n * 8 * W, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipStreamSynchronize(s));
+        sync();
         std::fprintf(stderr, "[dump] depth=%lld classes=%zu\n", (long long)b.depth, b.cls.size());
         for (uint64_t e = 0; e < n; ++e) {
             std::fprintf(stderr, "    e=%llu cls=%u mem=%u lo=%u hi=%u off=%u len=%u mask=", (unsigned long long)e,
@@ -757,7 +765,7 @@ struct Miner {
         ub.release();
         uint64_t nslots = 0;
         FSM_HIP(hipMemcpyAsync(&nslots, koff.as<uint64_t>() + E0, 8, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipStreamSynchronize(s));
+        sync();
         if (nslots >= (uint64_t(1) << 32)) return false;  // run offsets are kept in u32
         // the one enumeration
         DevBuf keys(std::max<uint64_t>(nslots, 1) * 2), nkey(uint64_t(E0) * 2);
@@ -808,7 +816,7 @@ struct Miner {
                            keys.as<uint16_t>(), D, per, F, cnt);
         FSM_LAUNCHED("k_group_count", s);
         clk->end(tk, int64_t(E0) * 8 + int64_t(nslots) * 2 + int64_t(K) * 4);
-        FSM_HIP(hipStreamSynchronize(s));  // temporaries released on return
+        sync();  // temporaries released on return
         return true;
     }
 
@@ -865,7 +873,7 @@ struct Miner {
         scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
         uint64_t nfreq = 0;
         FSM_HIP(hipMemcpyAsync(&nfreq, rowoff.as<uint64_t>() + nrows, 8, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipStreamSynchronize(s));
+        sync();
         std::vector<FreqRec> recs(nfreq);
         if (nfreq) {
             DevBuf d_recs(nfreq * sizeof(FreqRec));
@@ -877,7 +885,7 @@ struct Miner {
             clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
                                  nfreq * sizeof(FreqRec)));
             FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nfreq * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
-            FSM_HIP(hipStreamSynchronize(s));
+            sync();
         }
         cnt.release();
         if (shard) {  // every rank gets every frequent pair, in row order (slices ascend with the rank)
@@ -1022,7 +1030,7 @@ struct Miner {
 #undef FSM_EMIT
             FSM_HIP(hipMemcpyAsync(&written, off.as<uint64_t>() + b.E, 8, hipMemcpyDeviceToHost, s));
         }
-        FSM_HIP(hipStreamSynchronize(s));
+        sync();
         // the runs must add up exactly to the capacities (sum of child supports)
         if (written != total)
             throw Error(FSM_EDEVICE, "SPADE emit: wrote " + std::to_string(written) + " child entries, expected " +
@@ -1051,7 +1059,7 @@ struct Miner {
         uint32_t fl = 0;
         FSM_HIP(hipMemcpyAsync(&E0, roff.as<uint64_t>() + (r1 - r0), 8, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(&fl, flag.p, 4, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipStreamSynchronize(s));
+        sync();
         if (fl) throw Error(FSM_ELIMIT, "SPADE: a sequence has more than 65535 distinct frequent items");
         if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
         root.slab.alloc(E0, W);
@@ -1085,7 +1093,7 @@ struct Miner {
         root.root = true;
         root.root_rows = std::move(roff);
         root.R = r1 - r0;
-        FSM_HIP(hipStreamSynchronize(s));
+        sync();
     }
 
 };
@@ -1285,29 +1293,52 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     }
 
     // ---- output CSR in discovery order (the reference's order is discovery order too);
-    // sharded: rank 0 holds the shared root levels, every rank its own classes
+    // sharded: rank 0 holds the shared root levels, every rank its own classes.
+    // A node's parent precedes it, so item / itemset counts are one forward
+    // pass, and every pattern then fills its own slice by walking its parents
+    // (independent slices: split over host threads).
+    const double to0 = now_ms();
+    ctx->stats.ms_gpu_wait = mn.wait_ms;
     const auto& nodes = mn.nodes;
+    const int64_t NN = int64_t(nodes.size());
     const int64_t first = (comm && comm->rank() != 0) ? int64_t(mn.n_shared) : 0;
-    int64_t n = int64_t(nodes.size()) - first;
-    std::vector<int32_t> sup(static_cast<size_t>(n));
-    std::vector<int64_t> pat_off(size_t(n) + 1, 0), set_off(1, 0);
-    std::vector<int32_t> items;
-    std::vector<uint32_t> path_item, path_type;
-    for (int64_t k = first; k < int64_t(nodes.size()); ++k) {
-        path_item.clear();
-        path_type.clear();
-        for (int32_t q = int32_t(k); q >= 0; q = nodes[size_t(q)].parent) {
-            path_item.push_back(nodes[size_t(q)].item);
-            path_type.push_back(nodes[size_t(q)].type);
-        }
-        for (size_t t = path_item.size(); t-- > 0;) {
-            if (path_type[t] == kSeq && t != path_item.size() - 1) set_off.push_back(int64_t(items.size()));
-            items.push_back(db->spade.item_val[path_item[t]]);
-        }
-        set_off.push_back(int64_t(items.size()));
-        sup[size_t(k - first)] = int32_t(nodes[size_t(k)].support);
-        pat_off[size_t(k - first) + 1] = int64_t(set_off.size()) - 1;
+    int64_t n = NN - first;
+    std::vector<uint32_t> plen(static_cast<size_t>(NN)), pset(static_cast<size_t>(NN));
+    for (int64_t k = 0; k < NN; ++k) {
+        const int32_t q = nodes[size_t(k)].parent;
+        plen[size_t(k)] = (q < 0 ? 0u : plen[size_t(q)]) + 1u;
+        pset[size_t(k)] = (q < 0 ? 0u : pset[size_t(q)]) + ((q < 0 || nodes[size_t(k)].type == kSeq) ? 1u : 0u);
     }
+    std::vector<int32_t> sup(static_cast<size_t>(n));
+    std::vector<int64_t> pat_off(size_t(n) + 1, 0), item_off(size_t(n) + 1, 0);
+    for (int64_t k = 0; k < n; ++k) {
+        pat_off[size_t(k) + 1] = pat_off[size_t(k)] + pset[size_t(first + k)];
+        item_off[size_t(k) + 1] = item_off[size_t(k)] + plen[size_t(first + k)];
+    }
+    std::vector<int64_t> set_off(size_t(pat_off[size_t(n)]) + 1);
+    std::vector<int32_t> items(static_cast<size_t>(item_off[size_t(n)]));
+    set_off.back() = item_off[size_t(n)];
+    const int32_t* ival = db->spade.item_val.data();
+    auto fill = [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; ++k) {
+            int64_t pos = item_off[size_t(k) + 1], sidx = pat_off[size_t(k) + 1];
+            for (int32_t q = int32_t(first + k); q >= 0; q = nodes[size_t(q)].parent) {
+                const PNode& nd = nodes[size_t(q)];
+                items[size_t(--pos)] = ival[nd.item];
+                if (nd.parent < 0 || nd.type == kSeq) set_off[size_t(--sidx)] = pos;
+            }
+            sup[size_t(k)] = int32_t(nodes[size_t(first + k)].support);
+        }
+    };
+    const int64_t nthr = n >= (int64_t(1) << 17) ? int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)) : 1;
+    if (nthr > 1) {
+        std::vector<std::thread> th;
+        for (int64_t t = 0; t < nthr; ++t) th.emplace_back(fill, n * t / nthr, n * (t + 1) / nthr);
+        for (auto& x : th) x.join();
+    } else {
+        fill(0, n);
+    }
+    ctx->stats.ms_output = now_ms() - to0;
     if (comm) {
         gather_patterns(comm, ctx->stream, sup, pat_off, set_off, items);
         n = int64_t(sup.size());

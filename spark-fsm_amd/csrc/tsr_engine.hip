@@ -696,6 +696,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     std::unordered_map<Rule*, ExpResult> cache;
     int64_t expansions = 0, launches = 0, spec_pushback = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
+    double last_log_ms = now_ms();  // verbose progress line every 20 s
     std::vector<Side> sides;
     std::vector<uint64_t> drv_off, wave_off;
 
@@ -781,7 +782,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
 
     auto commit = [&](Rule* r, const std::vector<ExpRec>& er) {
         expansions += r->expandLR ? 2 : 1;
-        if (ctx->opts.verbose && (expansions & 0xFFFF) < 2)
+        if (ctx->opts.verbose && now_ms() - last_log_ms > 20000.0 && (last_log_ms = now_ms()) > 0)
             std::fprintf(stderr, "[fsm tsr] %lld expansions, minsup %u, candidates %zu, rules %zu, %.0f ms\n",
                          (long long)expansions, rp.minsup, rp.cand.size(), rp.krules.size(), now_ms() - t0);
         if (r->expandLR) {  // expandL: X u {c} => Y

@@ -120,11 +120,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--verbose", action="store_true", help="engine progress on stderr (long TSR runs)")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime per process, see _lib.py)
     import spark_fsm_amd as fsm
     want = [c for c in args.only.split(",") if c] or list(CONFIGS)
-    with fsm.Engine(0) as eng:
+    with fsm.Engine(0, verbose=args.verbose) as eng:
         for name in want:
             algo, shape, kw, par = CONFIGS[name]
             log("%s: generating %s" % (name, shape))
