@@ -263,11 +263,21 @@ __global__ __launch_bounds__(kBlock) void k_root_keys(uint32_t E0, const uint32_
 }
 
 // The same enumeration, one wave per root row of <= 64 entries (the
-// per-entry kernel above takes the longer rows): lane l holds entry rb + l in
-// registers; the rl^2 (i, q) pairs are spread over the lanes 64 at a time and
-// read both entries by shuffles, so each row is loaded once, coalesced, and no
-// lane idles behind a long row.  Entry i's keys are compacted into its run by
-// ballot prefixes over the lanes that carry its pairs in the step.
+// per-entry kernel above takes the longer rows): lane q holds entry rb + q in
+// registers for the whole row; the wave walks the row's entries i in order
+// (wave-uniform, operands of i broadcast by readlane into scalar registers)
+// and every lane tests its entry q as i's partner.  Entry i's keys of a step
+// are two ballots: temporal keys at popcount(tb below the lane), equality
+// keys after them, so each step writes one contiguous stretch of i's run.
+// No division or cross-lane search per pair: two ballots, two mbcnt and the
+// predicate per (i, row) step.
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) {
+    return uint32_t(__builtin_amdgcn_readlane(int(v), int(l)));
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
+    return uint64_t(rl32(uint32_t(v), l)) | (uint64_t(rl32(uint32_t(v >> 32), l)) << 32);
+}
+
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_root_keys_row(uint32_t R, const uint64_t* __restrict__ roff,
                                                           const uint32_t* __restrict__ mem,
@@ -277,64 +287,48 @@ __global__ __launch_bounds__(kBlock) void k_root_keys_row(uint32_t R, const uint
                                                           const uint64_t* __restrict__ koff,
                                                           uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey) {
     const uint32_t lane = lane_id();
+    const uint64_t lt = lanemask_lt();
     const uint32_t wstride = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < R; r += wstride) {
         const uint32_t rb = uint32_t(roff[r]), rl = uint32_t(roff[r + 1]) - rb;
         if (rl == 0 || rl > 64) continue;  // wave-uniform
-        uint32_t me = 0, mlh = 0, act = 0;
+        const bool v = lane < rl;
+        uint32_t me = 0, mlh = 0, act = 0, kb_lo = 0, kb_hi = 0, kbase = 0;
         uint64_t mm[W];
 #pragma unroll
         for (int k = 0; k < W; ++k) mm[k] = 0;
-        uint64_t kb = 0;
-        if (lane < rl) {
+        if (v) {
             me = mem[rb + lane];
             mlh = lohi[rb + lane];
             load_mask<W>(mask + size_t(rb + lane) * W, mm);
-            kb = koff[rb + lane];
+            const uint64_t kb = koff[rb + lane];
+            kb_lo = uint32_t(kb);
+            kb_hi = uint32_t(kb >> 32);
             act = (me - mlo < mhi - mlo) ? 1u : 0u;
+            const uint32_t ri = me >> 1;
+            kbase = ri * D - (ri / per) * per * D;  // entry's counter row, local to its rank group
         }
-        uint32_t cnt = 0;  // keys of entry `lane` written so far
-        const uint32_t npairs = rl * rl;
-        for (uint32_t p0 = 0; p0 < npairs; p0 += 64) {
-            const uint32_t p = p0 + lane;
-            const bool valid = p < npairs;
-            const uint32_t i = valid ? p / rl : 0u;
-            const uint32_t q = valid ? p - i * rl : 0u;
-            const uint32_t mi = uint32_t(__shfl(int(me), int(i), 64));
-            const uint32_t li = uint32_t(__shfl(int(mlh), int(i), 64));
-            const uint32_t ai = uint32_t(__shfl(int(act), int(i), 64));
-            const uint64_t kbi = __shfl(kb, int(i), 64);
-            const uint32_t ci = uint32_t(__shfl(int(cnt), int(i), 64));
-            const uint32_t mq = uint32_t(__shfl(int(me), int(q), 64));
-            const uint32_t lq = uint32_t(__shfl(int(mlh), int(q), 64));
+        const uint32_t rq = me >> 1, hq = mlh >> 16;
+        const uint64_t actb = __ballot(act != 0u);
+        uint32_t mycnt = 0;
+        for (uint32_t i = 0; i < rl; ++i) {
+            if (!((actb >> i) & 1ull)) continue;  // entry i counted by another rank (uniform)
+            const uint32_t ri = rl32(me, i) >> 1;
+            const uint32_t li = rl32(mlh, i) & 0xFFFFu;
             bool inter = false;
 #pragma unroll
-            for (int k = 0; k < W; ++k) inter |= (__shfl(mm[k], int(i), 64) & __shfl(mm[k], int(q), 64)) != 0ull;
-            const uint32_t ri = mi >> 1, rq = mq >> 1;
-            const bool t_ok = valid && ai && (lq >> 16) > (li & 0xFFFFu);
-            const bool e_ok = valid && ai && rq > ri && inter;
+            for (int k = 0; k < W; ++k) inter |= (mm[k] & rl64(mm[k], i)) != 0ull;
+            const bool t_ok = v && hq > li;
+            const bool e_ok = v && rq > ri && inter;
             const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
-            // lanes of entry i in this step: [a, b)
-            const uint32_t a = (i * rl > p0 ? i * rl - p0 : 0u);
-            const uint32_t b = ((i + 1) * rl - p0 < 64u ? (i + 1) * rl - p0 : 64u);
-            const uint64_t below = lane_range(a, lane), mine = lane_range(a, b);
-            const uint32_t gbase = (ri / per) * per * D;
-            const uint32_t kbase = ri * D - gbase + (rq << 1);
-            if (t_ok) keys[kbi + ci + uint32_t(__popcll(tb & below))] = uint16_t(kbase);
-            if (e_ok)
-                keys[kbi + ci + uint32_t(__popcll(tb & mine)) + uint32_t(__popcll(eb & below))] = uint16_t(kbase | 1u);
-            // every lane, as entry `lane`, adds the keys its pairs produced in this step
-            if (lane < rl) {
-                const uint32_t a2 = (lane * rl > p0 ? lane * rl - p0 : 0u);
-                const uint32_t e2 = (lane + 1) * rl;
-                if (e2 > p0 && a2 < 64u) {
-                    const uint32_t b2 = (e2 - p0 < 64u ? e2 - p0 : 64u);
-                    const uint64_t m2 = lane_range(a2, b2);
-                    cnt += uint32_t(__popcll(tb & m2)) + uint32_t(__popcll(eb & m2));
-                }
-            }
+            const uint64_t kbi = uint64_t(rl32(kb_lo, i)) | (uint64_t(rl32(kb_hi, i)) << 32);
+            const uint32_t key = rl32(kbase, i) + (rq << 1);
+            const uint32_t nt = uint32_t(__popcll(tb));
+            if (t_ok) keys[kbi + uint32_t(__popcll(tb & lt))] = uint16_t(key);
+            if (e_ok) keys[kbi + nt + uint32_t(__popcll(eb & lt))] = uint16_t(key | 1u);
+            if (lane == i) mycnt = nt + uint32_t(__popcll(eb));
         }
-        if (lane < rl) nkey[rb + lane] = uint16_t(cnt);
+        if (v) nkey[rb + lane] = uint16_t(mycnt);
     }
 }
 

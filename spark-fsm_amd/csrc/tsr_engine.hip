@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <deque>
 #include <memory>
 #include <queue>
 #include <set>
@@ -50,6 +52,20 @@ constexpr int kCollectBlocks = 8;   // collect blocks per rule slot
 constexpr int kExpBatch = 32;       // rules expanded per launch (speculative, committed in order)
 constexpr int kExpandBlocks = 128;  // bitmap path: expansion blocks per rule slot
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
+// FSM_TSR_GRID="expand,collect,dl" overrides the per-launch grids (tuning sweeps)
+struct TsrGrid {
+    unsigned expand = kExpandBlocks, collect = kCollectBlocks, dl = kDlBlocks;
+    TsrGrid() {
+        if (const char* v = std::getenv("FSM_TSR_GRID")) {
+            unsigned a = 0, b = 0, c = 0;
+            if (std::sscanf(v, "%u,%u,%u", &a, &b, &c) == 3 && a && b && c && a <= 4096 && b <= 4096 && c <= 4096) {
+                expand = a;
+                collect = b;
+                dl = c;
+            }
+        }
+    }
+};
 
 __global__ __launch_bounds__(kBlock) void k_vcount(const uint32_t* __restrict__ item, uint64_t E,
                                                    uint32_t* __restrict__ cnt) {
@@ -311,7 +327,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
             ctl->nout = 0;
             ctl->done = 0;
             ctl->nsid = 0;
-            __threadfence_system();
+            // no system-scope fence: the host reads hdr / out after the stream
+            // synchronizes, and kernel completion already releases to the host
         }
     }
 }
@@ -330,83 +347,77 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_build(const uint32_t* __restr
     }
 }
 
-// slot b (blockIdx.y): the sids holding every item of X u Y -> slot sid list
-__global__ __launch_bounds__(kBlock) void k_rule_sids(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
-                                                      uint32_t NW, uint32_t N, uint32_t* __restrict__ sidsb,
-                                                      ExpCtl* __restrict__ ctlb) {
-    const uint32_t b = blockIdx.y;
-    const Side& side = sides[b];
-    uint32_t* out = sidsb + uint64_t(b) * N;
-    ExpCtl* ctl = ctlb + b;
-    const uint32_t lane = lane_id();
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t w0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); w0 < NW; w0 += stride) {
-        const uint32_t w = w0 + lane;
-        uint32_t v = 0;
-        if (w < NW) {
-            v = ~0u;
-            for (uint32_t k = 0; k < side.nx; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
-            for (uint32_t k = 0; k < side.ny; ++k) v &= bm[uint64_t(side.Y[k]) * NW + w];
-        }
-        const uint32_t cnt = uint32_t(__popc(v));
-        const uint32_t incl = wave_incl_scan(cnt);
-        const uint32_t tot = uint32_t(__shfl(int(incl), 63, 64));
-        uint32_t base = 0;
-        if (lane == 63 && tot) base = atomicAdd(&ctl->nsid, tot);
-        base = uint32_t(__shfl(int(base), 63, 64));
-        uint32_t p = base + incl - cnt;
-        while (v) {
-            const uint32_t bit = uint32_t(__builtin_ctz(v));
-            out[p++] = w * 32u + bit;
-            v &= v - 1u;
-        }
-    }
-}
-
-// expansion over the slot's sid list (one wave per sid): TL / TR only
-__global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides,
-                                                      const uint32_t* __restrict__ sidsb, uint32_t N,
-                                                      const uint32_t* __restrict__ row_off,
+// Expansion of slot b (blockIdx.y) over the sids holding every item of X u Y.
+// Block x owns a contiguous range of bitmap words: it ANDs the rule's |X|+|Y|
+// item bitmaps over its range a chunk at a time, compacts the set sids into
+// LDS, and its waves then take those sids one per wave: TL / TR histograms.
+constexpr uint32_t kChunkWords = 256;  // bitmap words per LDS round (<= 8192 sids)
+__global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
+                                                      uint32_t NW, const uint32_t* __restrict__ row_off,
                                                       const uint32_t* __restrict__ item,
                                                       const uint32_t* __restrict__ first,
                                                       const uint32_t* __restrict__ last, uint32_t U,
                                                       uint32_t* __restrict__ TLb, uint32_t* __restrict__ TRb,
                                                       uint32_t* __restrict__ seenb, uint32_t* __restrict__ listb,
-                                                      ExpCtl* __restrict__ ctlb) {
+                                                      ExpCtl* __restrict__ ctlb, uint32_t* __restrict__ ndlw) {
+    __shared__ uint32_t lsid[kChunkWords * 32];
+    __shared__ uint32_t ln;
     const uint64_t b = blockIdx.y, U64 = U;
     const Side& side = sides[b];
-    const uint32_t* sids = sidsb + b * N;
     uint32_t* TL = TLb + b * U64;
     uint32_t* TR = TRb + b * U64;
     uint32_t* seen = seenb + b * U64;
     uint32_t* list = listb + b * U64;
     ExpCtl* ctl = ctlb + b;
-    const uint32_t nsid = ctl->nsid;
+    // k_expand_collect (next on the stream) appends the k_dl work list
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ndlw = 0u;
     const uint32_t lane = lane_id();
-    const uint32_t wpb = blockDim.x >> 6;
-    for (uint32_t v = blockIdx.x * wpb + (threadIdx.x >> 6); v < nsid; v += gridDim.x * wpb) {
-        const uint32_t s = sids[v];
-        const uint32_t rb = row_off[s], re = row_off[s + 1];
-        uint32_t fX = 0, lY = 0xFFFFFFFFu;
-        for (uint32_t k = lane; k < side.nx; k += 64) fX = max(fX, first[row_find(item, rb, re, side.X[k])]);
-        for (uint32_t k = lane; k < side.ny; k += 64) lY = min(lY, last[row_find(item, rb, re, side.Y[k])]);
-        fX = wave_max(fX);
-        lY = wave_min(lY);
-        if (fX >= lY) continue;  // X => Y does not hold in s
-        if (side.doL) {          // expandL: c > max(X), c not in Y, c before lastY(s)
-            const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
-            for (uint32_t q = q0 + lane; q < re; q += 64) {
-                const uint32_t c = item[q];
-                if (first[q] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
+    const uint32_t wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const uint32_t w0 = uint32_t(uint64_t(blockIdx.x) * NW / gridDim.x);
+    const uint32_t w1 = uint32_t(uint64_t(blockIdx.x + 1) * NW / gridDim.x);
+    for (uint32_t c0 = w0; c0 < w1; c0 += kChunkWords) {
+        const uint32_t c1 = min(w1, c0 + kChunkWords);
+        if (threadIdx.x == 0) ln = 0;
+        __syncthreads();
+        for (uint32_t w = c0 + threadIdx.x; w < c1; w += blockDim.x) {
+            uint32_t v = ~0u;
+            for (uint32_t k = 0; k < side.nx && v; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
+            for (uint32_t k = 0; k < side.ny && v; ++k) v &= bm[uint64_t(side.Y[k]) * NW + w];
+            if (v) {
+                uint32_t p = atomicAdd(&ln, uint32_t(__popc(v)));
+                while (v) {
+                    lsid[p++] = w * 32u + uint32_t(__builtin_ctz(v));
+                    v &= v - 1u;
+                }
             }
         }
-        if (side.doR) {          // expandR: c > max(Y), c not in X, c after firstX(s)
-            const uint32_t q0 = row_find(item, rb, re, side.maxY + 1);
-            for (uint32_t q = q0 + lane; q < re; q += 64) {
-                const uint32_t c = item[q];
-                if (last[q] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
+        __syncthreads();
+        const uint32_t n = ln;
+        for (uint32_t q = wv; q < n; q += wpb) {
+            const uint32_t s = lsid[q];
+            const uint32_t rb = row_off[s], re = row_off[s + 1];
+            uint32_t fX = 0, lY = 0xFFFFFFFFu;
+            for (uint32_t k = lane; k < side.nx; k += 64) fX = max(fX, first[row_find(item, rb, re, side.X[k])]);
+            for (uint32_t k = lane; k < side.ny; k += 64) lY = min(lY, last[row_find(item, rb, re, side.Y[k])]);
+            fX = wave_max(fX);
+            lY = wave_min(lY);
+            if (fX >= lY) continue;  // X => Y does not hold in s
+            if (side.doL) {          // expandL: c > max(X), c not in Y, c before lastY(s)
+                const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
+                for (uint32_t e = q0 + lane; e < re; e += 64) {
+                    const uint32_t c = item[e];
+                    if (first[e] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
+                }
+            }
+            if (side.doR) {          // expandR: c > max(Y), c not in X, c after firstX(s)
+                const uint32_t q0 = row_find(item, rb, re, side.maxY + 1);
+                for (uint32_t e = q0 + lane; e < re; e += 64) {
+                    const uint32_t c = item[e];
+                    if (last[e] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
+                }
             }
         }
+        __syncthreads();
     }
 }
 
@@ -440,53 +451,143 @@ __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, c
 }
 
 // ------------------------------------------------------------ host replay
+// Rules live in an arena (stable addresses, no per-rule heap vectors); their
+// items sit in one shared pool, X then Y.  k1 / k2 hold the comparator's
+// leading keys inline so heap sifts touch no rule object unless they tie.
 struct Rule {
-    std::vector<uint32_t> X, Y;  // dense ids, ascending
-    uint32_t sup = 0;
+    uint64_t k1 = 0;   // sup << 32 | |X| << 16 | |Y|
+    uint64_t k2 = 0;   // X[0] << 32 | (|X| > 1 ? X[1] : Y[0])
     double conf = 0;
-    uint32_t nX = 0;             // |sids(X)|
+    uint32_t sup = 0;
+    uint32_t nX = 0;   // |sids(X)|
+    uint32_t off = 0;  // X at pool[off], Y at pool[off + nx]
+    uint16_t nx = 0, ny = 0;
     bool expandLR = false;
 };
 
+struct RuleStore {
+    std::deque<Rule> rules;
+    std::vector<uint32_t> pool;
+    const uint32_t* X(const Rule* r) const { return pool.data() + r->off; }
+    const uint32_t* Y(const Rule* r) const { return pool.data() + r->off + r->nx; }
+};
+
 // RuleG.compareTo [EXT, recalled; SURVEY A.3]
-int rule_cmp(const Rule* a, const Rule* b) {
+int rule_cmp(const RuleStore& st, const Rule* a, const Rule* b) {
     if (a == b) return 0;
-    if (a->sup != b->sup) return a->sup < b->sup ? -1 : 1;
-    if (a->X.size() != b->X.size()) return a->X.size() < b->X.size() ? -1 : 1;
-    if (a->Y.size() != b->Y.size()) return a->Y.size() < b->Y.size() ? -1 : 1;
+    if (a->k1 != b->k1) return a->k1 < b->k1 ? -1 : 1;  // support, |X|, |Y|
+    // (int)(conf_a - conf_b): always 0 here (both in (0, 1]), kept for fidelity
     const int c4 = int(a->conf - b->conf);
     if (c4) return c4;
-    for (size_t k = 0; k < a->X.size(); ++k)
-        if (a->X[k] != b->X[k]) return a->X[k] < b->X[k] ? -1 : 1;
-    for (size_t k = 0; k < a->Y.size(); ++k)
-        if (a->Y[k] != b->Y[k]) return a->Y[k] < b->Y[k] ? -1 : 1;
+    if (a->k2 != b->k2) return a->k2 < b->k2 ? -1 : 1;  // X[0], then X[1] or Y[0]
+    const uint32_t *xa = st.X(a), *xb = st.X(b);
+    for (uint32_t k = 0; k < a->nx; ++k)
+        if (xa[k] != xb[k]) return xa[k] < xb[k] ? -1 : 1;
+    const uint32_t *ya = st.Y(a), *yb = st.Y(b);
+    for (uint32_t k = 0; k < a->ny; ++k)
+        if (ya[k] != yb[k]) return ya[k] < yb[k] ? -1 : 1;
     return 0;
 }
-struct MinFirst {  // std::priority_queue puts the "largest" on top
-    bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(a, b) > 0; }
-};
-struct MaxFirst {
-    bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(a, b) < 0; }
-};
-struct PendingOrder {  // largest first (the heap's pop order)
-    bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(a, b) > 0; }
+
+// heap entry with the leading keys inline (k1 then k2 decide almost every sift)
+struct HeapEnt {
+    uint64_t k1, k2;
+    Rule* r;
 };
 
 struct Replay {
     int32_t k;
     double minconf;
     uint32_t minsup = 1;
-    std::priority_queue<Rule*, std::vector<Rule*>, MinFirst> krules;
-    std::priority_queue<Rule*, std::vector<Rule*>, MaxFirst> cand;
-    std::vector<std::unique_ptr<Rule>> all;
+    RuleStore st;
+    struct MinFirst {  // std::priority_queue puts the "largest" on top
+        const RuleStore* st;
+        bool operator()(const HeapEnt& a, const HeapEnt& b) const {
+            if (a.k1 != b.k1) return a.k1 > b.k1;
+            if (a.k2 != b.k2) return a.k2 > b.k2;
+            return rule_cmp(*st, a.r, b.r) > 0;
+        }
+    };
+    struct MaxFirst {
+        const RuleStore* st;
+        bool operator()(const HeapEnt& a, const HeapEnt& b) const {
+            if (a.k1 != b.k1) return a.k1 < b.k1;
+            if (a.k2 != b.k2) return a.k2 < b.k2;  // conf key between them is always 0 (see rule_cmp)
+            return rule_cmp(*st, a.r, b.r) < 0;
+        }
+    };
+    // candidates: one max-heap per support value (the comparator's first key),
+    // so a pop sifts through the rules of one support only, and the buckets
+    // below minsup (never expandable: minsup only rises) are freed as it rises
+    struct CandQueue {
+        std::vector<std::vector<HeapEnt>> bucket;
+        uint32_t top_sup = 0, floor = 0;  // buckets < floor are dropped
+        size_t n = 0;
+        MaxFirst cmp;
+        explicit CandQueue(MaxFirst c) : cmp(c) {}
+        bool empty() const { return n == 0; }
+        size_t size() const { return n; }
+        void push(const HeapEnt& e) {
+            const uint32_t sp = uint32_t(e.k1 >> 32);
+            if (sp < floor) return;  // dead on arrival (cannot happen: callers register sup >= minsup)
+            if (sp >= bucket.size()) bucket.resize(size_t(sp) + 1);
+            std::vector<HeapEnt>& b = bucket[sp];
+            b.push_back(e);
+            std::push_heap(b.begin(), b.end(), cmp);
+            if (n == 0 || sp > top_sup) top_sup = sp;
+            ++n;
+        }
+        std::vector<HeapEnt>& settle() {  // n > 0
+            while (bucket[top_sup].empty()) --top_sup;
+            return bucket[top_sup];
+        }
+        const HeapEnt& top() { return settle().front(); }
+        void pop() {
+            std::vector<HeapEnt>& b = settle();
+            std::pop_heap(b.begin(), b.end(), cmp);
+            b.pop_back();
+            --n;
+        }
+        void drop_below(uint32_t ms) {
+            for (; floor < ms && floor < bucket.size(); ++floor) {
+                n -= bucket[floor].size();
+                std::vector<HeapEnt>().swap(bucket[floor]);
+            }
+            if (floor < ms) floor = ms;
+        }
+    };
+    std::priority_queue<HeapEnt, std::vector<HeapEnt>, MinFirst> krules;
+    CandQueue cand;
 
-    Rule* make() {
-        all.push_back(std::make_unique<Rule>());
-        return all.back().get();
+    Replay(int32_t k_, double mc) : k(k_), minconf(mc), krules(MinFirst{&st}), cand(MaxFirst{&st}) {}
+
+    // X = X(src) + ax, Y = Y(src) + ay (src == nullptr: X = {ax}, Y = {ay})
+    Rule* derive(const Rule* src, uint32_t ax, uint32_t ay, uint32_t sup, uint32_t nX) {
+        const uint32_t nx0 = src ? src->nx : 0u, ny0 = src ? src->ny : 0u;
+        const uint32_t mx = nx0 + (ax != kNone), my = ny0 + (ay != kNone);
+        if (mx >= uint32_t(kMaxSide) || my >= uint32_t(kMaxSide))
+            throw Error(FSM_ELIMIT, "TSR: rule side exceeds " + std::to_string(kMaxSide - 1) + " items");
+        if (st.pool.size() + mx + my >= kNone) throw Error(FSM_ELIMIT, "TSR: rule item pool exceeds 2^32");
+        const uint32_t so = src ? src->off : 0u;
+        Rule& r = st.rules.emplace_back();
+        r.off = uint32_t(st.pool.size());
+        for (uint32_t q = 0; q < nx0; ++q) st.pool.push_back(st.pool[so + q]);
+        if (ax != kNone) st.pool.push_back(ax);
+        for (uint32_t q = 0; q < ny0; ++q) st.pool.push_back(st.pool[so + nx0 + q]);
+        if (ay != kNone) st.pool.push_back(ay);
+        r.nx = uint16_t(mx);
+        r.ny = uint16_t(my);
+        r.sup = sup;
+        r.nX = nX;
+        r.conf = double(sup) / double(nX);
+        const uint32_t* x = st.X(&r);
+        r.k1 = uint64_t(sup) << 32 | uint64_t(mx) << 16 | uint64_t(my);
+        r.k2 = uint64_t(x[0]) << 32 | (mx > 1 ? x[1] : x[mx]);
+        return &r;
     }
     // AlgoTopSeqRules.save
     void save(Rule* r) {
-        krules.push(r);
+        krules.push(HeapEnt{r->k1, r->k2, r});
         if (int64_t(krules.size()) > k) {
             if (r->sup > minsup) {
                 do {
@@ -494,12 +595,13 @@ struct Replay {
                     krules.pop();
                 } while (int64_t(krules.size()) > k);
             }
-            minsup = krules.top()->sup;
+            minsup = krules.top().r->sup;
+            cand.drop_below(minsup);
         }
     }
     void reg(Rule* r, bool lr) {
         r->expandLR = lr;
-        cand.push(r);
+        cand.push(HeapEnt{r->k1, r->k2, r});
     }
 };
 
@@ -630,22 +732,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 const uint32_t j = pr.j;
                 if (sup[j] < rp.minsup) continue;
                 if (pr.ij >= rp.minsup) {
-                    Rule* r = rp.make();
-                    r->X = {i};
-                    r->Y = {j};
-                    r->sup = pr.ij;
-                    r->conf = double(pr.ij) / double(sup[i]);
-                    r->nX = sup[i];
+                    Rule* r = rp.derive(nullptr, i, j, pr.ij, sup[i]);
                     if (r->conf >= minconf) rp.save(r);
                     rp.reg(r, true);
                 }
                 if (pr.ji >= rp.minsup) {
-                    Rule* r = rp.make();
-                    r->X = {j};
-                    r->Y = {i};
-                    r->sup = pr.ji;
-                    r->conf = double(pr.ji) / double(sup[j]);
-                    r->nX = sup[j];
+                    Rule* r = rp.derive(nullptr, j, i, pr.ji, sup[j]);
                     if (r->conf >= minconf) rp.save(r);
                     rp.reg(r, true);
                 }
@@ -676,11 +768,19 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     FSM_HIP(hipMemsetAsync(TR.p, 0, SU * 4, s));
     FSM_HIP(hipMemsetAsync(seen.p, 0, SU * 4, s));
     FSM_HIP(hipMemsetAsync(ctl.p, 0, kExpBatch * sizeof(ExpCtl), s));
-    DevBuf d_sides(kExpBatch * sizeof(Side)), d_drv((kExpBatch + 1) * 8), d_wave((kExpBatch + 1) * 8);
+    // per-launch rule descriptors: staged in pinned host memory, one H2D copy
+    constexpr size_t kSidesB = kExpBatch * sizeof(Side), kOffB = (kExpBatch + 1) * 8;
+    PinnedBuf stage(kSidesB + 2 * kOffB);
+    DevBuf d_stage(kSidesB + 2 * kOffB);
+    Side* h_sides = static_cast<Side*>(stage.host);
+    uint64_t* h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(stage.host) + kSidesB);
+    uint64_t* h_wave = h_drv + (kExpBatch + 1);
+    Side* d_sides = d_stage.as<Side>();
+    uint64_t* d_drv = reinterpret_cast<uint64_t*>(d_stage.as<char>() + kSidesB);
+    uint64_t* d_wave = d_drv + (kExpBatch + 1);
     const bool use_bm = d->bm.p != nullptr;
-    DevBuf d_sids, d_dlw, d_ndlw(16);
+    DevBuf d_dlw, d_ndlw(16);
     if (use_bm) {
-        d_sids.alloc(uint64_t(kExpBatch) * std::max<int64_t>(d->N, 1) * 4);
         d_dlw.alloc(SU * sizeof(uint4));
     }
     // expansion results land in mapped pinned host memory (at most one record per item per slot)
@@ -697,10 +797,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     int64_t expansions = 0, launches = 0, spec_pushback = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     double last_log_ms = now_ms();  // verbose progress line every 20 s
+    double prep_ms = 0, post_ms = 0, commit_ms = 0, pop_ms = 0;  // host time split (verbose summary)
     std::vector<Side> sides;
     std::vector<uint64_t> drv_off, wave_off;
 
+    const TsrGrid grid;
     auto launch = [&](const std::vector<Rule*>& batch) {
+        const double tl0 = now_ms();
         const uint32_t nb = uint32_t(batch.size());
         sides.assign(nb, Side{});
         drv_off.assign(nb + 1, 0);
@@ -708,64 +811,61 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         std::vector<char> drv_in_x(nb, 1);
         for (uint32_t k = 0; k < nb; ++k) {
             const Rule* r = batch[k];
-            if (r->X.size() >= kMaxSide || r->Y.size() >= kMaxSide)
-                throw Error(FSM_ELIMIT, "TSR: rule side exceeds " + std::to_string(kMaxSide - 1) + " items");
+            const uint32_t *rx = rp.st.X(r), *ry = rp.st.Y(r);
             Side& sd = sides[k];
-            sd.nx = uint32_t(r->X.size());
-            sd.ny = uint32_t(r->Y.size());
+            sd.nx = r->nx;
+            sd.ny = r->ny;
             sd.doL = r->expandLR;
             sd.doR = 1;
-            sd.maxX = r->X.back();
-            sd.maxY = r->Y.back();
-            std::copy(r->X.begin(), r->X.end(), sd.X);
-            std::copy(r->Y.begin(), r->Y.end(), sd.Y);
+            sd.maxX = rx[r->nx - 1];
+            sd.maxY = ry[r->ny - 1];
+            std::copy(rx, rx + r->nx, sd.X);
+            std::copy(ry, ry + r->ny, sd.Y);
             // driver list: rarest item of X (expandL needs all of sids(X)), else of X u Y
-            uint32_t drv = r->X[0];
-            for (uint32_t x : r->X) if (sup[x] < sup[drv]) drv = x;
+            uint32_t drv = rx[0];
+            for (uint32_t q = 0; q < r->nx; ++q) if (sup[rx[q]] < sup[drv]) drv = rx[q];
             if (!r->expandLR)
-                for (uint32_t y : r->Y) if (sup[y] < sup[drv]) { drv = y; drv_in_x[k] = 0; }
+                for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < sup[drv]) { drv = ry[q]; drv_in_x[k] = 0; }
             drv_off[k] = voff[drv];
             wave_off[k + 1] = wave_off[k] + (voff[drv + 1] - voff[drv]);
         }
-        FSM_HIP(hipMemcpyAsync(d_sides.p, sides.data(), nb * sizeof(Side), hipMemcpyHostToDevice, s));
-        FSM_HIP(hipMemcpyAsync(d_drv.p, drv_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
-        FSM_HIP(hipMemcpyAsync(d_wave.p, wave_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
+        std::memcpy(h_sides, sides.data(), nb * sizeof(Side));
+        std::memcpy(h_drv, drv_off.data(), (nb + 1) * 8);
+        std::memcpy(h_wave, wave_off.data(), (nb + 1) * 8);
+        FSM_HIP(hipMemcpyAsync(d_stage.p, stage.host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
         const uint64_t waves = use_bm ? 0 : wave_off[nb];
         if (use_bm) {
-            FSM_HIP(hipMemsetAsync(d_ndlw.p, 0, 4, s));
-            const unsigned gx = unsigned(std::min<uint64_t>((uint64_t(d->NW) + kBlock - 1) / kBlock, 64));
-            hipLaunchKernelGGL(k_rule_sids, dim3(std::max(gx, 1u), nb), dim3(kBlock), 0, s, d_sides.as<Side>(),
-                               d->bm.as<uint32_t>(), d->NW, uint32_t(d->N), d_sids.as<uint32_t>(), ctl.as<ExpCtl>());
-            FSM_LAUNCHED("k_rule_sids", s);
-            hipLaunchKernelGGL(k_expand_bm, dim3(kExpandBlocks, nb), dim3(kBlock), 0, s, d_sides.as<Side>(),
-                               d_sids.as<uint32_t>(), uint32_t(d->N), d->row_off.as<uint32_t>(),
-                               d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(), U,
-                               TL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
-                               ctl.as<ExpCtl>());
+            hipLaunchKernelGGL(k_expand_bm, dim3(grid.expand, nb), dim3(kBlock), 0, s, d_sides,
+                               d->bm.as<uint32_t>(), d->NW, d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
+                               d->first.as<uint32_t>(), d->last.as<uint32_t>(), U, TL.as<uint32_t>(),
+                               TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(), ctl.as<ExpCtl>(),
+                               d_ndlw.as<uint32_t>());
             FSM_LAUNCHED("k_expand_bm", s);
         }
         if (waves) {
             hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               d_sides.as<Side>(), d_drv.as<uint64_t>(), d_wave.as<uint64_t>(), nb,
+                               d_sides, d_drv, d_wave, nb,
                                d->vert_sid.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
                                d->first.as<uint32_t>(), d->last.as<uint32_t>(), U, TL.as<uint32_t>(),
                                DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
                                ctl.as<ExpCtl>());
             FSM_LAUNCHED("k_expand", s);
         }
-        hipLaunchKernelGGL(k_expand_collect, dim3(kCollectBlocks, nb), dim3(kBlock), 0, s, TL.as<uint32_t>(),
+        hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, TL.as<uint32_t>(),
                            DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
                            ctl.as<ExpCtl>(), U, rp.minsup, d_rec, d_hdr, ecap,
                            use_bm ? d_dlw.as<uint4>() : nullptr, d_ndlw.as<uint32_t>());
         FSM_LAUNCHED("k_expand_collect", s);
         if (use_bm) {
-            hipLaunchKernelGGL(k_dl, dim3(kDlBlocks), dim3(kBlock), 0, s, d_sides.as<Side>(), d->bm.as<uint32_t>(),
+            hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, d_sides, d->bm.as<uint32_t>(),
                                d->NW, d_dlw.as<uint4>(), d_ndlw.as<uint32_t>(), d_rec, ecap);
             FSM_LAUNCHED("k_dl", s);
         }
         const double tw0 = now_ms();
+        prep_ms += tw0 - tl0;
         FSM_HIP(hipStreamSynchronize(s));
-        wait_ms += now_ms() - tw0;
+        const double tw1 = now_ms();
+        wait_ms += tw1 - tw0;
         ++launches;
         for (uint32_t k = 0; k < nb; ++k) {
             const ExpHdr h = h_hdr[k];
@@ -778,6 +878,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             res.recs.assign(rec, rec + h.nout);
             std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
         }
+        post_ms += now_ms() - tw1;
     };
 
     auto commit = [&](Rule* r, const std::vector<ExpRec>& er) {
@@ -788,26 +889,14 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         if (r->expandLR) {  // expandL: X u {c} => Y
             for (const ExpRec& e : er) {
                 if (e.tl == 0 || e.tl < rp.minsup) continue;
-                Rule* nr = rp.make();
-                nr->X = r->X;
-                nr->X.push_back(e.c);
-                nr->Y = r->Y;
-                nr->sup = e.tl;
-                nr->conf = double(e.tl) / double(e.dl);
-                nr->nX = e.dl;
+                Rule* nr = rp.derive(r, e.c, kNone, e.tl, e.dl);
                 if (nr->conf >= minconf) rp.save(nr);
                 rp.reg(nr, true);
             }
         }
         for (const ExpRec& e : er) {  // expandR: X => Y u {c}
             if (e.tr == 0 || e.tr < rp.minsup) continue;
-            Rule* nr = rp.make();
-            nr->X = r->X;
-            nr->Y = r->Y;
-            nr->Y.push_back(e.c);
-            nr->sup = e.tr;
-            nr->conf = double(e.tr) / double(r->nX);
-            nr->nX = r->nX;
+            Rule* nr = rp.derive(r, kNone, e.c, e.tr, r->nX);
             if (nr->conf >= minconf) rp.save(nr);
             rp.reg(nr, false);
         }
@@ -817,38 +906,49 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // cached) instead of going back to the heap: the next rule to commit is
     // always the larger of the heap top and the pending front, which is
     // exactly the one-at-a-time order; new rules only ever enter the heap.
-    std::set<Rule*, PendingOrder> pending;
+    struct PendingOrder {  // largest first (the heap's pop order)
+        const RuleStore* st;
+        bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(*st, a, b) > 0; }
+    };
+    std::set<Rule*, PendingOrder> pending(PendingOrder{&rp.st});
     std::vector<Rule*> batch;
     for (;;) {
         const bool have_h = !rp.cand.empty(), have_p = !pending.empty();
         if (!have_h && !have_p) break;
-        const bool from_p = have_p && (!have_h || rule_cmp(*pending.begin(), rp.cand.top()) > 0);
-        Rule* r = from_p ? *pending.begin() : rp.cand.top();
+        const bool from_p = have_p && (!have_h || rule_cmp(rp.st, *pending.begin(), rp.cand.top().r) > 0);
+        Rule* r = from_p ? *pending.begin() : rp.cand.top().r;
         if (r->sup < rp.minsup) break;
         if (from_p) {
             pending.erase(pending.begin());
+            const double tc0 = now_ms();
             auto ci = cache.find(r);
             commit(r, ci->second.recs);
             cache.erase(ci);
+            commit_ms += now_ms() - tc0;
             continue;
         }
         // r (uncached) and the next heap rules are expanded together
+        const double tp0 = now_ms();
         batch.clear();
-        while (batch.size() < size_t(kExpBatch) && !rp.cand.empty() && rp.cand.top()->sup >= rp.minsup) {
-            batch.push_back(rp.cand.top());
+        while (batch.size() < size_t(kExpBatch) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
+            batch.push_back(rp.cand.top().r);
             rp.cand.pop();
         }
+        pop_ms += now_ms() - tp0;
         launch(batch);
         spec_pushback += int64_t(batch.size()) - 1;
         for (Rule* c : batch) pending.insert(c);
     }
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] expansions %lld in %lld launches (%lld pushed back), %.0f ms waiting on the GPU\n",
-                     (long long)expansions, (long long)launches, (long long)spec_pushback, wait_ms);
+        std::fprintf(stderr,
+                     "[fsm tsr] expansions %lld in %lld launches (%lld pushed back), %.0f ms waiting on the GPU; "
+                     "host: %.0f ms launch prep, %.0f ms result intake, %.0f ms commit, %.0f ms batch pops; %zu rules made\n",
+                     (long long)expansions, (long long)launches, (long long)spec_pushback, wait_ms, prep_ms, post_ms,
+                     commit_ms, pop_ms, rp.st.rules.size());
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {
-        res.push_back(rp.krules.top());
+        res.push_back(rp.krules.top().r);
         rp.krules.pop();
     }
     auto* o = static_cast<fsm_rules*>(std::calloc(1, sizeof(fsm_rules)));
@@ -858,7 +958,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     o->total = d->N;
     o->final_minsup = int32_t(rp.minsup);
     size_t na = 0, nc = 0;
-    for (const Rule* r : res) { na += r->X.size(); nc += r->Y.size(); }
+    for (const Rule* r : res) { na += r->nx; nc += r->ny; }
     o->support = static_cast<int32_t*>(std::malloc(std::max<size_t>(n, 1) * 4));
     o->confidence = static_cast<double*>(std::malloc(std::max<size_t>(n, 1) * 8));
     o->ante_off = static_cast<int64_t*>(std::malloc((n + 1) * 8));
@@ -874,10 +974,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const Rule* r = res[q];
         o->support[q] = int32_t(r->sup);
         o->confidence[q] = r->conf;
-        for (size_t x = 0; x < r->X.size(); ++x) o->ante[o->ante_off[q] + int64_t(x)] = db->tsr.item_val[r->X[x]];
-        for (size_t x = 0; x < r->Y.size(); ++x) o->cons[o->cons_off[q] + int64_t(x)] = db->tsr.item_val[r->Y[x]];
-        o->ante_off[q + 1] = o->ante_off[q] + int64_t(r->X.size());
-        o->cons_off[q + 1] = o->cons_off[q] + int64_t(r->Y.size());
+        const uint32_t *rx = rp.st.X(r), *ry = rp.st.Y(r);
+        for (uint32_t x = 0; x < r->nx; ++x) o->ante[o->ante_off[q] + int64_t(x)] = db->tsr.item_val[rx[x]];
+        for (uint32_t x = 0; x < r->ny; ++x) o->cons[o->cons_off[q] + int64_t(x)] = db->tsr.item_val[ry[x]];
+        o->ante_off[q + 1] = o->ante_off[q] + int64_t(r->nx);
+        o->cons_off[q + 1] = o->cons_off[q] + int64_t(r->ny);
     }
     ctx->stats.expansions = expansions;
     ctx->stats.rules = int64_t(n);
