@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FSM_ABI_VERSION 2
+#define FSM_ABI_VERSION 3
 
 /* status codes */
 #define FSM_OK 0
