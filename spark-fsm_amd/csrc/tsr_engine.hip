@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <queue>
 #include <set>
@@ -48,10 +49,12 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kMaxSide = 64;
-constexpr int kCollectBlocks = 8;   // collect blocks per rule slot
+constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRID sweep: 4-8 best)
 constexpr int kExpBatch = 32;       // rules expanded per launch (speculative, committed in order)
 constexpr int kExpandBlocks = 128;  // bitmap path: expansion blocks per rule slot
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
+constexpr int kSpecDepth = 3;       // child speculation: levels per launch
+constexpr int kSpecMax = 128;       // child speculation: rules per level
 // FSM_TSR_GRID="expand,collect,dl" overrides the per-launch grids (tuning sweeps)
 struct TsrGrid {
     unsigned expand = kExpandBlocks, collect = kCollectBlocks, dl = kDlBlocks;
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
     const uint32_t* list = listb + b * U64;
     ExpCtl* ctl = ctlb + b;
     ExpRec* out = outb + b * uint64_t(cap);
-    ExpHdr* hdr = hdrb + b;
+    (void)hdrb;
     const uint32_t n = ctl->nlist;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t c = list[i];
@@ -315,22 +318,29 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
             }
         }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&ctl->done, 1u) == gridDim.x - 1) {
-            __threadfence();
-            hdr->nout = atomicAdd(&ctl->nout, 0u);
-            hdr->nx = atomicAdd(&ctl->nx, 0u);
-            ctl->nx = 0;
-            ctl->nlist = 0;
-            ctl->nout = 0;
-            ctl->done = 0;
-            ctl->nsid = 0;
-            // no system-scope fence: the host reads hdr / out after the stream
-            // synchronizes, and kernel completion already releases to the host
-        }
+}
+
+// Publish every slot's header and reset its control block for the next
+// launch.  Runs in the kernel after the collect (k_dl, or k_publish on the
+// list path): the kernel boundary orders it after every collect block, with
+// no cross-block completion counter (an agent-scope fence per block writes
+// back the XCD's L2, which cost more than the collect itself).
+__device__ __forceinline__ void publish_slots(ExpCtl* __restrict__ ctlb, ExpHdr* __restrict__ hdrb, uint32_t nslot) {
+    for (uint32_t b = threadIdx.x; b < nslot; b += blockDim.x) {
+        ExpCtl& c = ctlb[b];
+        hdrb[b].nout = c.nout;
+        hdrb[b].nx = c.nx;
+        c.nx = 0;
+        c.nlist = 0;
+        c.nout = 0;
+        c.done = 0;
+        c.nsid = 0;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_publish(ExpCtl* __restrict__ ctlb, ExpHdr* __restrict__ hdrb,
+                                                    uint32_t nslot) {
+    publish_slots(ctlb, hdrb, nslot);
 }
 
 // ---- sid bitmaps: one bit per sequence per item.  They replace
@@ -425,8 +435,10 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
 __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
                                                uint32_t NW, const uint4* __restrict__ dlw,
                                                const uint32_t* __restrict__ ndlw, ExpRec* __restrict__ outb,
-                                               uint32_t cap) {
+                                               uint32_t cap, ExpCtl* __restrict__ ctlb, ExpHdr* __restrict__ hdrb,
+                                               uint32_t nslot) {
     __shared__ uint32_t red[kBlock / 64];
+    if (blockIdx.x == 0) publish_slots(ctlb, hdrb, nslot);
     const uint32_t n = *ndlw;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint4 wk = dlw[i];
@@ -521,6 +533,7 @@ struct Replay {
     // below minsup (never expandable: minsup only rises) are freed as it rises
     struct CandQueue {
         std::vector<std::vector<HeapEnt>> bucket;
+        std::vector<uint64_t> occ;  // bit s: bucket[s] non-empty (the next lower bucket is a word scan away)
         uint32_t top_sup = 0, floor = 0;  // buckets < floor are dropped
         size_t n = 0;
         MaxFirst cmp;
@@ -530,15 +543,24 @@ struct Replay {
         void push(const HeapEnt& e) {
             const uint32_t sp = uint32_t(e.k1 >> 32);
             if (sp < floor) return;  // dead on arrival (cannot happen: callers register sup >= minsup)
-            if (sp >= bucket.size()) bucket.resize(size_t(sp) + 1);
+            if (sp >= bucket.size()) {
+                bucket.resize(size_t(sp) + 1);
+                occ.resize(size_t(sp) / 64 + 1, 0);
+            }
             std::vector<HeapEnt>& b = bucket[sp];
             b.push_back(e);
             std::push_heap(b.begin(), b.end(), cmp);
+            occ[sp >> 6] |= 1ull << (sp & 63u);
             if (n == 0 || sp > top_sup) top_sup = sp;
             ++n;
         }
-        std::vector<HeapEnt>& settle() {  // n > 0
-            while (bucket[top_sup].empty()) --top_sup;
+        std::vector<HeapEnt>& settle() {  // n > 0: move top_sup down to the highest non-empty bucket
+            if (bucket[top_sup].empty()) {
+                size_t w = top_sup >> 6;
+                uint64_t m = occ[w] & ((top_sup & 63u) ? ((1ull << (top_sup & 63u)) - 1ull) : 0ull);
+                while (!m) m = occ[--w];
+                top_sup = uint32_t(w * 64 + 63 - size_t(__builtin_clzll(m)));
+            }
             return bucket[top_sup];
         }
         const HeapEnt& top() { return settle().front(); }
@@ -546,12 +568,14 @@ struct Replay {
             std::vector<HeapEnt>& b = settle();
             std::pop_heap(b.begin(), b.end(), cmp);
             b.pop_back();
+            if (b.empty()) occ[top_sup >> 6] &= ~(1ull << (top_sup & 63u));
             --n;
         }
         void drop_below(uint32_t ms) {
             for (; floor < ms && floor < bucket.size(); ++floor) {
                 n -= bucket[floor].size();
                 std::vector<HeapEnt>().swap(bucket[floor]);
+                occ[floor >> 6] &= ~(1ull << (floor & 63u));
             }
             if (floor < ms) floor = ms;
         }
@@ -792,6 +816,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     ExpRec* d_rec = reinterpret_cast<ExpRec*>(d_hdr + kExpBatch);
     struct ExpResult {
         std::vector<ExpRec> recs;
+        std::vector<Rule*> preL, preR;  // children created (and expanded) ahead of the commit, by record
     };
     std::unordered_map<Rule*, ExpResult> cache;
     int64_t expansions = 0, launches = 0, spec_pushback = 0;
@@ -858,8 +883,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         FSM_LAUNCHED("k_expand_collect", s);
         if (use_bm) {
             hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, d_sides, d->bm.as<uint32_t>(),
-                               d->NW, d_dlw.as<uint4>(), d_ndlw.as<uint32_t>(), d_rec, ecap);
+                               d->NW, d_dlw.as<uint4>(), d_ndlw.as<uint32_t>(), d_rec, ecap, ctl.as<ExpCtl>(), d_hdr,
+                               nb);
             FSM_LAUNCHED("k_dl", s);
+        } else {
+            hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, ctl.as<ExpCtl>(), d_hdr, nb);
+            FSM_LAUNCHED("k_publish", s);
         }
         const double tw0 = now_ms();
         prep_ms += tw0 - tl0;
@@ -881,27 +910,6 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         post_ms += now_ms() - tw1;
     };
 
-    auto commit = [&](Rule* r, const std::vector<ExpRec>& er) {
-        expansions += r->expandLR ? 2 : 1;
-        if (ctx->opts.verbose && now_ms() - last_log_ms > 20000.0 && (last_log_ms = now_ms()) > 0)
-            std::fprintf(stderr, "[fsm tsr] %lld expansions, minsup %u, candidates %zu, rules %zu, %.0f ms\n",
-                         (long long)expansions, rp.minsup, rp.cand.size(), rp.krules.size(), now_ms() - t0);
-        if (r->expandLR) {  // expandL: X u {c} => Y
-            for (const ExpRec& e : er) {
-                if (e.tl == 0 || e.tl < rp.minsup) continue;
-                Rule* nr = rp.derive(r, e.c, kNone, e.tl, e.dl);
-                if (nr->conf >= minconf) rp.save(nr);
-                rp.reg(nr, true);
-            }
-        }
-        for (const ExpRec& e : er) {  // expandR: X => Y u {c}
-            if (e.tr == 0 || e.tr < rp.minsup) continue;
-            Rule* nr = rp.derive(r, kNone, e.c, e.tr, r->nX);
-            if (nr->conf >= minconf) rp.save(nr);
-            rp.reg(nr, false);
-        }
-    };
-
     // Speculated rules wait in `pending` (ordered like the heap, results
     // cached) instead of going back to the heap: the next rule to commit is
     // always the larger of the heap top and the pending front, which is
@@ -911,33 +919,137 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(*st, a, b) > 0; }
     };
     std::set<Rule*, PendingOrder> pending(PendingOrder{&rp.st});
+    // a speculated child that its parent's commit did not register: drop its
+    // cached results (and, recursively, those of its own speculated children)
+    std::function<void(Rule*)> drop_spec = [&](Rule* x) {
+        auto it = cache.find(x);
+        if (it == cache.end()) return;
+        ExpResult res = std::move(it->second);
+        cache.erase(it);
+        for (Rule* c : res.preL) if (c) drop_spec(c);
+        for (Rule* c : res.preR) if (c) drop_spec(c);
+    };
+    auto commit = [&](Rule* r, ExpResult& res) {
+        const std::vector<ExpRec>& er = res.recs;
+        const bool pre = !res.preL.empty();
+        expansions += r->expandLR ? 2 : 1;
+        if (ctx->opts.verbose && now_ms() - last_log_ms > 20000.0 && (last_log_ms = now_ms()) > 0)
+            std::fprintf(stderr, "[fsm tsr] %lld expansions, minsup %u, candidates %zu, rules %zu, %.0f ms\n",
+                         (long long)expansions, rp.minsup, rp.cand.size(), rp.krules.size(), now_ms() - t0);
+        if (r->expandLR) {  // expandL: X u {c} => Y
+            for (size_t i = 0; i < er.size(); ++i) {
+                const ExpRec& e = er[i];
+                Rule* sp = pre ? res.preL[i] : nullptr;
+                if (e.tl == 0 || e.tl < rp.minsup) {
+                    if (sp) drop_spec(sp);
+                    continue;
+                }
+                Rule* nr = sp ? sp : rp.derive(r, e.c, kNone, e.tl, e.dl);
+                if (nr->conf >= minconf) rp.save(nr);
+                rp.reg(nr, true);
+            }
+        }
+        for (size_t i = 0; i < er.size(); ++i) {  // expandR: X => Y u {c}
+            const ExpRec& e = er[i];
+            Rule* sp = pre ? res.preR[i] : nullptr;
+            if (e.tr == 0 || e.tr < rp.minsup) {
+                if (sp) drop_spec(sp);
+                continue;
+            }
+            Rule* nr = sp ? sp : rp.derive(r, kNone, e.c, e.tr, r->nX);
+            if (nr->conf >= minconf) rp.save(nr);
+            rp.reg(nr, false);
+        }
+    };
+
+    // Child speculation: after a launch, the children of its rules that rank
+    // at or above the lowest pending rule (sup >= T) are the ones whose
+    // registration would force the next launch (a fresh rule outranking the
+    // pending front).  They are created now, exactly as their parent's commit
+    // would create them, and expanded in follow-up launches of up to
+    // kExpBatch rules, a few levels deep; the commit then registers the
+    // pre-built rule (results cached) instead of deriving it again.
+    int64_t spec_made = 0, spec_launches = 0;
+    auto speculate = [&](std::vector<Rule*> level) {
+        for (int depth = 0; depth < kSpecDepth && !level.empty(); ++depth) {
+            uint32_t T = 0xFFFFFFFFu;
+            for (Rule* x : level) T = std::min(T, x->sup);
+            if (!pending.empty()) T = std::min(T, (*pending.rbegin())->sup);
+            T = std::max(T, rp.minsup);
+            std::vector<Rule*> next;
+            for (Rule* x : level) {
+                auto it = cache.find(x);
+                if (it == cache.end()) continue;
+                ExpResult& res = it->second;
+                const size_t n = res.recs.size();
+                res.preL.assign(n, nullptr);
+                res.preR.assign(n, nullptr);
+                for (size_t i = 0; i < n && next.size() < size_t(kSpecMax); ++i) {
+                    const ExpRec& e = res.recs[i];
+                    if (x->expandLR && e.tl >= T) {
+                        Rule* c = rp.derive(x, e.c, kNone, e.tl, e.dl);
+                        c->expandLR = true;
+                        res.preL[i] = c;
+                        next.push_back(c);
+                    }
+                    if (e.tr >= T && next.size() < size_t(kSpecMax)) {
+                        Rule* c = rp.derive(x, kNone, e.c, e.tr, x->nX);
+                        c->expandLR = false;
+                        res.preR[i] = c;
+                        next.push_back(c);
+                    }
+                }
+            }
+            spec_made += int64_t(next.size());
+            for (size_t a = 0; a < next.size(); a += size_t(kExpBatch)) {
+                const std::vector<Rule*> part(next.begin() + a,
+                                              next.begin() + std::min(next.size(), a + size_t(kExpBatch)));
+                launch(part);
+                ++spec_launches;
+            }
+            level = std::move(next);
+        }
+    };
+
     std::vector<Rule*> batch;
+    size_t sweep_at = size_t(1) << 16;
+    const bool spec_on = [] { const char* v = std::getenv("FSM_TSR_SPEC"); return !(v && v[0] == '0'); }();
     for (;;) {
         const bool have_h = !rp.cand.empty(), have_p = !pending.empty();
         if (!have_h && !have_p) break;
         const bool from_p = have_p && (!have_h || rule_cmp(rp.st, *pending.begin(), rp.cand.top().r) > 0);
         Rule* r = from_p ? *pending.begin() : rp.cand.top().r;
         if (r->sup < rp.minsup) break;
-        if (from_p) {
-            pending.erase(pending.begin());
+        auto ci = cache.find(r);
+        if (from_p || ci != cache.end()) {  // results at hand (speculated earlier): commit now
+            if (from_p) pending.erase(pending.begin());
+            else rp.cand.pop();
             const double tc0 = now_ms();
-            auto ci = cache.find(r);
-            commit(r, ci->second.recs);
+            ExpResult res = std::move(ci->second);
             cache.erase(ci);
+            commit(r, res);
             commit_ms += now_ms() - tc0;
+            if (cache.size() > sweep_at) {  // results of rules now below minsup can never be committed
+                for (auto it = cache.begin(); it != cache.end();)
+                    it = it->first->sup < rp.minsup ? cache.erase(it) : std::next(it);
+                sweep_at = std::max<size_t>(2 * cache.size(), 1u << 16);
+            }
             continue;
         }
         // r (uncached) and the next heap rules are expanded together
         const double tp0 = now_ms();
         batch.clear();
         while (batch.size() < size_t(kExpBatch) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
-            batch.push_back(rp.cand.top().r);
+            Rule* x = rp.cand.top().r;
             rp.cand.pop();
+            if (cache.count(x)) pending.insert(x);  // already expanded by speculation
+            else batch.push_back(x);
         }
         pop_ms += now_ms() - tp0;
         launch(batch);
         spec_pushback += int64_t(batch.size()) - 1;
         for (Rule* c : batch) pending.insert(c);
+        if (spec_on) speculate(batch);
     }
     if (ctx->opts.verbose)
         std::fprintf(stderr,
@@ -945,6 +1057,9 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      "host: %.0f ms launch prep, %.0f ms result intake, %.0f ms commit, %.0f ms batch pops; %zu rules made\n",
                      (long long)expansions, (long long)launches, (long long)spec_pushback, wait_ms, prep_ms, post_ms,
                      commit_ms, pop_ms, rp.st.rules.size());
+    if (ctx->opts.verbose)
+        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches\n", (long long)spec_made,
+                     (long long)spec_launches);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {
