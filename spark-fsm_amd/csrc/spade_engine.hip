@@ -591,9 +591,11 @@ struct Slab {
     }
 };
 
+// Per-class member tables live in flat per-batch arrays (no per-class heap
+// vectors: deep lattices have millions of small classes).
 struct ClassMeta {
-    std::vector<uint32_t> rank_item;  // rank -> dense item id
-    std::vector<int32_t> node_of;     // member id -> pattern node (-1: absent)
+    uint64_t ri_off = 0;  // rank -> dense item id:        Batch::rank_item[ri_off + rank]
+    uint64_t no_off = 0;  // member -> pattern node or -1:  Batch::node_of[no_off + member]
     uint32_t D = 0;
     uint32_t mshift = 0;
     uint64_t cnt_off = 0;
@@ -602,8 +604,7 @@ struct ClassMeta {
 
 struct ChildInfo {
     uint32_t pcls = 0, pmi = 0;
-    std::vector<uint32_t> rank_item;
-    std::vector<int32_t> node_of;
+    uint64_t ri_off = 0, no_off = 0;  // into the parent batch's child_rank_item / child_node_of
     uint32_t D = 0;
     uint64_t cap = 0;
 };
@@ -623,7 +624,11 @@ struct Batch {
     DevBuf kid_off, kid_slot, kid_cid;  // frequent children of every member (CSR over cbase + mi)
     uint64_t E = 0;                     // entries in the slab (runs of all classes, any order)
     uint64_t n_cnt = 0, cbase_total = 0;
+    std::vector<uint32_t> rank_item;  // member tables of cls (see ClassMeta)
+    std::vector<int32_t> node_of;
     std::vector<ChildInfo> children;
+    std::vector<uint32_t> child_rank_item;  // member tables of children
+    std::vector<int32_t> child_node_of;
     std::vector<std::pair<size_t, size_t>> groups;
     size_t next_group = 0;
     int64_t depth = 1;  // items per member pattern of this batch's classes
@@ -682,10 +687,11 @@ struct Miner {
         upload(b.d_cls, b.h_cls);
     }
 
-    void stats_for_class(const ClassMeta& m) {
+    void stats_for_class(const Batch& b, const ClassMeta& m) {
         uint64_t S = 0, I = 0, sS = 0, sI = 0;
+        const int32_t* node_of = b.node_of.data() + m.no_off;
         for (uint32_t mi = 0; mi < m.D; ++mi) {
-            const int32_t nd = m.node_of[mi];
+            const int32_t nd = node_of[mi];
             if (nd < 0) continue;
             const uint64_t sup = nodes[size_t(nd)].support;
             if ((mi & 1u) == kSeq) { ++S; sS += sup; } else { ++I; sI += sup; }
@@ -820,7 +826,7 @@ struct Miner {
         prepare(b);
         const bool shard = comm && b.root;  // root rows split over ranks, frequent pairs all-gathered
         if (!shard || comm->rank() == 0)
-            for (auto& m : b.cls) stats_for_class(m);
+            for (auto& m : b.cls) stats_for_class(b, m);
         fsm_stats& st = ctx->stats;
         st.batches += 1;
         const uint64_t tot_ent = b.E;
@@ -849,7 +855,7 @@ struct Miner {
         std::vector<DRow> rows;
         for (size_t c = 0; c < b.cls.size(); ++c)
             for (uint32_t mi = 0; mi < b.cls[c].D; ++mi)
-                if (b.cls[c].node_of[mi] >= 0) rows.push_back(DRow{uint32_t(c), mi});
+                if (b.node_of[b.cls[c].no_off + mi] >= 0) rows.push_back(DRow{uint32_t(c), mi});
         // root rows are rows[r] = rank r: a shard extracts its own slice of them
         const uint32_t rlo = shard ? std::min<uint32_t>(slice_lo, uint32_t(rows.size())) : 0u;
         const uint32_t rhi = shard ? std::min<uint32_t>(slice_hi, uint32_t(rows.size())) : uint32_t(rows.size());
@@ -904,6 +910,8 @@ struct Miner {
         upload(b.kid_cid, kcid);
         // children (new pattern nodes) in deterministic (row, slot) order
         b.children.clear();
+        b.child_rank_item.clear();
+        b.child_node_of.clear();
         for (size_t q = 0; q < recs.size();) {
             const uint32_t row = recs[q].row;
             const DRow pr = rows[row];
@@ -916,17 +924,19 @@ struct Miner {
             ch.pmi = pr.mi;
             const uint32_t R2 = (maxcid >> 1) + 1;
             ch.D = 2 * R2;
-            ch.rank_item.assign(R2, 0);
-            ch.node_of.assign(ch.D, -1);
-            const int32_t parent = pm.node_of[pr.mi];
+            ch.ri_off = b.child_rank_item.size();
+            ch.no_off = b.child_node_of.size();
+            b.child_rank_item.resize(ch.ri_off + R2, 0);
+            b.child_node_of.resize(ch.no_off + ch.D, -1);
+            const int32_t parent = b.node_of[pm.no_off + pr.mi];
             uint32_t last_type = 0;
             for (size_t k = q; k < q2; ++k) {
                 const FreqRec& fr = recs[k];
-                const uint32_t item = pm.rank_item[fr.slot >> 1];
+                const uint32_t item = b.rank_item[pm.ri_off + (fr.slot >> 1)];
                 const int32_t node = int32_t(nodes.size());
                 nodes.push_back(PNode{parent, item, fr.slot & 1u, fr.sup});
-                ch.rank_item[fr.cid >> 1] = item;
-                ch.node_of[fr.cid] = node;
+                b.child_rank_item[ch.ri_off + (fr.cid >> 1)] = item;
+                b.child_node_of[ch.no_off + fr.cid] = node;
                 ch.cap += fr.sup;
                 st.bytes_join_equiv += int64_t(12ull * fr.sup);
                 last_type = fr.slot & 1u;
@@ -985,8 +995,12 @@ struct Miner {
         for (size_t k = ga; k < gb; ++k) {
             ChildInfo& ch = b.children[k];
             ClassMeta& m = nb.cls[k - ga];
-            m.rank_item = std::move(ch.rank_item);
-            m.node_of = std::move(ch.node_of);
+            m.ri_off = nb.rank_item.size();
+            m.no_off = nb.node_of.size();
+            nb.rank_item.insert(nb.rank_item.end(), b.child_rank_item.begin() + int64_t(ch.ri_off),
+                                b.child_rank_item.begin() + int64_t(ch.ri_off + ch.D / 2));
+            nb.node_of.insert(nb.node_of.end(), b.child_node_of.begin() + int64_t(ch.no_off),
+                              b.child_node_of.begin() + int64_t(ch.no_off + ch.D));
             m.D = ch.D;
             m.nent = uint32_t(ch.cap);
             child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
@@ -1076,10 +1090,12 @@ struct Miner {
         const uint32_t F = uint32_t(freq_items.size());
         m.D = 2 * F;
         m.mshift = 1;  // root members are all sequence-extensions: counter rows by rank
-        m.rank_item = freq_items;
-        m.node_of.assign(m.D, -1);
+        m.ri_off = 0;
+        m.no_off = 0;
+        root.rank_item = freq_items;
+        root.node_of.assign(m.D, -1);
         for (uint32_t r = 0; r < F; ++r) {
-            m.node_of[2 * r] = int32_t(nodes.size());
+            root.node_of[2 * r] = int32_t(nodes.size());
             nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]]});
         }
         m.nent = uint32_t(E0);

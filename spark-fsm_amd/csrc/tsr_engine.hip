@@ -970,8 +970,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // kExpBatch rules, a few levels deep; the commit then registers the
     // pre-built rule (results cached) instead of deriving it again.
     int64_t spec_made = 0, spec_launches = 0;
+    int spec_depth = kSpecDepth, spec_max = kSpecMax;  // FSM_TSR_SPEC="depth,max" (tuning; "0" disables)
+    if (const char* v = std::getenv("FSM_TSR_SPEC")) {
+        int a = 0, b2 = 0;
+        if (std::sscanf(v, "%d,%d", &a, &b2) == 2 && a >= 0 && a <= 64 && b2 > 0 && b2 <= 4096) {
+            spec_depth = a;
+            spec_max = b2;
+        }
+    }
     auto speculate = [&](std::vector<Rule*> level) {
-        for (int depth = 0; depth < kSpecDepth && !level.empty(); ++depth) {
+        for (int depth = 0; depth < spec_depth && !level.empty(); ++depth) {
             uint32_t T = 0xFFFFFFFFu;
             for (Rule* x : level) T = std::min(T, x->sup);
             if (!pending.empty()) T = std::min(T, (*pending.rbegin())->sup);
@@ -984,7 +992,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 const size_t n = res.recs.size();
                 res.preL.assign(n, nullptr);
                 res.preR.assign(n, nullptr);
-                for (size_t i = 0; i < n && next.size() < size_t(kSpecMax); ++i) {
+                for (size_t i = 0; i < n && next.size() < size_t(spec_max); ++i) {
                     const ExpRec& e = res.recs[i];
                     if (x->expandLR && e.tl >= T) {
                         Rule* c = rp.derive(x, e.c, kNone, e.tl, e.dl);
@@ -992,7 +1000,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                         res.preL[i] = c;
                         next.push_back(c);
                     }
-                    if (e.tr >= T && next.size() < size_t(kSpecMax)) {
+                    if (e.tr >= T && next.size() < size_t(spec_max)) {
                         Rule* c = rp.derive(x, kNone, e.c, e.tr, x->nX);
                         c->expandLR = false;
                         res.preR[i] = c;
