@@ -1108,6 +1108,25 @@ struct Miner {
 
 };
 
+// malloc'd array without value-initialisation, released to the caller (freed by fsm_patterns_free)
+template <class T> struct MallocArr {
+    T* p = nullptr;
+    size_t n = 0;
+    explicit MallocArr(size_t n_) : n(n_) {
+        p = static_cast<T*>(std::malloc(std::max<size_t>(n, 1) * sizeof(T)));
+        if (!p) throw Error(FSM_ENOMEM, "malloc failed");
+    }
+    MallocArr(const MallocArr&) = delete;
+    MallocArr& operator=(const MallocArr&) = delete;
+    ~MallocArr() { std::free(p); }
+    T& operator[](size_t i) { return p[i]; }
+    T* release() {
+        T* r = p;
+        p = nullptr;
+        return r;
+    }
+};
+
 template <class T> void copy_out(T*& dst, const std::vector<T>& src) {
     dst = static_cast<T*>(std::malloc(std::max<size_t>(src.size(), 1) * sizeof(T)));
     if (!dst) throw Error(FSM_ENOMEM, "malloc failed");
@@ -1319,15 +1338,19 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         plen[size_t(k)] = (q < 0 ? 0u : plen[size_t(q)]) + 1u;
         pset[size_t(k)] = (q < 0 ? 0u : pset[size_t(q)]) + ((q < 0 || nodes[size_t(k)].type == kSeq) ? 1u : 0u);
     }
-    std::vector<int32_t> sup(static_cast<size_t>(n));
-    std::vector<int64_t> pat_off(size_t(n) + 1, 0), item_off(size_t(n) + 1, 0);
+    // the output arrays are filled in place (malloc'd, handed to the caller:
+    // no zero-fill and no second copy of multi-hundred-MB pattern sets)
+    MallocArr<int32_t> sup{static_cast<size_t>(n)};
+    MallocArr<int64_t> pat_off{static_cast<size_t>(n) + 1};
+    std::vector<int64_t> item_off(size_t(n) + 1, 0);
+    pat_off[0] = 0;
     for (int64_t k = 0; k < n; ++k) {
         pat_off[size_t(k) + 1] = pat_off[size_t(k)] + pset[size_t(first + k)];
         item_off[size_t(k) + 1] = item_off[size_t(k)] + plen[size_t(first + k)];
     }
-    std::vector<int64_t> set_off(size_t(pat_off[size_t(n)]) + 1);
-    std::vector<int32_t> items(static_cast<size_t>(item_off[size_t(n)]));
-    set_off.back() = item_off[size_t(n)];
+    MallocArr<int64_t> set_off{static_cast<size_t>(pat_off[size_t(n)]) + 1};
+    MallocArr<int32_t> items{static_cast<size_t>(item_off[size_t(n)])};
+    set_off[set_off.n - 1] = item_off[size_t(n)];
     const int32_t* ival = db->spade.item_val.data();
     auto fill = [&](int64_t k0, int64_t k1) {
         for (int64_t k = k0; k < k1; ++k) {
@@ -1349,22 +1372,31 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         fill(0, n);
     }
     ctx->stats.ms_output = now_ms() - to0;
-    if (comm) {
-        gather_patterns(comm, ctx->stream, sup, pat_off, set_off, items);
-        n = int64_t(sup.size());
-        gather_stats(comm, ctx->stream, ctx->stats);
-    }
     auto* p = static_cast<fsm_patterns*>(std::calloc(1, sizeof(fsm_patterns)));
     if (!p) throw Error(FSM_ENOMEM, "calloc failed");
-    p->n = n;
-    p->n_sets = int64_t(set_off.size()) - 1;
-    p->n_items = int64_t(items.size());
     p->total = total;
     p->minsup = int32_t(std::min<uint32_t>(mn.minsup, 0x7FFFFFFFu));
-    copy_out(p->support, sup);
-    copy_out(p->pat_off, pat_off);
-    copy_out(p->set_off, set_off);
-    copy_out(p->items, items);
+    if (comm) {  // every rank's CSR, concatenated in rank order
+        std::vector<int32_t> vs(sup.p, sup.p + sup.n), vi(items.p, items.p + items.n);
+        std::vector<int64_t> vp(pat_off.p, pat_off.p + pat_off.n), vo(set_off.p, set_off.p + set_off.n);
+        gather_patterns(comm, ctx->stream, vs, vp, vo, vi);
+        n = int64_t(vs.size());
+        gather_stats(comm, ctx->stream, ctx->stats);
+        p->n_sets = int64_t(vo.size()) - 1;
+        p->n_items = int64_t(vi.size());
+        copy_out(p->support, vs);
+        copy_out(p->pat_off, vp);
+        copy_out(p->set_off, vo);
+        copy_out(p->items, vi);
+    } else {
+        p->n_sets = int64_t(set_off.n) - 1;
+        p->n_items = int64_t(items.n);
+        p->support = sup.release();
+        p->pat_off = pat_off.release();
+        p->set_off = set_off.release();
+        p->items = items.release();
+    }
+    p->n = n;
     ctx->stats.patterns = n;
     ctx->stats.ms_mine = now_ms() - t0;
     *out = p;
