@@ -412,19 +412,15 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
             fX = wave_max(fX);
             lY = wave_min(lY);
             if (fX >= lY) continue;  // X => Y does not hold in s
-            if (side.doL) {          // expandL: c > max(X), c not in Y, c before lastY(s)
-                const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
-                for (uint32_t e = q0 + lane; e < re; e += 64) {
-                    const uint32_t c = item[e];
-                    if (first[e] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
-                }
-            }
-            if (side.doR) {          // expandR: c > max(Y), c not in X, c after firstX(s)
-                const uint32_t q0 = row_find(item, rb, re, side.maxY + 1);
-                for (uint32_t e = q0 + lane; e < re; e += 64) {
-                    const uint32_t c = item[e];
-                    if (last[e] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
-                }
+            // expandL (c > max(X), c not in Y, c before lastY(s)) and expandR
+            // (c > max(Y), c not in X, c after firstX(s)) in one pass over the
+            // row tail both need: each entry's item / first / last read once
+            const uint32_t qL = side.doL ? row_find(item, rb, re, side.maxX + 1) : re;
+            const uint32_t qR = side.doR ? row_find(item, rb, re, side.maxY + 1) : re;
+            for (uint32_t e = min(qL, qR) + lane; e < re; e += 64) {
+                const uint32_t c = item[e];
+                if (e >= qL && first[e] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
+                if (e >= qR && last[e] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
             }
         }
         __syncthreads();
