@@ -55,6 +55,7 @@ struct KernelClock {
     ~KernelClock() { release(); }
     size_t begin(const char* name);
     void end(size_t idx, int64_t alg_bytes);
+    void add_bytes(size_t idx, int64_t alg_bytes) { recs[idx].bytes += alg_bytes; }  // known after a later sync
     void finish(std::vector<fsm_kernel_stat>& out);
     void release();
 };

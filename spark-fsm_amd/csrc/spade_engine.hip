@@ -248,7 +248,11 @@ __global__ __launch_bounds__(kBlock) void k_root_keys(uint32_t E0, const uint32_
                                                       const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
                                                       uint32_t mlo, uint32_t mhi, const uint64_t* __restrict__ koff,
                                                       uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey,
-                                                      uint32_t min_rl) {
+                                                      uint32_t min_rl, unsigned long long* __restrict__ nkeys_total) {
+    __shared__ uint32_t blk_keys;
+    if (threadIdx.x == 0) blk_keys = 0;
+    __syncthreads();
+    uint32_t my_keys = 0;
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E0; e += gridDim.x * blockDim.x) {
         if ((pos[e] & 0xFFFFu) <= min_rl) continue;  // row handled by k_root_keys_row
         const uint32_t mi = mem[e];
@@ -259,7 +263,11 @@ __global__ __launch_bounds__(kBlock) void k_root_keys(uint32_t E0, const uint32_
             root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { out[n++] = uint16_t(key - gbase); });
         }
         nkey[e] = uint16_t(n);
+        my_keys += n;
     }
+    atomicAdd(&blk_keys, my_keys);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
 // The same enumeration, one wave per root row of <= 64 entries (the
@@ -284,8 +292,13 @@ __global__ __launch_bounds__(kBlock) void k_root_keys_row(uint32_t R, const uint
                                                           const uint32_t* __restrict__ lohi,
                                                           const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
                                                           uint32_t mlo, uint32_t mhi,
-                                                          const uint64_t* __restrict__ koff,
-                                                          uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey) {
+                                                          uint64_t* __restrict__ koff,
+                                                          uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey,
+                                                          unsigned long long* __restrict__ nkeys_total) {
+    __shared__ uint32_t blk_keys;
+    if (threadIdx.x == 0) blk_keys = 0;
+    __syncthreads();
+    uint32_t my_keys = 0;  // keys this lane's entries wrote (exact algorithmic bytes for the stats)
     const uint32_t lane = lane_id();
     const uint64_t lt = lanemask_lt();
     const uint32_t wstride = (gridDim.x * blockDim.x) >> 6;
@@ -310,6 +323,11 @@ __global__ __launch_bounds__(kBlock) void k_root_keys_row(uint32_t R, const uint
         }
         const uint32_t rq = me >> 1, hq = mlh >> 16;
         const uint64_t actb = __ballot(act != 0u);
+        // the row's keys are packed from the row's first run offset on (the
+        // upper-bound gaps collect at the row's end): every step's stretch
+        // continues the previous one, so the row writes whole lines
+        const uint64_t kb_row = uint64_t(rl32(kb_lo, 0)) | (uint64_t(rl32(kb_hi, 0)) << 32);
+        uint64_t run = 0, mystart = kb_row;
         uint32_t mycnt = 0;
         for (uint32_t i = 0; i < rl; ++i) {
             if (!((actb >> i) & 1ull)) continue;  // entry i counted by another rank (uniform)
@@ -321,15 +339,26 @@ __global__ __launch_bounds__(kBlock) void k_root_keys_row(uint32_t R, const uint
             const bool t_ok = v && hq > li;
             const bool e_ok = v && rq > ri && inter;
             const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
-            const uint64_t kbi = uint64_t(rl32(kb_lo, i)) | (uint64_t(rl32(kb_hi, i)) << 32);
+            const uint64_t kbi = kb_row + run;
             const uint32_t key = rl32(kbase, i) + (rq << 1);
-            const uint32_t nt = uint32_t(__popcll(tb));
+            const uint32_t nt = uint32_t(__popcll(tb)), n = nt + uint32_t(__popcll(eb));
             if (t_ok) keys[kbi + uint32_t(__popcll(tb & lt))] = uint16_t(key);
             if (e_ok) keys[kbi + nt + uint32_t(__popcll(eb & lt))] = uint16_t(key | 1u);
-            if (lane == i) mycnt = nt + uint32_t(__popcll(eb));
+            if (lane == i) {
+                mycnt = n;
+                mystart = kbi;
+            }
+            run += n;
         }
-        if (v) nkey[rb + lane] = uint16_t(mycnt);
+        if (v) {
+            nkey[rb + lane] = uint16_t(mycnt);
+            koff[rb + lane] = mystart;  // actual run start (k_group_scatter reads it)
+        }
+        my_keys += mycnt;
     }
+    atomicAdd(&blk_keys, my_keys);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
 __global__ __launch_bounds__(kBlock) void k_group_hist(uint32_t E0, const uint32_t* __restrict__ mem, uint32_t per,
@@ -377,7 +406,19 @@ __global__ __launch_bounds__(1024) void k_group_count(const uint64_t* __restrict
     for (uint32_t i = l0 + threadIdx.x; i < l1; i += blockDim.x) {
         const uint2 r = runs[i];
         const uint16_t* k = keys + r.x;
-        for (uint32_t j = 0; j < r.y; ++j) atomicAdd(&h[k[j]], 1u);
+        // a run is contiguous: 8-byte loads (4 keys) once aligned, so a lane
+        // touches each of its run's lines once instead of once per key
+        uint32_t j = 0;
+        const uint32_t head = min(r.y, (4u - (r.x & 3u)) & 3u);
+        for (; j < head; ++j) atomicAdd(&h[k[j]], 1u);
+        for (; j + 4 <= r.y; j += 4) {
+            const uint64_t q = *reinterpret_cast<const uint64_t*>(k + j);
+            atomicAdd(&h[uint32_t(q & 0xFFFFu)], 1u);
+            atomicAdd(&h[uint32_t((q >> 16) & 0xFFFFu)], 1u);
+            atomicAdd(&h[uint32_t((q >> 32) & 0xFFFFu)], 1u);
+            atomicAdd(&h[uint32_t(q >> 48)], 1u);
+        }
+        for (; j < r.y; ++j) atomicAdd(&h[k[j]], 1u);
     }
     __syncthreads();
     const uint32_t base = g * per * D, n = (min(F, (g + 1) * per) - g * per) * D;
@@ -773,26 +814,34 @@ struct Miner {
         // without row offsets): the per-entry kernel
         const bool rows = b.root_rows.p != nullptr && b.R > 0;
         const uint32_t min_rl = rows ? 64u : 0u;
+        DevBuf nkeys_row(16);  // [0] row kernel, [1] per-entry kernel
+        size_t tk_row = size_t(-1);
+        FSM_HIP(hipMemsetAsync(nkeys_row.p, 0, 16, s));
         if (rows) {
             tk = clk->begin("k_root_keys_row");
             const unsigned rgrid = unsigned(std::min<uint64_t>((b.R * 64 + kBlock - 1) / kBlock, 1u << 16));
 #define FSM_RKR(WW)                                                                                                 \
     hipLaunchKernelGGL(k_root_keys_row<WW>, dim3(rgrid), dim3(kBlock), 0, s, uint32_t(b.R),                       \
                        b.root_rows.as<uint64_t>(), sp.mem, sp.lohi, sp.mask, D, per, mlo, mhi, koff.as<uint64_t>(), \
-                       keys.as<uint16_t>(), nkey.as<uint16_t>())
+                       keys.as<uint16_t>(), nkey.as<uint16_t>(), nkeys_row.as<unsigned long long>())
             FSM_W_DISPATCH(W, FSM_RKR)
 #undef FSM_RKR
             FSM_LAUNCHED("k_root_keys_row", s);
-            clk->end(tk, slab_bytes + int64_t(E0) * 10 + int64_t(nslots) * 2);
+            // reads the slab + koff, writes nkey; the key bytes (2 B per key actually
+            // written) are added once the count is back on the host
+            clk->end(tk, slab_bytes + int64_t(E0) * 10);
+            tk_row = tk;
         }
         tk = clk->begin("k_root_keys");
 #define FSM_RK(WW)                                                                                             \
     hipLaunchKernelGGL(k_root_keys<WW>, dim3(grid), dim3(kBlock), 0, s, E0, sp.mem, sp.lohi, sp.pos, sp.mask, \
-                       D, per, mlo, mhi, koff.as<uint64_t>(), keys.as<uint16_t>(), nkey.as<uint16_t>(), min_rl)
+                       D, per, mlo, mhi, koff.as<uint64_t>(), keys.as<uint16_t>(), nkey.as<uint16_t>(), min_rl,  \
+                       nkeys_row.as<unsigned long long>() + 1)
         FSM_W_DISPATCH(W, FSM_RK)
 #undef FSM_RK
         FSM_LAUNCHED("k_root_keys", s);
-        clk->end(tk, rows ? int64_t(E0) * 4 : slab_bytes + int64_t(E0) * 10 + int64_t(nslots) * 2);
+        clk->end(tk, rows ? int64_t(E0) * 4 : slab_bytes + int64_t(E0) * 10);  // + its keys, added below
+        const size_t tk_ent = tk;
         // runs in group order
         const uint32_t chunk = root_chunk();
         const uint32_t nblk = (E0 + chunk - 1) / chunk;
@@ -815,8 +864,13 @@ struct Miner {
         hipLaunchKernelGGL(k_group_count, dim3(G), dim3(1024), 0, s, goff.as<uint64_t>(), nblk, runs.as<uint2>(),
                            keys.as<uint16_t>(), D, per, F, cnt);
         FSM_LAUNCHED("k_group_count", s);
-        clk->end(tk, int64_t(E0) * 8 + int64_t(nslots) * 2 + int64_t(K) * 4);
+        clk->end(tk, int64_t(E0) * 8 + int64_t(K) * 4);
+        unsigned long long nk[2] = {0, 0};  // keys written by the row kernel / the per-entry kernel
+        FSM_HIP(hipMemcpyAsync(nk, nkeys_row.p, 16, hipMemcpyDeviceToHost, s));
         sync();  // temporaries released on return
+        if (tk_row != size_t(-1)) clk->add_bytes(tk_row, int64_t(nk[0]) * 2);
+        clk->add_bytes(tk_ent, int64_t(nk[1]) * 2);
+        clk->add_bytes(tk, int64_t(nk[0] + nk[1]) * 2);  // k_group_count reads every key once
         return true;
     }
 
@@ -1317,7 +1371,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     clock.finish(ctx->kstats);
     for (const fsm_kernel_stat& k : ctx->kstats) {
         const std::string nm = k.name;
-        if (nm == "k_count" || nm.rfind("k_rootpair", 0) == 0 || nm == "k_bucket_count") ctx->stats.ms_count_kernel += k.ms;
+        if (nm == "k_count" || nm.rfind("k_root_keys", 0) == 0 || nm == "k_group_count") ctx->stats.ms_count_kernel += k.ms;
         if (nm.rfind("k_emit", 0) == 0) ctx->stats.ms_emit_kernel += k.ms;
     }
 
