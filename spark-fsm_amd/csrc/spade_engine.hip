@@ -406,19 +406,7 @@ __global__ __launch_bounds__(1024) void k_group_count(const uint64_t* __restrict
     for (uint32_t i = l0 + threadIdx.x; i < l1; i += blockDim.x) {
         const uint2 r = runs[i];
         const uint16_t* k = keys + r.x;
-        // a run is contiguous: 8-byte loads (4 keys) once aligned, so a lane
-        // touches each of its run's lines once instead of once per key
-        uint32_t j = 0;
-        const uint32_t head = min(r.y, (4u - (r.x & 3u)) & 3u);
-        for (; j < head; ++j) atomicAdd(&h[k[j]], 1u);
-        for (; j + 4 <= r.y; j += 4) {
-            const uint64_t q = *reinterpret_cast<const uint64_t*>(k + j);
-            atomicAdd(&h[uint32_t(q & 0xFFFFu)], 1u);
-            atomicAdd(&h[uint32_t((q >> 16) & 0xFFFFu)], 1u);
-            atomicAdd(&h[uint32_t((q >> 32) & 0xFFFFu)], 1u);
-            atomicAdd(&h[uint32_t(q >> 48)], 1u);
-        }
-        for (; j < r.y; ++j) atomicAdd(&h[k[j]], 1u);
+        for (uint32_t j = 0; j < r.y; ++j) atomicAdd(&h[k[j]], 1u);
     }
     __syncthreads();
     const uint32_t base = g * per * D, n = (min(F, (g + 1) * per) - g * per) * D;
