@@ -967,6 +967,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // pre-built rule (results cached) instead of deriving it again.
     int64_t spec_made = 0, spec_launches = 0;
     int spec_depth = kSpecDepth, spec_max = kSpecMax;  // FSM_TSR_SPEC="depth,max" (tuning; "0" disables)
+    double spec_frac = 1.0;  // FSM_TSR_SPEC_FRAC: speculate children with sup >= frac * T (tuning)
+    if (const char* v = std::getenv("FSM_TSR_SPEC_FRAC")) {
+        const double f = std::atof(v);
+        if (f > 0.0 && f <= 1.0) spec_frac = f;
+    }
     if (const char* v = std::getenv("FSM_TSR_SPEC")) {
         int a = 0, b2 = 0;
         if (std::sscanf(v, "%d,%d", &a, &b2) == 2 && a >= 0 && a <= 64 && b2 > 0 && b2 <= 4096) {
@@ -979,7 +984,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             uint32_t T = 0xFFFFFFFFu;
             for (Rule* x : level) T = std::min(T, x->sup);
             if (!pending.empty()) T = std::min(T, (*pending.rbegin())->sup);
-            T = std::max(T, rp.minsup);
+            T = std::max(uint32_t(double(T) * spec_frac), rp.minsup);
             std::vector<Rule*> next;
             for (Rule* x : level) {
                 auto it = cache.find(x);

@@ -325,3 +325,25 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
         db.free()
     rules.sort(key=lambda t: (-t[2], t[0], t[1]))
     assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
+
+
+@pytest.mark.parametrize("spec", ["0", "3,128", "8,16"])
+@pytest.mark.parametrize("grid", ["128,8,512", "16,2,64"])
+def test_tsr_speculation_and_grids_agree(eng, spec, grid, monkeypatch):
+    """Child speculation (FSM_TSR_SPEC: off / default / deep-narrow) and the
+    per-launch grids (FSM_TSR_GRID) change only which expansions run ahead and
+    how they are split over blocks: the rules and final minsup stay the oracle's."""
+    from oracle import oracle
+    from tools import gen
+    from spark_fsm_amd import MODE_TSR
+    monkeypatch.setenv("FSM_TSR_SPEC", spec)
+    monkeypatch.setenv("FSM_TSR_GRID", grid)
+    ds = gen.kosarak(D=5000, seed=5)
+    o = oracle.tsr(ds.records(), 200, 0.5)
+    db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)
+    try:
+        rules, meta = eng.tsr(db, 200, 0.5)
+    finally:
+        db.free()
+    rules.sort(key=lambda t: (-t[2], t[0], t[1]))
+    assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
