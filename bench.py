@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # all-cores CPU mode (SURVEY §8d ii); 16 = the box's CPU share per GPU (0 = skip)
+    ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,10 +166,21 @@ def main():
                                 want_patterns=False)
         line["cpu_baseline"] = {
             "value": r["joins"] / r["seconds"], "unit": "joins/s", "cores": 1, "kind": "port",
+            "lattice_value": r["joins"] / max(r["seconds"] - r["seconds_f1"], 1e-9), "seconds_f1": r["seconds_f1"],
             "sample": "same DB and minsup; first %.0f s of the single-thread vertical SPADE DFS "
                       "(oracle/fsm_oracle.c, F1 build included): %d joins%s; host %s" % (
                           args.cpu_seconds, r["joins"], "" if not r["complete"] else " (complete)",
                           cpu_model())}
+        if args.cpu_threads > 1:
+            r2 = oracle.spade_tokens(ds.seq_off, ds.tokens, args.support, time_limit_s=args.cpu_seconds,
+                                     want_patterns=False, threads=args.cpu_threads)
+            line["extra"]["cpu_baseline_all_cores"] = {
+                "value": r2["joins"] / r2["seconds"], "unit": "joins/s", "cores": args.cpu_threads,
+                "kind": "port", "complete": r2["complete"], "seconds": r2["seconds"], "joins": r2["joins"],
+                "lattice_value": r2["joins"] / max(r2["seconds"] - r2["seconds_f1"], 1e-9),
+                "seconds_f1": r2["seconds_f1"],
+                "sample": "same DB and minsup, same time bound; first-level classes on %d OpenMP threads "
+                          "(F1 build single-threaded)" % args.cpu_threads}
     print(json.dumps(line), flush=True)
     db.free()
     eng.close()

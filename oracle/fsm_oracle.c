@@ -360,8 +360,8 @@ static oracle_patterns* build_patterns(const nodevec* nodes) {
     return p;
 }
 
-static int spade_core(regvec* regs, int64_t n, double support, double time_limit_s, oracle_patterns** out,
-                      char* err, int errlen);
+static int spade_core(regvec* regs, int64_t n, double support, double time_limit_s, int nthreads,
+                      oracle_patterns** out, char* err, int errlen);
 
 int oracle_spade(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
                  double support, oracle_patterns** out, char* err, int errlen) {
@@ -381,7 +381,7 @@ int oracle_spade(const int32_t* sids, const char* const* lines, const int64_t* l
             goto done;
         }
     }
-    rc = spade_core(&regs, n, support, 0.0, out, err, errlen);
+    rc = spade_core(&regs, n, support, 0.0, 1, out, err, errlen);
 done:
     VFREE(regs);
     VFREE(toks);
@@ -394,6 +394,16 @@ done:
  * baseline sample: joins done / seconds). */
 int oracle_spade_tokens(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
                         double time_limit_s, oracle_patterns** out, char* err, int errlen) {
+    return oracle_spade_tokens_mt(seq_off, tokens, n, support, time_limit_s, 1, out, err, errlen);
+}
+
+/* All-cores variant (SURVEY.md §8d CPU mode ii): the first-level classes [x]
+ * are independent DFS roots, processed by nthreads OpenMP threads (dynamic
+ * schedule, one class per grab).  Each class's nodes are renumbered after the
+ * root nodes in class order, so a complete run returns exactly the pattern
+ * list of the sequential DFS. */
+int oracle_spade_tokens_mt(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
+                           double time_limit_s, int nthreads, oracle_patterns** out, char* err, int errlen) {
     *out = NULL;
     regvec regs = {0};
     for (int64_t r = 0; r < n; r++) {
@@ -409,13 +419,54 @@ int oracle_spade_tokens(const int64_t* seq_off, const int64_t* tokens, int64_t n
             VPUSH(regs, rg);
         }
     }
-    int rc = spade_core(&regs, n, support, time_limit_s, out, err, errlen);
+    int rc = spade_core(&regs, n, support, time_limit_s, nthreads < 1 ? 1 : nthreads, out, err, errlen);
     VFREE(regs);
     return rc;
 }
 
-static int spade_core(regvec* regsp, int64_t n, double support, double time_limit_s, oracle_patterns** out,
-                      char* err, int errlen) {
+/* Top level of process_class with one OpenMP task per first-level class.
+ * Task i owns a private ctx whose node table starts with copies of the root
+ * nodes (so parents < nroot are root nodes), then the merge appends each
+ * task's own nodes in i order, remapping parents. */
+static void process_root_mt(spade_ctx* c, member* m, int64_t n, int nthreads) {
+    const int64_t nroot = c->nodes.n;
+    spade_ctx* tc = calloc((size_t)(n ? n : 1), sizeof(spade_ctx));
+    volatile int stop = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (int64_t i = 0; i < n; i++) {
+        spade_ctx* t = &tc[i];
+        t->W = c->W;
+        t->minsup = c->minsup;
+        t->deadline = c->deadline;
+        if (stop) { t->stopped = 1; continue; }
+        for (int64_t k = 0; k < nroot; k++) VPUSH(t->nodes, c->nodes.a[k]);
+        membervec child = {0};
+        for (int64_t j = 0; j < n; j++) {  /* root members are all SEQ (P = {}) */
+            try_candidate(t, &m[i], &m[j], 1, &child);
+            if (m[j].item > m[i].item) try_candidate(t, &m[i], &m[j], 0, &child);
+        }
+        if (child.n && !t->stopped) process_class(t, child.a, child.n);
+        for (int64_t k = 0; k < child.n; k++) ilist_free(&child.a[k].L);
+        VFREE(child);
+        if (t->stopped) stop = 1;
+    }
+    for (int64_t i = 0; i < n; i++) {
+        spade_ctx* t = &tc[i];
+        const int64_t base = c->nodes.n;
+        for (int64_t k = nroot; k < t->nodes.n; k++) {
+            pnode nd = t->nodes.a[k];
+            if (nd.parent >= nroot) nd.parent = (int32_t)(base + (nd.parent - nroot));
+            VPUSH(c->nodes, nd);
+        }
+        c->joins += t->joins;
+        if (t->stopped) c->stopped = 1;
+        VFREE(t->nodes);
+    }
+    free(tc);
+}
+
+static int spade_core(regvec* regsp, int64_t n, double support, double time_limit_s, int nthreads,
+                      oracle_patterns** out, char* err, int errlen) {
     regvec regs = *regsp;
     int rc = 0;
     {
@@ -505,7 +556,9 @@ static int spade_core(regvec* regsp, int64_t n, double support, double time_limi
             }
         }
         free(vert);
-        process_class(&c, root.a, root.n);
+        const double t_f1 = mono_s() - t_start;
+        if (nthreads > 1) process_root_mt(&c, root.a, root.n, nthreads);
+        else process_class(&c, root.a, root.n);
         for (int64_t k = 0; k < root.n; k++) ilist_free(&root.a[k].L);
         VFREE(root);
         oracle_patterns* p = build_patterns(&c.nodes);
@@ -513,6 +566,7 @@ static int spade_core(regvec* regsp, int64_t n, double support, double time_limi
         p->minsup = c.minsup;
         p->complete = !c.stopped;
         p->seconds = mono_s() - t_start;
+        p->seconds_f1 = t_f1;
         *out = p;
         VFREE(c.nodes);
         free(uitems);

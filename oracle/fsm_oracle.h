@@ -41,6 +41,7 @@ typedef struct {
     int32_t  minsup;     /* absolute threshold used */
     int32_t  complete;   /* 0 if a time limit stopped the lattice early */
     double   seconds;    /* wall time of F1 build + lattice (after parse) */
+    double   seconds_f1; /* of which the F1 vertical build + filter */
 } oracle_patterns;
 
 typedef struct {
@@ -65,6 +66,9 @@ int oracle_spade(const int32_t* sids, const char* const* lines, const int64_t* l
 void oracle_patterns_free(oracle_patterns* p);
 int oracle_spade_tokens(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
                         double time_limit_s, oracle_patterns** out, char* err, int errlen);
+/* Same, first-level classes mined by nthreads OpenMP threads (CPU baseline mode ii). */
+int oracle_spade_tokens_mt(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
+                           double time_limit_s, int nthreads, oracle_patterns** out, char* err, int errlen);
 
 int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
                int32_t k, double minconf, oracle_rules** out, char* err, int errlen);

@@ -35,6 +35,7 @@ class _Patterns(ctypes.Structure):
         ("minsup", ctypes.c_int32),
         ("complete", ctypes.c_int32),
         ("seconds", ctypes.c_double),
+        ("seconds_f1", ctypes.c_double),
     ]
 
 
@@ -80,6 +81,10 @@ def lib():
         L.oracle_spade_tokens.argtypes = [I64P, I64P, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                           ctypes.POINTER(ctypes.POINTER(_Patterns)), ctypes.c_char_p, ctypes.c_int]
         L.oracle_spade_tokens.restype = ctypes.c_int
+        L.oracle_spade_tokens_mt.argtypes = [I64P, I64P, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.POINTER(_Patterns)),
+                                             ctypes.c_char_p, ctypes.c_int]
+        L.oracle_spade_tokens_mt.restype = ctypes.c_int
         L.oracle_pattern_support.argtypes = [I64P, I64P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                              I64P, ctypes.c_int64]
         L.oracle_pattern_support.restype = ctypes.c_int64
@@ -126,21 +131,22 @@ def _np64(a):
     return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
 
-def spade_tokens(seq_off, tokens, support, time_limit_s=0.0, want_patterns=True):
+def spade_tokens(seq_off, tokens, support, time_limit_s=0.0, want_patterns=True, threads=1):
     """Token-stream SPADE (sid = record index).  With time_limit_s > 0 the
     lattice stops after that long: returns joins done and seconds (the
-    bounded CPU-baseline sample used by bench.py)."""
+    bounded CPU-baseline sample used by bench.py).  threads > 1 mines the
+    first-level classes on that many OpenMP threads (SURVEY §8d mode ii)."""
     L = lib()
     so, so_p = _np64(seq_off)
     tk, tk_p = _np64(tokens)
     out = ctypes.POINTER(_Patterns)()
     err = ctypes.create_string_buffer(512)
-    rc = L.oracle_spade_tokens(so_p, tk_p, len(so) - 1, float(support), float(time_limit_s),
-                               ctypes.byref(out), err, 512)
+    rc = L.oracle_spade_tokens_mt(so_p, tk_p, len(so) - 1, float(support), float(time_limit_s), int(threads),
+                                  ctypes.byref(out), err, 512)
     if rc != 0:
         raise OracleError(err.value.decode())
     p = out.contents
-    res = {"joins": p.joins, "minsup": p.minsup, "complete": bool(p.complete), "seconds": p.seconds,
+    res = {"joins": p.joins, "minsup": p.minsup, "complete": bool(p.complete), "seconds": p.seconds, "seconds_f1": p.seconds_f1,
            "n_patterns": p.n}
     if want_patterns:
         res["patterns"] = sorted(_patterns_out(p))

@@ -130,3 +130,15 @@ def test_tsr_random_orders_are_definitional():
         k = rng.randint(1, 10)
         mc = rng.choice([0.0, 0.5])
         brute.check_tsr(oracle.tsr(recs, k, mc)["rules"], brute.brute_tsr_valid(recs, mc), k)
+
+
+def test_oracle_all_cores_mode_matches_single_thread():
+    """CPU baseline mode ii: first-level classes on OpenMP threads
+    must give the single-thread result (patterns, supports, join count)."""
+    from tools import gen
+    ds = gen.quest(3000, seed=4)
+    a = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.01)
+    b = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.01, threads=4)
+    assert a["complete"] and b["complete"]
+    assert a["joins"] == b["joins"] and a["patterns"] == b["patterns"]
+    assert a["n_patterns"] > 50
