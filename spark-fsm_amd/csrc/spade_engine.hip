@@ -51,7 +51,7 @@ namespace fsm {
 namespace {
 
 constexpr uint32_t kSeq = 0, kItm = 1;
-constexpr uint32_t kChunk = 2048;        // class entries per workgroup work item
+constexpr uint32_t kChunk = 512;         // class entries per k_count block (FSM_COUNT_CHUNK; swept on MI355X)
 constexpr uint32_t kRootChunk = 16384;     // root entries per block of the group histogram / scatter
 constexpr uint32_t kGroupCounters = 32768;  // root F2: u32 LDS counters of one rank group (128 KiB)
 constexpr uint32_t kMaxGroups = 16384;      // LDS histogram of k_group_hist (64 KiB)
@@ -163,9 +163,10 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
                                                   const DClass* __restrict__ cls,
                                                   const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
                                                   const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
-                                                  uint32_t mlo, uint32_t mhi, uint32_t* __restrict__ cnt) {
-    const uint32_t e1 = min(E, (blockIdx.x + 1) * kChunk);
-    for (uint32_t e = blockIdx.x * kChunk + threadIdx.x; e < e1; e += blockDim.x) {
+                                                  uint32_t mlo, uint32_t mhi, uint32_t chunk,
+                                                  uint32_t* __restrict__ cnt) {
+    const uint32_t e1 = min(E, (blockIdx.x + 1) * chunk);
+    for (uint32_t e = blockIdx.x * chunk + threadIdx.x; e < e1; e += blockDim.x) {
         const uint32_t mi = mem[e], p = pos[e];
         if (mi - mlo >= mhi - mlo) continue;  // member rows of another rank (sharded root)
         const DClass c = cls[cid[e]];
@@ -763,6 +764,11 @@ struct Miner {
         const char* v = std::getenv("FSM_ROOT_PATH");
         return v && !std::strcmp(v, "atomic");
     }
+    // class entries per block of k_count (FSM_COUNT_CHUNK overrides, for tuning)
+    static uint32_t count_chunk() {
+        const char* v = std::getenv("FSM_COUNT_CHUNK");
+        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kChunk;
+    }
     // root entries per block of the bucketed passes (FSM_ROOT_CHUNK overrides, for tuning)
     static uint32_t root_chunk() {
         const char* v = std::getenv("FSM_ROOT_CHUNK");
@@ -881,10 +887,11 @@ struct Miner {
             if (!done) {
                 FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
                 const SlabPtrs sp = b.slab.ptrs();
+                const uint32_t cchunk = count_chunk();
 #define FSM_COUNT(WW)                                                                                   \
-    hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + kChunk - 1) / kChunk)), dim3(kBlock), 0, s,   \
+    hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + cchunk - 1) / cchunk)), dim3(kBlock), 0, s,   \
                        uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
-                       member_lo(b), member_hi(b), cnt.as<uint32_t>())
+                       member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>())
                 const size_t tk = clk->begin("k_count");
                 FSM_W_DISPATCH(W, FSM_COUNT)
 #undef FSM_COUNT
