@@ -764,6 +764,11 @@ struct Miner {
         const char* v = std::getenv("FSM_ROOT_PATH");
         return v && !std::strcmp(v, "atomic");
     }
+    // grid cap of k_root_keys_row (FSM_ROW_GRID overrides, for tuning)
+    static uint64_t row_grid_cap() {
+        const char* v = std::getenv("FSM_ROW_GRID");
+        return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 22) : (1u << 14);
+    }
     // class entries per block of k_count (FSM_COUNT_CHUNK overrides, for tuning)
     static uint32_t count_chunk() {
         const char* v = std::getenv("FSM_COUNT_CHUNK");
@@ -813,7 +818,7 @@ struct Miner {
         FSM_HIP(hipMemsetAsync(nkeys_row.p, 0, 16, s));
         if (rows) {
             tk = clk->begin("k_root_keys_row");
-            const unsigned rgrid = unsigned(std::min<uint64_t>((b.R * 64 + kBlock - 1) / kBlock, 1u << 16));
+            const unsigned rgrid = unsigned(std::min<uint64_t>((b.R * 64 + kBlock - 1) / kBlock, row_grid_cap()));
 #define FSM_RKR(WW)                                                                                                 \
     hipLaunchKernelGGL(k_root_keys_row<WW>, dim3(rgrid), dim3(kBlock), 0, s, uint32_t(b.R),                       \
                        b.root_rows.as<uint64_t>(), sp.mem, sp.lohi, sp.mask, D, per, mlo, mhi, koff.as<uint64_t>(), \
