@@ -764,6 +764,11 @@ struct Miner {
         const char* v = std::getenv("FSM_ROOT_PATH");
         return v && !std::strcmp(v, "atomic");
     }
+    // grid cap of k_emit (FSM_EMIT_GRID overrides, for tuning)
+    static uint64_t emit_grid_cap() {
+        const char* v = std::getenv("FSM_EMIT_GRID");
+        return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 22) : (1u << 16);
+    }
     // grid cap of k_root_keys_row (FSM_ROW_GRID overrides, for tuning)
     static uint64_t row_grid_cap() {
         const char* v = std::getenv("FSM_ROW_GRID");
@@ -1070,7 +1075,7 @@ struct Miner {
         if (b.E) {
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
-            const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 1u << 16));
+            const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, emit_grid_cap()));
 #define FSM_EMIT(WW, WR)                                                                                            \
     hipLaunchKernelGGL((k_emit<WW, WR>), dim3(grid), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
                        sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),        \
