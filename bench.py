@@ -1,11 +1,20 @@
 """bench.py — SPADE id-list joins/sec + mine time on Quest D1M, minsup 0.1 %.
 
 BASELINE.json metric: "id-list joins/sec + end-to-end SPADE mine time, Quest
-D1M minsup 0.1%".  One step = one complete fsm_spade_mine (F1, root F2 pair
-matrix, whole lattice, pattern CSR back on the host) over the flattened DB,
-which is resident in HBM before the timed region (flatten + upload are timed
+D1M minsup 0.1%".  One step = one complete fsm_spade_mine (F1, root F2, the
+whole lattice, pattern CSR back on the host) over the flattened DB, which is
+resident in HBM before the timed region (flatten + upload are timed
 separately and reported in `extra`).  value = SURVEY A.2 candidate joins
-(including infrequent ones) / mine time.
+(including infrequent ones) / mine time.  Because most A.2 candidates at D1M
+are the F x F root pairs, `extra` also reports the work actually executed:
+the non-empty root pair joins the F2 counted, the A.2 joins of the classes
+below the root, and the lattice-only rate.
+
+CPU baseline: the CPU restatement (oracle/fsm_oracle.c) on the
+same DB and minsup, median of 3 bounded samples, in the same scope as `value`
+(DB build excluded on both sides: the GPU's flatten + upload, the CPU's F1
+vertical build), 1 thread (the reference's one driver thread) and all cores
+of this process's CPU share.
 
   python bench.py [--gpus N --steps K --warmup W]   (N > 1 via torch.distributed.run)
 
@@ -15,6 +24,7 @@ import argparse
 import json
 import os
 import platform
+import statistics
 import sys
 import time
 
@@ -25,6 +35,7 @@ for p in (ROOT, os.path.join(ROOT, "spark-fsm_amd")):
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
 PMC_FILE = "profiles/pmc_latest.json"  # tools/pmc_summary.py output of the committed rocprofv3 --pmc passes
+ROOT_F2_KERNELS = ("k_f2_plan", "k_f2_keys", "k_f2_count")
 
 
 def pmc_traffic(kernel):
@@ -51,6 +62,28 @@ def cpu_model():
     return platform.processor()
 
 
+def cpu_share():
+    """CPUs this process may run on (the GPU box gives each GPU a share of the host)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(ds, support, seconds, threads, reps):
+    """Median of `reps` bounded samples of the CPU restatement (joins/s over the
+    lattice, F1 vertical build excluded, and over the whole run)."""
+    from oracle import oracle
+    runs = [oracle.spade_tokens(ds.seq_off, ds.tokens, support, time_limit_s=seconds, want_patterns=False,
+                                threads=threads) for _ in range(reps)]
+    lat = [r["joins"] / max(r["seconds"] - r["seconds_f1"], 1e-9) for r in runs]
+    whole = [r["joins"] / r["seconds"] for r in runs]
+    return {"value": statistics.median(lat), "unit": "joins/s", "cores": threads, "kind": "port",
+            "incl_f1_build_value": statistics.median(whole), "samples": [round(v, 1) for v in lat],
+            "seconds_f1": statistics.median(r["seconds_f1"] for r in runs),
+            "complete": all(r["complete"] for r in runs), "joins_per_sample": [r["joins"] for r in runs]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,10 +92,12 @@ def main():
     ap.add_argument("--sequences", type=int, default=1000000)
     ap.add_argument("--support", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of one CPU sample")
+    ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    # all-cores CPU mode (SURVEY §8d ii); 16 = the box's CPU share per GPU (0 = skip)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    # all-cores CPU mode (SURVEY §8d ii); 0 = every CPU of this process's share (0 skips: -1)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: CPU dry run)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,21 +110,32 @@ def main():
     from tools import gen
 
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(args.dist_backend)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
+    def sync_device():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
     ds = gen.quest(args.sequences, seed=args.seed)
-    if world > 1:
+    if world > 1 and args.dist_backend == "nccl":
         # sharded SPADE over RCCL: rank 0 makes the unique id, torch broadcasts it
         uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(fsm.comm_unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         eng = fsm.Engine(device=local_rank, nranks=world, rank=rank, unique_id=bytes(uid.cpu().tolist()))
+    elif world > 1:
+        # host collectives over the torch group (gloo): several ranks may share one GPU
+        from spark_fsm_amd.dist import TorchHostComm
+        hc = TorchHostComm(dist.group.WORLD)
+        eng = fsm.Engine(device=local_rank % max(torch.cuda.device_count(), 1), nranks=world, rank=rank,
+                         host_comm=hc)
     else:
         eng = fsm.Engine(device=local_rank)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
@@ -99,20 +145,23 @@ def main():
         eng.spade_csr(db, args.support)
 
     barrier()
-    torch.cuda.synchronize()
+    sync_device()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         csr, meta = eng.spade_csr(db, args.support)
-    torch.cuda.synchronize()
+    sync_device()
     barrier()
     t1 = time.perf_counter()
     st = eng.stats()  # stats of the last timed step
+    ks = eng.kernel_stats()
 
     ms_local = (t1 - t0) * 1000.0 / max(args.steps, 1)
     ms = ms_local
     joins_all = st["joins"]
     if world > 1:
-        t = torch.tensor([ms_local], dtype=torch.float64, device="cuda")
+        t = torch.tensor([ms_local], dtype=torch.float64)
+        if args.dist_backend == "nccl":
+            t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
 
@@ -124,12 +173,16 @@ def main():
         return
 
     value = joins_all / (ms / 1000.0)  # joins of all ranks (libfsm sums them) / slowest rank
-    # roofline of the dominant kernel: algorithmic bytes / its device time (HIP
-    # events on libfsm's stream, summed over the launches of the last step)
-    ks = eng.kernel_stats()
+    # roofline of the dominant kernel: its algorithmic bytes / its device
+    # time (HIP events on libfsm's stream, summed over the launches of the last step)
     dom = max(ks, key=lambda k: k["ms"])
     achieved = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
     traffic = pmc_traffic(dom["name"])
+    # SURVEY §8(d) unit for the F2: 8 B per (item, sid) first/last pair read per pass,
+    # over the device time of the root F2 kernels
+    f2_ms = sum(k["ms"] for k in ks if k["name"] in ROOT_F2_KERNELS)
+    f2_bytes = 8 * st["root_entries"]
+    joins_lattice = st["joins"] - st["joins_root"]
     line = {
         "metric": "id-list joins/sec + end-to-end SPADE mine time, Quest D1M minsup 0.1%",
         "value": value,
@@ -145,42 +198,47 @@ def main():
         "data": "synthetic (seeded Quest-shaped generator, tools/fsmgen.c)",
         "config": {"workload": "quest-C10-T2.5-S4-I1.25-D%d-N10000-seed%d, minsup %g" % (
             args.sequences, args.seed, args.support), "parallelism": "single GPU" if world == 1 else
-            "prefix classes sharded over %d GPUs" % world},
+            "prefix classes sharded over %d ranks (%s)" % (world, args.dist_backend)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": dom["name"], "launches_per_step": dom["launches"],
                      "kernel_ms_per_step": dom["ms"], "alg_bytes_per_step": dom["alg_bytes"],
+                     "bytes_basis": "the kernel's compulsory reads + writes per launch (DESIGN.md §4)",
                      "traffic_source": PMC_FILE if traffic is not None else None},
+        "roofline_survey_f2": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                               "bytes_basis": "SURVEY §8(d): 8 B per root (item, sid) entry per F2 pass",
+                               "alg_bytes": f2_bytes, "kernels_ms": f2_ms,
+                               "achieved": (f2_bytes / 1e9) / (f2_ms / 1000.0) if f2_ms else 0.0,
+                               "frac": ((f2_bytes / 1e9) / (f2_ms / 1000.0)) / HBM_PEAK_GBS if f2_ms else 0.0},
         "extra": {"mine_ms": ms, "joins": joins_all, "patterns": meta["n"], "minsup": meta["minsup"],
+                  "joins_root": st["joins_root"], "joins_lattice": joins_lattice,
+                  "root_pair_joins_executed": st["root_keys"], "lattice_pair_tests": st["pair_tests"],
+                  "executed_joins": st["root_keys"] + joins_lattice,
+                  "lattice_joins_per_s": joins_lattice / (st["ms_lattice"] / 1000.0) if st["ms_lattice"] else 0.0,
                   "classes": st["classes"], "batches": st["batches"], "entries": st["entries"],
+                  "root_entries": st["root_entries"],
                   "ms_f1": st["ms_f1"], "ms_f2_root": st["ms_f2"], "ms_lattice": st["ms_lattice"],
+                  "ms_gpu_wait": st["ms_gpu_wait"], "ms_output": st["ms_output"],
                   "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
+                  "e2e_joins_per_s": joins_all / ((ms + prep["ms_flatten"] + prep["ms_upload"]) / 1000.0),
                   "join_equiv_GBps": (st["bytes_join_equiv"] / 1e9) / (ms / 1000.0),
                   "kernels": sorted(({"name": k["name"], "launches": k["launches"], "ms": round(k["ms"], 4),
                                       "GBps": round((k["alg_bytes"] / 1e9) / (k["ms"] / 1000.0), 1) if k["ms"] else 0}
                                      for k in ks), key=lambda k: -k["ms"])},
     }
     if not args.no_cpu_baseline and world == 1:
-        from oracle import oracle
-        r = oracle.spade_tokens(ds.seq_off, ds.tokens, args.support, time_limit_s=args.cpu_seconds,
-                                want_patterns=False)
-        line["cpu_baseline"] = {
-            "value": r["joins"] / r["seconds"], "unit": "joins/s", "cores": 1, "kind": "port",
-            "lattice_value": r["joins"] / max(r["seconds"] - r["seconds_f1"], 1e-9), "seconds_f1": r["seconds_f1"],
-            "sample": "same DB and minsup; first %.0f s of the single-thread vertical SPADE DFS "
-                      "(oracle/fsm_oracle.c, F1 build included): %d joins%s; host %s" % (
-                          args.cpu_seconds, r["joins"], "" if not r["complete"] else " (complete)",
-                          cpu_model())}
-        if args.cpu_threads > 1:
-            r2 = oracle.spade_tokens(ds.seq_off, ds.tokens, args.support, time_limit_s=args.cpu_seconds,
-                                     want_patterns=False, threads=args.cpu_threads)
-            line["extra"]["cpu_baseline_all_cores"] = {
-                "value": r2["joins"] / r2["seconds"], "unit": "joins/s", "cores": args.cpu_threads,
-                "kind": "port", "complete": r2["complete"], "seconds": r2["seconds"], "joins": r2["joins"],
-                "lattice_value": r2["joins"] / max(r2["seconds"] - r2["seconds_f1"], 1e-9),
-                "seconds_f1": r2["seconds_f1"],
-                "sample": "same DB and minsup, same time bound; first-level classes on %d OpenMP threads "
-                          "(F1 build single-threaded)" % args.cpu_threads}
+        host = "%s; nproc %d, this process's CPU share %d" % (cpu_model(), os.cpu_count() or 0, cpu_share())
+        cb = cpu_baseline(ds, args.support, args.cpu_seconds, 1, args.cpu_reps)
+        cb["sample"] = ("same DB and minsup; median of %d samples of %.0f s of the single-thread CPU restatement "
+                        "(oracle/fsm_oracle.c); joins/s over its lattice (F1 vertical build excluded, as the GPU's "
+                        "flatten + upload are); host %s" % (args.cpu_reps, args.cpu_seconds, host))
+        line["cpu_baseline"] = cb
+        nt = cpu_share() if args.cpu_threads == 0 else args.cpu_threads
+        if nt > 1:
+            ca = cpu_baseline(ds, args.support, args.cpu_seconds, nt, args.cpu_reps)
+            ca["sample"] = ("same DB, minsup, bound and scope; first-level classes on %d OpenMP threads "
+                            "(all CPUs of this process's share; F1 build single-threaded)" % nt)
+            line["extra"]["cpu_baseline_all_cores"] = ca
     print(json.dumps(line), flush=True)
     db.free()
     eng.close()

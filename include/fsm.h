@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FSM_ABI_VERSION 3
+#define FSM_ABI_VERSION 4
 
 /* status codes */
 #define FSM_OK 0
@@ -128,6 +128,10 @@ typedef struct {
     int64_t bytes_count_alg;    /* count kernel algorithmic bytes: entries * (12 + 8W) */
     double ms_gpu_wait;         /* SPADE: host time blocked on the stream during F1/F2/lattice */
     double ms_output;           /* SPADE: host build of the pattern CSR */
+    int64_t joins_root;         /* SPADE: A.2 candidate joins of the root class, F^2 + F(F-1)/2 (part of joins) */
+    int64_t root_keys;          /* SPADE: non-empty (sequence, frequent-item pair) joins the root F2 counted */
+    int64_t pair_tests;         /* SPADE: (entry, partner) join tests executed by the class count kernels */
+    int64_t root_entries;       /* SPADE: (frequent item, sequence) entries of the root class (F2 input) */
 } fsm_stats;
 
 /* Per-kernel device time of the last fsm_*_mine call (HIP events on the

@@ -154,6 +154,35 @@ def spade_tokens(seq_off, tokens, support, time_limit_s=0.0, want_patterns=True,
     return res
 
 
+def spade_tokens_csr(seq_off, tokens, support, threads=1):
+    """Token-stream SPADE returning the pattern CSR as numpy arrays
+    (support, pat_off, set_off, items) plus meta: the form the full-size
+    digests (tests/digest.py) are computed from without building millions of
+    Python tuples."""
+    import numpy as np
+    L = lib()
+    so, so_p = _np64(seq_off)
+    tk, tk_p = _np64(tokens)
+    out = ctypes.POINTER(_Patterns)()
+    err = ctypes.create_string_buffer(512)
+    rc = L.oracle_spade_tokens_mt(so_p, tk_p, len(so) - 1, float(support), 0.0, int(threads),
+                                  ctypes.byref(out), err, 512)
+    if rc != 0:
+        raise OracleError(err.value.decode())
+    p = out.contents
+    try:
+        n = p.n
+        sup = np.ctypeslib.as_array(p.support, shape=(max(n, 1),))[:n].copy()
+        po = np.ctypeslib.as_array(p.pat_off, shape=(n + 1,)).copy()
+        st = np.ctypeslib.as_array(p.set_off, shape=(p.n_sets + 1,)).copy()
+        it = np.ctypeslib.as_array(p.items, shape=(max(p.n_items, 1),))[:p.n_items].copy()
+        meta = {"joins": p.joins, "minsup": p.minsup, "complete": bool(p.complete), "seconds": p.seconds,
+                "seconds_f1": p.seconds_f1, "n": n}
+    finally:
+        L.oracle_patterns_free(out)
+    return (sup, po, st, it), meta
+
+
 def pattern_support(seq_off, tokens, itemsets):
     """Definitional support of one pattern over a token stream."""
     L = lib()

@@ -1,5 +1,5 @@
 // device_util.h — small CDNA4 building blocks shared by the engines:
-// wave64 lane masks, a three-phase exclusive scan (u32/u64 -> u64 offsets),
+// wave64 lane masks, a single-pass decoupled look-back exclusive scan (u32/u64 -> u64 offsets),
 // and eid-mask helpers for W-word masks.
 #pragma once
 

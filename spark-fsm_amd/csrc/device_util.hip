@@ -121,12 +121,20 @@ template <class T> void scan_impl(const T* in, uint64_t* out, size_t n, hipStrea
         scr = sc.p;
     }
     FSM_HIP(hipMemsetAsync(scr, 0, need, s));
+    KernelClock* clk = thread_clock();
+    const size_t tk = clk ? clk->begin("k_scan") : 0;
     hipLaunchKernelGGL(k_scan<T>, dim3(unsigned(nt)), dim3(kScanT), 0, s, in, out, n, static_cast<uint32_t*>(scr),
                        static_cast<uint64_t*>(scr) + 1);
     FSM_LAUNCHED("k_scan", s);
+    if (clk) clk->end(tk, int64_t(n * (sizeof(T) + 8) + 8));
 }
 
 }  // namespace
+
+KernelClock*& thread_clock() {
+    thread_local KernelClock* c = nullptr;
+    return c;
+}
 
 void scan_exclusive(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint32_t>(in, out, n, s); }
 void scan_exclusive(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint64_t>(in, out, n, s); }

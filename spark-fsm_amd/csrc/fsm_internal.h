@@ -60,6 +60,17 @@ struct KernelClock {
     void release();
 };
 
+// The clock of the mine call running on this thread: library-internal kernels
+// launched from shared helpers (the scan) record into it when it is set.
+KernelClock*& thread_clock();
+struct ClockScope {
+    KernelClock* prev;
+    explicit ClockScope(KernelClock* c) : prev(thread_clock()) { thread_clock() = c; }
+    ~ClockScope() { thread_clock() = prev; }
+    ClockScope(const ClockScope&) = delete;
+    ClockScope& operator=(const ClockScope&) = delete;
+};
+
 // Device memory pool: hipMalloc/hipFree synchronize and cost milliseconds for
 // the multi-hundred-MB frontier slabs, so freed blocks are cached per size
 // class (power of two >= 4 KiB) and reused by later batches and later calls.

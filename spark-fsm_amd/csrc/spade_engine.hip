@@ -52,9 +52,8 @@ namespace {
 
 constexpr uint32_t kSeq = 0, kItm = 1;
 constexpr uint32_t kChunk = 512;         // class entries per k_count block (FSM_COUNT_CHUNK; swept on MI355X)
-constexpr uint32_t kRootChunk = 16384;     // root entries per block of the group histogram / scatter
 constexpr uint32_t kGroupCounters = 32768;  // root F2: u32 LDS counters of one rank group (128 KiB)
-constexpr uint32_t kMaxGroups = 16384;      // LDS histogram of k_group_hist (64 KiB)
+constexpr uint32_t kMaxGroups = 16384;      // root F2 rank groups: LDS cursors of k_f2_keys (64 KiB)
 constexpr int kBlock = 256;
 
 
@@ -164,11 +163,17 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
                                                   const uint32_t* __restrict__ mem, const uint32_t* __restrict__ lohi,
                                                   const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
                                                   uint32_t mlo, uint32_t mhi, uint32_t chunk,
-                                                  uint32_t* __restrict__ cnt) {
+                                                  uint32_t* __restrict__ cnt,
+                                                  unsigned long long* __restrict__ tests) {
+    __shared__ uint32_t blk_tests;
+    if (threadIdx.x == 0) blk_tests = 0;
+    __syncthreads();
+    uint32_t my_tests = 0;  // (entry, partner) join tests executed (fsm_stats.pair_tests)
     const uint32_t e1 = min(E, (blockIdx.x + 1) * chunk);
     for (uint32_t e = blockIdx.x * chunk + threadIdx.x; e < e1; e += blockDim.x) {
         const uint32_t mi = mem[e], p = pos[e];
         if (mi - mlo >= mhi - mlo) continue;  // member rows of another rank (sharded root)
+        my_tests += p & 0xFFFFu;
         const DClass c = cls[cid[e]];
         const uint32_t lo_i = lohi[e] & 0xFFFFu;
         const uint32_t ti = mi & 1u, ri = mi >> 1;
@@ -192,6 +197,9 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
             }
         }
     }
+    atomicAdd(&blk_tests, my_tests);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
 }
 
 __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bits [a, b), 0 <= a <= b <= 64
@@ -200,218 +208,219 @@ __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bit
     return hi & ~lo;
 }
 
-// Root pair enumeration shared by the two bucket passes: calls f(key) for every
-// frequent-item pair (i, j) of the row whose join is non-empty, key = rank_i * D + slot.
-template <int W, class F>
-__device__ __forceinline__ void root_pairs(uint32_t e, const uint32_t* __restrict__ mem,
-                                           const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
-                                           const uint64_t* __restrict__ mask, uint32_t D, F&& f) {
-    const uint32_t ri = mem[e] >> 1, p = pos[e];
-    const uint32_t lo_i = lohi[e] & 0xFFFFu;
-    const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
-    uint64_t mk[W];
-    load_mask<W>(mask + size_t(e) * W, mk);
-    const uint32_t base = ri * D;
-    for (uint32_t q = 0; q < rl; ++q) {
-        const uint32_t g = rb + q;
-        const uint32_t rj = mem[g] >> 1;
-        if ((lohi[g] >> 16) > lo_i) f(base + (rj << 1));                                   // x -> y
-        if (rj > ri && and_nonzero<W>(mk, mask + size_t(g) * W)) f(base + (rj << 1 | 1u));  // (x y)
-    }
-}
-
 // Root F2 (the F x 2F counter matrix, 220 MB at D1M: far beyond LDS, and
-// global atomics into it run at the memory side).  Every key of a root entry
-// lies in the counter row of its own rank, so the matrix is cut into rank
-// groups of `per` ranks whose per*D counters fit 128 KiB of LDS, and:
-//   k_root_ub       upper bound of the keys of each entry (temporal: row length;
-//                   equality: partners of higher rank); exclusive scan -> koff
-//   k_root_keys     THE one partner enumeration (horizontal, coalesced row reads):
-//                   entry e writes its keys, local to its group (u16), at
-//                   koff[e]: a wave's writes form one contiguous stretch
-//   k_group_hist    entries per (group, block); exclusive scan -> order
-//   k_group_scatter run descriptors (koff, nkeys) in group order, row order inside
-//   k_group_count   one block per group: stream its runs into LDS counters, write
-//                   the group's slice of the matrix once (coalesced)
-__global__ __launch_bounds__(kBlock) void k_root_ub(uint32_t E0, const uint32_t* __restrict__ mem,
-                                                    const uint32_t* __restrict__ pos, uint32_t mlo, uint32_t mhi,
-                                                    uint32_t* __restrict__ ub) {
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E0; e += gridDim.x * blockDim.x) {
-        const uint32_t p = pos[e], rl = p & 0xFFFFu, off = p >> 16;
-        ub[e] = (mem[e] - mlo < mhi - mlo) ? 2 * rl - 1 - off : 0u;
-    }
-}
+// global atomics into it run at the memory side, 1.3 TB/s of added bytes).
+// Every key of a root entry lies in the counter row of its own rank, so the
+// matrix is cut into rank groups of `per` ranks whose per*D counters fit
+// 128 KiB of LDS, and the pairs are partitioned by group on the way out:
+//   k_f2_plan   per (group, row block): key capacity = sum of the entries'
+//               upper bounds (temporal <= row length, equality <= partners of
+//               higher rank); exclusive scan -> region bases, group-major
+//   k_f2_keys   THE one partner enumeration: row block b writes the keys of
+//               group g (u16, local to the group's counter tile) into region
+//               (g, b) through an LDS cursor per group.  Rows of <= 64 entries
+//               (W = 1) go lane-per-pair in power-of-two lane segments: a step
+//               evaluates 64 / S entries i at once, S = row length rounded up
+//   k_f2_count  one block per group: stream the group's regions with 16-byte
+//               loads into LDS counters, then ballot out the frequent pairs
+//               (support >= minsup) - the matrix itself never reaches HBM
+// PMC basis (profiles/r2/baseline_sq): the row-per-step enumeration of round 1
+// was instruction-issue bound (1.48 G VALU+SALU instructions, 44 % of wave
+// cycles waiting to issue) and the per-run key walk latency bound (93 % waiting).
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
 
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_root_keys(uint32_t E0, const uint32_t* __restrict__ mem,
-                                                      const uint32_t* __restrict__ lohi,
-                                                      const uint32_t* __restrict__ pos,
-                                                      const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
-                                                      uint32_t mlo, uint32_t mhi, const uint64_t* __restrict__ koff,
-                                                      uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey,
-                                                      uint32_t min_rl, unsigned long long* __restrict__ nkeys_total) {
-    __shared__ uint32_t blk_keys;
-    if (threadIdx.x == 0) blk_keys = 0;
-    __syncthreads();
-    uint32_t my_keys = 0;
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E0; e += gridDim.x * blockDim.x) {
-        if ((pos[e] & 0xFFFFu) <= min_rl) continue;  // row handled by k_root_keys_row
-        const uint32_t mi = mem[e];
-        uint32_t n = 0;
-        if (mi - mlo < mhi - mlo) {
-            const uint32_t gbase = ((mi >> 1) / per) * per * D;
-            uint16_t* out = keys + koff[e];
-            root_pairs<W>(e, mem, lohi, pos, mask, D, [&](uint32_t key) { out[n++] = uint16_t(key - gbase); });
-        }
-        nkey[e] = uint16_t(n);
-        my_keys += n;
-    }
-    atomicAdd(&blk_keys, my_keys);
-    __syncthreads();
-    if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
-}
+// rank -> group by multiply-high (exact for rank < 2^16, per < 2^15)
+__device__ __forceinline__ uint32_t group_of(uint32_t rank, uint32_t pm) { return __umulhi(rank, pm); }
 
-// The same enumeration, one wave per root row of <= 64 entries (the
-// per-entry kernel above takes the longer rows): lane q holds entry rb + q in
-// registers for the whole row; the wave walks the row's entries i in order
-// (wave-uniform, operands of i broadcast by readlane into scalar registers)
-// and every lane tests its entry q as i's partner.  Entry i's keys of a step
-// are two ballots: temporal keys at popcount(tb below the lane), equality
-// keys after them, so each step writes one contiguous stretch of i's run.
-// No division or cross-lane search per pair: two ballots, two mbcnt and the
-// predicate per (i, row) step.
-__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) {
-    return uint32_t(__builtin_amdgcn_readlane(int(v), int(l)));
-}
-__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l) {
-    return uint64_t(rl32(uint32_t(v), l)) | (uint64_t(rl32(uint32_t(v >> 32), l)) << 32);
-}
-
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_root_keys_row(uint32_t R, const uint64_t* __restrict__ roff,
-                                                          const uint32_t* __restrict__ mem,
-                                                          const uint32_t* __restrict__ lohi,
-                                                          const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
-                                                          uint32_t mlo, uint32_t mhi,
-                                                          uint64_t* __restrict__ koff,
-                                                          uint16_t* __restrict__ keys, uint16_t* __restrict__ nkey,
-                                                          unsigned long long* __restrict__ nkeys_total) {
-    __shared__ uint32_t blk_keys;
-    if (threadIdx.x == 0) blk_keys = 0;
-    __syncthreads();
-    uint32_t my_keys = 0;  // keys this lane's entries wrote (exact algorithmic bytes for the stats)
-    const uint32_t lane = lane_id();
-    const uint64_t lt = lanemask_lt();
-    const uint32_t wstride = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < R; r += wstride) {
-        const uint32_t rb = uint32_t(roff[r]), rl = uint32_t(roff[r + 1]) - rb;
-        if (rl == 0 || rl > 64) continue;  // wave-uniform
-        const bool v = lane < rl;
-        uint32_t me = 0, mlh = 0, act = 0, kb_lo = 0, kb_hi = 0, kbase = 0;
-        uint64_t mm[W];
-#pragma unroll
-        for (int k = 0; k < W; ++k) mm[k] = 0;
-        if (v) {
-            me = mem[rb + lane];
-            mlh = lohi[rb + lane];
-            load_mask<W>(mask + size_t(rb + lane) * W, mm);
-            const uint64_t kb = koff[rb + lane];
-            kb_lo = uint32_t(kb);
-            kb_hi = uint32_t(kb >> 32);
-            act = (me - mlo < mhi - mlo) ? 1u : 0u;
-            const uint32_t ri = me >> 1;
-            kbase = ri * D - (ri / per) * per * D;  // entry's counter row, local to its rank group
-        }
-        const uint32_t rq = me >> 1, hq = mlh >> 16;
-        const uint64_t actb = __ballot(act != 0u);
-        // the row's keys are packed from the row's first run offset on (the
-        // upper-bound gaps collect at the row's end): every step's stretch
-        // continues the previous one, so the row writes whole lines
-        const uint64_t kb_row = uint64_t(rl32(kb_lo, 0)) | (uint64_t(rl32(kb_hi, 0)) << 32);
-        uint64_t run = 0, mystart = kb_row;
-        uint32_t mycnt = 0;
-        for (uint32_t i = 0; i < rl; ++i) {
-            if (!((actb >> i) & 1ull)) continue;  // entry i counted by another rank (uniform)
-            const uint32_t ri = rl32(me, i) >> 1;
-            const uint32_t li = rl32(mlh, i) & 0xFFFFu;
-            bool inter = false;
-#pragma unroll
-            for (int k = 0; k < W; ++k) inter |= (mm[k] & rl64(mm[k], i)) != 0ull;
-            const bool t_ok = v && hq > li;
-            const bool e_ok = v && rq > ri && inter;
-            const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
-            const uint64_t kbi = kb_row + run;
-            const uint32_t key = rl32(kbase, i) + (rq << 1);
-            const uint32_t nt = uint32_t(__popcll(tb)), n = nt + uint32_t(__popcll(eb));
-            if (t_ok) keys[kbi + uint32_t(__popcll(tb & lt))] = uint16_t(key);
-            if (e_ok) keys[kbi + nt + uint32_t(__popcll(eb & lt))] = uint16_t(key | 1u);
-            if (lane == i) {
-                mycnt = n;
-                mystart = kbi;
-            }
-            run += n;
-        }
-        if (v) {
-            nkey[rb + lane] = uint16_t(mycnt);
-            koff[rb + lane] = mystart;  // actual run start (k_group_scatter reads it)
-        }
-        my_keys += mycnt;
-    }
-    atomicAdd(&blk_keys, my_keys);
-    __syncthreads();
-    if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
-}
-
-__global__ __launch_bounds__(kBlock) void k_group_hist(uint32_t E0, const uint32_t* __restrict__ mem, uint32_t per,
-                                                       uint32_t G, uint32_t nblk, uint32_t chunk, uint32_t mlo,
-                                                       uint32_t mhi, uint32_t* __restrict__ ghist) {
+__global__ __launch_bounds__(kBlock) void k_f2_plan(const uint64_t* __restrict__ roff, uint32_t R, uint32_t rpb,
+                                                    const uint32_t* __restrict__ mem, const uint32_t* __restrict__ pos,
+                                                    uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo, uint32_t mhi,
+                                                    uint32_t* __restrict__ cap) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
     __syncthreads();
-    const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
-    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+    const uint32_t r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+    const uint64_t e0 = roff[r0], e1 = roff[r1];
+    for (uint64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
         const uint32_t mi = mem[e];
-        if (mi - mlo < mhi - mlo) atomicAdd(&h[(mi >> 1) / per], 1u);
+        if (mi - mlo < mhi - mlo) {
+            const uint32_t p = pos[e], rl = p & 0xFFFFu, off = p >> 16;
+            atomicAdd(&h[group_of(mi >> 1, pm)], 2 * rl - 1 - off);
+        }
     }
     __syncthreads();
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) ghist[uint64_t(g) * nblk + blockIdx.x] = h[g];
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[uint64_t(g) * nblk + blockIdx.x] = h[g];
 }
 
-__global__ __launch_bounds__(kBlock) void k_group_scatter(uint32_t E0, const uint32_t* __restrict__ mem, uint32_t per,
-                                                          uint32_t G, uint32_t nblk, uint32_t chunk, uint32_t mlo,
-                                                          uint32_t mhi, const uint64_t* __restrict__ goff,
-                                                          const uint64_t* __restrict__ koff,
-                                                          const uint16_t* __restrict__ nkey,
-                                                          uint2* __restrict__ runs) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(goff[uint64_t(g) * nblk + blockIdx.x]);
+constexpr uint32_t kF2Threads = 1024;  // k_f2_keys / k_f2_count block
+constexpr uint32_t kF2Waves = kF2Threads / 64;
+
+// row entry staged in LDS for the lane-per-pair path (W = 1)
+struct F2Ent {
+    uint32_t x;     // rank | lo << 16 | active << 31
+    uint32_t y;     // group | local counter row base << 16
+    uint64_t mask;  // eid mask
+};
+
+template <int W>
+__global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restrict__ roff, uint32_t R, uint32_t rpb,
+                                                        const uint32_t* __restrict__ mem,
+                                                        const uint32_t* __restrict__ lohi,
+                                                        const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
+                                                        uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
+                                                        uint32_t mhi, const uint64_t* __restrict__ base,
+                                                        uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
+                                                        unsigned long long* __restrict__ nkeys_total) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    F2Ent* stage_all = reinterpret_cast<F2Ent*>(smem);  // kF2Waves x 64 entries
+    uint32_t* cur = smem + kF2Waves * 64 * (sizeof(F2Ent) / 4);
+    __shared__ uint32_t blk_keys;
+    const uint32_t b = blockIdx.x;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[uint64_t(g) * nblk + b]);
+    if (threadIdx.x == 0) blk_keys = 0;
     __syncthreads();
-    const uint32_t e0 = blockIdx.x * chunk, e1 = min(E0, e0 + chunk);
-    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-        const uint32_t mi = mem[e];
-        if (mi - mlo < mhi - mlo)
-            runs[atomicAdd(&cur[(mi >> 1) / per], 1u)] = make_uint2(uint32_t(koff[e]), nkey[e]);
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    F2Ent* stage = stage_all + wave * 64;
+    const uint64_t lt = lanemask_lt();
+    uint32_t my_keys = 0;
+    const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
+    for (uint32_t r = r0 + wave; r < r1; r += kF2Waves) {
+        const uint32_t rb = rfl(uint32_t(roff[r])), rl = rfl(uint32_t(roff[r + 1]) - rb);
+        if (rl == 0) continue;
+        if (W == 1 && rl <= 64) {
+            // ---- lane-per-pair: segments of S lanes, lane s0 + j tests partner j
+            if (lane < rl) {
+                const uint32_t me = mem[rb + lane], lh = lohi[rb + lane];
+                const uint32_t ri = me >> 1, g = group_of(ri, pm);
+                const uint32_t act = (me - mlo < mhi - mlo) ? 1u : 0u;
+                F2Ent en;
+                en.x = ri | ((lh & 0xFFFFu) << 16) | (act << 31);
+                en.y = g | ((ri - g * per) * D << 16);
+                en.mask = mask[rb + lane];
+                stage[lane] = en;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t lg = rl <= 1 ? 0u : 32u - uint32_t(__clz(rl - 1));  // S = 2^lg >= rl
+            const uint32_t S = 1u << lg, k = 64u >> lg;
+            const uint32_t j = lane & (S - 1), s0 = lane & ~(S - 1);
+            const uint64_t segm = S == 64 ? ~0ull : (((1ull << S) - 1ull) << s0);
+            const uint64_t seg_lt = lt & segm;
+            const bool vj = j < rl;
+            // this lane's partner j (fixed for the row)
+            const F2Ent ej = stage[vj ? j : 0];
+            const uint32_t hi_j = lohi[rb + (vj ? j : 0)] >> 16;
+            const uint32_t rj = ej.x & 0xFFFFu;
+            for (uint32_t i0 = 0; i0 < rl; i0 += k) {
+                const uint32_t i = i0 + (lane >> lg);  // this segment's entry
+                const bool vi = i < rl;
+                const F2Ent ei = stage[vi ? i : 0];
+                const bool act_i = vi && (ei.x >> 31);
+                const uint32_t li = (ei.x >> 16) & 0x7FFFu;
+                // x -> y: bits of L(j) after the first bit of L(i); (x y), y > x: L(i) & L(j)
+                const bool t_ok = act_i && vj && hi_j > li;
+                const bool e_ok = act_i && vj && j > i && (ej.mask & ei.mask) != 0ull;
+                const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
+                const uint32_t nt = uint32_t(__popcll(tb & segm)), n = nt + uint32_t(__popcll(eb & segm));
+                uint32_t off = 0;
+                if (lane == s0 && n) off = atomicAdd(&cur[ei.y & 0xFFFFu], n);
+                off = uint32_t(__shfl(int(off), int(s0), 64));
+                const uint32_t key = (ei.y >> 16) + (rj << 1);
+                if (t_ok) keys[off + uint32_t(__popcll(tb & seg_lt))] = uint16_t(key);
+                if (e_ok) keys[off + nt + uint32_t(__popcll(eb & seg_lt))] = uint16_t(key | 1u);
+                if (lane == s0) my_keys += n;
+            }
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            // ---- generic: entry i wave-uniform, partners in chunks of 64 lanes (any W, any length)
+            for (uint32_t i = 0; i < rl; ++i) {
+                const uint32_t me = rfl(mem[rb + i]);
+                if (!(me - mlo < mhi - mlo)) continue;
+                const uint32_t ri = me >> 1, g = group_of(ri, pm);
+                const uint32_t li = rfl(lohi[rb + i]) & 0xFFFFu;
+                const uint32_t kb = (ri - g * per) * D;
+                uint64_t mi[W];
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint64_t v = mask[size_t(rb + i) * W + w];
+                    mi[w] = uint64_t(rfl(uint32_t(v))) | (uint64_t(rfl(uint32_t(v >> 32))) << 32);
+                }
+                for (uint32_t c0 = 0; c0 < rl; c0 += 64) {
+                    const uint32_t q = c0 + lane;
+                    const bool v = q < rl;
+                    bool t_ok = false, e_ok = false;
+                    uint32_t rq = 0;
+                    if (v) {
+                        rq = mem[rb + q] >> 1;
+                        t_ok = (lohi[rb + q] >> 16) > li;
+                        if (q > i) e_ok = and_nonzero<W>(mi, mask + size_t(rb + q) * W);
+                    }
+                    const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
+                    const uint32_t nt = uint32_t(__popcll(tb)), n = nt + uint32_t(__popcll(eb));
+                    if (n == 0) continue;
+                    uint32_t off = 0;
+                    if (lane == 0) off = atomicAdd(&cur[g], n);
+                    off = rfl(off);
+                    const uint32_t key = kb + (rq << 1);
+                    if (t_ok) keys[off + uint32_t(__popcll(tb & lt))] = uint16_t(key);
+                    if (e_ok) keys[off + nt + uint32_t(__popcll(eb & lt))] = uint16_t(key | 1u);
+                    if (lane == 0) my_keys += n;
+                }
+            }
+        }
     }
+    atomicAdd(&blk_keys, my_keys);
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+        fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[uint64_t(g) * nblk + b]);
+    if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
-__global__ __launch_bounds__(1024) void k_group_count(const uint64_t* __restrict__ goff, uint32_t nblk,
-                                                      const uint2* __restrict__ runs,
-                                                      const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
-                                                      uint32_t F, uint32_t* __restrict__ cnt) {
+// One block per rank group: stream its regions (16-byte loads, 8 keys per
+// lane) into LDS counters, then extract the frequent pairs of the group's
+// counter rows [max(g*per, rlo), min((g+1)*per, rhi)) with a wave ballot and
+// one atomic per wave.  Records come out unordered; the host sorts them.
+__global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base,
+                                                         const uint32_t* __restrict__ fill, uint32_t nblk,
+                                                         const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
+                                                         uint32_t g0, uint32_t rlo, uint32_t rhi, uint32_t minsup,
+                                                         FreqRec* __restrict__ recs, uint32_t cap,
+                                                         uint32_t* __restrict__ nrec) {
     __shared__ uint32_t h[kGroupCounters];
-    const uint32_t g = blockIdx.x;
-    const uint32_t l0 = uint32_t(goff[uint64_t(g) * nblk]), l1 = uint32_t(goff[uint64_t(g + 1) * nblk]);
-    if (l0 == l1) return;  // no entries of this group here (another rank's slice)
-    for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x) h[t] = 0;
+    const uint32_t g = g0 + blockIdx.x;
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    for (uint32_t t = threadIdx.x; t < per * D; t += blockDim.x) h[t] = 0;
     __syncthreads();
-    for (uint32_t i = l0 + threadIdx.x; i < l1; i += blockDim.x) {
-        const uint2 r = runs[i];
-        const uint16_t* k = keys + r.x;
-        for (uint32_t j = 0; j < r.y; ++j) atomicAdd(&h[k[j]], 1u);
+    for (uint32_t s = wave; s < nblk; s += kF2Waves) {
+        const uint64_t gi = uint64_t(g) * nblk + s;
+        const uint32_t n = rfl(fill[gi]);
+        if (n == 0) continue;
+        const uint32_t start = rfl(uint32_t(base[gi])), end = start + n;
+        for (uint32_t p = (start & ~7u) + lane * 8; p < end; p += 512) {
+            const uint4 v = *reinterpret_cast<const uint4*>(keys + p);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t idx = p + uint32_t(q);
+                if (idx >= start && idx < end) atomicAdd(&h[(w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu], 1u);
+            }
+        }
     }
     __syncthreads();
-    const uint32_t base = g * per * D, n = (min(F, (g + 1) * per) - g * per) * D;
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) cnt[base + t] = h[t];
+    const uint32_t ra = max(g * per, rlo), rz = min((g + 1) * per, rhi);
+    for (uint32_t row = ra; row < rz; ++row) {
+        const uint32_t* hr = h + (row - g * per) * D;
+        for (uint32_t c0 = wave * 64; c0 < D; c0 += kF2Threads) {
+            const uint32_t c = c0 + lane;
+            const uint32_t v = c < D ? hr[c] : 0u;
+            const bool fr = c < D && v >= minsup;
+            const uint64_t fb = __ballot(fr);
+            if (!fb) continue;
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(nrec, uint32_t(__popcll(fb)));
+            at = rfl(at) + uint32_t(__popcll(fb & lanemask_lt()));
+            if (fr && at < cap) recs[at] = FreqRec{row, c, v, 0u};
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ rows, uint32_t nrows,
@@ -676,6 +685,7 @@ struct Miner {
     uint64_t budget;
     std::vector<PNode> nodes;
     KernelClock* clk = nullptr;
+    DevBuf d_tests;  // u64: (entry, partner) join tests of the class count kernels
     // sharded mining (nranks > 1): this rank counts the root rows of ranks
     // [slice_lo, slice_hi) and mines the first-level classes shard_plan gives it
     Comm* comm = nullptr;
@@ -727,7 +737,9 @@ struct Miner {
             if ((mi & 1u) == kSeq) { ++S; sS += sup; } else { ++I; sI += sup; }
         }
         fsm_stats& st = ctx->stats;
-        st.joins += int64_t(S * S + I * S + (S ? S * (S - 1) / 2 : 0) + (I ? I * (I - 1) / 2 : 0));
+        const int64_t j = int64_t(S * S + I * S + (S ? S * (S - 1) / 2 : 0) + (I ? I * (I - 1) / 2 : 0));
+        st.joins += j;
+        if (b.root) st.joins_root += j;
         const uint64_t in = 2 * S * sS + S * sI + I * sS + (S ? (S - 1) * sS : 0) + (I ? (I - 1) * sI : 0);
         st.bytes_join_equiv += int64_t(12 * in);
         st.classes += 1;
@@ -769,115 +781,119 @@ struct Miner {
         const char* v = std::getenv("FSM_EMIT_GRID");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 22) : (1u << 16);
     }
-    // grid cap of k_root_keys_row (FSM_ROW_GRID overrides, for tuning)
-    static uint64_t row_grid_cap() {
-        const char* v = std::getenv("FSM_ROW_GRID");
-        return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 22) : (1u << 14);
-    }
     // class entries per block of k_count (FSM_COUNT_CHUNK overrides, for tuning)
     static uint32_t count_chunk() {
         const char* v = std::getenv("FSM_COUNT_CHUNK");
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kChunk;
     }
-    // root entries per block of the bucketed passes (FSM_ROOT_CHUNK overrides, for tuning)
-    static uint32_t root_chunk() {
-        const char* v = std::getenv("FSM_ROOT_CHUNK");
-        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kRootChunk;
+    // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
+    static uint32_t f2_blocks() {
+        const char* v = std::getenv("FSM_F2_BLOCKS");
+        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 16)) : 1024u;
     }
 
-    // Root counters by rank groups (see k_root_keys).  Returns false when a
-    // counter row does not fit the LDS group tile or the groups are too many.
-    bool root_group_count(Batch& b, uint32_t* cnt) {
+    // Root F2 by rank groups (k_f2_plan / k_f2_keys / k_f2_count): the
+    // frequent (rank, slot) pairs of this rank's slice, sorted by (row, slot),
+    // with their child member ids.  Returns false when a counter row does not
+    // fit the LDS group tile, the groups are too many or the key slots exceed
+    // 2^32 (the caller then takes the global-atomic path).
+    bool root_f2(Batch& b, std::vector<FreqRec>& recs) {
         const ClassMeta& m = b.cls[0];
         const uint32_t D = m.D, F = m.D / 2;
-        const uint64_t K = uint64_t(F) * D;
-        if (m.nent == 0 || D > kGroupCounters || K >= (uint64_t(1) << 32)) return false;
+        if (m.nent == 0 || D > kGroupCounters || b.root_rows.p == nullptr || b.R == 0 || F >= (1u << 15)) return false;
         const uint32_t per = kGroupCounters / D;
         const uint32_t G = (F + per - 1) / per;
         if (G > kMaxGroups) return false;
-        const uint32_t E0 = m.nent;
+        const uint32_t pm = uint32_t(((uint64_t(1) << 32) + per - 1) / per);  // group_of multiplier
         const uint32_t mlo = member_lo(b), mhi = member_hi(b);
+        const uint32_t rlo = comm ? slice_lo : 0u, rhi = comm ? std::min(slice_hi, F) : F;
+        const uint32_t R = uint32_t(b.R);
+        const uint32_t rpb = std::max<uint32_t>(16u, (R + f2_blocks() - 1) / f2_blocks());
+        const uint32_t nblk = (R + rpb - 1) / rpb;
+        const uint64_t nd = uint64_t(G) * nblk;
         const SlabPtrs sp = b.slab.ptrs();
-        const int64_t slab_bytes = int64_t(E0) * int64_t(16 + 8 * W);
-        const unsigned grid = unsigned(std::min<uint64_t>((E0 + kBlock - 1) / kBlock, 1u << 16));
-        // key-run upper bounds -> offsets
-        DevBuf ub(uint64_t(E0) * 4), koff((uint64_t(E0) + 1) * 8);
-        size_t tk = clk->begin("k_root_ub");
-        hipLaunchKernelGGL(k_root_ub, dim3(grid), dim3(kBlock), 0, s, E0, sp.mem, sp.pos, mlo, mhi, ub.as<uint32_t>());
-        FSM_LAUNCHED("k_root_ub", s);
-        clk->end(tk, int64_t(E0) * 12);
-        scan_exclusive(ub.as<uint32_t>(), koff.as<uint64_t>(), E0, s);
-        ub.release();
+        const int64_t E0 = int64_t(m.nent);
+        // plan: region capacities -> bases
+        DevBuf cap(nd * 4), base((nd + 1) * 8), fill(nd * 4);
+        size_t tk = clk->begin("k_f2_plan");
+        hipLaunchKernelGGL(k_f2_plan, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, b.root_rows.as<uint64_t>(), R, rpb,
+                           sp.mem, sp.pos, pm, G, nblk, mlo, mhi, cap.as<uint32_t>());
+        FSM_LAUNCHED("k_f2_plan", s);
+        clk->end(tk, E0 * 8 + int64_t(nd) * 4);
+        scan_exclusive(cap.as<uint32_t>(), base.as<uint64_t>(), nd, s);
         uint64_t nslots = 0;
-        FSM_HIP(hipMemcpyAsync(&nslots, koff.as<uint64_t>() + E0, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(&nslots, base.as<uint64_t>() + nd, 8, hipMemcpyDeviceToHost, s));
         sync();
-        if (nslots >= (uint64_t(1) << 32)) return false;  // run offsets are kept in u32
-        // the one enumeration
-        DevBuf keys(std::max<uint64_t>(nslots, 1) * 2), nkey(uint64_t(E0) * 2);
-        // rows of <= 64 entries: one wave per row; longer rows (and a root
-        // without row offsets): the per-entry kernel
-        const bool rows = b.root_rows.p != nullptr && b.R > 0;
-        const uint32_t min_rl = rows ? 64u : 0u;
-        DevBuf nkeys_row(16);  // [0] row kernel, [1] per-entry kernel
-        size_t tk_row = size_t(-1);
-        FSM_HIP(hipMemsetAsync(nkeys_row.p, 0, 16, s));
-        if (rows) {
-            tk = clk->begin("k_root_keys_row");
-            const unsigned rgrid = unsigned(std::min<uint64_t>((b.R * 64 + kBlock - 1) / kBlock, row_grid_cap()));
-#define FSM_RKR(WW)                                                                                                 \
-    hipLaunchKernelGGL(k_root_keys_row<WW>, dim3(rgrid), dim3(kBlock), 0, s, uint32_t(b.R),                       \
-                       b.root_rows.as<uint64_t>(), sp.mem, sp.lohi, sp.mask, D, per, mlo, mhi, koff.as<uint64_t>(), \
-                       keys.as<uint16_t>(), nkey.as<uint16_t>(), nkeys_row.as<unsigned long long>())
-            FSM_W_DISPATCH(W, FSM_RKR)
-#undef FSM_RKR
-            FSM_LAUNCHED("k_root_keys_row", s);
-            // reads the slab + koff, writes nkey; the key bytes (2 B per key actually
-            // written) are added once the count is back on the host
-            clk->end(tk, slab_bytes + int64_t(E0) * 10);
-            tk_row = tk;
+        cap.release();
+        if (nslots >= (uint64_t(1) << 32) - 4096) return false;  // region cursors are u32
+        // the one enumeration (keys padded: k_f2_count reads whole 16-byte words past a region's end)
+        DevBuf keys((nslots + 1024) * 2), nk(8);
+        FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
+        tk = clk->begin("k_f2_keys");
+        const size_t kshm = size_t(kF2Waves) * 64 * sizeof(F2Ent) + size_t(G) * 4;
+#define FSM_F2K(WW)                                                                                                   \
+    hipLaunchKernelGGL(k_f2_keys<WW>, dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(), R, rpb,      \
+                       sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(),                   \
+                       fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>())
+        FSM_W_DISPATCH(W, FSM_F2K)
+#undef FSM_F2K
+        FSM_LAUNCHED("k_f2_keys", s);
+        // reads the slab (mem, lohi, mask) and the region bases, writes the fills;
+        // + 2 B per key actually written, added once the count is back
+        clk->end(tk, E0 * int64_t(8 + 8 * W) + int64_t(nd) * 12);
+        const size_t tk_keys = tk;
+        // count + frequent pairs of this rank's slice
+        const uint32_t g0 = rlo / per, g1 = rhi == 0 ? 0u : (rhi - 1) / per + 1;
+        uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * D, uint64_t(1) << 20));
+        DevBuf d_nrec(4);
+        DevBuf d_recs;
+        unsigned long long nkeys = 0;
+        size_t tk_cnt = 0;
+        for (int attempt = 0;; ++attempt) {
+            d_recs.alloc(std::max<uint32_t>(cap_recs, 1) * sizeof(FreqRec));
+            FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
+            tk_cnt = clk->begin("k_f2_count");
+            if (g1 > g0)
+                hipLaunchKernelGGL(k_f2_count, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
+                                   fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), D, per, g0, rlo, rhi, minsup,
+                                   d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>());
+            FSM_LAUNCHED("k_f2_count", s);
+            clk->end(tk_cnt, int64_t(g1 - g0) * nblk * 12);
+            uint32_t nrec = 0;
+            FSM_HIP(hipMemcpyAsync(&nrec, d_nrec.p, 4, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&nkeys, nk.p, 8, hipMemcpyDeviceToHost, s));
+            sync();
+            if (nrec <= cap_recs || attempt > 0) {
+                if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
+                recs.resize(nrec);
+                if (nrec)
+                    FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, size_t(nrec) * sizeof(FreqRec), hipMemcpyDeviceToHost,
+                                           s));
+                sync();
+                break;
+            }
+            cap_recs = nrec;  // rare: more frequent pairs than the first buffer held; count again
         }
-        tk = clk->begin("k_root_keys");
-#define FSM_RK(WW)                                                                                             \
-    hipLaunchKernelGGL(k_root_keys<WW>, dim3(grid), dim3(kBlock), 0, s, E0, sp.mem, sp.lohi, sp.pos, sp.mask, \
-                       D, per, mlo, mhi, koff.as<uint64_t>(), keys.as<uint16_t>(), nkey.as<uint16_t>(), min_rl,  \
-                       nkeys_row.as<unsigned long long>() + 1)
-        FSM_W_DISPATCH(W, FSM_RK)
-#undef FSM_RK
-        FSM_LAUNCHED("k_root_keys", s);
-        clk->end(tk, rows ? int64_t(E0) * 4 : slab_bytes + int64_t(E0) * 10);  // + its keys, added below
-        const size_t tk_ent = tk;
-        // runs in group order
-        const uint32_t chunk = root_chunk();
-        const uint32_t nblk = (E0 + chunk - 1) / chunk;
-        const uint64_t nh = uint64_t(G) * nblk;
-        DevBuf ghist(nh * 4), goff((nh + 1) * 8), runs(uint64_t(E0) * 8);
-        tk = clk->begin("k_group_hist");
-        hipLaunchKernelGGL(k_group_hist, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, E0, sp.mem, per, G, nblk, chunk,
-                           mlo, mhi, ghist.as<uint32_t>());
-        FSM_LAUNCHED("k_group_hist", s);
-        clk->end(tk, int64_t(E0) * 4 + int64_t(nh) * 4);
-        scan_exclusive(ghist.as<uint32_t>(), goff.as<uint64_t>(), nh, s);
-        tk = clk->begin("k_group_scatter");
-        hipLaunchKernelGGL(k_group_scatter, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, E0, sp.mem, per, G, nblk,
-                           chunk, mlo, mhi, goff.as<uint64_t>(), koff.as<uint64_t>(), nkey.as<uint16_t>(),
-                           runs.as<uint2>());
-        FSM_LAUNCHED("k_group_scatter", s);
-        clk->end(tk, int64_t(E0) * (4 + 8 + 2 + 8));
-        // one block per group
-        tk = clk->begin("k_group_count");
-        hipLaunchKernelGGL(k_group_count, dim3(G), dim3(1024), 0, s, goff.as<uint64_t>(), nblk, runs.as<uint2>(),
-                           keys.as<uint16_t>(), D, per, F, cnt);
-        FSM_LAUNCHED("k_group_count", s);
-        clk->end(tk, int64_t(E0) * 8 + int64_t(K) * 4);
-        unsigned long long nk[2] = {0, 0};  // keys written by the row kernel / the per-entry kernel
-        FSM_HIP(hipMemcpyAsync(nk, nkeys_row.p, 16, hipMemcpyDeviceToHost, s));
-        sync();  // temporaries released on return
-        if (tk_row != size_t(-1)) clk->add_bytes(tk_row, int64_t(nk[0]) * 2);
-        clk->add_bytes(tk_ent, int64_t(nk[1]) * 2);
-        clk->add_bytes(tk, int64_t(nk[0] + nk[1]) * 2);  // k_group_count reads every key once
+        clk->add_bytes(tk_keys, int64_t(nkeys) * 2);
+        clk->add_bytes(tk_cnt, int64_t(nkeys) * 2 + int64_t(recs.size() * sizeof(FreqRec)));
+        ctx->stats.root_keys += int64_t(nkeys);
+        // (row, slot) order and child member ids: rank among the row's slots with a frequent
+        // temporal or equality candidate, << 1 | type (as k_freq_write assigns them)
+        std::sort(recs.begin(), recs.end(), [](const FreqRec& x, const FreqRec& y) {
+            return x.row != y.row ? x.row < y.row : x.slot < y.slot;
+        });
+        for (size_t q = 0; q < recs.size();) {
+            size_t q2 = q;
+            uint32_t crank = 0;
+            while (q2 < recs.size() && recs[q2].row == recs[q].row) {
+                if (q2 > q && (recs[q2].slot >> 1) != (recs[q2 - 1].slot >> 1)) ++crank;
+                recs[q2].cid = crank << 1 | (recs[q2].slot & 1u);
+                ++q2;
+            }
+            q = q2;
+        }
         return true;
     }
-
     // count kernel + frequent-candidate extraction; fills b.children / b.groups / kids
     void count_and_freq(Batch& b) {
         dump(b);
@@ -891,25 +907,6 @@ struct Miner {
         st.entries += int64_t(tot_ent);
         st.bytes_streamed += int64_t(tot_ent * entry_bytes());
         st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
-        DevBuf cnt(std::max<uint64_t>(b.n_cnt, 1) * 4);
-        if (b.E) {
-            const bool done = b.root && !root_atomic() && root_group_count(b, cnt.as<uint32_t>());
-            if (!done) {
-                FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
-                const SlabPtrs sp = b.slab.ptrs();
-                const uint32_t cchunk = count_chunk();
-#define FSM_COUNT(WW)                                                                                   \
-    hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + cchunk - 1) / cchunk)), dim3(kBlock), 0, s,   \
-                       uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
-                       member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>())
-                const size_t tk = clk->begin("k_count");
-                FSM_W_DISPATCH(W, FSM_COUNT)
-#undef FSM_COUNT
-                FSM_LAUNCHED("k_count", s);
-                clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));
-            }
-            st.count_launches += 1;
-        }
         // member rows of the counter matrix
         std::vector<DRow> rows;
         for (size_t c = 0; c < b.cls.size(); ++c)
@@ -919,33 +916,56 @@ struct Miner {
         const uint32_t rlo = shard ? std::min<uint32_t>(slice_lo, uint32_t(rows.size())) : 0u;
         const uint32_t rhi = shard ? std::min<uint32_t>(slice_hi, uint32_t(rows.size())) : uint32_t(rows.size());
         const uint32_t nrows = rhi - rlo;
-        DevBuf d_rows, rowcnt((size_t(nrows) + 1) * 4), rowoff((size_t(nrows) + 1) * 8);
-        upload(d_rows, std::vector<DRow>(rows.begin() + rlo, rows.begin() + rhi));
-        const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
-        if (nrows) {
-            const size_t tk = clk->begin("k_freq_count");
-            hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
-                               b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
-            FSM_LAUNCHED("k_freq_count", s);
-            clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4));
-        }
-        scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
-        uint64_t nfreq = 0;
-        FSM_HIP(hipMemcpyAsync(&nfreq, rowoff.as<uint64_t>() + nrows, 8, hipMemcpyDeviceToHost, s));
-        sync();
-        std::vector<FreqRec> recs(nfreq);
-        if (nfreq) {
-            DevBuf d_recs(nfreq * sizeof(FreqRec));
-            const size_t tk = clk->begin("k_freq_write");
-            hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
-                               b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
-                               d_recs.as<FreqRec>());
-            FSM_LAUNCHED("k_freq_write", s);
-            clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
-                                 nfreq * sizeof(FreqRec)));
-            FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nfreq * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
+        std::vector<FreqRec> recs;
+        // the root: pairs counted per rank group, only the frequent ones leave the device
+        const bool root_done = b.E && b.root && !root_atomic() && root_f2(b, recs);
+        if (b.E) st.count_launches += 1;
+        DevBuf cnt;
+        if (!root_done) {
+            cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
+            FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
+            if (b.E) {
+                const SlabPtrs sp = b.slab.ptrs();
+                const uint32_t cchunk = count_chunk();
+#define FSM_COUNT(WW)                                                                                   \
+    hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + cchunk - 1) / cchunk)), dim3(kBlock), 0, s,   \
+                       uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
+                       member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>(), d_tests.as<unsigned long long>())
+                const size_t tk = clk->begin("k_count");
+                FSM_W_DISPATCH(W, FSM_COUNT)
+#undef FSM_COUNT
+                FSM_LAUNCHED("k_count", s);
+                clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));
+            }
+            DevBuf d_rows, rowcnt((size_t(nrows) + 1) * 4), rowoff((size_t(nrows) + 1) * 8);
+            upload(d_rows, std::vector<DRow>(rows.begin() + rlo, rows.begin() + rhi));
+            const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
+            if (nrows) {
+                const size_t tk = clk->begin("k_freq_count");
+                hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
+                                   b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
+                FSM_LAUNCHED("k_freq_count", s);
+                clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4));
+            }
+            scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
+            uint64_t nf = 0;
+            FSM_HIP(hipMemcpyAsync(&nf, rowoff.as<uint64_t>() + nrows, 8, hipMemcpyDeviceToHost, s));
             sync();
+            recs.resize(nf);
+            if (nf) {
+                DevBuf d_recs(nf * sizeof(FreqRec));
+                const size_t tk = clk->begin("k_freq_write");
+                hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
+                                   b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
+                                   d_recs.as<FreqRec>());
+                FSM_LAUNCHED("k_freq_write", s);
+                clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
+                                     nf * sizeof(FreqRec)));
+                FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nf * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
+                sync();
+            }
         }
+        uint64_t nfreq = recs.size();
         cnt.release();
         if (shard) {  // every rank gets every frequent pair, in row order (slices ascend with the rank)
             std::vector<uint8_t> mine(recs.size() * sizeof(FreqRec));
@@ -1131,6 +1151,7 @@ struct Miner {
         if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
         root.slab.alloc(E0, W);
         root.E = E0;
+        ctx->stats.root_entries = int64_t(E0);
         FSM_HIP(hipMemsetAsync(root.slab.cid.p, 0, E0 * 4, s));
         if (r1 > r0) {
             const SlabPtrs op = root.slab.ptrs();
@@ -1233,7 +1254,8 @@ void gather_patterns(Comm* comm, hipStream_t s, std::vector<int32_t>& sup, std::
 // sum the work counters of all ranks (joins etc. are counted where the work ran)
 void gather_stats(Comm* comm, hipStream_t s, fsm_stats& st) {
     int64_t* f[] = {&st.joins, &st.classes, &st.batches, &st.entries, &st.bytes_join_equiv,
-                    &st.bytes_streamed, &st.bytes_count_alg, &st.count_launches};
+                    &st.bytes_streamed, &st.bytes_count_alg, &st.count_launches, &st.joins_root,
+                    &st.root_keys, &st.pair_tests};
     constexpr size_t K = sizeof(f) / sizeof(f[0]);
     std::vector<uint8_t> mine(K * 8);
     for (size_t k = 0; k < K; ++k) std::memcpy(mine.data() + 8 * k, f[k], 8);
@@ -1285,6 +1307,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     const int64_t total = db->spade.total;
     Miner mn{ctx, d, ctx->stream, d->W, 1, 0, {}};
     KernelClock clock(ctx->stream);
+    ClockScope clock_scope(&clock);
     mn.clk = &clock;
     mn.comm = ctx->comm;
     Comm* comm = ctx->comm;
@@ -1296,6 +1319,8 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     size_t free_b = 0, total_b = 0;
     FSM_HIP(hipMemGetInfo(&free_b, &total_b));
     mn.budget = ctx->opts.mem_budget > 0 ? uint64_t(ctx->opts.mem_budget) : uint64_t(free_b / 2);
+    mn.d_tests.alloc(8);
+    FSM_HIP(hipMemsetAsync(mn.d_tests.p, 0, 8, ctx->stream));
 
     // ---- F1 (K1)
     std::vector<uint32_t> f1(size_t(d->U), 0);
@@ -1371,7 +1396,12 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         mn.count_and_freq(*nb);
         stack.push_back(std::move(nb));
     }
-    FSM_HIP(hipStreamSynchronize(ctx->stream));
+    {
+        unsigned long long tests = 0;
+        FSM_HIP(hipMemcpyAsync(&tests, mn.d_tests.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        FSM_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->stats.pair_tests = int64_t(tests);
+    }
     ctx->stats.ms_lattice = now_ms() - t2;
     clock.finish(ctx->kstats);
     for (const fsm_kernel_stat& k : ctx->kstats) {
