@@ -249,7 +249,8 @@ __global__ __launch_bounds__(kBlock) void k_f2_plan(const uint64_t* __restrict__
         }
     }
     __syncthreads();
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[uint64_t(g) * nblk + blockIdx.x] = h[g];
+    // regions start on 16-byte boundaries (8 keys): k_f2_count reads them in aligned chunks
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[uint64_t(g) * nblk + blockIdx.x] = (h[g] + 7u) & ~7u;
 }
 
 constexpr uint32_t kF2Threads = 1024;  // k_f2_keys / k_f2_count block
@@ -257,10 +258,11 @@ constexpr uint32_t kF2Waves = kF2Threads / 64;
 
 // row entry staged in LDS for the lane-per-pair path (W = 1)
 struct F2Ent {
-    uint32_t x;     // rank | lo << 16 | active << 31
-    uint32_t y;     // group | local counter row base << 16
+    uint32_t x;     // rank | lo << 16
+    uint32_t y;     // group (0xFFFF: entry counted by another rank) | local counter row base << 16
     uint64_t mask;  // eid mask
 };
+constexpr uint32_t kF2MaxRows = 4096;  // rows per block of k_f2_keys (row offsets staged in LDS)
 
 template <int W>
 __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restrict__ roff, uint32_t R, uint32_t rpb,
@@ -273,30 +275,47 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                                                         unsigned long long* __restrict__ nkeys_total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     F2Ent* stage_all = reinterpret_cast<F2Ent*>(smem);  // kF2Waves x 64 entries
-    uint32_t* cur = smem + kF2Waves * 64 * (sizeof(F2Ent) / 4);
+    uint32_t* srow = smem + kF2Waves * 64 * (sizeof(F2Ent) / 4);  // row offsets of the block [rpb + 1]
+    uint32_t* cur = srow + kF2MaxRows + 1;                          // region cursors [G]
     __shared__ uint32_t blk_keys;
     const uint32_t b = blockIdx.x;
+    const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[uint64_t(g) * nblk + b]);
+    for (uint32_t r = r0 + threadIdx.x; r <= r1; r += blockDim.x) srow[r - r0] = uint32_t(roff[r]);
     if (threadIdx.x == 0) blk_keys = 0;
     __syncthreads();
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     F2Ent* stage = stage_all + wave * 64;
     const uint64_t lt = lanemask_lt();
     uint32_t my_keys = 0;
-    const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
+    // the next row's entries are loaded while the current row is enumerated
+    uint32_t nrb = 0, nrl = 0, nme = 0, nlh = 0;
+    uint64_t nmk = 0;
+    auto fetch = [&](uint32_t rr) {
+        if (rr >= r1) return;
+        nrb = srow[rr - r0];
+        nrl = srow[rr - r0 + 1] - nrb;
+        if (W == 1 && nrl <= 64 && lane < nrl) {
+            nme = mem[nrb + lane];
+            nlh = lohi[nrb + lane];
+            nmk = mask[nrb + lane];
+        }
+    };
+    fetch(r0 + wave);
     for (uint32_t r = r0 + wave; r < r1; r += kF2Waves) {
-        const uint32_t rb = rfl(uint32_t(roff[r])), rl = rfl(uint32_t(roff[r + 1]) - rb);
+        const uint32_t rb = rfl(nrb), rl = rfl(nrl), me = nme, lh = nlh;
+        const uint64_t mk = nmk;
+        fetch(r + kF2Waves);
         if (rl == 0) continue;
         if (W == 1 && rl <= 64) {
             // ---- lane-per-pair: segments of S lanes, lane s0 + j tests partner j
             if (lane < rl) {
-                const uint32_t me = mem[rb + lane], lh = lohi[rb + lane];
                 const uint32_t ri = me >> 1, g = group_of(ri, pm);
-                const uint32_t act = (me - mlo < mhi - mlo) ? 1u : 0u;
+                const bool act = me - mlo < mhi - mlo;
                 F2Ent en;
-                en.x = ri | ((lh & 0xFFFFu) << 16) | (act << 31);
-                en.y = g | ((ri - g * per) * D << 16);
-                en.mask = mask[rb + lane];
+                en.x = ri | ((lh & 0xFFFFu) << 16);
+                en.y = (act ? g : 0xFFFFu) | ((ri - g * per) * D << 16);
+                en.mask = mk;
                 stage[lane] = en;
             }
             __builtin_amdgcn_wave_barrier();
@@ -308,21 +327,22 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
             const bool vj = j < rl;
             // this lane's partner j (fixed for the row)
             const F2Ent ej = stage[vj ? j : 0];
-            const uint32_t hi_j = lohi[rb + (vj ? j : 0)] >> 16;
+            const uint32_t hi_j = uint32_t(__shfl(int(lh), int(j), 64)) >> 16;
             const uint32_t rj = ej.x & 0xFFFFu;
             for (uint32_t i0 = 0; i0 < rl; i0 += k) {
                 const uint32_t i = i0 + (lane >> lg);  // this segment's entry
                 const bool vi = i < rl;
                 const F2Ent ei = stage[vi ? i : 0];
-                const bool act_i = vi && (ei.x >> 31);
-                const uint32_t li = (ei.x >> 16) & 0x7FFFu;
+                const uint32_t gi = ei.y & 0xFFFFu;
+                const bool act_i = vi && gi != 0xFFFFu;
+                const uint32_t li = ei.x >> 16;
                 // x -> y: bits of L(j) after the first bit of L(i); (x y), y > x: L(i) & L(j)
                 const bool t_ok = act_i && vj && hi_j > li;
                 const bool e_ok = act_i && vj && j > i && (ej.mask & ei.mask) != 0ull;
                 const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
                 const uint32_t nt = uint32_t(__popcll(tb & segm)), n = nt + uint32_t(__popcll(eb & segm));
                 uint32_t off = 0;
-                if (lane == s0 && n) off = atomicAdd(&cur[ei.y & 0xFFFFu], n);
+                if (lane == s0 && n) off = atomicAdd(&cur[gi], n);
                 off = uint32_t(__shfl(int(off), int(s0), 64));
                 const uint32_t key = (ei.y >> 16) + (rj << 1);
                 if (t_ok) keys[off + uint32_t(__popcll(tb & seg_lt))] = uint16_t(key);
@@ -375,10 +395,16 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
-// One block per rank group: stream its regions (16-byte loads, 8 keys per
-// lane) into LDS counters, then extract the frequent pairs of the group's
-// counter rows [max(g*per, rlo), min((g+1)*per, rhi)) with a wave ballot and
-// one atomic per wave.  Records come out unordered; the host sorts them.
+// One block per rank group.  The group's regions (one per row block, each
+// starting on a 16-byte boundary, holes after their fills) are read as one
+// logical stream of 8-key chunks: the block loads the regions' fills and
+// bases into LDS and prefix-sums their chunk counts; every thread then takes
+// 4 chunks per round (4 independent 16-byte loads in flight), finds each
+// chunk's region by binary search in LDS and adds its keys into the LDS
+// counters.  Then the frequent pairs of the group's counter rows
+// [max(g*per, rlo), min((g+1)*per, rhi)) are balloted out with one atomic per
+// wave; records come out unordered and the host sorts them.
+constexpr uint32_t kF2MaxBlocks = 2048;  // row blocks (regions per group) k_f2_count can index in LDS
 __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base,
                                                          const uint32_t* __restrict__ fill, uint32_t nblk,
                                                          const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
@@ -386,39 +412,82 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
                                                          FreqRec* __restrict__ recs, uint32_t cap,
                                                          uint32_t* __restrict__ nrec) {
     __shared__ uint32_t h[kGroupCounters];
+    __shared__ uint32_t cpre[kF2MaxBlocks + 1];  // first logical chunk of each region
+    __shared__ uint32_t cst[kF2MaxBlocks];       // first physical chunk of each region
+    __shared__ uint32_t sfill[kF2MaxBlocks];     // keys in each region
+    __shared__ uint32_t wsum[kF2Waves];
     const uint32_t g = g0 + blockIdx.x;
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     for (uint32_t t = threadIdx.x; t < per * D; t += blockDim.x) h[t] = 0;
+    // region chunk counts -> exclusive prefix (nblk <= 2 * blockDim.x: two per thread)
+    const uint64_t gi = uint64_t(g) * nblk;
+    const uint32_t s0 = 2 * threadIdx.x;
+    const uint32_t f0 = s0 < nblk ? fill[gi + s0] : 0u, f1 = s0 + 1 < nblk ? fill[gi + s0 + 1] : 0u;
+    if (s0 < nblk) {
+        cst[s0] = uint32_t(base[gi + s0]) >> 3;
+        sfill[s0] = f0;
+    }
+    if (s0 + 1 < nblk) {
+        cst[s0 + 1] = uint32_t(base[gi + s0 + 1]) >> 3;
+        sfill[s0 + 1] = f1;
+    }
+    const uint32_t c0 = (f0 + 7) >> 3, c1 = (f1 + 7) >> 3;
+    const uint32_t pair = c0 + c1, incl = wave_incl_scan(pair);
+    if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    for (uint32_t s = wave; s < nblk; s += kF2Waves) {
-        const uint64_t gi = uint64_t(g) * nblk + s;
-        const uint32_t n = rfl(fill[gi]);
-        if (n == 0) continue;
-        const uint32_t start = rfl(uint32_t(base[gi])), end = start + n;
-        for (uint32_t p = (start & ~7u) + lane * 8; p < end; p += 512) {
-            const uint4 v = *reinterpret_cast<const uint4*>(keys + p);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t woff = 0, total = 0;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t idx = p + uint32_t(q);
-                if (idx >= start && idx < end) atomicAdd(&h[(w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu], 1u);
+    for (uint32_t w = 0; w < kF2Waves; ++w) {
+        woff += w < wave ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    const uint32_t ex = woff + incl - pair;
+    if (s0 < nblk) cpre[s0] = ex;
+    if (s0 + 1 < nblk) cpre[s0 + 1] = ex + c0;
+    if (threadIdx.x == 0) cpre[nblk] = total;
+    __syncthreads();
+    const uint4* kv = reinterpret_cast<const uint4*>(keys);
+    constexpr uint32_t kU = 4;  // chunks per thread per round
+    for (uint32_t q0 = threadIdx.x; q0 < total; q0 += kF2Threads * kU) {
+        uint4 v[kU];
+        uint32_t nv[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t c = q0 + u * kF2Threads;
+            nv[u] = 0;
+            if (c < total) {
+                uint32_t lo = 0, hi = nblk;  // region of c: the last s with cpre[s] <= c
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (cpre[mid] <= c) lo = mid; else hi = mid;
+                }
+                const uint32_t k = c - cpre[lo];
+                nv[u] = min(8u, sfill[lo] - 8 * k);
+                v[u] = kv[cst[lo] + k];
             }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q)
+                if (q < nv[u]) atomicAdd(&h[(w[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu], 1u);
         }
     }
     __syncthreads();
     const uint32_t ra = max(g * per, rlo), rz = min((g + 1) * per, rhi);
     for (uint32_t row = ra; row < rz; ++row) {
         const uint32_t* hr = h + (row - g * per) * D;
-        for (uint32_t c0 = wave * 64; c0 < D; c0 += kF2Threads) {
-            const uint32_t c = c0 + lane;
-            const uint32_t v = c < D ? hr[c] : 0u;
-            const bool fr = c < D && v >= minsup;
+        for (uint32_t cc = wave * 64; cc < D; cc += kF2Threads) {
+            const uint32_t c = cc + lane;
+            const uint32_t val = c < D ? hr[c] : 0u;
+            const bool fr = c < D && val >= minsup;
             const uint64_t fb = __ballot(fr);
             if (!fb) continue;
             uint32_t at = 0;
             if (lane == 0) at = atomicAdd(nrec, uint32_t(__popcll(fb)));
             at = rfl(at) + uint32_t(__popcll(fb & lanemask_lt()));
-            if (fr && at < cap) recs[at] = FreqRec{row, c, v, 0u};
+            if (fr && at < cap) recs[at] = FreqRec{row, c, val, 0u};
         }
     }
 }
@@ -789,7 +858,7 @@ struct Miner {
     // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
     static uint32_t f2_blocks() {
         const char* v = std::getenv("FSM_F2_BLOCKS");
-        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 16)) : 1024u;
+        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, kF2MaxBlocks)) : 1024u;
     }
 
     // Root F2 by rank groups (k_f2_plan / k_f2_keys / k_f2_count): the
@@ -808,7 +877,9 @@ struct Miner {
         const uint32_t mlo = member_lo(b), mhi = member_hi(b);
         const uint32_t rlo = comm ? slice_lo : 0u, rhi = comm ? std::min(slice_hi, F) : F;
         const uint32_t R = uint32_t(b.R);
-        const uint32_t rpb = std::max<uint32_t>(16u, (R + f2_blocks() - 1) / f2_blocks());
+        const uint32_t nb_want = std::min<uint32_t>(f2_blocks(), kF2MaxBlocks);
+        const uint32_t rpb = std::min<uint32_t>(kF2MaxRows, std::max<uint32_t>(16u, (R + nb_want - 1) / nb_want));
+        if (uint64_t(rpb) * kF2MaxBlocks < R) return false;  // more rows than the LDS-indexed blocks cover
         const uint32_t nblk = (R + rpb - 1) / rpb;
         const uint64_t nd = uint64_t(G) * nblk;
         const SlabPtrs sp = b.slab.ptrs();
@@ -830,7 +901,7 @@ struct Miner {
         DevBuf keys((nslots + 1024) * 2), nk(8);
         FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
         tk = clk->begin("k_f2_keys");
-        const size_t kshm = size_t(kF2Waves) * 64 * sizeof(F2Ent) + size_t(G) * 4;
+        const size_t kshm = size_t(kF2Waves) * 64 * sizeof(F2Ent) + (size_t(kF2MaxRows) + 1) * 4 + size_t(G) * 4;
 #define FSM_F2K(WW)                                                                                                   \
     hipLaunchKernelGGL(k_f2_keys<WW>, dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(), R, rpb,      \
                        sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(),                   \
