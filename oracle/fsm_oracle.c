@@ -932,16 +932,19 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
             } else {
                 int32_t v = 0;
                 parse_java_int(tk.p, tk.n, &v);
-                if (v < 0) {
-                    set_err(err, errlen, "TSR: negative item %d in sid=%d (Vertical array index)", v, sids[r]);
-                    rc = -1;
-                    goto done;
-                }
                 VPUSH(vals, v);
             }
         }
         /* drop items after the last -1 */
         vals.n = item_off.a[item_off.n - 1];
+        /* a negative item of a closed itemset indexes the Vertical arrays (TSR.scala:63-75):
+           ArrayIndexOutOfBounds; one in the dropped trailing itemset is never used */
+        for (int64_t q = item_off.a[set_off.a[set_off.n - 1]]; q < vals.n; q++)
+            if (vals.a[q] < 0) {
+                set_err(err, errlen, "TSR: negative item %d in sid=%d (Vertical array index)", vals.a[q], sids[r]);
+                rc = -1;
+                goto done;
+            }
     }
     VPUSH(set_off, item_off.n - 1);
     if (!any_item) {

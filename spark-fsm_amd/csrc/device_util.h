@@ -91,5 +91,7 @@ template <int W> __device__ __forceinline__ void mask_clear_upto(uint64_t (&m)[W
 // exclusive scan in[0..n) -> out[0..n], out[n] = total (u64 offsets)
 void scan_exclusive(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s);
 void scan_exclusive(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s);
+// free the scan scratch of a stream that is about to be destroyed
+void scan_release(hipStream_t s);
 
 }  // namespace fsm

@@ -136,18 +136,21 @@ KernelClock*& thread_clock() {
     return c;
 }
 
+void scan_release(hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_scan_mu);
+    auto& m = scan_scratch();
+    auto it = m.find(s);
+    if (it == m.end()) return;
+    if (it->second.p) (void)hipFree(it->second.p);
+    m.erase(it);
+}
+
 void scan_exclusive(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint32_t>(in, out, n, s); }
 void scan_exclusive(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) { scan_impl<uint64_t>(in, out, n, s); }
 
-namespace {
-std::mutex g_pool_mu;
-std::multimap<size_t, void*>& pool_map() {
-    static auto* m = new std::multimap<size_t, void*>();  // leaked on exit on purpose
-    return *m;
-}
-}  // namespace
+Pool::~Pool() { trim(); }
 
-void* pool_alloc(size_t bytes, size_t* granted) {
+void* Pool::alloc(size_t bytes, size_t* granted) {
     // size classes: powers of two up to 1 MiB, then sz/16 steps
     size_t sz = 4096;
     while (sz < bytes) sz <<= 1;
@@ -156,20 +159,19 @@ void* pool_alloc(size_t bytes, size_t* granted) {
         sz = (bytes + step - 1) / step * step;
     }
     {
-        std::lock_guard<std::mutex> g(g_pool_mu);
-        auto& m = pool_map();
-        auto it = m.lower_bound(sz);  // smallest cached block that fits, at most 2x larger
-        if (it != m.end() && it->first <= 2 * sz) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = free_.lower_bound(sz);  // smallest cached block that fits, at most 2x larger
+        if (it != free_.end() && it->first <= 2 * sz) {
             void* p = it->second;
             *granted = it->first;
-            m.erase(it);
+            free_.erase(it);
             return p;
         }
     }
     void* p = nullptr;
     hipError_t e = hipMalloc(&p, sz);
     if (e != hipSuccess) {
-        pool_trim();  // give cached blocks back and retry once
+        trim();  // give cached blocks back and retry once
         e = hipMalloc(&p, sz);
         if (e != hipSuccess)
             throw Error(FSM_ENOMEM, "hipMalloc(" + std::to_string(sz) + " bytes) failed: " + hipGetErrorString(e));
@@ -178,15 +180,50 @@ void* pool_alloc(size_t bytes, size_t* granted) {
     return p;
 }
 
-void pool_free(void* p, size_t granted) {
-    std::lock_guard<std::mutex> g(g_pool_mu);
-    pool_map().emplace(granted, p);
+void Pool::give(void* p, size_t granted) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.emplace(granted, p);
 }
 
-void pool_trim() {
-    std::lock_guard<std::mutex> g(g_pool_mu);
-    for (auto& kv : pool_map()) (void)hipFree(kv.second);
-    pool_map().clear();
+void Pool::trim() {
+    std::lock_guard<std::mutex> g(mu_);
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    for (auto& kv : free_) (void)hipFree(kv.second);
+    free_.clear();
+    if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
+}
+
+size_t Pool::cached_blocks() {
+    std::lock_guard<std::mutex> g(mu_);
+    return free_.size();
+}
+
+std::shared_ptr<Pool>& thread_pool() {
+    thread_local std::shared_ptr<Pool> p;
+    return p;
+}
+
+std::shared_ptr<Pool> default_pool(int device) {
+    static std::mutex mu;
+    static auto* pools = new std::map<int, std::shared_ptr<Pool>>();  // leaked on exit on purpose
+    std::lock_guard<std::mutex> g(mu);
+    std::shared_ptr<Pool>& q = (*pools)[device];
+    if (!q) q = std::make_shared<Pool>(device);
+    return q;
+}
+
+void DevBuf::alloc(size_t n) {
+    release();
+    std::shared_ptr<Pool> q = thread_pool();
+    if (!q) {
+        int dev = 0;
+        FSM_HIP(hipGetDevice(&dev));
+        q = default_pool(dev);
+    }
+    p = q->alloc(n ? n : 16, &bytes);
+    pool = std::move(q);
 }
 
 bool debug_sync() {

@@ -389,12 +389,9 @@ void flatten_tsr(const Source& src, FlatTsr& out) {
             uint32_t pos = 0;
             size_t open_from = 0;  // ip index where the open itemset starts
             bool ok = true;
-            auto item = [&](int64_t v, const std::string& what) {
-                if (v < 0) {
-                    er.set(r, FSM_EPARSE, "TSR: negative item " + what + " in sid=" + std::to_string(r) +
-                                              " (Vertical array index)");
-                    return false;
-                }
+            // negative items are checked once the trailing itemset is dropped: only those of
+            // closed itemsets index the Vertical arrays (TSR.scala:63-75)
+            auto item = [&](int64_t v, const std::string&) {
                 ip.push_back({int32_t(v), pos});
                 return true;
             };
@@ -428,6 +425,14 @@ void flatten_tsr(const Source& src, FlatTsr& out) {
             }
             if (!ok) break;
             ip.resize(open_from);  // items after the last -1 are dropped
+            for (const auto& x : ip)
+                if (x.first < 0) {
+                    er.set(r, FSM_EPARSE, "TSR: negative item " + std::to_string(x.first) + " in sid=" +
+                                              std::to_string(r) + " (Vertical array index)");
+                    ok = false;
+                    break;
+                }
+            if (!ok) break;
             std::sort(ip.begin(), ip.end());
             uint32_t len = 0;
             for (size_t q = 0; q < ip.size();) {

@@ -6,6 +6,7 @@
 #include <new>
 
 #include "comm.h"
+#include "device_util.h"
 #include "fsm_internal.h"
 
 using fsm::Error;
@@ -22,6 +23,7 @@ int fail(fsm_ctx* ctx, int code, const std::string& msg) {
 template <class F> int guarded(fsm_ctx* ctx, F&& f) {
     try {
         if (ctx) ctx->err.clear();
+        fsm::PoolScope pool_scope(ctx ? ctx->pool : nullptr);
         f();
         return FSM_OK;
     } catch (const Error& e) {
@@ -125,6 +127,7 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
         if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             throw Error(FSM_EDEVICE, std::string("libfsm is built for gfx950; device is ") + prop.gcnArchName);
         FSM_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->pool = std::make_shared<fsm::Pool>(ctx->opts.device);
         ctx->comm = fsm::make_comm(ctx->opts).release();
     });
     if (rc != FSM_OK) {
@@ -140,8 +143,12 @@ void fsm_ctx_destroy(fsm_ctx* ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     delete ctx->comm;
-    fsm::pool_trim();
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->pool) ctx->pool->trim();  // this context's cached blocks only; live DBs keep their pool alive
+    ctx->pool.reset();
+    if (ctx->stream) {
+        fsm::scan_release(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+    }
     delete ctx;
 }
 

@@ -6,6 +6,9 @@
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -74,9 +77,37 @@ struct ClockScope {
 // Device memory pool: hipMalloc/hipFree synchronize and cost milliseconds for
 // the multi-hundred-MB frontier slabs, so freed blocks are cached per size
 // class (power of two >= 4 KiB) and reused by later batches and later calls.
-void* pool_alloc(size_t bytes, size_t* granted);
-void pool_free(void* p, size_t granted);
-void pool_trim();  // hipFree every cached block (fsm_ctx_destroy)
+// One pool per context (its device and its one stream): a block released while
+// kernels queued on that stream may still read it is only ever handed out
+// again to later work on the same stream, so stream order keeps it safe, and
+// blocks never cross devices or contexts.  The pool is shared-owned by every
+// block it handed out, so DBs may outlive their context's destroy call.
+struct Pool {
+    explicit Pool(int dev) : device(dev) {}
+    ~Pool();
+    Pool(const Pool&) = delete;
+    Pool& operator=(const Pool&) = delete;
+    void* alloc(size_t bytes, size_t* granted);
+    void give(void* p, size_t granted);
+    void trim();  // hipFree every cached block
+    size_t cached_blocks();
+    const int device;
+
+  private:
+    std::mutex mu_;
+    std::multimap<size_t, void*> free_;
+};
+// The pool of the context whose API call runs on this thread (set by the
+// entry points through PoolScope); outside any call, a per-device default.
+std::shared_ptr<Pool>& thread_pool();
+std::shared_ptr<Pool> default_pool(int device);
+struct PoolScope {
+    std::shared_ptr<Pool> prev;
+    explicit PoolScope(std::shared_ptr<Pool> p) : prev(thread_pool()) { thread_pool() = std::move(p); }
+    ~PoolScope() { thread_pool() = std::move(prev); }
+    PoolScope(const PoolScope&) = delete;
+    PoolScope& operator=(const PoolScope&) = delete;
+};
 
 // Mapped pinned host memory (kernels write results straight into it; the host
 // reads them after a stream sync, with no copy launch).
@@ -96,28 +127,34 @@ struct PinnedBuf {
     ~PinnedBuf() { (void)hipHostFree(host); }
 };
 
-// Owning device allocation from the pool, RAII.
+// Owning device allocation from the current pool, RAII.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    std::shared_ptr<Pool> pool;
     DevBuf() = default;
     explicit DevBuf(size_t n) { alloc(n); }
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), pool(std::move(o.pool)) { o.p = nullptr; o.bytes = 0; }
     DevBuf& operator=(DevBuf&& o) noexcept {
-        if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+        if (this != &o) {
+            release();
+            p = o.p;
+            bytes = o.bytes;
+            pool = std::move(o.pool);
+            o.p = nullptr;
+            o.bytes = 0;
+        }
         return *this;
     }
     ~DevBuf() { release(); }
-    void alloc(size_t n) {
-        release();
-        p = pool_alloc(n ? n : 16, &bytes);
-    }
+    void alloc(size_t n);
     void release() {
-        if (p) pool_free(p, bytes);
+        if (p) pool->give(p, bytes);
         p = nullptr;
         bytes = 0;
+        pool.reset();
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
@@ -176,6 +213,7 @@ struct fsm_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     fsm::Comm* comm = nullptr;  // nranks > 1 (owned)
+    std::shared_ptr<fsm::Pool> pool;  // device blocks of this context (see fsm::Pool)
     std::vector<fsm_kernel_stat> kstats;  // of the last mine call
 };
 

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
     if (threadIdx.x == 0) blk_tests = 0;
     __syncthreads();
     uint32_t my_tests = 0;  // (entry, partner) join tests executed (fsm_stats.pair_tests)
-    const uint32_t e1 = min(E, (blockIdx.x + 1) * chunk);
+    const uint32_t e1 = uint32_t(min(uint64_t(E), (uint64_t(blockIdx.x) + 1) * chunk));
     for (uint32_t e = blockIdx.x * chunk + threadIdx.x; e < e1; e += blockDim.x) {
         const uint32_t mi = mem[e], p = pos[e];
         if (mi - mlo >= mhi - mlo) continue;  // member rows of another rank (sharded root)
@@ -561,13 +561,13 @@ __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __r
                                                  const uint64_t* __restrict__ off, SlabPtrs o) {
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
-    const uint32_t wstride = gridDim.x * wpb * 64;
-    for (uint32_t w0 = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 64; w0 < E; w0 += wstride) {
-        const uint32_t e = w0 + lane;
+    const uint64_t wstride = uint64_t(gridDim.x) * wpb * 64;  // 64-bit: no wrap for E near 2^32
+    for (uint64_t w0 = (uint64_t(blockIdx.x) * wpb + (threadIdx.x >> 6)) * 64; w0 < E; w0 += wstride) {
+        const uint32_t e = uint32_t(w0) + lane;
         // this lane's entry: its frequent children kid_slot[k0 .. k0 + nk)
         uint32_t k0 = 0, nk = 0, cc = kNone, rb = 0, re = 0, lt = 0, n_run = 0;
         uint64_t base = 0;
-        if (e < E) {
+        if (w0 + lane < E) {
             const DClass c = cls[cid[e]];
             const uint32_t mi = mem[e];
             cc = child_of[c.cbase + mi];
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __r
             const uint32_t o_re = uint32_t(__shfl(int(re), int(ow), 64));
             const uint32_t o_lt = uint32_t(__shfl(int(lt), int(ow), 64));
             const uint32_t o_done = uint32_t(__shfl(int(done), int(ow), 64));
-            const uint32_t o_e = w0 + ow;
+            const uint32_t o_e = uint32_t(w0 + ow);
             bool ok = false;
             uint32_t q = 0, f = 0, slot = 0;
             if (pp < total) {
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __r
             if (bnd > a) done += uint32_t(__popcll(succ & lane_range(a - p0, bnd - p0)));
         }
         if constexpr (!kWrite) {
-            if (e < E) ncnt[e] = done;
+            if (w0 + lane < E) ncnt[e] = done;
         }
     }
 }
@@ -762,6 +762,54 @@ struct Miner {
     size_t n_shared = 0;  // pattern nodes every rank holds (root + its frequent children)
 
     double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
+
+    // Sharded mining: a failure on one rank must not leave its peers blocked in
+    // a collective.  The work between two collectives runs through
+    // run_or_defer, which records a throw instead of unwinding (nranks > 1);
+    // agree(), called by every rank before the next collective, all-reduces
+    // the failure flags and throws the same FSM_E* code on every rank.
+    int err_code = 0;
+    std::string err_msg;
+    template <class F> void run_or_defer(F&& f) {
+        if (!comm) {
+            f();
+            return;
+        }
+        if (err_code) return;
+        try {
+            f();
+        } catch (const Error& e) {
+            err_code = e.code;
+            err_msg = e.what();
+        } catch (const std::bad_alloc&) {
+            err_code = FSM_ENOMEM;
+            err_msg = "host allocation failed";
+        } catch (const std::exception& e) {
+            err_code = FSM_EDEVICE;
+            err_msg = e.what();
+        }
+    }
+    // FSM_INJECT_FAIL="<rank>,<root|lattice>": throw FSM_ELIMIT on that rank at
+    // that phase (test hook for the failure agreement of sharded mining)
+    void maybe_inject(const char* phase) const {
+        const char* v = std::getenv("FSM_INJECT_FAIL");
+        if (!v || !comm) return;
+        char ph[16] = {0};
+        int r = -1;
+        if (std::sscanf(v, "%d,%15s", &r, ph) == 2 && r == comm->rank() && !std::strcmp(ph, phase))
+            throw Error(FSM_ELIMIT, std::string("SPADE: injected failure (FSM_INJECT_FAIL, ") + phase + ")");
+    }
+    void agree() {
+        if (!comm) return;
+        std::vector<uint32_t> v(8, 0u);
+        if (err_code) v[size_t(std::clamp(err_code, 1, 7))] = 1u;
+        comm->host_allreduce_u32(v.data(), v.size(), s);
+        if (err_code) throw Error(err_code, err_msg);
+        for (int c = 1; c < 8; ++c)
+            if (v[size_t(c)])
+                throw Error(c, "SPADE: a peer rank failed (FSM error " + std::to_string(c) +
+                                   "); the sharded mine is aborted on every rank");
+    }
     void sync() {
         const double t = now_ms();
         FSM_HIP(hipStreamSynchronize(s));
@@ -988,10 +1036,11 @@ struct Miner {
         const uint32_t rhi = shard ? std::min<uint32_t>(slice_hi, uint32_t(rows.size())) : uint32_t(rows.size());
         const uint32_t nrows = rhi - rlo;
         std::vector<FreqRec> recs;
+        DevBuf cnt;
+        auto compute = [&] {
         // the root: pairs counted per rank group, only the frequent ones leave the device
         const bool root_done = b.E && b.root && !root_atomic() && root_f2(b, recs);
         if (b.E) st.count_launches += 1;
-        DevBuf cnt;
         if (!root_done) {
             cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
             FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
@@ -1035,6 +1084,13 @@ struct Miner {
                 FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nf * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
                 sync();
             }
+        }
+        };
+        if (shard) {  // a failure here or in run_root reaches every rank before the gather below
+            run_or_defer(compute);
+            agree();
+        } else {
+            compute();
         }
         uint64_t nfreq = recs.size();
         cnt.release();
@@ -1435,7 +1491,10 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     std::vector<std::unique_ptr<Batch>> stack;
     if (!freq.empty()) {
         auto root = std::make_unique<Batch>();
-        mn.run_root(*root, freq, f1);
+        mn.run_or_defer([&] {  // agreed on in the root count
+            mn.maybe_inject("root");
+            mn.run_root(*root, freq, f1);
+        });
         const double t1 = now_ms();
         ctx->stats.ms_f1 = t1 - t0;
         mn.count_and_freq(*root);
@@ -1445,7 +1504,10 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         ctx->stats.ms_f1 = now_ms() - t0;
     }
     const double t2 = now_ms();
-    // ---- lattice: DFS over class batches (each group of children = one batch)
+    // ---- lattice: DFS over class batches (each group of children = one batch);
+    // sharded: rank-local, failures agreed on before the pattern gather
+    mn.run_or_defer([&] {
+    mn.maybe_inject("lattice");
     while (!stack.empty()) {
         Batch& top = *stack.back();
         if (top.next_group >= top.groups.size()) {
@@ -1467,6 +1529,8 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         mn.count_and_freq(*nb);
         stack.push_back(std::move(nb));
     }
+    });
+    mn.agree();
     {
         unsigned long long tests = 0;
         FSM_HIP(hipMemcpyAsync(&tests, mn.d_tests.p, 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -4,6 +4,7 @@ tests/test_parity_gpu.py as a plain child process).
   python tests/dist_worker.py <mode> <out.json> [args...]
   mode selftest       : fsm_comm_selftest over a gloo TorchHostComm (no GPU)
   mode spade D sup    : sharded SPADE on cuda:0 over a gloo TorchHostComm
+  mode spade_fail D sup : the same with a failure injected on one rank (FSM_INJECT_FAIL)
 Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (torch.distributed, gloo).
 """
 import json
@@ -38,6 +39,19 @@ def main():
             st = eng.stats()
             db.free()
         res.update(patterns=sorted(pats), minsup=meta["minsup"], joins=st["joins"], classes=st["classes"])
+    elif mode == "spade_fail":
+        # sharded SPADE with FSM_INJECT_FAIL set for one rank: every rank must fail, none may hang
+        from tools import gen
+        D, sup = int(sys.argv[3]), float(sys.argv[4])
+        ds = gen.quest(D, seed=1)
+        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc) as eng:
+            db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+            try:
+                eng.spade(db, sup)
+                res.update(code=0, msg="")
+            except fsm.FsmError as e:
+                res.update(code=e.code, msg=e.msg)
+            db.free()
     with open(out, "w") as f:
         json.dump(res, f)
     dist.destroy_process_group()

@@ -72,10 +72,6 @@ def test_threshold_is_ceil_of_support_times_total():
     assert [p for p, _ in oracle.spade(recs, 0.26)["patterns"]] == [((1,),)]
 
 
-def _db(draw_items, rng, ts):
-    pass
-
-
 records_st = st.lists(
     st.lists(st.lists(st.integers(1, 4), min_size=1, max_size=3), min_size=0, max_size=4),
     min_size=1, max_size=7)
@@ -142,3 +138,13 @@ def test_oracle_all_cores_mode_matches_single_thread():
     assert a["complete"] and b["complete"]
     assert a["joins"] == b["joins"] and a["patterns"] == b["patterns"]
     assert a["n_patterns"] > 50
+
+
+def test_tsr_negative_item_only_fails_in_closed_itemsets():
+    """TSR.scala:63-75 index the Vertical arrays with the items of closed
+    itemsets only; the unclosed trailing itemset is dropped by newSequence."""
+    from oracle import oracle
+    r = oracle.tsr([(0, "1 -1 2 -1 -5 -2"), (1, "1 -1 2 -1 3"), (2, "1 2 -1 -7")], 3, 0.5)
+    assert r["rules"] == [((1,), (2,), 2, 2 / 3)]
+    with pytest.raises(oracle.OracleError):
+        oracle.tsr([(0, "1 -1 -5 -1")], 3, 0.5)

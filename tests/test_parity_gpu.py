@@ -99,6 +99,17 @@ def test_tsr_errors(eng, fsm, case):
         gpu_tsr(eng, [tuple(r) for r in case["records"]], 3, 0.5)
 
 
+def test_tsr_negative_item_in_dropped_trailing_itemset(eng):
+    """TSR.newSequence drops the unclosed trailing itemset, so a negative item
+    there never indexes the Vertical arrays: the reference succeeds.
+    In a closed itemset it still fails (error_cases.json)."""
+    from oracle import oracle
+    recs = [(0, "1 -1 2 -1 -5 -2"), (1, "1 -1 2 -1 3"), (2, "1 2 -1 -7")]
+    o = oracle.tsr(recs, 3, 0.5)
+    rules, meta, _ = gpu_tsr(eng, recs, 3, 0.5)
+    assert rules == o["rules"] and rules and meta["final_minsup"] == o["final_minsup"]
+
+
 def test_tsr_k_zero_rejected(eng, fsm):
     with pytest.raises(fsm.FsmError):
         gpu_tsr(eng, [(0, "1 -1 2 -1")], 0, 0.5)
@@ -176,6 +187,51 @@ def test_small_memory_budget_splits_groups(fsm):
         pats, _, st = gpu_spade(e, recs, 0.008)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
     assert st["batches"] > 3
+
+
+def test_two_contexts_on_two_threads(fsm):
+    """Two contexts mining at the same time on two threads (the reference runs
+    concurrent requests on one SparkContext, RequestContext.scala:30): each
+    context draws device blocks from its own pool, so the results
+    are exactly the single-context ones; a DB may outlive its context."""
+    import threading
+    from oracle import oracle
+    from tools import gen
+    ds = gen.quest(20000, seed=7)
+    exp_s = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.004)["patterns"]
+    kds = gen.kosarak(D=4000, seed=2)
+    exp_t = oracle.tsr(kds.records(), 100, 0.5)["rules"]
+    ok, errs = [], []
+
+    def spade_worker():
+        try:
+            with fsm.Engine(0) as e:
+                for _ in range(3):
+                    pats, _, _ = gpu_spade(e, None, 0.004, tokens=ds)
+                    ok.append(pats == exp_s)
+        except Exception as x:  # noqa: BLE001
+            errs.append(repr(x))
+
+    def tsr_worker():
+        try:
+            with fsm.Engine(0) as e:
+                for _ in range(3):
+                    rules, _, _ = gpu_tsr(e, None, 100, 0.5, tokens=kds)
+                    ok.append(rules == exp_t)
+        except Exception as x:  # noqa: BLE001
+            errs.append(repr(x))
+
+    th = [threading.Thread(target=f) for f in (spade_worker, spade_worker, tsr_worker)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=110)
+    assert not errs and len(ok) == 9 and all(ok), (errs, ok)
+    # a DB freed after its context was destroyed returns its blocks to that context's pool
+    e = fsm.Engine(0)
+    db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+    e.close()
+    db.free()
 
 
 # ------------------------------------------------------ dataset shapes
@@ -306,6 +362,19 @@ def test_sharded_spade_two_ranks(eng, world, D, sup, ref, tmp_path):
         assert canon(r["patterns"]) == exp
         assert r["joins"] == joins
     assert sum(1 for _ in exp) > 100
+
+
+@pytest.mark.parametrize("phase", ["root", "lattice"])
+def test_sharded_spade_failure_reaches_every_rank(phase, tmp_path, monkeypatch):
+    """A failure on one rank of a sharded mine (injected FSM_ELIMIT on rank 1)
+    comes back as the same FSM_E* code on every rank instead of leaving the
+    peers blocked in a collective."""
+    from test_dist import run_ranks
+    from spark_fsm_amd import FSM_ELIMIT
+    monkeypatch.setenv("FSM_INJECT_FAIL", "1,%s" % phase)
+    res = run_ranks(2, ["spade_fail", "20000", "0.003"], tmp_path, timeout=100)
+    assert [r["code"] for r in res] == [FSM_ELIMIT, FSM_ELIMIT]
+    assert "injected" in res[1]["msg"] and "peer rank failed" in res[0]["msg"]
 
 
 @pytest.mark.parametrize("bitmap", ["1", "0"])
