@@ -132,6 +132,7 @@ typedef struct {
     int64_t root_keys;          /* SPADE: non-empty (sequence, frequent-item pair) joins the root F2 counted */
     int64_t pair_tests;         /* SPADE: (entry, partner) join tests executed by the class count kernels */
     int64_t root_entries;       /* SPADE: (frequent item, sequence) entries of the root class (F2 input) */
+    int64_t k0_device;          /* 1: the last fsm_db_* built the DB on the GPU (K0), 0: host flatten + upload */
 } fsm_stats;
 
 /* Per-kernel device time of the last fsm_*_mine call (HIP events on the
@@ -174,6 +175,29 @@ int fsm_db_from_spmf(fsm_ctx* ctx, int32_t mode, const int32_t* sids, const char
 int fsm_db_from_tokens(fsm_ctx* ctx, int32_t mode, const int32_t* sids, const int64_t* seq_off,
                        const int64_t* tokens, int64_t n, fsm_db** out);
 void fsm_db_free(fsm_db* db);
+
+/* Host copy of a flattened DB as it sits in HBM (verification and debugging:
+ * the device-built DB is compared byte for byte with the host flatten's).
+ * SPADE: rows = distinct sequence ids, item = dense ids (ascending value
+ * order, item_val maps them back), mask = mask_words u64 eid bits per entry.
+ * TSR: rows = sequences, first / last = itemset indexes.  Library-owned until
+ * fsm_db_image_free. */
+typedef struct {
+    int32_t mode;
+    int32_t mask_words;
+    int64_t rows;
+    int64_t entries;
+    int64_t items;
+    int64_t max_occ;            /* SPADE: closed item tokens of the longest row */
+    uint32_t* row_off;          /* [rows+1] */
+    uint32_t* item;             /* [entries] */
+    uint64_t* mask;             /* SPADE: [entries * mask_words] */
+    uint32_t* first;            /* TSR: [entries] */
+    uint32_t* last;             /* TSR: [entries] */
+    int32_t* item_val;          /* [items] */
+} fsm_db_image;
+int fsm_db_export(fsm_ctx* ctx, const fsm_db* db, fsm_db_image** out);
+void fsm_db_image_free(fsm_db_image* img);
 
 int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_patterns** out);
 void fsm_patterns_free(fsm_patterns* p);

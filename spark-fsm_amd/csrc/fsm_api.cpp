@@ -2,10 +2,12 @@
 // catches everything: no C++ exception crosses the ABI, failures come back as
 // FSM_E* codes with the message in fsm_last_error (the Scala shim turns them
 // into java.lang.Exception so TrainActor records FAILURE, TrainActor.scala:65-67).
+#include <algorithm>
 #include <cstdlib>
 #include <new>
 
 #include "comm.h"
+#include "dev_db.h"
 #include "device_util.h"
 #include "fsm_internal.h"
 
@@ -37,6 +39,29 @@ template <class F> int guarded(fsm_ctx* ctx, F&& f) {
     }
 }
 
+// per-mine stats start from zero; the DB-build figures of the last fsm_db_* stay
+void reset_stats(fsm_ctx* ctx) {
+    const fsm_stats prev = ctx->stats;
+    ctx->stats = fsm_stats{};
+    ctx->stats.ms_flatten = prev.ms_flatten;
+    ctx->stats.ms_upload = prev.ms_upload;
+    ctx->stats.k0_device = prev.k0_device;
+    ctx->kstats.clear();
+}
+
+template <class T> T* host_copy(const fsm::DevBuf& d, size_t n, hipStream_t s) {
+    T* h = static_cast<T*>(std::malloc(std::max<size_t>(n, 1) * sizeof(T)));
+    if (!h) throw Error(FSM_ENOMEM, "malloc failed");
+    if (n) {
+        const hipError_t e = hipMemcpyAsync(h, d.p, n * sizeof(T), hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) {
+            std::free(h);
+            throw Error(FSM_EDEVICE, std::string("hipMemcpyAsync failed: ") + hipGetErrorString(e));
+        }
+    }
+    return h;
+}
+
 int make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out) {
     if (!ctx || !out) return fail(ctx, FSM_EINVAL, "null argument");
     *out = nullptr;
@@ -48,6 +73,8 @@ int make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out) {
     db->mode = mode;
     const int rc = guarded(ctx, [&] {
         FSM_HIP(hipSetDevice(ctx->opts.device));
+        ctx->stats.k0_device = 0;
+        if (fsm::k0_build(ctx, mode, src, db)) return;  // K0 on the GPU (token input)
         const double t0 = fsm::now_ms();
         if (mode == FSM_MODE_SPADE) fsm::flatten_spade(src, db->spade);
         else fsm::flatten_tsr(src, db->tsr);
@@ -189,6 +216,63 @@ int fsm_db_from_tokens(fsm_ctx* ctx, int32_t mode, const int32_t* sids, const in
     return make_db(ctx, mode, src, out);
 }
 
+int fsm_db_export(fsm_ctx* ctx, const fsm_db* db, fsm_db_image** out) {
+    if (!ctx || !db || !out) return fail(ctx, FSM_EINVAL, "null argument");
+    *out = nullptr;
+    if (db->ctx != ctx) return fail(ctx, FSM_EINVAL, "db belongs to another context");
+    auto* img = static_cast<fsm_db_image*>(std::calloc(1, sizeof(fsm_db_image)));
+    if (!img) return fail(ctx, FSM_ENOMEM, "calloc failed");
+    const int rc = guarded(ctx, [&] {
+        FSM_HIP(hipSetDevice(ctx->opts.device));
+        hipStream_t s = ctx->stream;
+        img->mode = db->mode;
+        if (db->mode == FSM_MODE_SPADE) {
+            const SpadeDevDB* d = db->spade_dev;
+            img->mask_words = d->W;
+            img->rows = d->R;
+            img->entries = d->E;
+            img->max_occ = db->spade.max_occ;
+            img->row_off = host_copy<uint32_t>(d->row_off, size_t(d->R + 1), s);
+            img->item = host_copy<uint32_t>(d->item, size_t(d->E), s);
+            img->mask = host_copy<uint64_t>(d->mask, size_t(d->E) * size_t(d->W), s);
+            img->items = int64_t(db->spade.item_val.size());
+            img->item_val = static_cast<int32_t*>(std::malloc(std::max<size_t>(db->spade.item_val.size(), 1) * 4));
+            if (!img->item_val) throw Error(FSM_ENOMEM, "malloc failed");
+            std::memcpy(img->item_val, db->spade.item_val.data(), db->spade.item_val.size() * 4);
+        } else {
+            const TsrDevDB* d = db->tsr_dev;
+            img->rows = d->N;
+            img->entries = d->E;
+            img->row_off = host_copy<uint32_t>(d->row_off, size_t(d->N + 1), s);
+            img->item = host_copy<uint32_t>(d->item, size_t(d->E), s);
+            img->first = host_copy<uint32_t>(d->first, size_t(d->E), s);
+            img->last = host_copy<uint32_t>(d->last, size_t(d->E), s);
+            img->items = int64_t(db->tsr.item_val.size());
+            img->item_val = static_cast<int32_t*>(std::malloc(std::max<size_t>(db->tsr.item_val.size(), 1) * 4));
+            if (!img->item_val) throw Error(FSM_ENOMEM, "malloc failed");
+            std::memcpy(img->item_val, db->tsr.item_val.data(), db->tsr.item_val.size() * 4);
+        }
+        FSM_HIP(hipStreamSynchronize(s));
+    });
+    if (rc != FSM_OK) {
+        fsm_db_image_free(img);
+        return rc;
+    }
+    *out = img;
+    return FSM_OK;
+}
+
+void fsm_db_image_free(fsm_db_image* img) {
+    if (!img) return;
+    std::free(img->row_off);
+    std::free(img->item);
+    std::free(img->mask);
+    std::free(img->first);
+    std::free(img->last);
+    std::free(img->item_val);
+    std::free(img);
+}
+
 void fsm_db_free(fsm_db* db) {
     if (!db) return;
     fsm::spade_release(db);
@@ -204,11 +288,7 @@ int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_pa
     if (db->mode != FSM_MODE_SPADE) return fail(ctx, FSM_EINVAL, "db was not flattened for SPADE");
     return guarded(ctx, [&] {
         FSM_HIP(hipSetDevice(ctx->opts.device));
-        const double fl = ctx->stats.ms_flatten, up = ctx->stats.ms_upload;
-        ctx->stats = fsm_stats{};
-        ctx->stats.ms_flatten = fl;
-        ctx->stats.ms_upload = up;
-        ctx->kstats.clear();
+        reset_stats(ctx);
         fsm::spade_mine(ctx, db, support, out);
     });
 }
@@ -221,11 +301,7 @@ int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules*
     if (k < 1) return fail(ctx, FSM_EINVAL, "TSR: k must be >= 1 (got " + std::to_string(k) + ")");
     return guarded(ctx, [&] {
         FSM_HIP(hipSetDevice(ctx->opts.device));
-        const double fl = ctx->stats.ms_flatten, up = ctx->stats.ms_upload;
-        ctx->stats = fsm_stats{};
-        ctx->stats.ms_flatten = fl;
-        ctx->stats.ms_upload = up;
-        ctx->kstats.clear();
+        reset_stats(ctx);
         fsm::tsr_mine(ctx, db, k, minconf, out);
     });
 }

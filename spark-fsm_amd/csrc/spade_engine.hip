@@ -37,15 +37,9 @@
 #include <thread>
 
 #include "comm.h"
+#include "dev_db.h"
 #include "device_util.h"
 
-struct SpadeDevDB {
-    fsm::DevBuf row_off;  // u32 [R+1]
-    fsm::DevBuf item;     // u32 [E]
-    fsm::DevBuf mask;     // u64 [E*W]
-    int64_t R = 0, E = 0, U = 0;
-    int W = 1;
-};
 
 namespace fsm {
 namespace {

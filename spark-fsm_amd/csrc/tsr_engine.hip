@@ -33,16 +33,9 @@
 #include <set>
 #include <unordered_map>
 
+#include "dev_db.h"
 #include "device_util.h"
 
-struct TsrDevDB {
-    fsm::DevBuf row_off, item, first, last;  // horizontal
-    fsm::DevBuf vert_off, vert_sid, vert_item;
-    fsm::DevBuf bm;                          // sid bitmaps: U x NW u32 (empty when over budget)
-    int64_t N = 0, E = 0, U = 0;
-    uint32_t NW = 0;                         // u32 words per item bitmap = ceil(N / 32)
-    std::vector<uint32_t> sup;  // |sids(item)|
-};
 
 namespace fsm {
 namespace {
@@ -644,6 +637,14 @@ void tsr_upload(fsm_ctx* ctx, fsm_db* db) {
         FSM_HIP(hipMemcpyAsync(d->first.p, f.ent_first.data(), size_t(d->E) * 4, hipMemcpyHostToDevice, s));
         FSM_HIP(hipMemcpyAsync(d->last.p, f.ent_last.data(), size_t(d->E) * 4, hipMemcpyHostToDevice, s));
     }
+    tsr_finish(ctx, d.get());
+    db->tsr_dev = d.release();
+}
+
+// The vertical transpose (item -> sids), the sid bitmaps and the item
+// supports from the horizontal rows already in HBM (host upload or K0).
+void tsr_finish(fsm_ctx* ctx, TsrDevDB* d) {
+    hipStream_t s = ctx->stream;
     // vertical transpose on the device (K0)
     DevBuf cnt(size_t(std::max<int64_t>(d->U, 1)) * 4), cursor(size_t(std::max<int64_t>(d->U, 1)) * 4);
     d->vert_off.alloc(size_t(d->U + 1) * 8);
@@ -683,7 +684,6 @@ void tsr_upload(fsm_ctx* ctx, fsm_db* db) {
     d->sup.resize(size_t(d->U));
     if (d->U) FSM_HIP(hipMemcpyAsync(d->sup.data(), cnt.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, s));
     FSM_HIP(hipStreamSynchronize(s));
-    db->tsr_dev = d.release();
 }
 
 void tsr_release(fsm_db* db) {

@@ -80,6 +80,23 @@ class Rules(ctypes.Structure):
     ]
 
 
+class DbImage(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int32),
+        ("mask_words", ctypes.c_int32),
+        ("rows", ctypes.c_int64),
+        ("entries", ctypes.c_int64),
+        ("items", ctypes.c_int64),
+        ("max_occ", ctypes.c_int64),
+        ("row_off", ctypes.POINTER(ctypes.c_uint32)),
+        ("item", ctypes.POINTER(ctypes.c_uint32)),
+        ("mask", ctypes.POINTER(ctypes.c_uint64)),
+        ("first", ctypes.POINTER(ctypes.c_uint32)),
+        ("last", ctypes.POINTER(ctypes.c_uint32)),
+        ("item_val", ctypes.POINTER(ctypes.c_int32)),
+    ]
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 40), ("launches", ctypes.c_int64), ("alg_bytes", ctypes.c_int64),
                 ("ms", ctypes.c_double)]
@@ -93,7 +110,7 @@ class Stats(ctypes.Structure):
         "ms_count_kernel", "ms_emit_kernel")] + [(n, ctypes.c_int64) for n in (
         "count_launches", "mask_words", "bytes_count_alg")] + [(n, ctypes.c_double) for n in (
         "ms_gpu_wait", "ms_output")] + [(n, ctypes.c_int64) for n in (
-        "joins_root", "root_keys", "pair_tests", "root_entries")]
+        "joins_root", "root_keys", "pair_tests", "root_entries", "k0_device")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -104,6 +121,7 @@ EXPORTS = [
     "fsm_abi_version", "fsm_comm_unique_id", "fsm_shard_plan", "fsm_comm_selftest", "fsm_ctx_create", "fsm_ctx_destroy",
     "fsm_last_error", "fsm_get_stats", "fsm_get_kernel_stats", "fsm_db_from_spmf", "fsm_db_from_tokens",
     "fsm_db_free", "fsm_spade_mine", "fsm_patterns_free", "fsm_tsr_mine", "fsm_rules_free",
+    "fsm_db_export", "fsm_db_image_free",
 ]
 
 _lib = None
@@ -137,6 +155,9 @@ def load():
                                    P(ctypes.c_int64), ctypes.c_int64, P(vp)]
     L.fsm_db_from_tokens.argtypes = [vp, ctypes.c_int32, P(ctypes.c_int32), P(ctypes.c_int64),
                                      P(ctypes.c_int64), ctypes.c_int64, P(vp)]
+    L.fsm_db_export.argtypes = [vp, vp, P(P(DbImage))]
+    L.fsm_db_image_free.argtypes = [P(DbImage)]
+    L.fsm_db_image_free.restype = None
     L.fsm_db_free.argtypes = [vp]
     L.fsm_db_free.restype = None
     L.fsm_spade_mine.argtypes = [vp, vp, ctypes.c_double, ctypes.c_int32, P(P(Patterns))]

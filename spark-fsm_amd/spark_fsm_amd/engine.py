@@ -71,6 +71,28 @@ class Engine:
             tokens.ctypes.data_as(P(ctypes.c_int64)), n, ctypes.byref(db)), self._ctx)
         return DB(self, db, mode)
 
+    def db_export(self, db):
+        """fsm_db_export: the flattened DB as it sits in HBM, as numpy arrays."""
+        out = ctypes.POINTER(_lib.DbImage)()
+        check(self._L.fsm_db_export(self._ctx, db.handle, ctypes.byref(out)), self._ctx)
+        try:
+            m = out.contents
+
+            def arr(ptr, n):
+                return np.ctypeslib.as_array(ptr, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0)
+
+            img = {"mode": m.mode, "mask_words": m.mask_words, "rows": m.rows, "entries": m.entries,
+                   "items": m.items, "max_occ": m.max_occ, "row_off": arr(m.row_off, m.rows + 1),
+                   "item": arr(m.item, m.entries), "item_val": arr(m.item_val, m.items)}
+            if m.mode == MODE_SPADE:
+                img["mask"] = arr(m.mask, m.entries * m.mask_words)
+            else:
+                img["first"] = arr(m.first, m.entries)
+                img["last"] = arr(m.last, m.entries)
+        finally:
+            self._L.fsm_db_image_free(out)
+        return img
+
     # ------------------------------------------------------------ mining
     def spade_csr(self, db, support, dfs=True):
         """fsm_spade_mine -> CSR numpy arrays (support, pat_off, set_off, items), meta."""
