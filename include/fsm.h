@@ -133,6 +133,9 @@ typedef struct {
     int64_t pair_tests;         /* SPADE: (entry, partner) join tests executed by the class count kernels */
     int64_t root_entries;       /* SPADE: (frequent item, sequence) entries of the root class (F2 input) */
     int64_t k0_device;          /* 1: the last fsm_db_* built the DB on the GPU (K0), 0: host flatten + upload */
+    int64_t exp_domain;         /* TSR: sids expanded over (sum over expansions of |sids(X u Y)|) */
+    int64_t exp_entries;        /* TSR: row entries read by the expansions */
+    int64_t exp_bitmap_bytes;   /* TSR: sid-bitmap operand bytes ANDed by the expansions */
 } fsm_stats;
 
 /* Per-kernel device time of the last fsm_*_mine call (HIP events on the

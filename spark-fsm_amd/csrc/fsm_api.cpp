@@ -169,6 +169,8 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
 void fsm_ctx_destroy(fsm_ctx* ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (hipEvent_t e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
     delete ctx->comm;
     if (ctx->pool) ctx->pool->trim();  // this context's cached blocks only; live DBs keep their pool alive
     ctx->pool.reset();

@@ -43,7 +43,8 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxSide = 64;
 constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRID sweep: 4-8 best)
-constexpr int kExpBatch = 32;       // rules expanded per launch (speculative, committed in order)
+constexpr int kExpBatch = 256;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
+constexpr int kMaxBatch = 256;
 constexpr int kExpandBlocks = 128;  // bitmap path: expansion blocks per rule slot
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kSpecDepth = 3;       // child speculation: levels per launch
@@ -115,6 +116,44 @@ __global__ __launch_bounds__(kBlock) void k_pairs(const uint32_t* __restrict__ v
     }
 }
 
+// Rows restricted to the items with support >= t (one wave per row, ballot
+// compaction, item order kept): pass 1 counts (out == nullptr), pass 2 writes.
+__global__ __launch_bounds__(kBlock) void k_rows_keep(const uint32_t* __restrict__ row_off,
+                                                      const uint32_t* __restrict__ item,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ last,
+                                                      const uint32_t* __restrict__ isup, uint32_t t, uint64_t N,
+                                                      uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+                                                      uint32_t* __restrict__ o_item, uint32_t* __restrict__ o_first,
+                                                      uint32_t* __restrict__ o_last) {
+    const uint64_t wstride = (uint64_t(gridDim.x) * blockDim.x) >> 6;
+    for (uint64_t r = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; r < N; r += wstride) {
+        const uint32_t rb = row_off[r], re = row_off[r + 1];
+        uint64_t o = off ? off[r] : 0;
+        uint32_t n = 0;
+        for (uint32_t e0 = rb; e0 < re; e0 += 64) {
+            const uint32_t e = e0 + lane_id();
+            const bool keep = e < re && isup[item[e]] >= t;
+            const uint64_t b = __ballot(keep);
+            if (off && keep) {
+                const uint64_t d = o + uint32_t(__popcll(b & lanemask_lt()));
+                o_item[d] = item[e];
+                o_first[d] = first[e];
+                o_last[d] = last[e];
+            }
+            o += uint32_t(__popcll(b));
+            n += uint32_t(__popcll(b));
+        }
+        if (!off && lane_id() == 0) cnt[r] = n;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_off32(const uint64_t* __restrict__ off, uint64_t n,
+                                                  uint32_t* __restrict__ out) {
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i <= n; i += uint64_t(gridDim.x) * blockDim.x)
+        out[i] = uint32_t(off[i]);
+}
+
 struct PairRec {
     uint32_t i, j, ij, ji;
 };
@@ -154,6 +193,31 @@ struct Side {
     uint32_t Y[kMaxSide];
 };
 
+// First index in [lo, hi) of the item-sorted row with item >= key, found by
+// the whole wave: 64 probes per round narrow the range 64-fold (rows of up to
+// 4096 entries take 2 dependent rounds instead of 12 binary-search steps).
+__device__ __forceinline__ uint32_t wave_find(const uint32_t* __restrict__ item, uint32_t lo, uint32_t hi,
+                                              uint32_t key) {
+    const uint32_t lane = lane_id();
+    while (hi - lo > 64) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t p = lo + lane * step;
+        const bool ge = p < hi && item[p] >= key;
+        const uint64_t b = __ballot(ge);
+        if (!b) {  // every probe inside the range is < key: the answer lies after the last one
+            lo = lo + min(63u, (hi - 1 - lo) / step) * step + 1;
+            continue;
+        }
+        const uint32_t f = uint32_t(__ffsll((long long)b)) - 1;
+        const uint32_t pf = min(hi, lo + f * step);
+        lo = f ? lo + (f - 1) * step + 1 : lo;
+        hi = pf;
+    }
+    const uint32_t p = lo + lane;
+    const uint64_t b = __ballot(p < hi && item[p] >= key);
+    return b ? lo + uint32_t(__ffsll((long long)b)) - 1 : hi;
+}
+
 __device__ __forceinline__ bool in_sorted(const uint32_t* s, uint32_t n, uint32_t c) {
     for (uint32_t k = 0; k < n; ++k) {
         if (s[k] == c) return true;
@@ -168,8 +232,9 @@ struct ExpCtl {
     uint32_t nlist;  // items touched (list entries)
     uint32_t nout;   // candidates kept
     uint32_t done;   // collect blocks finished
-    uint32_t nsid;   // bitmap path: sids containing X u Y (slot list length)
-    uint32_t pad[3];
+    uint32_t nsid;   // bitmap path: sids containing X u Y (the expansion domain)
+    uint32_t nent;   // bitmap path: row entries read over the domain (algorithmic bytes)
+    uint32_t pad[2];
 };
 
 // histogram bump (no returned value: the lanes' atomics stay in flight) that
@@ -210,11 +275,12 @@ __global__ __launch_bounds__(kBlock) void k_expand(const Side* __restrict__ side
                                                    const uint32_t* __restrict__ last, uint32_t U,
                                                    uint32_t* __restrict__ TLb, uint32_t* __restrict__ DLb,
                                                    uint32_t* __restrict__ TRb, uint32_t* __restrict__ seenb,
-                                                   uint32_t* __restrict__ listb, ExpCtl* __restrict__ ctlb) {
+                                                   uint32_t* __restrict__ listb, ExpCtl* __restrict__ ctlb,
+                                                   const uint32_t* __restrict__ isup, uint32_t t) {
     const uint64_t w = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     if (w >= wave_off[nslot]) return;
     uint32_t b = 0;  // slot of this wave: the last b with wave_off[b] <= w
-    for (uint32_t step = kExpBatch / 2; step > 0; step >>= 1)
+    for (uint32_t step = kMaxBatch / 2; step > 0; step >>= 1)
         if (b + step < nslot && wave_off[b + step] <= w) b += step;
     const Side& side = sides[b];
     const uint64_t U64 = U;
@@ -240,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(const Side* __restrict__ side
     if (side.doL) {  // |sids(X u {c})| for candidate left extensions
         const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
         for (uint32_t q = q0 + lane; q < re; q += 64)
-            if (!in_sorted(side.Y, side.ny, item[q])) bump(DL, item[q], seen, list, ctl);
+            if (isup[item[q]] >= t && !in_sorted(side.Y, side.ny, item[q])) bump(DL, item[q], seen, list, ctl);
     }
     uint32_t lY = 0xFFFFFFFFu;
     for (uint32_t k = lane; k < side.ny; k += 64) {
@@ -255,14 +321,14 @@ __global__ __launch_bounds__(kBlock) void k_expand(const Side* __restrict__ side
         const uint32_t q0 = row_find(item, rb, re, side.maxX + 1);
         for (uint32_t q = q0 + lane; q < re; q += 64) {
             const uint32_t c = item[q];
-            if (first[q] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
+            if (first[q] < lY && isup[c] >= t && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
         }
     }
     if (side.doR) {        // expandR: c > max(Y), c not in X, c after firstX(s)
         const uint32_t q0 = row_find(item, rb, re, side.maxY + 1);
         for (uint32_t q = q0 + lane; q < re; q += 64) {
             const uint32_t c = item[q];
-            if (last[q] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
+            if (last[q] > fX && isup[c] >= t && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
         }
     }
 }
@@ -271,7 +337,7 @@ struct ExpRec {
     uint32_t c, tl, dl, tr;
 };
 struct ExpHdr {
-    uint32_t nout, nx, pad0, pad1;
+    uint32_t nout, nx, nsid, nent;
 };
 
 // Visit the touched items of this expansion: keep the candidates with count
@@ -323,11 +389,14 @@ __device__ __forceinline__ void publish_slots(ExpCtl* __restrict__ ctlb, ExpHdr*
         ExpCtl& c = ctlb[b];
         hdrb[b].nout = c.nout;
         hdrb[b].nx = c.nx;
+        hdrb[b].nsid = c.nsid;
+        hdrb[b].nent = c.nent;
         c.nx = 0;
         c.nlist = 0;
         c.nout = 0;
         c.done = 0;
         c.nsid = 0;
+        c.nent = 0;
     }
 }
 
@@ -354,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_build(const uint32_t* __restr
 // Block x owns a contiguous range of bitmap words: it ANDs the rule's |X|+|Y|
 // item bitmaps over its range a chunk at a time, compacts the set sids into
 // LDS, and its waves then take those sids one per wave: TL / TR histograms.
-constexpr uint32_t kChunkWords = 256;  // bitmap words per LDS round (<= 8192 sids)
+constexpr uint32_t kChunkWords = 64;  // bitmap words per LDS round (<= 2048 sids; 8 KiB of LDS keeps 7 blocks per CU)
 __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
                                                       uint32_t NW, const uint32_t* __restrict__ row_off,
                                                       const uint32_t* __restrict__ item,
@@ -362,7 +431,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
                                                       const uint32_t* __restrict__ last, uint32_t U,
                                                       uint32_t* __restrict__ TLb, uint32_t* __restrict__ TRb,
                                                       uint32_t* __restrict__ seenb, uint32_t* __restrict__ listb,
-                                                      ExpCtl* __restrict__ ctlb, uint32_t* __restrict__ ndlw) {
+                                                      ExpCtl* __restrict__ ctlb, uint32_t* __restrict__ ndlw,
+                                                      const uint32_t* __restrict__ isup, uint32_t t) {
     __shared__ uint32_t lsid[kChunkWords * 32];
     __shared__ uint32_t ln;
     const uint64_t b = blockIdx.y, U64 = U;
@@ -376,6 +446,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ndlw = 0u;
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint32_t my_ent = 0;  // row entries this wave read (lane 0)
     const uint32_t w0 = uint32_t(uint64_t(blockIdx.x) * NW / gridDim.x);
     const uint32_t w1 = uint32_t(uint64_t(blockIdx.x + 1) * NW / gridDim.x);
     for (uint32_t c0 = w0; c0 < w1; c0 += kChunkWords) {
@@ -396,33 +467,72 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
         }
         __syncthreads();
         const uint32_t n = ln;
+        if (threadIdx.x == 0 && n) atomicAdd(&ctl->nsid, n);
         for (uint32_t q = wv; q < n; q += wpb) {
             const uint32_t s = lsid[q];
             const uint32_t rb = row_off[s], re = row_off[s + 1];
+            if (lane == 0) my_ent += re - rb;
+            if (re - rb <= 64) {
+                // the whole row in one round of loads, one entry per lane; X and Y
+                // items found by ballot (every item of X u Y is in the row: s came
+                // from the bitmap AND), no dependent binary searches
+                const bool v = lane < re - rb;
+                uint32_t c = 0xFFFFFFFFu, fi = 0, la = 0;
+                if (v) {
+                    c = item[rb + lane];
+                    fi = first[rb + lane];
+                    la = last[rb + lane];
+                }
+                uint32_t fX = 0, lY = 0xFFFFFFFFu;
+                bool inX = false, inY = false;
+                for (uint32_t k = 0; k < side.nx; ++k) {
+                    const bool hit = c == side.X[k];
+                    inX |= hit;
+                    const uint64_t hb = __ballot(hit);
+                    fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(fi), int(__ffsll((long long)hb) - 1))));
+                }
+                for (uint32_t k = 0; k < side.ny; ++k) {
+                    const bool hit = c == side.Y[k];
+                    inY |= hit;
+                    const uint64_t hb = __ballot(hit);
+                    lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(la), int(__ffsll((long long)hb) - 1))));
+                }
+                if (fX >= lY) continue;  // X => Y does not hold in s
+                // a candidate whose own support is below the launch's minsup can never reach it
+                const bool fq = v && isup[c] >= t;
+                if (side.doL && fq && c > side.maxX && fi < lY && !inY) bump(TL, c, seen, list, ctl);
+                if (side.doR && fq && c > side.maxY && la > fX && !inX) bump(TR, c, seen, list, ctl);
+                continue;
+            }
+            // longer rows: X / Y items and the tails located by wave 64-ary searches
             uint32_t fX = 0, lY = 0xFFFFFFFFu;
-            for (uint32_t k = lane; k < side.nx; k += 64) fX = max(fX, first[row_find(item, rb, re, side.X[k])]);
-            for (uint32_t k = lane; k < side.ny; k += 64) lY = min(lY, last[row_find(item, rb, re, side.Y[k])]);
-            fX = wave_max(fX);
-            lY = wave_min(lY);
+            for (uint32_t k = 0; k < side.nx; ++k) fX = max(fX, first[wave_find(item, rb, re, side.X[k])]);
+            for (uint32_t k = 0; k < side.ny; ++k) lY = min(lY, last[wave_find(item, rb, re, side.Y[k])]);
             if (fX >= lY) continue;  // X => Y does not hold in s
             // expandL (c > max(X), c not in Y, c before lastY(s)) and expandR
             // (c > max(Y), c not in X, c after firstX(s)) in one pass over the
             // row tail both need: each entry's item / first / last read once
-            const uint32_t qL = side.doL ? row_find(item, rb, re, side.maxX + 1) : re;
-            const uint32_t qR = side.doR ? row_find(item, rb, re, side.maxY + 1) : re;
+            const uint32_t qL = side.doL ? wave_find(item, rb, re, side.maxX + 1) : re;
+            const uint32_t qR = side.doR ? wave_find(item, rb, re, side.maxY + 1) : re;
             for (uint32_t e = min(qL, qR) + lane; e < re; e += 64) {
                 const uint32_t c = item[e];
+                if (isup[c] < t) continue;
                 if (e >= qL && first[e] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
                 if (e >= qR && last[e] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
             }
         }
         __syncthreads();
     }
+    if (lane == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
 }
 
 // |sids(X u {c})| for the kept left-extension candidates: AND + popcount
+// A candidate c with fewer sids than bitmap words is counted over its own
+// sid list (vertical list of c: one X-bitmap bit test per sid, the X bitmaps
+// stay cache resident) instead of ANDing whole bitmaps.
 __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
-                                               uint32_t NW, const uint4* __restrict__ dlw,
+                                               uint32_t NW, const uint64_t* __restrict__ vert_off,
+                                               const uint32_t* __restrict__ vert_sid, const uint4* __restrict__ dlw,
                                                const uint32_t* __restrict__ ndlw, ExpRec* __restrict__ outb,
                                                uint32_t cap, ExpCtl* __restrict__ ctlb, ExpHdr* __restrict__ hdrb,
                                                uint32_t nslot) {
@@ -433,10 +543,20 @@ __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, c
         const uint4 wk = dlw[i];
         const Side& side = sides[wk.x];
         uint32_t acc = 0;
-        for (uint32_t w = threadIdx.x; w < NW; w += blockDim.x) {
-            uint32_t v = bm[uint64_t(wk.y) * NW + w];
-            for (uint32_t k = 0; k < side.nx; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
-            acc += uint32_t(__popc(v));
+        const uint64_t v0 = vert_off[wk.y], v1 = vert_off[wk.y + 1];
+        if (v1 - v0 < NW) {
+            for (uint64_t q = v0 + threadIdx.x; q < v1; q += blockDim.x) {
+                const uint32_t sid = vert_sid[q], w = sid >> 5, bit = 1u << (sid & 31u);
+                bool all = true;
+                for (uint32_t k = 0; k < side.nx && all; ++k) all = (bm[uint64_t(side.X[k]) * NW + w] & bit) != 0u;
+                acc += all ? 1u : 0u;
+            }
+        } else {
+            for (uint32_t w = threadIdx.x; w < NW; w += blockDim.x) {
+                uint32_t v = bm[uint64_t(wk.y) * NW + w];
+                for (uint32_t k = 0; k < side.nx; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
+                acc += uint32_t(__popc(v));
+            }
         }
 #pragma unroll
         for (int d = 32; d > 0; d >>= 1) acc += uint32_t(__shfl_xor(int(acc), d, 64));
@@ -768,6 +888,41 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         a = b;
     }
     scr.release();
+    // The expansions scan rows restricted to the items that can still be in a
+    // rule: support >= the pair phase's minsup, which only rises from here
+    // (the first / last itemset indexes of the kept items are unchanged).
+    DevBuf k_off, k_item, k_first, k_last;
+    uint64_t E2 = 0;
+    {
+        const uint64_t N = uint64_t(d->N);
+        DevBuf rc(std::max<uint64_t>(N, 1) * 4), off64((N + 1) * 8);
+        const unsigned g = unsigned(std::min<uint64_t>((N * 64 + kBlock - 1) / kBlock, 65536));
+        if (N) {
+            hipLaunchKernelGGL(k_rows_keep, dim3(g), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
+                               d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
+                               d_sup.as<uint32_t>(), rp.minsup, N, rc.as<uint32_t>(), (const uint64_t*)nullptr,
+                               (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
+            FSM_LAUNCHED("k_rows_keep", s);
+        }
+        scan_exclusive(rc.as<uint32_t>(), off64.as<uint64_t>(), N, s);
+        FSM_HIP(hipMemcpyAsync(&E2, off64.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        k_off.alloc((N + 1) * 4);
+        k_item.alloc(std::max<uint64_t>(E2, 1) * 4);
+        k_first.alloc(std::max<uint64_t>(E2, 1) * 4);
+        k_last.alloc(std::max<uint64_t>(E2, 1) * 4);
+        hipLaunchKernelGGL(k_off32, dim3(unsigned(std::min<uint64_t>((N + 256) / 256, 4096))), dim3(256), 0, s,
+                           off64.as<uint64_t>(), N, k_off.as<uint32_t>());
+        FSM_LAUNCHED("k_off32", s);
+        if (N) {
+            hipLaunchKernelGGL(k_rows_keep, dim3(g), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
+                               d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
+                               d_sup.as<uint32_t>(), rp.minsup, N, (uint32_t*)nullptr, off64.as<uint64_t>(),
+                               k_item.as<uint32_t>(), k_first.as<uint32_t>(), k_last.as<uint32_t>());
+            FSM_LAUNCHED("k_rows_keep", s);
+        }
+        FSM_HIP(hipStreamSynchronize(s));
+    }
     const double t1 = now_ms();
     if (ctx->opts.verbose)
         std::fprintf(stderr, "[fsm tsr] pair phase %.0f ms: minsup %u, candidates %zu, rules %zu\n", t1 - t0,
@@ -781,23 +936,27 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // heap with their results cached (results are minsup-independent supersets,
     // re-filtered against the current minsup at commit), so no expansion is
     // computed twice and the outcome equals the one-at-a-time replay.
-    const uint64_t SU = uint64_t(kExpBatch) * std::max<uint32_t>(U, 1);
-    DevBuf TL(SU * 4), DL(SU * 4), TR(SU * 4), seen(SU * 4), list(SU * 4), ctl(kExpBatch * sizeof(ExpCtl));
+    const uint32_t B = [] {  // rules per launch (FSM_TSR_BATCH overrides, for tuning)
+        const char* v = std::getenv("FSM_TSR_BATCH");
+        return v ? uint32_t(std::clamp<long>(std::strtol(v, nullptr, 10), 1, kMaxBatch)) : uint32_t(kExpBatch);
+    }();
+    const uint64_t SU = uint64_t(B) * std::max<uint32_t>(U, 1);
+    DevBuf TL(SU * 4), DL(SU * 4), TR(SU * 4), seen(SU * 4), list(SU * 4), ctl(B * sizeof(ExpCtl));
     FSM_HIP(hipMemsetAsync(TL.p, 0, SU * 4, s));
     FSM_HIP(hipMemsetAsync(DL.p, 0, SU * 4, s));
     FSM_HIP(hipMemsetAsync(TR.p, 0, SU * 4, s));
     FSM_HIP(hipMemsetAsync(seen.p, 0, SU * 4, s));
-    FSM_HIP(hipMemsetAsync(ctl.p, 0, kExpBatch * sizeof(ExpCtl), s));
+    FSM_HIP(hipMemsetAsync(ctl.p, 0, B * sizeof(ExpCtl), s));
     // per-launch rule descriptors: staged in pinned host memory, one H2D copy
-    constexpr size_t kSidesB = kExpBatch * sizeof(Side), kOffB = (kExpBatch + 1) * 8;
+    const size_t kSidesB = B * sizeof(Side), kOffB = (B + 1) * 8;
     PinnedBuf stage(kSidesB + 2 * kOffB);
     DevBuf d_stage(kSidesB + 2 * kOffB);
     Side* h_sides = static_cast<Side*>(stage.host);
     uint64_t* h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(stage.host) + kSidesB);
-    uint64_t* h_wave = h_drv + (kExpBatch + 1);
+    uint64_t* h_wave = h_drv + (B + 1);
     Side* d_sides = d_stage.as<Side>();
     uint64_t* d_drv = reinterpret_cast<uint64_t*>(d_stage.as<char>() + kSidesB);
-    uint64_t* d_wave = d_drv + (kExpBatch + 1);
+    uint64_t* d_wave = d_drv + (B + 1);
     const bool use_bm = d->bm.p != nullptr;
     DevBuf d_dlw, d_ndlw(16);
     if (use_bm) {
@@ -805,11 +964,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     }
     // expansion results land in mapped pinned host memory (at most one record per item per slot)
     const uint32_t ecap = std::max<uint32_t>(U, 1);
-    PinnedBuf pin(kExpBatch * sizeof(ExpHdr) + kExpBatch * size_t(ecap) * sizeof(ExpRec));
+    PinnedBuf pin(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
     ExpHdr* h_hdr = static_cast<ExpHdr*>(pin.host);
-    ExpRec* h_rec = reinterpret_cast<ExpRec*>(h_hdr + kExpBatch);
+    ExpRec* h_rec = reinterpret_cast<ExpRec*>(h_hdr + B);
     ExpHdr* d_hdr = static_cast<ExpHdr*>(pin.dev);
-    ExpRec* d_rec = reinterpret_cast<ExpRec*>(d_hdr + kExpBatch);
+    ExpRec* d_rec = reinterpret_cast<ExpRec*>(d_hdr + B);
     struct ExpResult {
         std::vector<ExpRec> recs;
         std::vector<Rule*> preL, preR;  // children created (and expanded) ahead of the commit, by record
@@ -823,6 +982,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     std::vector<uint64_t> drv_off, wave_off;
 
     const TsrGrid grid;
+    // per-kernel device time: every launch ends in a stream sync, so one set
+    // of events is recorded and read back per launch (ctx->kstats rows)
+    struct Seg {
+        double ms = 0;  // over the timed launches
+        int64_t n = 0, timed = 0, bytes = 0;
+    } seg[3];  // expansion, collect, k_dl / k_publish
+    const char* seg_name[3] = {use_bm ? "k_expand_bm" : "k_expand", "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
+    for (hipEvent_t& e : ctx->ev)
+        if (!e) FSM_HIP(hipEventCreate(&e));
+    int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0;
     auto launch = [&](const std::vector<Rule*>& batch) {
         const double tl0 = now_ms();
         const uint32_t nb = uint32_t(batch.size());
@@ -855,45 +1024,67 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         std::memcpy(h_wave, wave_off.data(), (nb + 1) * 8);
         FSM_HIP(hipMemcpyAsync(d_stage.p, stage.host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
         const uint64_t waves = use_bm ? 0 : wave_off[nb];
+        const bool timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
+        if (timed) FSM_HIP(hipEventRecord(ctx->ev[0], s));
         if (use_bm) {
             hipLaunchKernelGGL(k_expand_bm, dim3(grid.expand, nb), dim3(kBlock), 0, s, d_sides,
-                               d->bm.as<uint32_t>(), d->NW, d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
-                               d->first.as<uint32_t>(), d->last.as<uint32_t>(), U, TL.as<uint32_t>(),
+                               d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), k_item.as<uint32_t>(),
+                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, TL.as<uint32_t>(),
                                TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(), ctl.as<ExpCtl>(),
-                               d_ndlw.as<uint32_t>());
+                               d_ndlw.as<uint32_t>(), d_sup.as<uint32_t>(), rp.minsup);
             FSM_LAUNCHED("k_expand_bm", s);
         }
         if (waves) {
             hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                                d_sides, d_drv, d_wave, nb,
-                               d->vert_sid.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
-                               d->first.as<uint32_t>(), d->last.as<uint32_t>(), U, TL.as<uint32_t>(),
+                               d->vert_sid.as<uint32_t>(), k_off.as<uint32_t>(), k_item.as<uint32_t>(),
+                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, TL.as<uint32_t>(),
                                DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
-                               ctl.as<ExpCtl>());
+                               ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
             FSM_LAUNCHED("k_expand", s);
         }
+        if (timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
         hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, TL.as<uint32_t>(),
                            DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
                            ctl.as<ExpCtl>(), U, rp.minsup, d_rec, d_hdr, ecap,
                            use_bm ? d_dlw.as<uint4>() : nullptr, d_ndlw.as<uint32_t>());
         FSM_LAUNCHED("k_expand_collect", s);
+        if (timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
         if (use_bm) {
             hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, d_sides, d->bm.as<uint32_t>(),
-                               d->NW, d_dlw.as<uint4>(), d_ndlw.as<uint32_t>(), d_rec, ecap, ctl.as<ExpCtl>(), d_hdr,
-                               nb);
+                               d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), d_dlw.as<uint4>(),
+                               d_ndlw.as<uint32_t>(), d_rec, ecap, ctl.as<ExpCtl>(), d_hdr, nb);
             FSM_LAUNCHED("k_dl", s);
         } else {
             hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, ctl.as<ExpCtl>(), d_hdr, nb);
             FSM_LAUNCHED("k_publish", s);
         }
+        if (timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
         const double tw0 = now_ms();
         prep_ms += tw0 - tl0;
         FSM_HIP(hipStreamSynchronize(s));
         const double tw1 = now_ms();
         wait_ms += tw1 - tw0;
         ++launches;
+        for (int q = 0; q < 3; ++q) {
+            float ms = 0;
+            if (timed && hipEventElapsedTime(&ms, ctx->ev[q], ctx->ev[q + 1]) == hipSuccess) {
+                seg[q].ms += ms;
+                seg[q].timed += 1;
+            }
+            seg[q].n += 1;
+        }
+        uint64_t nout_all = 0;
         for (uint32_t k = 0; k < nb; ++k) {
             const ExpHdr h = h_hdr[k];
+            nout_all += h.nout;
+            if (use_bm) {  // algorithmic bytes: the |X|+|Y| bitmap operands + the domain's row entries
+                const uint64_t bmb = uint64_t(batch[k]->nx + batch[k]->ny) * d->NW * 4;
+                exp_domain += h.nsid;
+                exp_entries += h.nent;
+                exp_bitmap_bytes += int64_t(bmb);
+                seg[0].bytes += int64_t(bmb + 12ull * h.nent + 8ull * h.nsid);
+            }
             if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
             if (!use_bm && drv_in_x[k] && h.nx != batch[k]->nX)
                 throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(h.nx) + " vs " +
@@ -903,6 +1094,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             res.recs.assign(rec, rec + h.nout);
             std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
         }
+        seg[1].bytes += int64_t(nout_all * sizeof(ExpRec));
         post_ms += now_ms() - tw1;
     };
 
@@ -1010,9 +1202,9 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 }
             }
             spec_made += int64_t(next.size());
-            for (size_t a = 0; a < next.size(); a += size_t(kExpBatch)) {
+            for (size_t a = 0; a < next.size(); a += size_t(B)) {
                 const std::vector<Rule*> part(next.begin() + a,
-                                              next.begin() + std::min(next.size(), a + size_t(kExpBatch)));
+                                              next.begin() + std::min(next.size(), a + size_t(B)));
                 launch(part);
                 ++spec_launches;
             }
@@ -1048,7 +1240,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         // r (uncached) and the next heap rules are expanded together
         const double tp0 = now_ms();
         batch.clear();
-        while (batch.size() < size_t(kExpBatch) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
+        while (batch.size() < size_t(B) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
             Rule* x = rp.cand.top().r;
             rp.cand.pop();
             if (cache.count(x)) pending.insert(x);  // already expanded by speculation
@@ -1104,6 +1296,18 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         o->ante_off[q + 1] = o->ante_off[q] + int64_t(r->nx);
         o->cons_off[q + 1] = o->cons_off[q] + int64_t(r->ny);
     }
+    ctx->kstats.clear();
+    for (int q = 0; q < 3; ++q) {
+        fsm_kernel_stat k{};
+        std::snprintf(k.name, sizeof(k.name), "%s", seg_name[q]);
+        k.launches = seg[q].n;
+        k.ms = seg[q].timed ? seg[q].ms * double(seg[q].n) / double(seg[q].timed) : 0.0;  // sampled, scaled
+        k.alg_bytes = seg[q].bytes;
+        ctx->kstats.push_back(k);
+    }
+    ctx->stats.exp_domain = exp_domain;
+    ctx->stats.exp_entries = exp_entries;
+    ctx->stats.exp_bitmap_bytes = exp_bitmap_bytes;
     ctx->stats.expansions = expansions;
     ctx->stats.rules = int64_t(n);
     ctx->stats.ms_f2 = t1 - t0;          // pair phase

@@ -110,7 +110,8 @@ class Stats(ctypes.Structure):
         "ms_count_kernel", "ms_emit_kernel")] + [(n, ctypes.c_int64) for n in (
         "count_launches", "mask_words", "bytes_count_alg")] + [(n, ctypes.c_double) for n in (
         "ms_gpu_wait", "ms_output")] + [(n, ctypes.c_int64) for n in (
-        "joins_root", "root_keys", "pair_tests", "root_entries", "k0_device")]
+        "joins_root", "root_keys", "pair_tests", "root_entries", "k0_device", "exp_domain", "exp_entries",
+        "exp_bitmap_bytes")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -396,6 +396,25 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
     assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
 
 
+@pytest.mark.parametrize("batch", ["1", "7", "128"])
+def test_tsr_batch_sizes_agree(eng, batch, monkeypatch):
+    """Rules expanded per launch (FSM_TSR_BATCH) change only how much runs
+    ahead speculatively: the rules and final minsup stay the oracle's."""
+    from oracle import oracle
+    from tools import gen
+    from spark_fsm_amd import MODE_TSR
+    monkeypatch.setenv("FSM_TSR_BATCH", batch)
+    ds = gen.kosarak(D=5000, seed=6)
+    o = oracle.tsr(ds.records(), 150, 0.5)
+    db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)
+    try:
+        rules, meta = eng.tsr(db, 150, 0.5)
+    finally:
+        db.free()
+    rules.sort(key=lambda t: (-t[2], t[0], t[1]))
+    assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
+
+
 @pytest.mark.parametrize("spec", ["0", "3,128", "8,16"])
 @pytest.mark.parametrize("grid", ["128,8,512", "16,2,64"])
 def test_tsr_speculation_and_grids_agree(eng, spec, grid, monkeypatch):
