@@ -123,17 +123,19 @@ def main():
             torch.cuda.synchronize()
 
     ds = gen.quest(args.sequences, seed=args.seed)
-    if world > 1 and args.dist_backend == "nccl":
-        # sharded SPADE over RCCL: rank 0 makes the unique id, torch broadcasts it
+    if world > 1 and args.dist_backend == "nccl" and os.environ.get("FSM_BENCH_COMM") == "rccl":
+        # libfsm's own RCCL communicator: rank 0 makes the unique id, torch broadcasts it
         uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(fsm.comm_unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         eng = fsm.Engine(device=local_rank, nranks=world, rank=rank, unique_id=bytes(uid.cpu().tolist()))
     elif world > 1:
-        # host collectives over the torch group (gloo): several ranks may share one GPU
+        # libfsm's collectives over torch's process group: RCCL (staged through a
+        # device tensor) for nccl, CPU tensors for gloo (several ranks may share a GPU)
         from spark_fsm_amd.dist import TorchHostComm
-        hc = TorchHostComm(dist.group.WORLD)
+        dev = "cuda:%d" % local_rank if args.dist_backend == "nccl" else None
+        hc = TorchHostComm(dist.group.WORLD, device=dev)
         eng = fsm.Engine(device=local_rank % max(torch.cuda.device_count(), 1), nranks=world, rank=rank,
                          host_comm=hc)
     else:

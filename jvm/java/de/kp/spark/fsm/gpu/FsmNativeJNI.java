@@ -1,0 +1,19 @@
+package de.kp.spark.fsm.gpu;
+
+/**
+ * Static JNI declarations bound by jvm/native/fsm_jni.c
+ * (Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade / _tsr).  Declared in Java so
+ * the symbols are plain static methods (a Scala object's natives would bind as
+ * instance methods of FsmNative$).  Callers go through FsmNative.scala, which
+ * loads the library and turns load failures into java.lang.Exception.
+ */
+public final class FsmNativeJNI {
+    private FsmNativeJNI() {}
+
+    /** [support int[], patOff long[], setOff long[], items int[], {total, minsup} long[]] */
+    public static native Object[] spade(int[] sids, String[] lines, double support, int device);
+
+    /** [support int[], confidence double[], anteOff long[], ante int[], consOff long[], cons int[],
+     *  {total, finalMinsup} long[]] */
+    public static native Object[] tsr(int[] sids, String[] lines, int k, double minconf, int device);
+}

@@ -270,7 +270,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     F2Ent* stage_all = reinterpret_cast<F2Ent*>(smem);  // kF2Waves x 64 entries
     uint32_t* srow = smem + kF2Waves * 64 * (sizeof(F2Ent) / 4);  // row offsets of the block [rpb + 1]
-    uint32_t* cur = srow + kF2MaxRows + 1;                          // region cursors [G]
+    uint32_t* actx_all = srow + kF2MaxRows + 1;                     // kF2Waves x 64 active entry positions
+    uint32_t* cur = actx_all + kF2Waves * 64;                       // region cursors [G]
     __shared__ uint32_t blk_keys;
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
@@ -280,6 +281,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     __syncthreads();
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     F2Ent* stage = stage_all + wave * 64;
+    uint32_t* actx = actx_all + wave * 64;
     const uint64_t lt = lanemask_lt();
     uint32_t my_keys = 0;
     // the next row's entries are loaded while the current row is enumerated
@@ -303,15 +305,20 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
         if (rl == 0) continue;
         if (W == 1 && rl <= 64) {
             // ---- lane-per-pair: segments of S lanes, lane s0 + j tests partner j
+            // entries i are this rank's members only (sharded root: the other
+            // ranks count the rest); every entry of the row is a partner j
+            const bool act = lane < rl && me - mlo < mhi - mlo;
+            const uint64_t actb = __ballot(act);
+            const uint32_t nact = uint32_t(__popcll(actb));
             if (lane < rl) {
                 const uint32_t ri = me >> 1, g = group_of(ri, pm);
-                const bool act = me - mlo < mhi - mlo;
                 F2Ent en;
                 en.x = ri | ((lh & 0xFFFFu) << 16);
                 en.y = (act ? g : 0xFFFFu) | ((ri - g * per) * D << 16);
                 en.mask = mk;
                 stage[lane] = en;
             }
+            if (act) actx[__popcll(actb & lt)] = lane;
             __builtin_amdgcn_wave_barrier();
             const uint32_t lg = rl <= 1 ? 0u : 32u - uint32_t(__clz(rl - 1));  // S = 2^lg >= rl
             const uint32_t S = 1u << lg, k = 64u >> lg;
@@ -323,10 +330,11 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
             const F2Ent ej = stage[vj ? j : 0];
             const uint32_t hi_j = uint32_t(__shfl(int(lh), int(j), 64)) >> 16;
             const uint32_t rj = ej.x & 0xFFFFu;
-            for (uint32_t i0 = 0; i0 < rl; i0 += k) {
-                const uint32_t i = i0 + (lane >> lg);  // this segment's entry
-                const bool vi = i < rl;
-                const F2Ent ei = stage[vi ? i : 0];
+            for (uint32_t i0 = 0; i0 < nact; i0 += k) {
+                const uint32_t ia = i0 + (lane >> lg);  // this segment's active entry
+                const bool vi = ia < nact;
+                const uint32_t i = vi ? actx[ia] : 0u;
+                const F2Ent ei = stage[i];
                 const uint32_t gi = ei.y & 0xFFFFu;
                 const bool act_i = vi && gi != 0xFFFFu;
                 const uint32_t li = ei.x >> 16;
@@ -943,7 +951,7 @@ struct Miner {
         DevBuf keys((nslots + 1024) * 2), nk(8);
         FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
         tk = clk->begin("k_f2_keys");
-        const size_t kshm = size_t(kF2Waves) * 64 * sizeof(F2Ent) + (size_t(kF2MaxRows) + 1) * 4 + size_t(G) * 4;
+        const size_t kshm = size_t(kF2Waves) * 64 * (sizeof(F2Ent) + 4) + (size_t(kF2MaxRows) + 1) * 4 + size_t(G) * 4;
 #define FSM_F2K(WW)                                                                                                   \
     hipLaunchKernelGGL(k_f2_keys<WW>, dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(), R, rpb,      \
                        sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(),                   \

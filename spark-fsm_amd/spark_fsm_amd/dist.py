@@ -34,12 +34,19 @@ def shard_plan(volumes, nranks):
 
 
 class TorchHostComm:
-    """fsm_host_comm over a torch.distributed process group (CPU tensors)."""
+    """fsm_host_comm over a torch.distributed process group.
 
-    def __init__(self, group=None):
+    With a gloo group the host buffers are reduced in place as CPU tensors.
+    With an NCCL (= RCCL on ROCm) group they are staged through a tensor on
+    `device`, so libfsm's few small collectives (F1 histogram, frequent pairs,
+    failure flags, pattern CSRs) run over the same RCCL communicator torch
+    already set up for the job."""
+
+    def __init__(self, group=None, device=None):
         import torch.distributed as dist
         self._dist = dist
         self._group = group
+        self._device = device
         self._ar = _lib.ALLREDUCE_FN(self._allreduce)
         self._ag = _lib.ALLGATHER_FN(self._allgather)
         self.struct = _lib.HostComm(None, self._ar, self._ag)
@@ -52,7 +59,12 @@ class TorchHostComm:
             if n > 0:
                 a = np.ctypeslib.as_array(buf, shape=(n,)).view(np.int32)  # u32 sums mod 2^32 == i32 bits
                 t = torch.from_numpy(a)  # shares the C buffer: reduced in place
-                self._dist.all_reduce(t, group=self._group)
+                if self._device is not None:
+                    d = t.to(self._device)
+                    self._dist.all_reduce(d, group=self._group)
+                    t.copy_(d.cpu())
+                else:
+                    self._dist.all_reduce(t, group=self._group)
             return 0
         except Exception:  # noqa: BLE001 - must not unwind through C
             return 1
@@ -63,12 +75,13 @@ class TorchHostComm:
             if nbytes > 0:
                 s = torch.from_numpy(np.ctypeslib.as_array(ctypes.cast(send, ctypes.POINTER(ctypes.c_uint8)),
                                                            shape=(nbytes,)).copy())
-                out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
-                self._dist.all_gather(out, s, group=self._group)
+                dev = self._device if self._device is not None else "cpu"
+                s = s.to(dev)
+                out = torch.empty(nbytes * self.world, dtype=torch.uint8, device=dev)
+                self._dist.all_gather_into_tensor(out, s, group=self._group)
                 r = np.ctypeslib.as_array(ctypes.cast(recv, ctypes.POINTER(ctypes.c_uint8)),
                                           shape=(nbytes * self.world,))
-                for k, t in enumerate(out):
-                    r[k * nbytes:(k + 1) * nbytes] = t.numpy()
+                r[:] = out.cpu().numpy()
             return 0
         except Exception:  # noqa: BLE001
             return 1

@@ -5,6 +5,7 @@ tests/test_parity_gpu.py as a plain child process).
   mode selftest       : fsm_comm_selftest over a gloo TorchHostComm (no GPU)
   mode spade D sup    : sharded SPADE on cuda:0 over a gloo TorchHostComm
   mode spade_fail D sup : the same with a failure injected on one rank (FSM_INJECT_FAIL)
+  mode spade_digest shape D sup : sharded SPADE, digest of the result (full-size configs)
 Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (torch.distributed, gloo).
 """
 import json
@@ -12,7 +13,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (ROOT, os.path.join(ROOT, "spark-fsm_amd")):
+for p in (ROOT, os.path.join(ROOT, "spark-fsm_amd"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
@@ -39,6 +40,18 @@ def main():
             st = eng.stats()
             db.free()
         res.update(patterns=sorted(pats), minsup=meta["minsup"], joins=st["joins"], classes=st["classes"])
+    elif mode == "spade_digest":
+        # sharded SPADE at a BASELINE config: the digest of the gathered pattern set
+        from digest import pattern_digest
+        from tools import gen
+        shape, D, sup = sys.argv[3], int(sys.argv[4]), float(sys.argv[5])
+        ds = gen.quest(D, seed=1) if shape == "quest" else getattr(gen, shape)(seed=1)
+        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc) as eng:
+            db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+            csr, meta = eng.spade_csr(db, sup)
+            st = eng.stats()
+            db.free()
+        res.update(digest=pattern_digest(*csr), minsup=meta["minsup"], joins=st["joins"])
     elif mode == "spade_fail":
         # sharded SPADE with FSM_INJECT_FAIL set for one rank: every rank must fail, none may hang
         from tools import gen

@@ -102,3 +102,40 @@ def test_tsr_c4_fullsize_properties(eng):
         sup, nx = oracle.rule_support(ds.seq_off, ds.tokens, list(x), list(y))
         assert sup == s, (x, y)
         assert c == sup / nx and c >= mc, (x, y)
+
+
+@pytest.mark.parametrize("name,world", [("c3", 2), ("c5-bible", 3)])
+def test_spade_fullsize_sharded(name, world, tmp_path):
+    """The sharded path (F1 all-reduce, root counter rows by rank slice,
+    frequent pairs all-gathered, first-level classes by the LPT plan, patterns
+    all-gathered) at full BASELINE size, `world` ranks on this GPU over gloo
+    host collectives: every rank returns the complete pattern set."""
+    from test_dist import run_ranks
+    exp = FULL[name]
+    shape, D = SPADE_CFG[name]
+    res = run_ranks(world, ["spade_digest", shape, str(D or 0), str(exp["support"])], tmp_path, timeout=110)
+    for r in res:
+        assert r["digest"] == exp["digest"] and r["joins"] == exp["joins"] and r["minsup"] == exp["minsup"]
+
+
+def test_bench_two_ranks_dry_run(tmp_path):
+    """bench.py's N > 1 code path (torch.distributed.run, barrier + max over
+    ranks, sharded engine, one JSON line from rank 0), with two ranks sharing
+    this GPU over gloo; the driver runs the same path over RCCL on 8 GPUs."""
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--dist-backend", "gloo", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0
+    assert d["extra"]["patterns"] == FULL["c3"]["digest"]["n"] and d["extra"]["joins"] == FULL["c3"]["joins"]

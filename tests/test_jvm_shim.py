@@ -1,0 +1,108 @@
+"""The JVM drop-in: jvm/native/fsm_jni.c is compiled here
+against tests/jni/jni.h (the JNI subset it uses; the image has no JDK) and
+driven through tests/jni/jni_harness.c, an in-process JNIEnv that renders the
+results exactly as the Scala bodies (jvm/scala/.../GpuSPADE.scala, GpuTSR.scala)
+map them: GpuPattern.serialize() lines, GpuRule lines.
+
+CPU: the shim builds, exports the two JNI symbols FsmNativeJNI.java binds, and
+turns a failure (no GPU here) into a java.lang.Exception, never a crash or an
+Error (TrainActor.scala:66 only catches Exception).
+GPU: the shim's results equal the engine's through the Python mirror
+(spark_fsm_amd.extract_rdd_patterns / extract_rdd_rules) on the golden records.
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "spark-fsm_amd", "spark_fsm_amd")
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("jni") / "libjniharness.so")
+    subprocess.run(["gcc", "-O1", "-fPIC", "-shared", "-Wall", "-Wextra", "-Werror",
+                    "-I" + os.path.join(ROOT, "tests", "jni"), "-I" + os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "jvm", "native", "fsm_jni.c"), os.path.join(ROOT, "tests", "jni", "jni_harness.c"),
+                    "-L" + LIBDIR, "-lfsm", "-Wl,-rpath," + LIBDIR, "-o", out], check=True)
+    import spark_fsm_amd  # noqa: F401  (torch first: one HIP runtime per process)
+    L = ctypes.CDLL(out)
+    for name in ("harness_spade", "harness_tsr"):
+        getattr(L, name).restype = ctypes.c_void_p
+    L.harness_spade.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
+                                ctypes.c_double, ctypes.c_int]
+    L.harness_tsr.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
+                              ctypes.c_int, ctypes.c_double, ctypes.c_int]
+    L.harness_free.argtypes = [ctypes.c_void_p]
+    L.path = out
+    return L
+
+
+def call(L, fn, records, *args):
+    n = len(records)
+    sids = (ctypes.c_int * max(n, 1))(*[s for s, _ in records])
+    lines = (ctypes.c_char_p * max(n, 1))(*[l.encode() for _, l in records])
+    p = getattr(L, fn)(n, sids, lines, *args)
+    try:
+        return ctypes.string_at(p).decode()
+    finally:
+        L.harness_free(p)
+
+
+def gpu_present():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except ImportError:
+        return False
+
+
+def test_shim_exports_the_bound_symbols(harness):
+    out = subprocess.run(["nm", "-D", "--defined-only", harness.path], capture_output=True, text=True).stdout
+    assert "Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade" in out
+    assert "Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr" in out
+    java = open(os.path.join(ROOT, "jvm", "java", "de", "kp", "spark", "fsm", "gpu", "FsmNativeJNI.java")).read()
+    assert "static native Object[] spade(" in java and "static native Object[] tsr(" in java
+
+
+@pytest.mark.skipif(gpu_present(), reason="the no-device failure path needs a machine without a GPU")
+def test_shim_turns_failures_into_exceptions(harness):
+    s = call(harness, "harness_spade", [(0, "1 -1 2 -1")], 0.5, 0)
+    assert s.startswith("EXCEPTION java/lang/Exception: libfsm fsm_ctx_create failed (FSM error 3)")
+    t = call(harness, "harness_tsr", [(0, "1 -1 2 -1")], 3, 0.5, 0)
+    assert t.startswith("EXCEPTION java/lang/Exception: libfsm fsm_ctx_create failed")
+
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.mark.gpu
+def test_shim_spade_matches_engine(harness):
+    import spark_fsm_amd as fsm
+    cases = json.load(open(os.path.join(GOLD, "spade_cases.json")))[:12]
+    for case in cases:
+        recs = [tuple(r) for r in case["records"]]
+        got = call(harness, "harness_spade", recs, case["support"], 0)
+        exp = "".join(p.serialize() + "\n" for p in fsm.extract_rdd_patterns(recs, case["support"], stats=False))
+        assert sorted(got.splitlines()) == sorted(exp.splitlines()), case["name"]
+    err = json.load(open(os.path.join(GOLD, "error_cases.json")))["spade"][0]
+    assert call(harness, "harness_spade", [tuple(r) for r in err["records"]], 0.5, 0).startswith(
+        "EXCEPTION java/lang/Exception: libfsm fsm_db_from_spmf failed (FSM error 2)")
+
+
+@pytest.mark.gpu
+def test_shim_tsr_matches_engine(harness):
+    import spark_fsm_amd as fsm
+    cases = json.load(open(os.path.join(GOLD, "tsr_cases.json")))[:12]
+    for case in cases:
+        recs = [tuple(r) for r in case["records"]]
+        got = call(harness, "harness_tsr", recs, case["k"], case["minconf"], 0)
+        exp = "".join("%s ==> %s #SUP: %d #CONF: %s\n" % (",".join(map(str, r.getItemset1())),
+                                                           ",".join(map(str, r.getItemset2())),
+                                                           r.getAbsoluteSupport(), repr(r.getConfidence()))
+                      for r in fsm.extract_rdd_rules(recs, case["k"], case["minconf"]))
+        norm = lambda s: sorted((l.rsplit(" ", 1)[0], float(l.rsplit(" ", 1)[1])) for l in s.splitlines())
+        assert norm(got) == norm(exp), case["name"]
