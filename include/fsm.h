@@ -202,11 +202,56 @@ typedef struct {
 int fsm_db_export(fsm_ctx* ctx, const fsm_db* db, fsm_db_image** out);
 void fsm_db_image_free(fsm_db_image* img);
 
+/* Native input conversion (util/SPMFBuilder.scala:27-198): a whole input file
+ * image in one of the builder's formats -> the token arrays of
+ * fsm_db_from_tokens (sid, seq_off, tokens; every item its own itemset as the
+ * builder writes it, -1 / -2 separators), numbered 0, 1, 2 ... in file order
+ * like SPMFBuilder.index, keeping the first `limit` sequences (take(limit):
+ * 0 keeps none; < 0 keeps all, an extension).
+ * FSM_FMT_INDEXED reads the builder's own "idx|sequence" output.  Malformed
+ * input returns FSM_EPARSE (message in fsm_last_error(NULL)). */
+#define FSM_FMT_SPMF 0
+#define FSM_FMT_INDEXED 1
+#define FSM_FMT_BMS 2
+#define FSM_FMT_CSV 3
+#define FSM_FMT_KOSARAK 4
+#define FSM_FMT_SNAKE 5
+typedef struct {
+    int64_t n;                  /* sequences */
+    int32_t* sids;              /* [n] */
+    int64_t* seq_off;           /* [n+1] */
+    int64_t* tokens;            /* [n_tokens] */
+    int64_t n_tokens;
+} fsm_token_db;
+int fsm_ingest(int32_t format, const char* data, int64_t len, int64_t limit, fsm_token_db** out);
+void fsm_token_db_free(fsm_token_db* t);
+
 int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_patterns** out);
 void fsm_patterns_free(fsm_patterns* p);
 
 int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** out);
 void fsm_rules_free(fsm_rules* r);
+
+/* Result persistence (SPADEActor.scala:47-68, TSRActor.scala:52-71): the
+ * mined CSR rendered in bulk as the documents the actors hand to their sinks.
+ *   fsm_patterns_serialize: one SPMF serialize() line per pattern,
+ *     "i j -1 k -1 | support\n" (SPADE.scala:111-122 / GpuPattern.serialize)
+ *   fsm_patterns_json: json4s write(Patterns(List[Pattern(support, itemsets)]))
+ *   fsm_rules_json: json4s write(Rules(List[Rule(antecedent, consequent,
+ *     support, total, confidence)])), confidence as java.lang.Double.toString
+ * *out is NUL-terminated, *len excludes the NUL; free with fsm_buffer_free.
+ * Errors: fsm_last_error(NULL). */
+int fsm_patterns_serialize(const fsm_patterns* p, char** out, int64_t* len);
+int fsm_patterns_json(const fsm_patterns* p, char** out, int64_t* len);
+int fsm_rules_json(const fsm_rules* r, char** out, int64_t* len);
+void fsm_buffer_free(char* p);
+
+/* Rule queries (FSMQuestor.scala:46-98, get:antecedent / get:consequent):
+ * side 0 = antecedent, 1 = consequent; writes the indexes (ascending) of the
+ * rules whose side's items all occur in items[0..n) to out_idx (capacity
+ * r->n) and their count to *n_out. */
+int fsm_rules_query(const fsm_rules* r, int32_t side, const int32_t* items, int64_t n, int64_t* out_idx,
+                    int64_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -94,6 +94,8 @@ int make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out) {
 
 }  // namespace
 
+void fsm::set_thread_error(const std::string& msg) { g_err = msg; }
+
 extern "C" {
 
 int fsm_abi_version(void) { return FSM_ABI_VERSION; }

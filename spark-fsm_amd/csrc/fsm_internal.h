@@ -195,6 +195,9 @@ struct Source {
     int64_t n = 0;
 };
 
+// the message fsm_last_error(NULL) returns (context-free entry points)
+void set_thread_error(const std::string& msg);
+
 void flatten_spade(const Source& src, FlatSpade& out);
 void flatten_tsr(const Source& src, FlatTsr& out);
 

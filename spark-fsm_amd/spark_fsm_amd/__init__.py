@@ -9,3 +9,5 @@ from .engine import Engine, DB, default_engine  # noqa: F401
 from .dist import comm_unique_id, shard_plan, TorchHostComm  # noqa: F401
 from .api import (Pattern, Rule, extract_rdd_patterns, extract_rdd_rules,  # noqa: F401
                   spade_actor_patterns, tsr_actor_rules)
+from .builder import TokenDB, ingest, build as spmf_build  # noqa: F401
+from .results import PatternSet, RuleSet  # noqa: F401

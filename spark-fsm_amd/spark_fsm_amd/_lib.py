@@ -97,6 +97,19 @@ class DbImage(ctypes.Structure):
     ]
 
 
+class TokenDb(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64),
+        ("sids", ctypes.POINTER(ctypes.c_int32)),
+        ("seq_off", ctypes.POINTER(ctypes.c_int64)),
+        ("tokens", ctypes.POINTER(ctypes.c_int64)),
+        ("n_tokens", ctypes.c_int64),
+    ]
+
+
+FMT_SPMF, FMT_INDEXED, FMT_BMS, FMT_CSV, FMT_KOSARAK, FMT_SNAKE = range(6)
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 40), ("launches", ctypes.c_int64), ("alg_bytes", ctypes.c_int64),
                 ("ms", ctypes.c_double)]
@@ -122,7 +135,8 @@ EXPORTS = [
     "fsm_abi_version", "fsm_comm_unique_id", "fsm_shard_plan", "fsm_comm_selftest", "fsm_ctx_create", "fsm_ctx_destroy",
     "fsm_last_error", "fsm_get_stats", "fsm_get_kernel_stats", "fsm_db_from_spmf", "fsm_db_from_tokens",
     "fsm_db_free", "fsm_spade_mine", "fsm_patterns_free", "fsm_tsr_mine", "fsm_rules_free",
-    "fsm_db_export", "fsm_db_image_free",
+    "fsm_db_export", "fsm_db_image_free", "fsm_ingest", "fsm_token_db_free", "fsm_patterns_serialize",
+    "fsm_patterns_json", "fsm_rules_json", "fsm_buffer_free", "fsm_rules_query",
 ]
 
 _lib = None
@@ -167,6 +181,15 @@ def load():
     L.fsm_tsr_mine.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_double, P(P(Rules))]
     L.fsm_rules_free.argtypes = [P(Rules)]
     L.fsm_rules_free.restype = None
+    L.fsm_ingest.argtypes = [ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, P(P(TokenDb))]
+    L.fsm_token_db_free.argtypes = [P(TokenDb)]
+    L.fsm_token_db_free.restype = None
+    for fn, st in (("fsm_patterns_serialize", Patterns), ("fsm_patterns_json", Patterns), ("fsm_rules_json", Rules)):
+        getattr(L, fn).argtypes = [P(st), P(vp), P(ctypes.c_int64)]
+    L.fsm_buffer_free.argtypes = [vp]
+    L.fsm_buffer_free.restype = None
+    L.fsm_rules_query.argtypes = [P(Rules), ctypes.c_int32, P(ctypes.c_int32), ctypes.c_int64, P(ctypes.c_int64),
+                                  P(ctypes.c_int64)]
     _lib = L
     return L
 

@@ -176,6 +176,39 @@ def test_long_sequences_multiword_masks(eng):
             assert st["mask_words"] >= 2 and len(pats) > 5
 
 
+@pytest.mark.parametrize("nsets,W", [(1000, 16), (4000, 64)])
+def test_very_long_sequences_wide_masks(eng, nsets, W):
+    """~1,000 and ~4,000 distinct timestamps per sequence: W = 16 and W = 64
+    mask words (the widest the engine instantiates; more than 4,096 distinct
+    timestamps in one sequence is FSM_ELIMIT).  Planted patterns
+    across the whole eid range, unique noise items elsewhere; the text path
+    (host flatten) and the token path (K0 on the device) against the oracle."""
+    import numpy as np
+    from oracle import oracle
+    rng = random.Random(nsets)
+    sets_all = []
+    for s in range(12):
+        sets = [[100000 + s * 10000 + k] for k in range(nsets)]
+        pos = sorted(rng.sample(range(nsets), 6))
+        for p, it in zip(pos, (1, 2, 3, 1, 4, 2)):
+            sets[p] = [it] + ([5] if rng.random() < 0.5 else [])
+        sets_all.append(sets)
+    recs = [(s, " ".join(" ".join(map(str, t)) + " -1" for t in sets) + " -2") for s, sets in enumerate(sets_all)]
+    toks = [[x for t in sets for x in t + [-1]] + [-2] for sets in sets_all]
+
+    class Tok:
+        seq_off = np.concatenate([[0], np.cumsum([len(t) for t in toks])]).astype(np.int64)
+        tokens = np.array([x for t in toks for x in t], dtype=np.int64)
+        sids = np.arange(len(toks), dtype=np.int32)
+
+    for sup in (0.5, 0.75):
+        o = oracle.spade(recs, sup)
+        pats, _, st = gpu_spade(eng, recs, sup)
+        assert pats == o["patterns"] and st["joins"] == o["joins"] and st["mask_words"] == W
+        pats2, _, st2 = gpu_spade(eng, None, sup, tokens=Tok)
+        assert pats2 == o["patterns"] and st2["mask_words"] == W and len(pats) > 5
+
+
 def test_small_memory_budget_splits_groups(fsm):
     """Force the frontier into many small class groups: same answer."""
     from oracle import oracle
@@ -435,3 +468,36 @@ def test_tsr_speculation_and_grids_agree(eng, spec, grid, monkeypatch):
         db.free()
     rules.sort(key=lambda t: (-t[2], t[0], t[1]))
     assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
+
+
+def test_ingested_files_mine_like_their_lines(eng):
+    """§8f rows 2-4 end to end: a KOSARAK file converted by fsm_ingest goes
+    straight to fsm_db_from_tokens (K0) and mines to the oracle's patterns /
+    rules on the builder's "idx|seq" lines; the persisted documents of the
+    engine's results equal the restatement's renderings of the oracle's."""
+    import random
+    from oracle import oracle, spmf_builder as ref
+    from spark_fsm_amd import MODE_SPADE, MODE_TSR, PatternSet, RuleSet, ingest
+    rng = random.Random(12)
+    text = "".join(" ".join(str(rng.randint(1, 40)) for _ in range(rng.randint(1, 12))) + "\n" for _ in range(3000))
+    t = ingest(text.encode(), "KOSARAK")
+    recs = [(int(l.split("|")[0]), l.split("|", 1)[1]) for l in ref.build(text, "KOSARAK", 10 ** 9)]
+    db = eng.db_from_tokens(t.sids, t.seq_off, t.tokens, MODE_SPADE)
+    try:
+        csr, meta = eng.spade_csr(db, 0.02)
+    finally:
+        db.free()
+    o = oracle.spade(recs, 0.02)
+    ps = PatternSet.from_csr(csr, meta)
+    got = sorted(ps.serialize().splitlines())
+    exp = sorted(ref.patterns_serialize([(s, [list(x) for x in sets]) for sets, s in o["patterns"]]).splitlines())
+    assert got == exp and meta["minsup"] == o["minsup"]
+    db = eng.db_from_tokens(t.sids, t.seq_off, t.tokens, MODE_TSR)
+    try:
+        rules, rmeta = eng.tsr(db, 60, 0.3)
+    finally:
+        db.free()
+    rules.sort(key=lambda r: (-r[2], r[0], r[1]))
+    ot = oracle.tsr(recs, 60, 0.3)
+    assert rules == ot["rules"]
+    assert RuleSet(rules, rmeta["total"]).to_json() == ref.rules_json(ot["rules"], ot["total"])
