@@ -551,6 +551,128 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
 // are heavily skewed (popular members have dozens of frequent children), so a
 // thread-per-entry loop would leave most lanes idle behind the longest list.
 
+// one lane's parent entry for the flattened (entry, kid) pair loop
+struct EmitEnt {
+    uint32_t k0, nk, cc, rb, re, lt;  // kids [k0, k0 + nk), child class, run [rb, re), lo | type << 16
+};
+
+__device__ __forceinline__ EmitEnt emit_ent(uint64_t e64, uint32_t E, const uint32_t* __restrict__ cid,
+                                            const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                            const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                            const uint32_t* __restrict__ kid_off,
+                                            const uint32_t* __restrict__ child_of) {
+    EmitEnt t{0, 0, kNone, 0, 0, 0};
+    if (e64 < E) {
+        const uint32_t e = uint32_t(e64);
+        const DClass c = cls[cid[e]];
+        const uint32_t mi = mem[e];
+        t.cc = child_of[c.cbase + mi];
+        if (t.cc != kNone) {
+            t.k0 = kid_off[c.cbase + mi];
+            t.nk = kid_off[c.cbase + mi + 1] - t.k0;
+            const uint32_t p = pos[e];
+            t.rb = e - (p >> 16);
+            t.re = t.rb + (p & 0xFFFFu);
+            t.lt = (lohi[e] & 0xFFFFu) | ((mi & 1u) << 16);
+        }
+    }
+    return t;
+}
+
+// The pair loop of one wave over its 64 entries (entry w0 + lane): every
+// (entry, kid) pair binary-searches its partner in the member-sorted run and
+// tests the join.  on_ok(ok, owner lane, owner entry, owner lo|type, kid q,
+// partner f, kid slot, k) runs on EVERY lane each step (it may shuffle); k is
+// the rank of a non-empty join within the owner's child run.  Returns the
+// lane's own non-empty join count (its child run length).
+template <int W, class OnOk>
+__device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, const uint32_t* __restrict__ mem,
+                                               const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask,
+                                               const uint32_t* __restrict__ kid_slot, OnOk&& on_ok) {
+    const uint32_t lane = lane_id();
+    const uint32_t incl = wave_incl_scan(t.nk), excl = incl - t.nk;
+    const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
+    uint32_t done = 0;  // this lane's (as owner) non-empty joins so far
+    for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+        const uint32_t pp = p0 + lane;
+        // owner: the largest lane whose first pair index <= pp
+        uint32_t ow = 0;
+#pragma unroll
+        for (uint32_t step = 32; step > 0; step >>= 1) {
+            const uint32_t cand = ow + step;
+            if (uint32_t(__shfl(int(excl), int(cand), 64)) <= pp) ow = cand;
+        }
+        const uint32_t o_k0 = uint32_t(__shfl(int(t.k0), int(ow), 64));
+        const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
+        const uint32_t o_rb = uint32_t(__shfl(int(t.rb), int(ow), 64));
+        const uint32_t o_re = uint32_t(__shfl(int(t.re), int(ow), 64));
+        const uint32_t o_lt = uint32_t(__shfl(int(t.lt), int(ow), 64));
+        const uint32_t o_done = uint32_t(__shfl(int(done), int(ow), 64));
+        const uint64_t o_e = w0 + ow;
+        bool ok = false;
+        uint32_t q = 0, f = 0, slot = 0;
+        if (pp < total) {
+            q = o_k0 + (pp - o_ex);
+            slot = kid_slot[q];
+            const uint32_t ct = slot & 1u;
+            const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : (o_lt >> 16));  // partner member id
+            uint32_t lo = o_rb, hi = o_re;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (mem[mid] < target) lo = mid + 1; else hi = mid;
+            }
+            f = lo;
+            if (f < o_re && mem[f] == target) {
+                if (ct == kSeq) {
+                    ok = (lohi[f] >> 16) > (o_lt & 0xFFFFu);
+                } else {
+                    uint64_t mk[W];
+                    load_mask<W>(mask + size_t(o_e) * W, mk);
+                    ok = and_nonzero<W>(mk, mask + size_t(f) * W);
+                }
+            }
+        }
+        const uint64_t succ = __ballot(ok);
+        const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
+        const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
+        on_ok(ok, ow, o_e, o_lt, q, f, slot, k);
+        // each lane, as owner, adds its joins of this step
+        const uint32_t a = (excl > p0 ? excl : p0), bnd = (incl < p0 + 64 ? incl : p0 + 64);
+        if (bnd > a) done += uint32_t(__popcll(succ & lane_range(a - p0, bnd - p0)));
+    }
+    return done;
+}
+
+// one child entry: the join of parent entry o_e with partner f at slab slot d
+template <int W>
+__device__ __forceinline__ void emit_write(const SlabPtrs& o, uint64_t cap, uint64_t d, uint32_t cc, uint32_t kidc, uint32_t k,
+                                           uint32_t n, uint64_t o_e, uint32_t o_lt, uint32_t f, uint32_t slot,
+                                           const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask) {
+    if (d >= cap) return;  // a count mismatch: the host reports it, nothing lands past the slab
+    uint64_t m[W];
+    load_mask<W>(mask + size_t(f) * W, m);
+    uint32_t lo2, hi2;
+    if ((slot & 1u) == kSeq) {
+        hi2 = lohi[f] >> 16;
+        mask_clear_upto<W>(m, o_lt & 0xFFFFu);
+        lo2 = mask_lo<W>(m);
+    } else {
+        uint64_t mk[W];
+        load_mask<W>(mask + size_t(o_e) * W, mk);
+#pragma unroll
+        for (int x = 0; x < W; ++x) m[x] &= mk[x];
+        lo2 = mask_lo<W>(m);
+        hi2 = mask_hi<W>(m);
+    }
+    o.cid[d] = cc;
+    o.mem[d] = kidc;
+    o.lohi[d] = lo2 | (hi2 << 16);
+    o.pos[d] = (k << 16) | n;
+    store_mask<W>(o.mask + d * W, m);
+}
+
+// Two-pass emission (FSM_EMIT_PATH=twopass): count pass -> exclusive scan of
+// the run lengths -> write pass that joins again; runs in parent-entry order.
 template <int W, bool kWrite>
 __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __restrict__ cid,
                                                  const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
@@ -560,114 +682,144 @@ __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __r
                                                  const uint32_t* __restrict__ kid_slot,
                                                  const uint32_t* __restrict__ kid_cid,
                                                  const uint32_t* __restrict__ child_of, uint32_t* __restrict__ ncnt,
-                                                 const uint64_t* __restrict__ off, SlabPtrs o) {
+                                                 const uint64_t* __restrict__ off, SlabPtrs o, uint64_t cap) {
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wstride = uint64_t(gridDim.x) * wpb * 64;  // 64-bit: no wrap for E near 2^32
     for (uint64_t w0 = (uint64_t(blockIdx.x) * wpb + (threadIdx.x >> 6)) * 64; w0 < E; w0 += wstride) {
-        const uint32_t e = uint32_t(w0) + lane;
-        // this lane's entry: its frequent children kid_slot[k0 .. k0 + nk)
-        uint32_t k0 = 0, nk = 0, cc = kNone, rb = 0, re = 0, lt = 0, n_run = 0;
+        EmitEnt t = emit_ent(w0 + lane, E, cid, cls, mem, lohi, pos, kid_off, child_of);
         uint64_t base = 0;
-        if (w0 + lane < E) {
-            const DClass c = cls[cid[e]];
-            const uint32_t mi = mem[e];
-            cc = child_of[c.cbase + mi];
-            if (cc != kNone) {
-                k0 = kid_off[c.cbase + mi];
-                nk = kid_off[c.cbase + mi + 1] - k0;
-                const uint32_t p = pos[e];
-                rb = e - (p >> 16);
-                re = rb + (p & 0xFFFFu);
-                lt = (lohi[e] & 0xFFFFu) | ((mi & 1u) << 16);  // lo | type << 16
-            }
-            if constexpr (kWrite) {
-                base = off[e];
-                n_run = uint32_t(off[e + 1] - base);
-                if (n_run == 0) nk = 0;
+        uint32_t n_run = 0;
+        if constexpr (kWrite) {
+            if (w0 + lane < E) {
+                base = off[w0 + lane];
+                n_run = uint32_t(off[w0 + lane + 1] - base);
+                if (n_run == 0) t.nk = 0;
             }
         }
-        const uint32_t incl = wave_incl_scan(nk), excl = incl - nk;
-        const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
-        uint32_t done = 0;  // this lane's (as owner) non-empty joins so far
-        for (uint32_t p0 = 0; p0 < total; p0 += 64) {
-            const uint32_t pp = p0 + lane;
-            // owner: the largest lane whose first pair index <= pp
-            uint32_t ow = 0;
-#pragma unroll
-            for (uint32_t step = 32; step > 0; step >>= 1) {
-                const uint32_t cand = ow + step;
-                if (uint32_t(__shfl(int(excl), int(cand), 64)) <= pp) ow = cand;
-            }
-            const uint32_t o_k0 = uint32_t(__shfl(int(k0), int(ow), 64));
-            const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
-            const uint32_t o_rb = uint32_t(__shfl(int(rb), int(ow), 64));
-            const uint32_t o_re = uint32_t(__shfl(int(re), int(ow), 64));
-            const uint32_t o_lt = uint32_t(__shfl(int(lt), int(ow), 64));
-            const uint32_t o_done = uint32_t(__shfl(int(done), int(ow), 64));
-            const uint32_t o_e = uint32_t(w0 + ow);
-            bool ok = false;
-            uint32_t q = 0, f = 0, slot = 0;
-            if (pp < total) {
-                q = o_k0 + (pp - o_ex);
-                slot = kid_slot[q];
-                const uint32_t ct = slot & 1u;
-                const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : (o_lt >> 16));  // partner member id
-                uint32_t lo = o_rb, hi = o_re;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (mem[mid] < target) lo = mid + 1; else hi = mid;
+        const uint32_t done = emit_pairs<W>(
+            t, w0, mem, lohi, mask, kid_slot,
+            [&](bool ok, uint32_t ow, uint64_t o_e, uint32_t o_lt, uint32_t q, uint32_t f, uint32_t slot, uint32_t k) {
+                if constexpr (kWrite) {
+                    // shuffles stay outside the branch: a source lane must be active
+                    const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
+                    const uint64_t o_base = __shfl(base, int(ow), 64);
+                    const uint32_t o_cc = uint32_t(__shfl(int(t.cc), int(ow), 64));
+                    if (ok) emit_write<W>(o, cap, o_base + k, o_cc, kid_cid[q], k, o_n, o_e, o_lt, f, slot, lohi, mask);
                 }
-                f = lo;
-                if (f < o_re && mem[f] == target) {
-                    if (ct == kSeq) {
-                        ok = (lohi[f] >> 16) > (o_lt & 0xFFFFu);
-                    } else {
-                        uint64_t mk[W];
-                        load_mask<W>(mask + size_t(o_e) * W, mk);
-                        ok = and_nonzero<W>(mk, mask + size_t(f) * W);
-                    }
-                }
-            }
-            const uint64_t succ = __ballot(ok);
-            if constexpr (kWrite) {
-                // shuffles stay outside the branch: a source lane must be active
-                const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
-                const uint64_t o_base = __shfl(base, int(ow), 64);
-                const uint32_t o_cc = uint32_t(__shfl(int(cc), int(ow), 64));
-                if (ok) {
-                    const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
-                    const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
-                    uint64_t m[W];
-                    load_mask<W>(mask + size_t(f) * W, m);
-                    uint32_t lo2, hi2;
-                    if ((slot & 1u) == kSeq) {
-                        hi2 = lohi[f] >> 16;
-                        mask_clear_upto<W>(m, o_lt & 0xFFFFu);
-                        lo2 = mask_lo<W>(m);
-                    } else {
-                        uint64_t mk[W];
-                        load_mask<W>(mask + size_t(o_e) * W, mk);
-#pragma unroll
-                        for (int x = 0; x < W; ++x) m[x] &= mk[x];
-                        lo2 = mask_lo<W>(m);
-                        hi2 = mask_hi<W>(m);
-                    }
-                    const uint64_t d = o_base + k;
-                    o.cid[d] = o_cc;
-                    o.mem[d] = kid_cid[q];
-                    o.lohi[d] = lo2 | (hi2 << 16);
-                    o.pos[d] = (k << 16) | o_n;
-                    store_mask<W>(o.mask + d * W, m);
-                }
-            }
-            // each lane, as owner, adds its joins of this step
-            const uint32_t a = (excl > p0 ? excl : p0), bnd = (incl < p0 + 64 ? incl : p0 + 64);
-            if (bnd > a) done += uint32_t(__popcll(succ & lane_range(a - p0, bnd - p0)));
-        }
+            });
         if constexpr (!kWrite) {
-            if (w0 + lane < E) ncnt[e] = done;
+            if (w0 + lane < E) ncnt[w0 + lane] = done;
         }
+    }
+}
+
+// One-pass emission (default).  A block takes a chunk of kEmitRounds x 256
+// parent entries; each wave joins its entries once, keeping every non-empty
+// join (partner, kid, owner, rank in run) in LDS, then the block reserves its
+// child entries with ONE atomic on the slab cursor and writes the runs from
+// LDS.  Child runs stay contiguous and member-sorted; only their order in the
+// slab follows the chunks' reservation order, which nothing downstream reads
+// (k_count and k_emit address runs through pos).  A wave whose joins overflow
+// its rcap (<= kEmitCap) LDS records joins again in the write phase.
+#ifndef FSM_EMIT_ROUNDS
+#define FSM_EMIT_ROUNDS 2
+#endif
+#ifndef FSM_EMIT_BLOCK
+#define FSM_EMIT_BLOCK 256
+#endif
+constexpr int kEmitBlock = FSM_EMIT_BLOCK;  // threads of a k_emit1 block (one slab reservation per chunk)
+#ifndef FSM_EMIT_RECORDS
+#define FSM_EMIT_RECORDS 256
+#endif
+constexpr int kEmitRounds = FSM_EMIT_ROUNDS;      // 64-entry rounds per wave per chunk
+constexpr uint32_t kEmitCap = FSM_EMIT_RECORDS;  // LDS join records per wave
+
+template <int W>
+__global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t* __restrict__ cid,
+                                                  const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                  const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                                  const uint64_t* __restrict__ mask,
+                                                  const uint32_t* __restrict__ kid_off,
+                                                  const uint32_t* __restrict__ kid_slot,
+                                                  const uint32_t* __restrict__ kid_cid,
+                                                  const uint32_t* __restrict__ child_of,
+                                                  unsigned long long* __restrict__ cursor, SlabPtrs o,
+                                                  uint64_t cap, uint32_t rcap) {
+    constexpr uint32_t kWaves = kEmitBlock / 64;
+    constexpr uint32_t kPer = 64 * kEmitRounds;  // entries of one wave per chunk
+    __shared__ uint32_t r_f[kWaves][kEmitCap], r_q[kWaves][kEmitCap], r_ek[kWaves][kEmitCap];
+    __shared__ uint32_t i_n[kWaves][kPer], i_off[kWaves][kPer], i_cc[kWaves][kPer], i_lt[kWaves][kPer];
+    __shared__ uint32_t w_tot[kWaves];
+    __shared__ unsigned long long b_base;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
+    for (uint64_t c0 = uint64_t(blockIdx.x) * chunk; c0 < E; c0 += uint64_t(gridDim.x) * chunk) {
+        uint32_t nrec = 0, wsum = 0;
+        for (int r = 0; r < kEmitRounds; ++r) {
+            const uint64_t w0 = c0 + uint64_t(r) * kEmitBlock + uint64_t(w) * 64;
+            const EmitEnt t = emit_ent(w0 + lane, E, cid, cls, mem, lohi, pos, kid_off, child_of);
+            const uint32_t done = emit_pairs<W>(
+                t, w0, mem, lohi, mask, kid_slot,
+                [&](bool ok, uint32_t ow, uint64_t, uint32_t, uint32_t q, uint32_t f, uint32_t, uint32_t k) {
+                    const uint64_t b = __ballot(ok);
+                    if (ok) {
+                        const uint32_t x = nrec + uint32_t(__popcll(b & lanemask_lt()));
+                        if (x < rcap) {
+                            r_f[w][x] = f;
+                            r_q[w][x] = q;
+                            r_ek[w][x] = ((uint32_t(r) * 64u + ow) << 16) | k;
+                        }
+                    }
+                    nrec += uint32_t(__popcll(b));
+                });
+            const uint32_t incl = wave_incl_scan(done);
+            const uint32_t el = uint32_t(r) * 64u + lane;
+            i_n[w][el] = done;
+            i_off[w][el] = wsum + incl - done;
+            i_cc[w][el] = t.cc;
+            i_lt[w][el] = t.lt;
+            wsum += uint32_t(__shfl(int(incl), 63, 64));
+        }
+        if (lane == 0) w_tot[w] = wsum;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+            for (uint32_t k = 0; k < kWaves; ++k) tot += w_tot[k];
+            b_base = tot ? atomicAdd(cursor, tot) : 0ull;
+        }
+        __syncthreads();
+        uint64_t wb = b_base;
+        for (uint32_t k = 0; k < w; ++k) wb += w_tot[k];
+        if (nrec <= rcap) {
+            for (uint32_t x = lane; x < nrec; x += 64) {
+                const uint32_t f = r_f[w][x], q = r_q[w][x], ek = r_ek[w][x];
+                const uint32_t el = ek >> 16, k = ek & 0xFFFFu;
+                const uint64_t o_e = c0 + uint64_t(el >> 6) * kEmitBlock + uint64_t(w) * 64 + (el & 63u);
+                emit_write<W>(o, cap, wb + i_off[w][el] + k, i_cc[w][el], kid_cid[q], k, i_n[w][el], o_e, i_lt[w][el], f,
+                              kid_slot[q], lohi, mask);
+            }
+        } else {
+            for (int r = 0; r < kEmitRounds; ++r) {
+                const uint64_t w0 = c0 + uint64_t(r) * kEmitBlock + uint64_t(w) * 64;
+                EmitEnt t = emit_ent(w0 + lane, E, cid, cls, mem, lohi, pos, kid_off, child_of);
+                const uint32_t el = uint32_t(r) * 64u + lane;
+                const uint64_t base = wb + i_off[w][el];
+                const uint32_t n_run = i_n[w][el];
+                if (n_run == 0) t.nk = 0;
+                emit_pairs<W>(t, w0, mem, lohi, mask, kid_slot,
+                              [&](bool ok, uint32_t ow, uint64_t o_e, uint32_t o_lt, uint32_t q, uint32_t f,
+                                  uint32_t slot, uint32_t k) {
+                                  const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
+                                  const uint64_t o_base = __shfl(base, int(ow), 64);
+                                  const uint32_t o_cc = uint32_t(__shfl(int(t.cc), int(ow), 64));
+                                  if (ok)
+                                      emit_write<W>(o, cap, o_base + k, o_cc, kid_cid[q], k, o_n, o_e, o_lt, f, slot, lohi,
+                                                    mask);
+                              });
+            }
+        }
+        __syncthreads();  // the LDS records are reused by the next chunk
     }
 }
 
@@ -899,6 +1051,16 @@ struct Miner {
     static uint64_t emit_grid_cap() {
         const char* v = std::getenv("FSM_EMIT_GRID");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 22) : (1u << 16);
+    }
+    // FSM_EMIT_PATH=twopass: count pass + scan + write pass instead of k_emit1 (tests, profiling)
+    static bool emit_twopass() {
+        const char* v = std::getenv("FSM_EMIT_PATH");
+        return v && !std::strcmp(v, "twopass");
+    }
+    // LDS join records per wave of k_emit1 (FSM_EMIT_CAP lowers it: tests of the overflow path)
+    static uint32_t emit_cap() {
+        const char* v = std::getenv("FSM_EMIT_CAP");
+        return v ? uint32_t(std::min<uint64_t>(std::strtoull(v, nullptr, 10), kEmitCap)) : kEmitCap;
     }
     // class entries per block of k_count (FSM_COUNT_CHUNK overrides, for tuning)
     static uint32_t count_chunk() {
@@ -1193,8 +1355,8 @@ struct Miner {
                          b.children.size(), b.groups.size());
     }
 
-    // emit child rows of group g of batch b into a new batch: count pass,
-    // exclusive scan of the per-entry run lengths, write pass
+    // emit child rows of group g of batch b into a new batch (k_emit1: one
+    // pass, LDS join records, slab cursor; or the two-pass count/scan/write)
     void emit(Batch& b, size_t g, Batch& nb) {
         const auto [ga, gb] = b.groups[g];
         nb.cls.resize(gb - ga);
@@ -1217,19 +1379,39 @@ struct Miner {
         if (total >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch exceeds 2^32 entries");
         nb.slab.alloc(total, W);
         nb.E = total;
-        DevBuf d_child_of, ncnt(std::max<uint64_t>(b.E, 1) * 4), off((b.E + 1) * 8);
+        DevBuf d_child_of;
         upload(d_child_of, child_of);
-        ctx->stats.bytes_streamed += int64_t((total + 2 * b.E) * entry_bytes());
+        ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
         uint64_t written = 0;
-        if (b.E) {
+        if (b.E && !emit_twopass()) {
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
+            DevBuf cursor(8);
+            FSM_HIP(hipMemsetAsync(cursor.p, 0, 8, s));
+            const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
+            const unsigned grid = unsigned(std::min<uint64_t>((b.E + chunk - 1) / chunk, emit_grid_cap()));
+            const size_t tk = clk->begin("k_emit");
+#define FSM_EMIT1(WW)                                                                                               \
+    hipLaunchKernelGGL(k_emit1<WW>, dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),     \
+                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),       \
+                       b.kid_cid.as<uint32_t>(), d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
+                       nb.slab.cap, emit_cap())
+            FSM_W_DISPATCH(W, FSM_EMIT1)
+#undef FSM_EMIT1
+            FSM_LAUNCHED("k_emit", s);
+            // reads every parent entry once, writes every child entry once
+            clk->end(tk, int64_t(b.E * entry_bytes() + total * entry_bytes()));
+            FSM_HIP(hipMemcpyAsync(&written, cursor.p, 8, hipMemcpyDeviceToHost, s));
+        } else if (b.E) {
+            const SlabPtrs sp = b.slab.ptrs();
+            const SlabPtrs op = nb.slab.ptrs();
+            DevBuf ncnt(std::max<uint64_t>(b.E, 1) * 4), off((b.E + 1) * 8);
             const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, emit_grid_cap()));
 #define FSM_EMIT(WW, WR)                                                                                            \
     hipLaunchKernelGGL((k_emit<WW, WR>), dim3(grid), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
                        sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),        \
                        b.kid_cid.as<uint32_t>(), d_child_of.as<uint32_t>(), ncnt.as<uint32_t>(),                   \
-                       off.as<uint64_t>(), op)
+                       off.as<uint64_t>(), op, nb.slab.cap)
 #define FSM_EMIT_COUNT(WW) FSM_EMIT(WW, false)
 #define FSM_EMIT_WRITE(WW) FSM_EMIT(WW, true)
             size_t tk = clk->begin("k_emit<count>");

@@ -11,7 +11,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfsm.so")
+LIB_PATH = os.environ.get("FSM_LIB_PATH") or os.path.join(HERE, "libfsm.so")  # override: tuning variants
 
 FSM_OK, FSM_EINVAL, FSM_EPARSE, FSM_EDEVICE, FSM_ENOMEM, FSM_ECOMM, FSM_ELIMIT = range(7)
 MODE_SPADE, MODE_TSR = 0, 1

@@ -355,7 +355,7 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["group", "group-small-chunk", "atomic"])
+@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
     """The root F2 implementations (key runs counted per rank group, at the
     default and at a small block chunk; global atomics) give the oracle's
@@ -364,11 +364,37 @@ def test_root_f2_paths_agree(eng, path, monkeypatch):
     from tools import gen
     if path == "atomic":
         monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
-    if path == "group-small-chunk":
-        monkeypatch.setenv("FSM_ROOT_CHUNK", "300")
+    if path == "group-few-blocks":
+        monkeypatch.setenv("FSM_F2_BLOCKS", "3")
     ds = gen.quest(20000, seed=4)
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
     pats, meta, st = gpu_spade(eng, None, 0.003, tokens=ds)
+    assert pats == o["patterns"] and st["joins"] == o["joins"]
+
+
+@pytest.mark.parametrize("path", ["onepass", "twopass", "overflow-all", "overflow-some"])
+@pytest.mark.parametrize("shape", ["quest", "sign", "bible"])
+def test_emit_paths_agree(eng, path, shape, monkeypatch):
+    """Child-run emission: the one-pass k_emit1 (LDS join records, slab
+    cursor), its overflow path (records capped at 0 / 17 per wave, so waves
+    join again while writing) and the two-pass count/scan/write give the
+    oracle's patterns and joins."""
+    from oracle import oracle
+    from tools import gen
+    if path == "twopass":
+        monkeypatch.setenv("FSM_EMIT_PATH", "twopass")
+    elif path == "overflow-all":
+        monkeypatch.setenv("FSM_EMIT_CAP", "0")
+    elif path == "overflow-some":
+        monkeypatch.setenv("FSM_EMIT_CAP", "17")
+    if shape == "quest":
+        ds, sup = gen.quest(20000, seed=9), 0.003
+    elif shape == "sign":
+        ds, sup = gen.sign(seed=2).head(400), 0.3
+    else:
+        ds, sup = gen.bible(seed=2).head(1500), 0.03
+    o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
+    pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
 
 
