@@ -45,7 +45,8 @@ constexpr int kMaxSide = 64;
 constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRID sweep: 4-8 best)
 constexpr int kExpBatch = 256;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
 constexpr int kMaxBatch = 256;
-constexpr int kExpandBlocks = 128;  // bitmap path: expansion blocks per rule slot
+constexpr int kExpandBlocks = 64;   // bitmap path: at most this many expansion blocks per rule slot
+constexpr int kExpSpb = 12;         // bitmap path: expected domain sids per expansion block (swept: 1..96)
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kSpecDepth = 3;       // child speculation: levels per launch
 constexpr int kSpecMax = 128;       // child speculation: rules per level
@@ -117,7 +118,9 @@ __global__ __launch_bounds__(kBlock) void k_pairs(const uint32_t* __restrict__ v
 }
 
 // Rows restricted to the items with support >= t (one wave per row, ballot
-// compaction, item order kept): pass 1 counts (out == nullptr), pass 2 writes.
+// compaction, item order kept): pass 1 counts (out == nullptr), pass 2 writes
+// item / first / last and the item's support (read beside the entry by the
+// expansions: no dependent support lookup per entry).
 __global__ __launch_bounds__(kBlock) void k_rows_keep(const uint32_t* __restrict__ row_off,
                                                       const uint32_t* __restrict__ item,
                                                       const uint32_t* __restrict__ first,
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_keep(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ isup, uint32_t t, uint64_t N,
                                                       uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
                                                       uint32_t* __restrict__ o_item, uint32_t* __restrict__ o_first,
-                                                      uint32_t* __restrict__ o_last) {
+                                                      uint32_t* __restrict__ o_last, uint32_t* __restrict__ o_sup) {
     const uint64_t wstride = (uint64_t(gridDim.x) * blockDim.x) >> 6;
     for (uint64_t r = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; r < N; r += wstride) {
         const uint32_t rb = row_off[r], re = row_off[r + 1];
@@ -133,13 +136,16 @@ __global__ __launch_bounds__(kBlock) void k_rows_keep(const uint32_t* __restrict
         uint32_t n = 0;
         for (uint32_t e0 = rb; e0 < re; e0 += 64) {
             const uint32_t e = e0 + lane_id();
-            const bool keep = e < re && isup[item[e]] >= t;
+            const uint32_t c = e < re ? item[e] : 0u;
+            const uint32_t sp = e < re ? isup[c] : 0u;
+            const bool keep = e < re && sp >= t;
             const uint64_t b = __ballot(keep);
             if (off && keep) {
                 const uint64_t d = o + uint32_t(__popcll(b & lanemask_lt()));
-                o_item[d] = item[e];
+                o_item[d] = c;
                 o_first[d] = first[e];
                 o_last[d] = last[e];
+                o_sup[d] = sp;
             }
             o += uint32_t(__popcll(b));
             n += uint32_t(__popcll(b));
@@ -420,22 +426,68 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_build(const uint32_t* __restr
 }
 
 // Expansion of slot b (blockIdx.y) over the sids holding every item of X u Y.
-// Block x owns a contiguous range of bitmap words: it ANDs the rule's |X|+|Y|
-// item bitmaps over its range a chunk at a time, compacts the set sids into
-// LDS, and its waves then take those sids one per wave: TL / TR histograms.
-constexpr uint32_t kChunkWords = 64;  // bitmap words per LDS round (<= 2048 sids; 8 KiB of LDS keeps 7 blocks per CU)
-__global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides, const uint32_t* __restrict__ bm,
+// Block x owns a contiguous range of bitmap words, one word per thread per
+// pass: the rule's |X|+|Y| item bitmaps are ANDed (operand loads issued
+// together), a block scan places the set sids and their row bounds in LDS
+// windows, and the waves take the window's sids kExpSids at a time: the row
+// loads of those sids are all in flight before any is examined (the domain
+// is sparse - a couple of sids per wave - so the per-sid load latency, not
+// bandwidth, bounds the kernel).  TL / TR histograms in HBM.
+#ifndef FSM_TSR_SIDS
+#define FSM_TSR_SIDS 4
+#endif
+constexpr int kExpSids = FSM_TSR_SIDS;  // sids per wave step
+constexpr uint32_t kExpWin = 1024;      // sids per LDS window
+constexpr int kExpGrp = 4;              // rows > 64 entries: 64-entry chunks of loads in flight per round
+__device__ __forceinline__ void expand_short(uint32_t c, uint32_t fi, uint32_t la, uint32_t sp,
+                                             const uint32_t* sX, uint32_t nx, const uint32_t* sY, uint32_t ny,
+                                             uint32_t maxX, uint32_t maxY, uint32_t doL, uint32_t doR, uint32_t t,
+                                             uint32_t* __restrict__ TL, uint32_t* __restrict__ TR,
+                                             uint32_t* __restrict__ seen, uint32_t* __restrict__ list,
+                                             ExpCtl* __restrict__ ctl) {
+    // every item of X u Y is in the row (s came from the bitmap AND): found by ballot
+    uint32_t fX = 0, lY = 0xFFFFFFFFu;
+    bool inX = false, inY = false;
+    for (uint32_t k = 0; k < nx; ++k) {
+        const bool hit = c == sX[k];
+        inX |= hit;
+        const uint64_t hb = __ballot(hit);
+        fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(fi), int(__ffsll((long long)hb) - 1))));
+    }
+    for (uint32_t k = 0; k < ny; ++k) {
+        const bool hit = c == sY[k];
+        inY |= hit;
+        const uint64_t hb = __ballot(hit);
+        lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(la), int(__ffsll((long long)hb) - 1))));
+    }
+    if (fX >= lY) return;  // X => Y does not hold in s
+    // a candidate whose own support is below the launch's minsup can never reach it
+    const bool fq = sp >= t && c != 0xFFFFFFFFu;
+    if (doL && fq && c > maxX && fi < lY && !inY) bump(TL, c, seen, list, ctl);
+    if (doR && fq && c > maxY && la > fX && !inX) bump(TR, c, seen, list, ctl);
+}
+
+__global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides,
+                                                      const uint64_t* __restrict__ blk_off, uint32_t nslot,
+                                                      const uint32_t* __restrict__ bm,
                                                       uint32_t NW, const uint32_t* __restrict__ row_off,
                                                       const uint32_t* __restrict__ item,
                                                       const uint32_t* __restrict__ first,
-                                                      const uint32_t* __restrict__ last, uint32_t U,
+                                                      const uint32_t* __restrict__ last,
+                                                      const uint32_t* __restrict__ esup, uint32_t U,
                                                       uint32_t* __restrict__ TLb, uint32_t* __restrict__ TRb,
                                                       uint32_t* __restrict__ seenb, uint32_t* __restrict__ listb,
                                                       ExpCtl* __restrict__ ctlb, uint32_t* __restrict__ ndlw,
-                                                      const uint32_t* __restrict__ isup, uint32_t t) {
-    __shared__ uint32_t lsid[kChunkWords * 32];
-    __shared__ uint32_t ln;
-    const uint64_t b = blockIdx.y, U64 = U;
+                                                      uint32_t t) {
+    __shared__ uint32_t lrb[kExpWin], lre[kExpWin];
+    __shared__ uint32_t sXY[2 * kMaxSide];  // X then Y
+    __shared__ uint32_t wsum[kBlock / 64];
+    // slot of this block: the last b with blk_off[b] <= blockIdx.x (blocks per slot sized by its domain)
+    uint32_t b = 0;
+    for (uint32_t step = kMaxBatch / 2; step > 0; step >>= 1)
+        if (b + step < nslot && blk_off[b + step] <= blockIdx.x) b += step;
+    const uint64_t U64 = U;
+    const uint32_t bx = uint32_t(blockIdx.x - blk_off[b]), nbx = uint32_t(blk_off[b + 1] - blk_off[b]);
     const Side& side = sides[b];
     uint32_t* TL = TLb + b * U64;
     uint32_t* TR = TRb + b * U64;
@@ -443,86 +495,144 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
     uint32_t* list = listb + b * U64;
     ExpCtl* ctl = ctlb + b;
     // k_expand_collect (next on the stream) appends the k_dl work list
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ndlw = 0u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ndlw = 0u;
+    const uint32_t nx = side.nx, ny = side.ny, nxy = nx + ny;
+    const uint32_t maxX = side.maxX, maxY = side.maxY, doL = side.doL, doR = side.doR;
+    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) sXY[k] = k < nx ? side.X[k] : side.Y[k - nx];
+    __syncthreads();
+    const uint32_t* sX = sXY;
+    const uint32_t* sY = sXY + nx;
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
-    uint32_t my_ent = 0;  // row entries this wave read (lane 0)
-    const uint32_t w0 = uint32_t(uint64_t(blockIdx.x) * NW / gridDim.x);
-    const uint32_t w1 = uint32_t(uint64_t(blockIdx.x + 1) * NW / gridDim.x);
-    for (uint32_t c0 = w0; c0 < w1; c0 += kChunkWords) {
-        const uint32_t c1 = min(w1, c0 + kChunkWords);
-        if (threadIdx.x == 0) ln = 0;
-        __syncthreads();
-        for (uint32_t w = c0 + threadIdx.x; w < c1; w += blockDim.x) {
-            uint32_t v = ~0u;
-            for (uint32_t k = 0; k < side.nx && v; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
-            for (uint32_t k = 0; k < side.ny && v; ++k) v &= bm[uint64_t(side.Y[k]) * NW + w];
-            if (v) {
-                uint32_t p = atomicAdd(&ln, uint32_t(__popc(v)));
-                while (v) {
-                    lsid[p++] = w * 32u + uint32_t(__builtin_ctz(v));
-                    v &= v - 1u;
-                }
+    uint32_t my_ent = 0, my_sid = 0;  // row entries / domain sids this wave / thread saw
+    const uint32_t w0 = uint32_t(uint64_t(bx) * NW / nbx);
+    const uint32_t w1 = uint32_t(uint64_t(bx + 1) * NW / nbx);
+    for (uint32_t c0 = w0; c0 < w1; c0 += blockDim.x) {
+        const uint32_t w = c0 + threadIdx.x;
+        uint32_t v = 0;
+        if (w < w1) {
+            v = ~0u;
+            for (uint32_t k0 = 0; k0 < nxy && v; k0 += 8) {  // 8 operand loads in flight per round
+                uint32_t o[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = k0 + j < nxy ? bm[uint64_t(sXY[k0 + j]) * NW + w] : ~0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v &= o[j];
             }
         }
+        const uint32_t cnt = uint32_t(__popc(v));
+        my_sid += cnt;
+        const uint32_t incl = wave_incl_scan(cnt);
+        if (lane == 63) wsum[wv] = incl;
         __syncthreads();
-        const uint32_t n = ln;
-        if (threadIdx.x == 0 && n) atomicAdd(&ctl->nsid, n);
-        for (uint32_t q = wv; q < n; q += wpb) {
-            const uint32_t s = lsid[q];
-            const uint32_t rb = row_off[s], re = row_off[s + 1];
-            if (lane == 0) my_ent += re - rb;
-            if (re - rb <= 64) {
-                // the whole row in one round of loads, one entry per lane; X and Y
-                // items found by ballot (every item of X u Y is in the row: s came
-                // from the bitmap AND), no dependent binary searches
-                const bool v = lane < re - rb;
-                uint32_t c = 0xFFFFFFFFu, fi = 0, la = 0;
-                if (v) {
-                    c = item[rb + lane];
-                    fi = first[rb + lane];
-                    la = last[rb + lane];
-                }
-                uint32_t fX = 0, lY = 0xFFFFFFFFu;
-                bool inX = false, inY = false;
-                for (uint32_t k = 0; k < side.nx; ++k) {
-                    const bool hit = c == side.X[k];
-                    inX |= hit;
-                    const uint64_t hb = __ballot(hit);
-                    fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(fi), int(__ffsll((long long)hb) - 1))));
-                }
-                for (uint32_t k = 0; k < side.ny; ++k) {
-                    const bool hit = c == side.Y[k];
-                    inY |= hit;
-                    const uint64_t hb = __ballot(hit);
-                    lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(la), int(__ffsll((long long)hb) - 1))));
-                }
-                if (fX >= lY) continue;  // X => Y does not hold in s
-                // a candidate whose own support is below the launch's minsup can never reach it
-                const bool fq = v && isup[c] >= t;
-                if (side.doL && fq && c > side.maxX && fi < lY && !inY) bump(TL, c, seen, list, ctl);
-                if (side.doR && fq && c > side.maxY && la > fX && !inX) bump(TR, c, seen, list, ctl);
-                continue;
-            }
-            // longer rows: X / Y items and the tails located by wave 64-ary searches
-            uint32_t fX = 0, lY = 0xFFFFFFFFu;
-            for (uint32_t k = 0; k < side.nx; ++k) fX = max(fX, first[wave_find(item, rb, re, side.X[k])]);
-            for (uint32_t k = 0; k < side.ny; ++k) lY = min(lY, last[wave_find(item, rb, re, side.Y[k])]);
-            if (fX >= lY) continue;  // X => Y does not hold in s
-            // expandL (c > max(X), c not in Y, c before lastY(s)) and expandR
-            // (c > max(Y), c not in X, c after firstX(s)) in one pass over the
-            // row tail both need: each entry's item / first / last read once
-            const uint32_t qL = side.doL ? wave_find(item, rb, re, side.maxX + 1) : re;
-            const uint32_t qR = side.doR ? wave_find(item, rb, re, side.maxY + 1) : re;
-            for (uint32_t e = min(qL, qR) + lane; e < re; e += 64) {
-                const uint32_t c = item[e];
-                if (isup[c] < t) continue;
-                if (e >= qL && first[e] < lY && !in_sorted(side.Y, side.ny, c)) bump(TL, c, seen, list, ctl);
-                if (e >= qR && last[e] > fX && !in_sorted(side.X, side.nx, c)) bump(TR, c, seen, list, ctl);
-            }
+        uint32_t base = 0, tot = 0;
+        for (uint32_t k = 0; k < wpb; ++k) {
+            base += k < wv ? wsum[k] : 0u;
+            tot += wsum[k];
         }
-        __syncthreads();
+        const uint32_t pos = base + incl - cnt;
+        for (uint32_t win = 0; win < tot; win += kExpWin) {
+            // this thread's sids with block positions in the window -> row bounds in LDS
+            uint32_t vv = v, p = pos;
+            while (vv) {
+                if (p >= win && p < win + kExpWin) {
+                    const uint32_t sid = w * 32u + uint32_t(__builtin_ctz(vv));
+                    lrb[p - win] = row_off[sid];
+                    lre[p - win] = row_off[sid + 1];
+                }
+                vv &= vv - 1u;
+                ++p;
+            }
+            __syncthreads();
+            const uint32_t n = min(kExpWin, tot - win);
+            for (uint32_t q0 = wv; q0 < n; q0 += wpb * kExpSids) {
+                uint32_t rb[kExpSids], re[kExpSids], c[kExpSids], fi[kExpSids], la[kExpSids], sp[kExpSids];
+#pragma unroll
+                for (int j = 0; j < kExpSids; ++j) {  // all kExpSids rows in flight
+                    const uint32_t q = q0 + uint32_t(j) * wpb;
+                    rb[j] = q < n ? lrb[q] : 0u;
+                    re[j] = q < n ? lre[q] : 0u;
+                    const uint32_t e = rb[j] + lane;
+                    const bool ok = e < re[j] && re[j] - rb[j] <= 64u;
+                    c[j] = ok ? item[e] : 0xFFFFFFFFu;
+                    fi[j] = ok ? first[e] : 0u;
+                    la[j] = ok ? last[e] : 0u;
+                    sp[j] = ok ? esup[e] : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < kExpSids; ++j) {
+                    if (q0 + uint32_t(j) * wpb >= n) break;
+                    const uint32_t len = re[j] - rb[j];
+                    if (lane == 0) my_ent += len;
+                    if (len <= 64u) {
+                        expand_short(c[j], fi[j], la[j], sp[j], sX, nx, sY, ny, maxX, maxY, doL, doR, t, TL, TR,
+                                     seen, list, ctl);
+                        continue;
+                    }
+                    // longer rows: two ballot passes over 64-entry chunks, kExpGrp chunks of
+                    // loads in flight per round (no dependent searches): pass 1 finds the X / Y
+                    // items (firstX, lastY) and the first entry past min(maxX, maxY); pass 2
+                    // bumps from there
+                    const uint32_t rbj = rb[j], rej = re[j];
+                    const uint32_t mlo = doL ? (doR ? min(maxX, maxY) : maxX) : maxY;
+                    uint32_t fX = 0, lY = 0xFFFFFFFFu, qs = rej;
+                    for (uint32_t g0 = rbj; g0 < rej; g0 += 64u * kExpGrp) {
+                        uint32_t cg[kExpGrp], fg[kExpGrp], lg[kExpGrp];
+#pragma unroll
+                        for (int h = 0; h < kExpGrp; ++h) {
+                            const uint32_t e = g0 + uint32_t(h) * 64u + lane;
+                            const bool v = e < rej;
+                            cg[h] = v ? item[e] : 0xFFFFFFFFu;
+                            fg[h] = v ? first[e] : 0u;
+                            lg[h] = v ? last[e] : 0u;
+                        }
+#pragma unroll
+                        for (int h = 0; h < kExpGrp; ++h) {
+                            const uint64_t gt = __ballot(cg[h] != 0xFFFFFFFFu && cg[h] > mlo);
+                            if (gt && qs == rej) qs = g0 + uint32_t(h) * 64u + uint32_t(__ffsll((long long)gt)) - 1u;
+                            for (uint32_t k = 0; k < nx; ++k) {
+                                const uint64_t hb = __ballot(cg[h] == sX[k]);
+                                if (hb) fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(fg[h]), int(__ffsll((long long)hb) - 1))));
+                            }
+                            for (uint32_t k = 0; k < ny; ++k) {
+                                const uint64_t hb = __ballot(cg[h] == sY[k]);
+                                if (hb) lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(lg[h]), int(__ffsll((long long)hb) - 1))));
+                            }
+                        }
+                    }
+                    if (fX >= lY) continue;  // X => Y does not hold in s
+                    // expandL (c > max(X), c not in Y, c before lastY(s)) and expandR
+                    // (c > max(Y), c not in X, c after firstX(s)); each entry read once more
+                    for (uint32_t g0 = qs; g0 < rej; g0 += 64u * kExpGrp) {
+                        uint32_t cg[kExpGrp], fg[kExpGrp], lg[kExpGrp], sg[kExpGrp];
+#pragma unroll
+                        for (int h = 0; h < kExpGrp; ++h) {
+                            const uint32_t e = g0 + uint32_t(h) * 64u + lane;
+                            const bool v = e < rej;
+                            cg[h] = v ? item[e] : 0xFFFFFFFFu;
+                            fg[h] = v ? first[e] : 0u;
+                            lg[h] = v ? last[e] : 0u;
+                            sg[h] = v ? esup[e] : 0u;
+                        }
+#pragma unroll
+                        for (int h = 0; h < kExpGrp; ++h) {
+                            const uint32_t ce = cg[h];
+                            if (sg[h] < t || ce == 0xFFFFFFFFu) continue;
+                            bool inX = false, inY = false;
+                            for (uint32_t k = 0; k < nx; ++k) inX |= ce == sX[k];
+                            for (uint32_t k = 0; k < ny; ++k) inY |= ce == sY[k];
+                            if (doL && ce > maxX && fg[h] < lY && !inY) bump(TL, ce, seen, list, ctl);
+                            if (doR && ce > maxY && lg[h] > fX && !inX) bump(TR, ce, seen, list, ctl);
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // the window's LDS is rewritten next
+        }
     }
+    // domain and entry counters (one atomic per wave)
+    my_sid = uint32_t(__shfl(int(wave_incl_scan(my_sid)), 63, 64));
+    if (lane == 0 && my_sid) atomicAdd(&ctl->nsid, my_sid);
     if (lane == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
 }
 
@@ -891,7 +1001,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // The expansions scan rows restricted to the items that can still be in a
     // rule: support >= the pair phase's minsup, which only rises from here
     // (the first / last itemset indexes of the kept items are unchanged).
-    DevBuf k_off, k_item, k_first, k_last;
+    DevBuf k_off, k_item, k_first, k_last, k_sup;
     uint64_t E2 = 0;
     {
         const uint64_t N = uint64_t(d->N);
@@ -901,7 +1011,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             hipLaunchKernelGGL(k_rows_keep, dim3(g), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
                                d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
                                d_sup.as<uint32_t>(), rp.minsup, N, rc.as<uint32_t>(), (const uint64_t*)nullptr,
-                               (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
+                               (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
             FSM_LAUNCHED("k_rows_keep", s);
         }
         scan_exclusive(rc.as<uint32_t>(), off64.as<uint64_t>(), N, s);
@@ -911,6 +1021,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         k_item.alloc(std::max<uint64_t>(E2, 1) * 4);
         k_first.alloc(std::max<uint64_t>(E2, 1) * 4);
         k_last.alloc(std::max<uint64_t>(E2, 1) * 4);
+        k_sup.alloc(std::max<uint64_t>(E2, 1) * 4);
         hipLaunchKernelGGL(k_off32, dim3(unsigned(std::min<uint64_t>((N + 256) / 256, 4096))), dim3(256), 0, s,
                            off64.as<uint64_t>(), N, k_off.as<uint32_t>());
         FSM_LAUNCHED("k_off32", s);
@@ -918,7 +1029,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             hipLaunchKernelGGL(k_rows_keep, dim3(g), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
                                d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
                                d_sup.as<uint32_t>(), rp.minsup, N, (uint32_t*)nullptr, off64.as<uint64_t>(),
-                               k_item.as<uint32_t>(), k_first.as<uint32_t>(), k_last.as<uint32_t>());
+                               k_item.as<uint32_t>(), k_first.as<uint32_t>(), k_last.as<uint32_t>(),
+                               k_sup.as<uint32_t>());
             FSM_LAUNCHED("k_rows_keep", s);
         }
         FSM_HIP(hipStreamSynchronize(s));
@@ -982,6 +1094,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     std::vector<uint64_t> drv_off, wave_off;
 
     const TsrGrid grid;
+    const uint64_t exp_spb = [] {  // bitmap path: target domain sids per expansion block (FSM_TSR_SPB, tuning)
+        const char* v = std::getenv("FSM_TSR_SPB");
+        return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
+    }();
     // per-kernel device time: every launch ends in a stream sync, so one set
     // of events is recorded and read back per launch (ctx->kstats rows)
     struct Seg {
@@ -1017,7 +1133,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (!r->expandLR)
                 for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < sup[drv]) { drv = ry[q]; drv_in_x[k] = 0; }
             drv_off[k] = voff[drv];
-            wave_off[k + 1] = wave_off[k] + (voff[drv + 1] - voff[drv]);
+            // list path: one wave per driver sid; bitmap path: blocks sized by the
+            // expected domain (about twice the rule's support: sids holding X u Y
+            // in either order), exp_spb sids per block, at most grid.expand
+            wave_off[k + 1] = wave_off[k] + (use_bm ? std::clamp<uint64_t>((2ull * r->sup + exp_spb - 1) / exp_spb, 1,
+                                                                             grid.expand)
+                                                    : (voff[drv + 1] - voff[drv]));
         }
         std::memcpy(h_sides, sides.data(), nb * sizeof(Side));
         std::memcpy(h_drv, drv_off.data(), (nb + 1) * 8);
@@ -1027,11 +1148,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const bool timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
         if (timed) FSM_HIP(hipEventRecord(ctx->ev[0], s));
         if (use_bm) {
-            hipLaunchKernelGGL(k_expand_bm, dim3(grid.expand, nb), dim3(kBlock), 0, s, d_sides,
+            hipLaunchKernelGGL(k_expand_bm, dim3(unsigned(wave_off[nb])), dim3(kBlock), 0, s, d_sides, d_wave, nb,
                                d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), k_item.as<uint32_t>(),
-                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, TL.as<uint32_t>(),
-                               TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(), ctl.as<ExpCtl>(),
-                               d_ndlw.as<uint32_t>(), d_sup.as<uint32_t>(), rp.minsup);
+                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), k_sup.as<uint32_t>(), U,
+                               TL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
+                               ctl.as<ExpCtl>(), d_ndlw.as<uint32_t>(), rp.minsup);
             FSM_LAUNCHED("k_expand_bm", s);
         }
         if (waves) {
