@@ -48,6 +48,7 @@ constexpr int kMaxBatch = 256;
 constexpr int kExpandBlocks = 64;   // bitmap path: at most this many expansion blocks per rule slot
 constexpr int kExpSpb = 12;         // bitmap path: expected domain sids per expansion block (swept: 1..96)
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
+constexpr int kDlUnroll = 8;        // k_dl: independent words / sids per thread per round
 constexpr int kSpecDepth = 3;       // child speculation: levels per launch
 constexpr int kSpecMax = 128;       // child speculation: rules per level
 // FSM_TSR_GRID="expand,collect,dl" overrides the per-launch grids (tuning sweeps)
@@ -654,18 +655,53 @@ __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, c
         const Side& side = sides[wk.x];
         uint32_t acc = 0;
         const uint64_t v0 = vert_off[wk.y], v1 = vert_off[wk.y + 1];
+        const uint32_t nx = side.nx;
+        // latency-bound (a few hundred KiB per candidate): kDlUnroll independent
+        // steps per thread, every load of a round issued before any is used
         if (v1 - v0 < NW) {
-            for (uint64_t q = v0 + threadIdx.x; q < v1; q += blockDim.x) {
-                const uint32_t sid = vert_sid[q], w = sid >> 5, bit = 1u << (sid & 31u);
-                bool all = true;
-                for (uint32_t k = 0; k < side.nx && all; ++k) all = (bm[uint64_t(side.X[k]) * NW + w] & bit) != 0u;
-                acc += all ? 1u : 0u;
+            for (uint64_t q0 = v0 + threadIdx.x; q0 < v1; q0 += uint64_t(blockDim.x) * kDlUnroll) {
+                uint32_t sid[kDlUnroll];
+#pragma unroll
+                for (int u = 0; u < kDlUnroll; ++u) {
+                    const uint64_t q = q0 + uint64_t(u) * blockDim.x;
+                    sid[u] = q < v1 ? vert_sid[q] : 0xFFFFFFFFu;
+                }
+                bool all[kDlUnroll];
+#pragma unroll
+                for (int u = 0; u < kDlUnroll; ++u) all[u] = sid[u] != 0xFFFFFFFFu;
+                for (uint32_t k = 0; k < nx; ++k) {
+                    const uint32_t* row = bm + uint64_t(side.X[k]) * NW;
+                    uint32_t wv[kDlUnroll];
+#pragma unroll
+                    for (int u = 0; u < kDlUnroll; ++u) wv[u] = all[u] ? row[sid[u] >> 5] : 0u;
+#pragma unroll
+                    for (int u = 0; u < kDlUnroll; ++u) all[u] = all[u] && ((wv[u] >> (sid[u] & 31u)) & 1u);
+                }
+#pragma unroll
+                for (int u = 0; u < kDlUnroll; ++u) acc += all[u] ? 1u : 0u;
             }
         } else {
-            for (uint32_t w = threadIdx.x; w < NW; w += blockDim.x) {
-                uint32_t v = bm[uint64_t(wk.y) * NW + w];
-                for (uint32_t k = 0; k < side.nx; ++k) v &= bm[uint64_t(side.X[k]) * NW + w];
-                acc += uint32_t(__popc(v));
+            const uint32_t* rc = bm + uint64_t(wk.y) * NW;
+            for (uint32_t w0 = threadIdx.x; w0 < NW; w0 += blockDim.x * kDlUnroll) {
+                uint32_t v[kDlUnroll];
+#pragma unroll
+                for (int u = 0; u < kDlUnroll; ++u) {
+                    const uint32_t w = w0 + uint32_t(u) * blockDim.x;
+                    v[u] = w < NW ? rc[w] : 0u;
+                }
+                for (uint32_t k = 0; k < nx; ++k) {
+                    const uint32_t* row = bm + uint64_t(side.X[k]) * NW;
+                    uint32_t o[kDlUnroll];
+#pragma unroll
+                    for (int u = 0; u < kDlUnroll; ++u) {
+                        const uint32_t w = w0 + uint32_t(u) * blockDim.x;
+                        o[u] = w < NW ? row[w] : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kDlUnroll; ++u) v[u] &= o[u];
+                }
+#pragma unroll
+                for (int u = 0; u < kDlUnroll; ++u) acc += uint32_t(__popc(v[u]));
             }
         }
 #pragma unroll
