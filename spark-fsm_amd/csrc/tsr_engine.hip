@@ -33,6 +33,7 @@
 #include <set>
 #include <unordered_map>
 
+#include "comm.h"
 #include "dev_db.h"
 #include "device_util.h"
 
@@ -97,6 +98,7 @@ __device__ __forceinline__ uint32_t row_find(const uint32_t* __restrict__ item, 
 
 __global__ __launch_bounds__(kBlock) void k_pairs(const uint32_t* __restrict__ vsid, const uint32_t* __restrict__ vitem,
                                                   uint64_t v0, uint64_t v1, uint32_t a, uint32_t U, uint32_t t,
+                                                  uint32_t slo, uint32_t shi,
                                                   const uint32_t* __restrict__ sup,
                                                   const uint32_t* __restrict__ row_off,
                                                   const uint32_t* __restrict__ item, const uint32_t* __restrict__ first,
@@ -106,6 +108,7 @@ __global__ __launch_bounds__(kBlock) void k_pairs(const uint32_t* __restrict__ v
     const uint32_t i = vitem[v];
     if (sup[i] < t) return;
     const uint32_t s = vsid[v];
+    if (s - slo >= shi - slo) return;  // sharded pair phase: another rank's sequences
     const uint32_t rb = row_off[s], re = row_off[s + 1];
     const uint32_t k = row_find(item, rb, re, i);
     const uint32_t fi = first[k], li = last[k];
@@ -165,11 +168,12 @@ struct PairRec {
     uint32_t i, j, ij, ji;
 };
 
-// one wave per item row of the block: count (out == nullptr) or write+zero
+// one wave per item row of the block: count (out == nullptr) or write (+ re-zero the
+// counters when `zero`; the sharded pair phase still reads them afterwards)
 __global__ __launch_bounds__(kBlock) void k_pairs_compact(uint32_t* __restrict__ scr, uint32_t a, uint32_t nb,
                                                           uint32_t U, uint32_t t, uint32_t* __restrict__ rowcnt,
                                                           const uint64_t* __restrict__ rowoff,
-                                                          PairRec* __restrict__ out) {
+                                                          PairRec* __restrict__ out, int zero) {
     const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (g >= nb) return;
     const uint32_t i = a + g;
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void k_pairs_compact(uint32_t* __restrict__
         const uint64_t b = __ballot(keep);
         if (out) {
             if (keep) out[o + __popcll(b & lanemask_lt())] = PairRec{i, j, ij, ji};
-            if (j < U && (ij | ji)) { row[2 * j] = 0; row[2 * j + 1] = 0; }
+            if (zero && j < U && (ij | ji)) { row[2 * j] = 0; row[2 * j + 1] = 0; }
             o += uint64_t(__popcll(b));
         } else {
             n += uint32_t(__popcll(b));
@@ -193,37 +197,24 @@ __global__ __launch_bounds__(kBlock) void k_pairs_compact(uint32_t* __restrict__
     if (!out && lane_id() == 0) rowcnt[g] = n;
 }
 
+// sharded pair phase: this rank's partial (ij, ji) of every candidate key (i, j)
+__global__ __launch_bounds__(kBlock) void k_pairs_gather(const uint32_t* __restrict__ scr, uint32_t a, uint32_t U,
+                                                         const uint2* __restrict__ keys, uint32_t n,
+                                                         uint32_t* __restrict__ out) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const uint2 k = keys[q];
+    const uint32_t* row = scr + uint64_t(k.x - a) * U * 2;
+    out[2 * q] = row[2 * k.y];
+    out[2 * q + 1] = row[2 * k.y + 1];
+}
+
 struct Side {
     uint32_t nx, ny, doL, doR;
     uint32_t maxX, maxY, pad0, pad1;
     uint32_t X[kMaxSide];
     uint32_t Y[kMaxSide];
 };
-
-// First index in [lo, hi) of the item-sorted row with item >= key, found by
-// the whole wave: 64 probes per round narrow the range 64-fold (rows of up to
-// 4096 entries take 2 dependent rounds instead of 12 binary-search steps).
-__device__ __forceinline__ uint32_t wave_find(const uint32_t* __restrict__ item, uint32_t lo, uint32_t hi,
-                                              uint32_t key) {
-    const uint32_t lane = lane_id();
-    while (hi - lo > 64) {
-        const uint32_t step = (hi - lo + 63) / 64;
-        const uint32_t p = lo + lane * step;
-        const bool ge = p < hi && item[p] >= key;
-        const uint64_t b = __ballot(ge);
-        if (!b) {  // every probe inside the range is < key: the answer lies after the last one
-            lo = lo + min(63u, (hi - 1 - lo) / step) * step + 1;
-            continue;
-        }
-        const uint32_t f = uint32_t(__ffsll((long long)b)) - 1;
-        const uint32_t pf = min(hi, lo + f * step);
-        lo = f ? lo + (f - 1) * step + 1 : lo;
-        hi = pf;
-    }
-    const uint32_t p = lo + lane;
-    const uint64_t b = __ballot(p < hi && item[p] >= key);
-    return b ? lo + uint32_t(__ffsll((long long)b)) - 1 : hi;
-}
 
 __device__ __forceinline__ bool in_sorted(const uint32_t* s, uint32_t n, uint32_t c) {
     for (uint32_t k = 0; k < n; ++k) {
@@ -347,17 +338,18 @@ struct ExpHdr {
     uint32_t nout, nx, nsid, nent;
 };
 
-// Visit the touched items of this expansion: keep the candidates with count
-// >= t (records go to mapped pinned host memory, any order; the host sorts
-// them by item), re-zero their counters and flags; the last block to finish
-// publishes the header and resets the control block for the next expansion.
+// Visit the candidate items of this expansion - the kept items (bitmap path:
+// the expansion bumps without any touched-item bookkeeping) or the touched
+// list (list path) - keep the counts >= t (records go to mapped pinned host
+// memory, any order; the host sorts them by item) and re-zero the counters.
 __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict__ TLb, uint32_t* __restrict__ DLb,
                                                            uint32_t* __restrict__ TRb, uint32_t* __restrict__ seenb,
                                                            const uint32_t* __restrict__ listb,
                                                            ExpCtl* __restrict__ ctlb, uint32_t U, uint32_t t,
                                                            ExpRec* __restrict__ outb, ExpHdr* __restrict__ hdrb,
                                                            uint32_t cap, uint4* __restrict__ dlw,
-                                                           uint32_t* __restrict__ ndlw) {
+                                                           uint32_t* __restrict__ ndlw,
+                                                           const uint32_t* __restrict__ kept, uint32_t nkept) {
     const uint64_t b = blockIdx.y, U64 = U;
     uint32_t* TL = TLb + b * U64;
     uint32_t* DL = DLb + b * U64;
@@ -367,14 +359,22 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
     ExpCtl* ctl = ctlb + b;
     ExpRec* out = outb + b * uint64_t(cap);
     (void)hdrb;
-    const uint32_t n = ctl->nlist;
+    // bitmap path: every item that can still be a candidate (kept), no touched list;
+    // list path: the items the expansion touched
+    const uint32_t n = kept ? nkept : ctl->nlist;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t c = list[i];
-        const uint32_t tl = TL[c], dl = DL[c], tr = TR[c];
-        TL[c] = 0;
-        DL[c] = 0;
-        TR[c] = 0;
-        seen[c] = 0;
+        const uint32_t c = kept ? kept[i] : list[i];
+        const uint32_t tl = TL[c], dl = kept ? 0u : DL[c], tr = TR[c];
+        if (kept) {
+            if ((tl | tr) == 0u) continue;
+            TL[c] = 0;
+            TR[c] = 0;
+        } else {
+            TL[c] = 0;
+            DL[c] = 0;
+            TR[c] = 0;
+            seen[c] = 0;
+        }
         if (tl >= t || tr >= t) {
             const uint32_t idx = atomicAdd(&ctl->nout, 1u);
             if (idx < cap) {
@@ -443,9 +443,7 @@ constexpr int kExpGrp = 4;              // rows > 64 entries: 64-entry chunks of
 __device__ __forceinline__ void expand_short(uint32_t c, uint32_t fi, uint32_t la, uint32_t sp,
                                              const uint32_t* sX, uint32_t nx, const uint32_t* sY, uint32_t ny,
                                              uint32_t maxX, uint32_t maxY, uint32_t doL, uint32_t doR, uint32_t t,
-                                             uint32_t* __restrict__ TL, uint32_t* __restrict__ TR,
-                                             uint32_t* __restrict__ seen, uint32_t* __restrict__ list,
-                                             ExpCtl* __restrict__ ctl) {
+                                             uint32_t* __restrict__ TL, uint32_t* __restrict__ TR) {
     // every item of X u Y is in the row (s came from the bitmap AND): found by ballot
     uint32_t fX = 0, lY = 0xFFFFFFFFu;
     bool inX = false, inY = false;
@@ -464,8 +462,8 @@ __device__ __forceinline__ void expand_short(uint32_t c, uint32_t fi, uint32_t l
     if (fX >= lY) return;  // X => Y does not hold in s
     // a candidate whose own support is below the launch's minsup can never reach it
     const bool fq = sp >= t && c != 0xFFFFFFFFu;
-    if (doL && fq && c > maxX && fi < lY && !inY) bump(TL, c, seen, list, ctl);
-    if (doR && fq && c > maxY && la > fX && !inX) bump(TR, c, seen, list, ctl);
+    if (doL && fq && c > maxX && fi < lY && !inY) atomicAdd(&TL[c], 1u);
+    if (doR && fq && c > maxY && la > fX && !inX) atomicAdd(&TR[c], 1u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides,
@@ -477,7 +475,6 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
                                                       const uint32_t* __restrict__ last,
                                                       const uint32_t* __restrict__ esup, uint32_t U,
                                                       uint32_t* __restrict__ TLb, uint32_t* __restrict__ TRb,
-                                                      uint32_t* __restrict__ seenb, uint32_t* __restrict__ listb,
                                                       ExpCtl* __restrict__ ctlb, uint32_t* __restrict__ ndlw,
                                                       uint32_t t) {
     __shared__ uint32_t lrb[kExpWin], lre[kExpWin];
@@ -492,8 +489,6 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
     const Side& side = sides[b];
     uint32_t* TL = TLb + b * U64;
     uint32_t* TR = TRb + b * U64;
-    uint32_t* seen = seenb + b * U64;
-    uint32_t* list = listb + b * U64;
     ExpCtl* ctl = ctlb + b;
     // k_expand_collect (next on the stream) appends the k_dl work list
     if (blockIdx.x == 0 && threadIdx.x == 0) *ndlw = 0u;
@@ -566,8 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
                     const uint32_t len = re[j] - rb[j];
                     if (lane == 0) my_ent += len;
                     if (len <= 64u) {
-                        expand_short(c[j], fi[j], la[j], sp[j], sX, nx, sY, ny, maxX, maxY, doL, doR, t, TL, TR,
-                                     seen, list, ctl);
+                        expand_short(c[j], fi[j], la[j], sp[j], sX, nx, sY, ny, maxX, maxY, doL, doR, t, TL, TR);
                         continue;
                     }
                     // longer rows: two ballot passes over 64-entry chunks, kExpGrp chunks of
@@ -622,8 +616,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
                             bool inX = false, inY = false;
                             for (uint32_t k = 0; k < nx; ++k) inX |= ce == sX[k];
                             for (uint32_t k = 0; k < ny; ++k) inY |= ce == sY[k];
-                            if (doL && ce > maxX && fg[h] < lY && !inY) bump(TL, ce, seen, list, ctl);
-                            if (doR && ce > maxY && lg[h] > fX && !inX) bump(TR, ce, seen, list, ctl);
+                            if (doL && ce > maxX && fg[h] < lY && !inY) atomicAdd(&TL[ce], 1u);
+                            if (doR && ce > maxY && lg[h] > fX && !inX) atomicAdd(&TR[ce], 1u);
                         }
                     }
                 }
@@ -971,6 +965,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     const std::vector<uint32_t>& sup = d->sup;
 
     // ---------------- pair phase (i ascending, j > i; IJ then JI)
+    // nranks > 1: each rank counts the pairs of its own sequence range; the candidate
+    // keys are exchanged and their partial counts summed.  The
+    // expansions then run on every rank alike (replicated, no exchange).
+    Comm* comm = ctx->comm;
+    const bool shard = comm && comm->nranks() > 1;
+    const int R = shard ? comm->nranks() : 1;
+    const uint32_t slo = shard ? uint32_t(uint64_t(d->N) * uint64_t(comm->rank()) / uint64_t(R)) : 0u;
+    const uint32_t shi = shard ? uint32_t(uint64_t(d->N) * uint64_t(comm->rank() + 1) / uint64_t(R))
+                               : uint32_t(d->N);
+    uint64_t rp_pair_exchanged = 0;  // union keys exchanged (verbose)
     uint32_t nb_items = 16;
     const uint64_t scr_cap_items = std::max<uint64_t>(1, (uint64_t(256) << 20) / (uint64_t(std::max<uint32_t>(U, 1)) * 8));
     DevBuf scr;
@@ -988,15 +992,18 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const uint64_t v0 = voff[a], v1 = voff[b];
         if (v1 > v0) {
             hipLaunchKernelGGL(k_pairs, dim3(unsigned((v1 - v0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               d->vert_sid.as<uint32_t>(), d->vert_item.as<uint32_t>(), v0, v1, a, U, t,
+                               d->vert_sid.as<uint32_t>(), d->vert_item.as<uint32_t>(), v0, v1, a, U, t, slo, shi,
                                d_sup.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
                                d->first.as<uint32_t>(), d->last.as<uint32_t>(), scr.as<uint32_t>());
             FSM_LAUNCHED("k_pairs", s);
         }
+        // compaction threshold: t, or ceil(t / R) for a rank's partial counts (a pair whose
+        // total reaches t has a partial >= t / R on some rank)
+        const uint32_t tq = shard ? (t + uint32_t(R) - 1) / uint32_t(R) : t;
         DevBuf rowcnt(size_t(nb) * 4 + 4), rowoff((size_t(nb) + 1) * 8);
         const unsigned grid = unsigned((uint64_t(nb) * 64 + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
-                           rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), (PairRec*)nullptr);
+        hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, tq,
+                           rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), (PairRec*)nullptr, 0);
         FSM_LAUNCHED("k_pairs_compact", s);
         scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nb, s);
         std::vector<uint64_t> hoff(size_t(nb) + 1);
@@ -1004,12 +1011,63 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         FSM_HIP(hipStreamSynchronize(s));
         const uint64_t nrec = hoff[nb];
         DevBuf d_recs(std::max<uint64_t>(nrec, 1) * sizeof(PairRec));
-        hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
-                           rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>());
-        FSM_LAUNCHED("k_pairs_compact", s);
-        recs.resize(nrec);
-        if (nrec) FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipStreamSynchronize(s));
+        if (!shard) {  // the compaction also re-zeroes the counters it visits
+            hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
+                               rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>(), 1);
+            FSM_LAUNCHED("k_pairs_compact", s);
+            recs.resize(nrec);
+            if (nrec)
+                FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipStreamSynchronize(s));
+        } else {
+            // candidate keys of this rank -> union over ranks -> every rank's partials of
+            // the union summed -> the exact counts, kept at t like the one-rank compaction
+            std::vector<PairRec> mine(nrec);
+            if (nrec) {
+                hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, tq,
+                                   rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>(), 0);
+                FSM_LAUNCHED("k_pairs_compact", s);
+                FSM_HIP(hipMemcpyAsync(mine.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
+                FSM_HIP(hipStreamSynchronize(s));
+            }
+            std::vector<uint8_t> blob(mine.size() * 8);
+            for (size_t q = 0; q < mine.size(); ++q) {
+                std::memcpy(blob.data() + q * 8, &mine[q].i, 4);
+                std::memcpy(blob.data() + q * 8 + 4, &mine[q].j, 4);
+            }
+            std::vector<size_t> sizes;
+            const std::vector<uint8_t> all = comm->gather_blobs(blob, sizes, s);
+            std::vector<uint2> keys(all.size() / 8);
+            for (size_t q = 0; q < keys.size(); ++q) std::memcpy(&keys[q], all.data() + q * 8, 8);
+            std::sort(keys.begin(), keys.end(),
+                      [](const uint2& x, const uint2& y) { return x.x != y.x ? x.x < y.x : x.y < y.y; });
+            keys.erase(std::unique(keys.begin(), keys.end(),
+                                   [](const uint2& x, const uint2& y) { return x.x == y.x && x.y == y.y; }),
+                       keys.end());
+            std::vector<uint32_t> part(keys.size() * 2, 0u);
+            if (!keys.empty()) {
+                DevBuf d_keys(keys.size() * 8), d_part(keys.size() * 8);
+                FSM_HIP(hipMemcpyAsync(d_keys.p, keys.data(), keys.size() * 8, hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL(k_pairs_gather, dim3(unsigned((keys.size() + kBlock - 1) / kBlock)), dim3(kBlock),
+                                   0, s, scr.as<uint32_t>(), a, U, d_keys.as<uint2>(), uint32_t(keys.size()),
+                                   d_part.as<uint32_t>());
+                FSM_LAUNCHED("k_pairs_gather", s);
+                FSM_HIP(hipMemcpyAsync(part.data(), d_part.p, keys.size() * 8, hipMemcpyDeviceToHost, s));
+                FSM_HIP(hipStreamSynchronize(s));
+            }
+            comm->host_allreduce_u32(part.data(), part.size(), s);
+            FSM_HIP(hipMemsetAsync(scr.p, 0, uint64_t(nb) * U * 8, s));
+            recs.clear();
+            std::fill(hoff.begin(), hoff.end(), 0);
+            for (size_t q = 0; q < keys.size(); ++q) {
+                const uint32_t ij = part[2 * q], ji = part[2 * q + 1];
+                if (ij < t && ji < t) continue;
+                recs.push_back(PairRec{keys[q].x, keys[q].y, ij, ji});
+                hoff[keys[q].x - a + 1] += 1;
+            }
+            for (uint32_t g = 0; g < nb; ++g) hoff[g + 1] += hoff[g];
+            rp_pair_exchanged += keys.size();
+        }
         for (uint32_t g = 0; g < nb; ++g) {
             const uint32_t i = a + g;
             if (sup[i] < rp.minsup) continue;
@@ -1071,10 +1129,18 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
         FSM_HIP(hipStreamSynchronize(s));
     }
+    // candidate items of every later expansion (support >= the pair phase's minsup)
+    std::vector<uint32_t> kept_items;
+    for (uint32_t c = 0; c < U; ++c)
+        if (sup[c] >= rp.minsup) kept_items.push_back(c);
+    DevBuf d_kept(std::max<size_t>(kept_items.size(), 1) * 4);
+    if (!kept_items.empty())
+        FSM_HIP(hipMemcpyAsync(d_kept.p, kept_items.data(), kept_items.size() * 4, hipMemcpyHostToDevice, s));
+    FSM_HIP(hipStreamSynchronize(s));
     const double t1 = now_ms();
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] pair phase %.0f ms: minsup %u, candidates %zu, rules %zu\n", t1 - t0,
-                     rp.minsup, rp.cand.size(), rp.krules.size());
+        std::fprintf(stderr, "[fsm tsr] pair phase %.0f ms: minsup %u, candidates %zu, rules %zu (ranks %d, keys exchanged %llu)\n",
+                     t1 - t0, rp.minsup, rp.cand.size(), rp.krules.size(), R, (unsigned long long)rp_pair_exchanged);
 
     // ---------------- expansions
     // Batched speculation, committed in the exact sequential order: the next
@@ -1187,8 +1253,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             hipLaunchKernelGGL(k_expand_bm, dim3(unsigned(wave_off[nb])), dim3(kBlock), 0, s, d_sides, d_wave, nb,
                                d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), k_item.as<uint32_t>(),
                                k_first.as<uint32_t>(), k_last.as<uint32_t>(), k_sup.as<uint32_t>(), U,
-                               TL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
-                               ctl.as<ExpCtl>(), d_ndlw.as<uint32_t>(), rp.minsup);
+                               TL.as<uint32_t>(), TR.as<uint32_t>(), ctl.as<ExpCtl>(), d_ndlw.as<uint32_t>(),
+                               rp.minsup);
             FSM_LAUNCHED("k_expand_bm", s);
         }
         if (waves) {
@@ -1204,7 +1270,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, TL.as<uint32_t>(),
                            DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
                            ctl.as<ExpCtl>(), U, rp.minsup, d_rec, d_hdr, ecap,
-                           use_bm ? d_dlw.as<uint4>() : nullptr, d_ndlw.as<uint32_t>());
+                           use_bm ? d_dlw.as<uint4>() : nullptr, d_ndlw.as<uint32_t>(),
+                           use_bm ? d_kept.as<uint32_t>() : nullptr, uint32_t(kept_items.size()));
         FSM_LAUNCHED("k_expand_collect", s);
         if (timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
         if (use_bm) {

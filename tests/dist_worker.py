@@ -6,6 +6,7 @@ tests/test_parity_gpu.py as a plain child process).
   mode spade D sup    : sharded SPADE on cuda:0 over a gloo TorchHostComm
   mode spade_fail D sup : the same with a failure injected on one rank (FSM_INJECT_FAIL)
   mode spade_digest shape D sup : sharded SPADE, digest of the result (full-size configs)
+  mode tsr D k minconf : TSR with the pair phase sharded by sequence range
 Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (torch.distributed, gloo).
 """
 import json
@@ -52,6 +53,19 @@ def main():
             st = eng.stats()
             db.free()
         res.update(digest=pattern_digest(*csr), minsup=meta["minsup"], joins=st["joins"])
+    elif mode == "tsr":
+        # TSR on a Kosarak-shaped DB: pair phase sharded by sequence range (candidate keys
+        # exchanged, partial counts summed), expansions on every rank alike
+        from tools import gen
+        D, k, mc = int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5])
+        ds = gen.kosarak(D=D, seed=3)
+        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc,
+                        verbose=os.environ.get("FSM_WORKER_VERBOSE") == "1") as eng:
+            db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
+            rules, meta = eng.tsr(db, k, mc)
+            db.free()
+        res.update(rules=sorted([list(x), list(y), s, c] for x, y, s, c in rules),
+                   final_minsup=meta["final_minsup"])
     elif mode == "spade_fail":
         # sharded SPADE with FSM_INJECT_FAIL set for one rank: every rank must fail, none may hang
         from tools import gen

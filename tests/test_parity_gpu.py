@@ -399,6 +399,23 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
 
 
 # ------------------------------------------------------ sharded (N > 1)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tsr_pair_phase(eng, world, tmp_path):
+    """TSR with `world` ranks on this GPU over gloo: each rank counts the pairs of
+    its own sequence range, the candidate keys (partial >= ceil(t / world)) are
+    exchanged and every rank's partials of their union summed.  Every rank must
+    return exactly the oracle's rules and final minsup."""
+    from oracle import oracle
+    from test_dist import run_ranks
+    from tools import gen
+    res = run_ranks(world, ["tsr", "8000", "120", "0.4"], tmp_path, timeout=110)
+    ds = gen.kosarak(D=8000, seed=3)
+    o = oracle.tsr(ds.records(), 120, 0.4)
+    exp = sorted([list(x), list(y), s, c] for x, y, s, c in o["rules"])
+    for r in res:
+        assert r["rules"] == exp and r["final_minsup"] == o["final_minsup"]
+
+
 @pytest.mark.parametrize("world,D,sup,ref", [(2, 20000, 0.003, "oracle"), (3, 20000, 0.003, "oracle"),
                                              (2, 200000, 0.002, "gpu1")])
 def test_sharded_spade_two_ranks(eng, world, D, sup, ref, tmp_path):
