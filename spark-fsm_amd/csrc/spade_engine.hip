@@ -862,6 +862,7 @@ struct ClassMeta {
     uint32_t mshift = 0;
     uint64_t cnt_off = 0;
     uint32_t nent = 0, cbase = 0;  // entries of the class in the batch slab (= sum of member supports)
+    bool split = false;  // sharded: a heavy first-level class every rank counts; its sub-classes are split
 };
 
 struct ChildInfo {
@@ -869,6 +870,7 @@ struct ChildInfo {
     uint64_t ri_off = 0, no_off = 0;  // into the parent batch's child_rank_item / child_node_of
     uint32_t D = 0;
     uint64_t cap = 0;
+    bool split = false;
 };
 
 struct PNode {
@@ -914,6 +916,7 @@ struct Miner {
     Comm* comm = nullptr;
     uint32_t slice_lo = 0, slice_hi = kNone;
     size_t n_shared = 0;  // pattern nodes every rank holds (root + its frequent children)
+    std::vector<uint8_t> node_dup;  // sharded: nodes of split classes, output by rank 0 only
 
     double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
 
@@ -1052,6 +1055,13 @@ struct Miner {
         const char* v = std::getenv("FSM_EMIT_GRID");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 22) : (1u << 16);
     }
+    // sharded mining: a first-level class whose estimated volume exceeds this fraction of a
+    // rank's fair share is split (FSM_SPLIT_FRAC overrides; 0 or less disables splitting)
+    static double split_frac() {
+        const char* v = std::getenv("FSM_SPLIT_FRAC");
+        const double f = v ? std::atof(v) : 0.5;
+        return f > 0.0 ? f : 1e300;
+    }
     // FSM_EMIT_PATH=twopass: count pass + scan + write pass instead of k_emit1 (tests, profiling)
     static bool emit_twopass() {
         const char* v = std::getenv("FSM_EMIT_PATH");
@@ -1182,8 +1192,9 @@ struct Miner {
         dump(b);
         prepare(b);
         const bool shard = comm && b.root;  // root rows split over ranks, frequent pairs all-gathered
-        if (!shard || comm->rank() == 0)
-            for (auto& m : b.cls) stats_for_class(b, m);
+        // the root and split classes are counted by every rank: their stats come from rank 0
+        for (auto& m : b.cls)
+            if (!comm || (!shard && !m.split) || comm->rank() == 0) stats_for_class(b, m);
         fsm_stats& st = ctx->stats;
         st.batches += 1;
         const uint64_t tot_ent = b.E;
@@ -1299,16 +1310,21 @@ struct Miner {
             b.child_rank_item.resize(ch.ri_off + R2, 0);
             b.child_node_of.resize(ch.no_off + ch.D, -1);
             const int32_t parent = b.node_of[pm.no_off + pr.mi];
+            const bool dup = comm && pm.split && comm->rank() != 0;  // a split class's nodes: rank 0 outputs them
             uint32_t last_type = 0;
             for (size_t k = q; k < q2; ++k) {
                 const FreqRec& fr = recs[k];
                 const uint32_t item = b.rank_item[pm.ri_off + (fr.slot >> 1)];
                 const int32_t node = int32_t(nodes.size());
                 nodes.push_back(PNode{parent, item, fr.slot & 1u, fr.sup});
+                if (dup) {
+                    node_dup.resize(nodes.size(), 0);
+                    node_dup[size_t(node)] = 1;
+                }
                 b.child_rank_item[ch.ri_off + (fr.cid >> 1)] = item;
                 b.child_node_of[ch.no_off + fr.cid] = node;
                 ch.cap += fr.sup;
-                st.bytes_join_equiv += int64_t(12ull * fr.sup);
+                if (!dup) st.bytes_join_equiv += int64_t(12ull * fr.sup);
                 last_type = fr.slot & 1u;
             }
             const size_t nch = q2 - q;
@@ -1319,15 +1335,60 @@ struct Miner {
         }
         if (shard) {
             // first-level classes: largest-first by estimated id-list volume (the
-            // class's entries), same plan on every rank; keep this rank's share
+            // class's entries), same plan on every rank; keep this rank's share.
+            // A class heavier than split_frac() of a rank's fair share is split instead:
+            // every rank counts it, and its sub-classes are planned over the ranks.
             n_shared = nodes.size();
-            std::vector<uint64_t> vol(b.children.size());
-            std::vector<int32_t> owner(b.children.size());
-            for (size_t k = 0; k < vol.size(); ++k) vol[k] = b.children[k].cap;
+            const size_t nc = b.children.size();
+            const uint64_t N = uint64_t(comm->nranks());
+            uint64_t tot = 0;
+            for (const ChildInfo& c : b.children) tot += c.cap;
+            std::vector<uint64_t> vol;
+            std::vector<size_t> idx;
+            std::vector<uint8_t> heavy(nc, 0);
+            for (size_t k = 0; k < nc; ++k) {
+                heavy[k] = nc > 1 && double(b.children[k].cap) * double(N) > split_frac() * double(tot);
+                if (!heavy[k]) {
+                    vol.push_back(b.children[k].cap);
+                    idx.push_back(k);
+                }
+            }
+            std::vector<int32_t> owner(vol.size());
             shard_plan(vol.data(), int64_t(vol.size()), comm->nranks(), owner.data());
+            std::vector<uint8_t> keep(nc, 0);
+            for (size_t q = 0; q < idx.size(); ++q) keep[idx[q]] = owner[q] == comm->rank();
             std::vector<ChildInfo> kept;
-            for (size_t k = 0; k < vol.size(); ++k)
-                if (owner[k] == comm->rank()) kept.push_back(std::move(b.children[k]));
+            size_t nheavy = 0;
+            for (size_t k = 0; k < nc; ++k) {
+                b.children[k].split = heavy[k] != 0;
+                nheavy += heavy[k];
+                if (heavy[k] || keep[k]) kept.push_back(std::move(b.children[k]));
+            }
+            b.children = std::move(kept);
+            if (ctx->opts.verbose)
+                std::fprintf(stderr, "[fsm] rank %d: %zu first-level classes, %zu kept, %zu heavy (split)\n",
+                             comm->rank(), nc, b.children.size(), nheavy);
+        } else if (comm) {
+            // sub-classes of a split class: LPT over that class's sub-classes alone
+            // (the same on every rank whatever the batching), this rank keeps its share
+            std::vector<ChildInfo> kept;
+            for (size_t k = 0; k < b.children.size();) {
+                size_t k2 = k;
+                const uint32_t pc = b.children[k].pcls;
+                while (k2 < b.children.size() && b.children[k2].pcls == pc) ++k2;
+                if (!b.cls[pc].split) {
+                    for (size_t x = k; x < k2; ++x) kept.push_back(std::move(b.children[x]));
+                } else {
+                    std::vector<uint64_t> vol(k2 - k);
+                    std::vector<int32_t> owner(k2 - k);
+                    for (size_t x = k; x < k2; ++x) vol[x - k] = b.children[x].cap;
+                    shard_plan(vol.data(), int64_t(vol.size()), comm->nranks(), owner.data());
+                    for (size_t x = k; x < k2; ++x)
+                        if (owner[x - k] == comm->rank()) kept.push_back(std::move(b.children[x]));
+                }
+                k = k2;
+            }
+            for (ChildInfo& c : kept) c.split = false;
             b.children = std::move(kept);
         }
         // groups of children that fit the frontier budget
@@ -1373,6 +1434,7 @@ struct Miner {
                               b.child_node_of.begin() + int64_t(ch.no_off + ch.D));
             m.D = ch.D;
             m.nent = uint32_t(ch.cap);
+            m.split = ch.split;
             child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
             total += ch.cap;
         }
@@ -1739,7 +1801,16 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     const auto& nodes = mn.nodes;
     const int64_t NN = int64_t(nodes.size());
     const int64_t first = (comm && comm->rank() != 0) ? int64_t(mn.n_shared) : 0;
-    int64_t n = NN - first;
+    // this rank's output nodes: [first, NN) minus the nodes of split classes rank 0 outputs
+    std::vector<int32_t> outn;
+    const bool any_dup = !mn.node_dup.empty();
+    if (any_dup) {
+        outn.reserve(size_t(NN - first));
+        for (int64_t k = first; k < NN; ++k)
+            if (size_t(k) >= mn.node_dup.size() || !mn.node_dup[size_t(k)]) outn.push_back(int32_t(k));
+    }
+    auto node_at = [&](int64_t k) -> int64_t { return any_dup ? int64_t(outn[size_t(k)]) : first + k; };
+    int64_t n = any_dup ? int64_t(outn.size()) : NN - first;
     std::vector<uint32_t> plen(static_cast<size_t>(NN)), pset(static_cast<size_t>(NN));
     for (int64_t k = 0; k < NN; ++k) {
         const int32_t q = nodes[size_t(k)].parent;
@@ -1753,8 +1824,8 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     std::vector<int64_t> item_off(size_t(n) + 1, 0);
     pat_off[0] = 0;
     for (int64_t k = 0; k < n; ++k) {
-        pat_off[size_t(k) + 1] = pat_off[size_t(k)] + pset[size_t(first + k)];
-        item_off[size_t(k) + 1] = item_off[size_t(k)] + plen[size_t(first + k)];
+        pat_off[size_t(k) + 1] = pat_off[size_t(k)] + pset[size_t(node_at(k))];
+        item_off[size_t(k) + 1] = item_off[size_t(k)] + plen[size_t(node_at(k))];
     }
     MallocArr<int64_t> set_off{static_cast<size_t>(pat_off[size_t(n)]) + 1};
     MallocArr<int32_t> items{static_cast<size_t>(item_off[size_t(n)])};
@@ -1763,12 +1834,12 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     auto fill = [&](int64_t k0, int64_t k1) {
         for (int64_t k = k0; k < k1; ++k) {
             int64_t pos = item_off[size_t(k) + 1], sidx = pat_off[size_t(k) + 1];
-            for (int32_t q = int32_t(first + k); q >= 0; q = nodes[size_t(q)].parent) {
+            for (int32_t q = int32_t(node_at(k)); q >= 0; q = nodes[size_t(q)].parent) {
                 const PNode& nd = nodes[size_t(q)];
                 items[size_t(--pos)] = ival[nd.item];
                 if (nd.parent < 0 || nd.type == kSeq) set_off[size_t(--sidx)] = pos;
             }
-            sup[size_t(k)] = int32_t(nodes[size_t(first + k)].support);
+            sup[size_t(k)] = int32_t(nodes[size_t(node_at(k))].support);
         }
     };
     const int64_t nthr = n >= (int64_t(1) << 17) ? int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)) : 1;

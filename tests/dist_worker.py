@@ -47,7 +47,8 @@ def main():
         from tools import gen
         shape, D, sup = sys.argv[3], int(sys.argv[4]), float(sys.argv[5])
         ds = gen.quest(D, seed=1) if shape == "quest" else getattr(gen, shape)(seed=1)
-        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc) as eng:
+        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc,
+                        verbose=os.environ.get("FSM_WORKER_VERBOSE") == "1") as eng:
             db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
             csr, meta = eng.spade_csr(db, sup)
             st = eng.stats()

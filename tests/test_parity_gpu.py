@@ -399,6 +399,26 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
 
 
 # ------------------------------------------------------ sharded (N > 1)
+@pytest.mark.parametrize("frac", ["0.1", "0"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_heavy_class_split(eng, world, frac, tmp_path, monkeypatch):
+    """Heavy first-level classes (volume > FSM_SPLIT_FRAC of a rank's share;
+    0.1 splits the largest SIGN-shaped classes, 0 disables splitting) are counted
+    by every rank and their sub-classes planned over the ranks.  Every rank
+    returns the complete pattern set (no pattern twice) and the single-rank
+    join count."""
+    from digest import pattern_digest
+    from oracle import oracle
+    from test_dist import run_ranks
+    from tools import gen
+    monkeypatch.setenv("FSM_SPLIT_FRAC", frac)
+    res = run_ranks(world, ["spade_digest", "sign", "0", "0.07"], tmp_path, timeout=110)
+    ds = gen.sign(seed=1)
+    csr, meta = oracle.spade_tokens_csr(ds.seq_off, ds.tokens, 0.07, threads=4)
+    exp = pattern_digest(*csr)
+    for r in res:
+        assert r["digest"] == exp and r["joins"] == meta["joins"] and r["minsup"] == meta["minsup"]
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_tsr_pair_phase(eng, world, tmp_path):
     """TSR with `world` ranks on this GPU over gloo: each rank counts the pairs of
