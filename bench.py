@@ -16,6 +16,9 @@ same DB and minsup, median of 3 bounded samples, in the same scope as `value`
 vertical build), 1 thread (the reference's one driver thread) and all cores
 of this process's CPU share.
 
+The config-4 TSR leg (`tsr_c4`: expansions/s, its own roofline and CPU
+baseline) runs after the SPADE steps at N = 1 (--no-tsr skips it).
+
   python bench.py [--gpus N --steps K --warmup W]   (N > 1 via torch.distributed.run)
 
 Prints ONE JSON line on rank 0.
@@ -84,6 +87,63 @@ def cpu_baseline(ds, support, seconds, threads, reps):
             "complete": all(r["complete"] for r in runs), "joins_per_sample": [r["joins"] for r in runs]}
 
 
+def tsr_leg(fsm, gen, cpu_seconds, cpu_reps, cpu):
+    """BASELINE config 4 (TSR, 990,002 Kosarak-shaped sequences, k = 1000,
+    minconf 0.5): one mine after a warmup mine, expansions/s, the roofline of
+    its dominant kernel (SURVEY §8(d) TSR unit: 12 B per row entry scanned +
+    the sid-bitmap operands, per k_expand_bm launch) and the CPU restatement
+    on a bounded sample of the same DB (expansions/s)."""
+    k, minconf = 1000, 0.5
+    ds = gen.kosarak(D=990002, seed=1)
+    with fsm.Engine(0) as eng:
+        db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
+        eng.tsr(db, k, minconf)  # warmup (allocations, code objects)
+        t0 = time.perf_counter()
+        rules, meta = eng.tsr(db, k, minconf)
+        ms = (time.perf_counter() - t0) * 1000.0
+        st, ks = eng.stats(), eng.kernel_stats()
+        db.free()
+    dom = max(ks, key=lambda q: q["ms"])
+    ach = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] else 0.0
+    leg = {"metric": "TSR expansions/s, Kosarak-shaped 990,002 sequences, k = 1000, minconf 0.5",
+           "value": st["expansions"] / (ms / 1000.0), "unit": "expansions/s", "mine_ms": ms,
+           "rules": len(rules), "final_minsup": meta["final_minsup"], "expansions": st["expansions"],
+           "ms_pair_phase": st["ms_f2"], "ms_expansions": st["ms_lattice"], "launches": st["count_launches"],
+           "ms_gpu_wait": st["ms_count_kernel"],
+           "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": ach, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": dom["ms"],
+                        "alg_bytes": dom["alg_bytes"], "launches": dom["launches"],
+                        "bytes_basis": "SURVEY §8(d) TSR unit: 12 B per scanned row entry (item, first, last) + "
+                                       "8 B per domain sid + the |X|+|Y| sid-bitmap operands (N/8 B each); "
+                                       "kernel time sampled every 16th launch with HIP events"},
+           "kernels": [{"name": q["name"], "launches": q["launches"], "ms": round(q["ms"], 1)} for q in ks]}
+    if cpu:
+        # the restatement's pair phase alone outlasts the bound at 990K sequences, so
+        # both sides run the same 20,000-sequence prefix (like for like)
+        from oracle import oracle
+        pre = ds.head(20000)
+        with fsm.Engine(0) as eng:
+            db = eng.db_from_tokens(pre.sids, pre.seq_off, pre.tokens, fsm.MODE_TSR)
+            eng.tsr(db, k, minconf)
+            t0 = time.perf_counter()
+            eng.tsr(db, k, minconf)
+            gms = (time.perf_counter() - t0) * 1000.0
+            gexp = eng.stats()["expansions"]
+            db.free()
+        recs = pre.records()
+        runs = [oracle.tsr(recs, k, minconf, time_limit_s=cpu_seconds) for _ in range(cpu_reps)]
+        rates = [r["expansions"] / max(r["seconds"], 1e-9) for r in runs]
+        leg["cpu_baseline"] = {
+            "value": statistics.median(rates), "unit": "expansions/s", "cores": 1, "kind": "port",
+            "sample": "the 20,000-sequence prefix of the same DB, same k and minconf; median of %d runs of the "
+                      "single-thread CPU restatement (oracle/fsm_oracle.c) bounded to %.0f s each, expansions/s "
+                      "over the sample (at 990K its pair phase alone outlasts the bound)" % (cpu_reps, cpu_seconds),
+            "complete": all(r["complete"] for r in runs), "samples": [round(v, 1) for v in rates],
+            "gpu_same_prefix": {"value": gexp / (gms / 1000.0), "unit": "expansions/s", "mine_ms": gms,
+                                "expansions": gexp}}
+    return leg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +158,7 @@ def main():
     # all-cores CPU mode (SURVEY §8d ii); 0 = every CPU of this process's share (0 skips: -1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: CPU dry run)")
+    ap.add_argument("--no-tsr", action="store_true", help="skip the config-4 TSR leg (N = 1 only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -241,9 +302,11 @@ def main():
             ca["sample"] = ("same DB, minsup, bound and scope; first-level classes on %d OpenMP threads "
                             "(all CPUs of this process's share; F1 build single-threaded)" % nt)
             line["extra"]["cpu_baseline_all_cores"] = ca
-    print(json.dumps(line), flush=True)
     db.free()
     eng.close()
+    if not args.no_tsr and world == 1:
+        line["tsr_c4"] = tsr_leg(fsm, gen, args.cpu_seconds, args.cpu_reps, not args.no_cpu_baseline)
+    print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
