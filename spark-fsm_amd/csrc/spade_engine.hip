@@ -226,10 +226,17 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return uint32_t(__builtin_
 // rank -> group by multiply-high (exact for rank < 2^16, per < 2^15)
 __device__ __forceinline__ uint32_t group_of(uint32_t rank, uint32_t pm) { return __umulhi(rank, pm); }
 
+// region (group g, row block b) in scan order: group-major [g][b] (each group's keys one
+// contiguous stream for k_f2_count) or block-major [b][g] (each block's keys one contiguous
+// stretch: region boundary lines are written by one block, in one XCD's L2)
+__device__ __forceinline__ uint64_t f2_region(uint32_t g, uint32_t b, uint32_t G, uint32_t nblk, int bg) {
+    return bg ? uint64_t(b) * G + g : uint64_t(g) * nblk + b;
+}
+
 __global__ __launch_bounds__(kBlock) void k_f2_plan(const uint64_t* __restrict__ roff, uint32_t R, uint32_t rpb,
                                                     const uint32_t* __restrict__ mem, const uint32_t* __restrict__ pos,
                                                     uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo, uint32_t mhi,
-                                                    uint32_t* __restrict__ cap) {
+                                                    int bg, uint32_t* __restrict__ cap) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
     __syncthreads();
@@ -244,7 +251,8 @@ __global__ __launch_bounds__(kBlock) void k_f2_plan(const uint64_t* __restrict__
     }
     __syncthreads();
     // regions start on 16-byte boundaries (8 keys): k_f2_count reads them in aligned chunks
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[uint64_t(g) * nblk + blockIdx.x] = (h[g] + 7u) & ~7u;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+        cap[f2_region(g, blockIdx.x, G, nblk, bg)] = (h[g] + 7u) & ~7u;
 }
 
 constexpr uint32_t kF2Threads = 1024;  // k_f2_keys / k_f2_count block
@@ -264,7 +272,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                                                         const uint32_t* __restrict__ lohi,
                                                         const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
                                                         uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
-                                                        uint32_t mhi, const uint64_t* __restrict__ base,
+                                                        uint32_t mhi, const uint64_t* __restrict__ base, int bg,
                                                         uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
                                                         unsigned long long* __restrict__ nkeys_total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     __shared__ uint32_t blk_keys;
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[uint64_t(g) * nblk + b]);
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[f2_region(g, b, G, nblk, bg)]);
     for (uint32_t r = r0 + threadIdx.x; r <= r1; r += blockDim.x) srow[r - r0] = uint32_t(roff[r]);
     if (threadIdx.x == 0) blk_keys = 0;
     __syncthreads();
@@ -393,7 +401,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     atomicAdd(&blk_keys, my_keys);
     __syncthreads();
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
-        fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[uint64_t(g) * nblk + b]);
+        fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[f2_region(g, b, G, nblk, bg)]);
     if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
@@ -407,7 +415,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
 // [max(g*per, rlo), min((g+1)*per, rhi)) are balloted out with one atomic per
 // wave; records come out unordered and the host sorts them.
 constexpr uint32_t kF2MaxBlocks = 2048;  // row blocks (regions per group) k_f2_count can index in LDS
-__global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base,
+__global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base, uint32_t G, int bg,
                                                          const uint32_t* __restrict__ fill, uint32_t nblk,
                                                          const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
                                                          uint32_t g0, uint32_t rlo, uint32_t rhi, uint32_t minsup,
@@ -426,11 +434,11 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
     const uint32_t s0 = 2 * threadIdx.x;
     const uint32_t f0 = s0 < nblk ? fill[gi + s0] : 0u, f1 = s0 + 1 < nblk ? fill[gi + s0 + 1] : 0u;
     if (s0 < nblk) {
-        cst[s0] = uint32_t(base[gi + s0]) >> 3;
+        cst[s0] = uint32_t(base[f2_region(g, s0, G, nblk, bg)]) >> 3;
         sfill[s0] = f0;
     }
     if (s0 + 1 < nblk) {
-        cst[s0 + 1] = uint32_t(base[gi + s0 + 1]) >> 3;
+        cst[s0 + 1] = uint32_t(base[f2_region(g, s0 + 1, G, nblk, bg)]) >> 3;
         sfill[s0 + 1] = f1;
     }
     const uint32_t c0 = (f0 + 7) >> 3, c1 = (f1 + 7) >> 3;
@@ -1078,6 +1086,11 @@ struct Miner {
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kChunk;
     }
     // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
+    // FSM_F2_LAYOUT=bg: key regions block-major instead of group-major (A/B knob)
+    static bool f2_block_major() {
+        const char* v = std::getenv("FSM_F2_LAYOUT");
+        return v && !std::strcmp(v, "bg");
+    }
     static uint32_t f2_blocks() {
         const char* v = std::getenv("FSM_F2_BLOCKS");
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, kF2MaxBlocks)) : 1024u;
@@ -1104,13 +1117,14 @@ struct Miner {
         if (uint64_t(rpb) * kF2MaxBlocks < R) return false;  // more rows than the LDS-indexed blocks cover
         const uint32_t nblk = (R + rpb - 1) / rpb;
         const uint64_t nd = uint64_t(G) * nblk;
+        const int bg = f2_block_major() ? 1 : 0;
         const SlabPtrs sp = b.slab.ptrs();
         const int64_t E0 = int64_t(m.nent);
         // plan: region capacities -> bases
         DevBuf cap(nd * 4), base((nd + 1) * 8), fill(nd * 4);
         size_t tk = clk->begin("k_f2_plan");
         hipLaunchKernelGGL(k_f2_plan, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, b.root_rows.as<uint64_t>(), R, rpb,
-                           sp.mem, sp.pos, pm, G, nblk, mlo, mhi, cap.as<uint32_t>());
+                           sp.mem, sp.pos, pm, G, nblk, mlo, mhi, bg, cap.as<uint32_t>());
         FSM_LAUNCHED("k_f2_plan", s);
         clk->end(tk, E0 * 8 + int64_t(nd) * 4);
         scan_exclusive(cap.as<uint32_t>(), base.as<uint64_t>(), nd, s);
@@ -1126,7 +1140,7 @@ struct Miner {
         const size_t kshm = size_t(kF2Waves) * 64 * (sizeof(F2Ent) + 4) + (size_t(kF2MaxRows) + 1) * 4 + size_t(G) * 4;
 #define FSM_F2K(WW)                                                                                                   \
     hipLaunchKernelGGL(k_f2_keys<WW>, dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(), R, rpb,      \
-                       sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(),                   \
+                       sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(), bg,               \
                        fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>())
         FSM_W_DISPATCH(W, FSM_F2K)
 #undef FSM_F2K
@@ -1147,7 +1161,7 @@ struct Miner {
             FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
             tk_cnt = clk->begin("k_f2_count");
             if (g1 > g0)
-                hipLaunchKernelGGL(k_f2_count, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
+                hipLaunchKernelGGL(k_f2_count, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(), G, bg,
                                    fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), D, per, g0, rlo, rhi, minsup,
                                    d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>());
             FSM_LAUNCHED("k_f2_count", s);

@@ -24,6 +24,8 @@ def kernel_name(demangled):
     base, targs = m.group(1), m.group(3) or ""
     if base == "k_emit":
         return "k_emit<write>" if "true" in targs else "k_emit<count>"
+    if base == "k_emit1":  # the one-pass emit: fsm_get_kernel_stats calls it "k_emit"
+        return "k_emit"
     return base
 
 
