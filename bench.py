@@ -240,7 +240,8 @@ def main():
     # time (HIP events on libfsm's stream, summed over the launches of the last step)
     dom = max(ks, key=lambda k: k["ms"])
     achieved = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
-    traffic = pmc_traffic(dom["name"])
+    traffic = pmc_traffic(dom["name"])  # per step
+    traffic_launch = traffic / dom["launches"] if traffic is not None and dom["launches"] else None
     # SURVEY §8(d) unit for the F2: 8 B per (item, sid) first/last pair read per pass,
     # over the device time of the root F2 kernels
     f2_ms = sum(k["ms"] for k in ks if k["name"] in ROOT_F2_KERNELS)
@@ -263,9 +264,13 @@ def main():
             args.sequences, args.seed, args.support), "parallelism": "single GPU" if world == 1 else
             "prefix classes sharded over %d ranks (%s)" % (world, args.dist_backend)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_launch,
                      "kernel": dom["name"], "launches_per_step": dom["launches"],
                      "kernel_ms_per_step": dom["ms"], "alg_bytes_per_step": dom["alg_bytes"],
+                     "alg_bytes_per_launch": dom["alg_bytes"] / max(dom["launches"], 1),
+                     "traffic_per_step": traffic,
+                     "traffic_basis": "HBM bytes per launch (average over the step's launches) = "
+                                      "(2 x FETCH_SIZE + WRITE_SIZE) / launches from the committed PMC passes",
                      "bytes_basis": "the kernel's compulsory reads + writes per launch (DESIGN.md §4)",
                      "traffic_source": PMC_FILE if traffic is not None else None},
         "roofline_survey_f2": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,

@@ -218,6 +218,11 @@ struct fsm_ctx {
     fsm::Comm* comm = nullptr;  // nranks > 1 (owned)
     std::shared_ptr<fsm::Pool> pool;  // device blocks of this context (see fsm::Pool)
     std::vector<fsm_kernel_stat> kstats;  // of the last mine call
+    std::unique_ptr<fsm::PinnedBuf> pin;  // small mapped readback slots, made on first use
+    uint64_t* pinned_u64() {              // 8 u64 slots of pinned host memory
+        if (!pin) pin = std::make_unique<fsm::PinnedBuf>(64);
+        return static_cast<uint64_t*>(pin->host);
+    }
 };
 
 struct fsm_db {

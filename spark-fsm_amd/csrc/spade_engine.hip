@@ -927,6 +927,8 @@ struct Miner {
     std::vector<uint8_t> node_dup;  // sharded: nodes of split classes, output by rank 0 only
 
     double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
+    // FSM_HOST_TRACE=1: host time of the bookkeeping phases, printed at the end of the mine
+    double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f2 sort, kids CSR+upload, children, plan/groups, emit tables, slab alloc
 
     // Sharded mining: a failure on one rank must not leave its peers blocked in
     // a collective.  The work between two collectives runs through
@@ -979,7 +981,11 @@ struct Miner {
         const double t = now_ms();
         FSM_HIP(hipStreamSynchronize(s));
         wait_ms += now_ms() - t;
+        check_emit();
     }
+    uint64_t* pend = nullptr;  // pinned slot: the last emit's slab cursor (ctx->pinned_u64())
+    uint64_t pend_total = 0;
+    bool pend_check = false;
 
     uint64_t entry_bytes() const { return 16ull + 8ull * uint64_t(W); }  // cid, mem, lohi, pos, mask
 
@@ -1186,9 +1192,20 @@ struct Miner {
         ctx->stats.root_keys += int64_t(nkeys);
         // (row, slot) order and child member ids: rank among the row's slots with a frequent
         // temporal or equality candidate, << 1 | type (as k_freq_write assigns them)
-        std::sort(recs.begin(), recs.end(), [](const FreqRec& x, const FreqRec& y) {
-            return x.row != y.row ? x.row < y.row : x.slot < y.slot;
-        });
+        const double th0 = now_ms();
+        {  // (row, slot) order: counting sort by row, then the few slots of each row
+            std::vector<uint32_t> off(size_t(F) + 1, 0);
+            for (const FreqRec& r : recs) ++off[size_t(r.row) + 1];
+            for (uint32_t x = 0; x < F; ++x) off[x + 1] += off[x];
+            std::vector<FreqRec> tmp(recs.size());
+            std::vector<uint32_t> at(off.begin(), off.end() - 1);
+            for (const FreqRec& r : recs) tmp[at[r.row]++] = r;
+            for (uint32_t x = 0; x < F; ++x)
+                if (off[x + 1] - off[x] > 1)
+                    std::sort(tmp.begin() + off[x], tmp.begin() + off[x + 1],
+                              [](const FreqRec& a, const FreqRec& c) { return a.slot < c.slot; });
+            recs.swap(tmp);
+        }
         for (size_t q = 0; q < recs.size();) {
             size_t q2 = q;
             uint32_t crank = 0;
@@ -1199,6 +1216,7 @@ struct Miner {
             }
             q = q2;
         }
+        hp[0] += now_ms() - th0;
         return true;
     }
     // count kernel + frequent-candidate extraction; fills b.children / b.groups / kids
@@ -1292,6 +1310,7 @@ struct Miner {
             recs.resize(nfreq);
             if (nfreq) std::memcpy(recs.data(), all.data(), all.size());
         }
+        double th = now_ms();
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
         std::vector<uint32_t> koff(b.cbase_total + 1, 0), kslot(nfreq), kcid(nfreq);
         for (const FreqRec& fr : recs) koff[b.cls[rows[fr.row].cls].cbase + rows[fr.row].mi + 1] += 1;
@@ -1303,6 +1322,8 @@ struct Miner {
         upload(b.kid_off, koff);
         upload(b.kid_slot, kslot);
         upload(b.kid_cid, kcid);
+        hp[1] += now_ms() - th;
+        th = now_ms();
         // children (new pattern nodes) in deterministic (row, slot) order
         b.children.clear();
         b.child_rank_item.clear();
@@ -1405,6 +1426,8 @@ struct Miner {
             for (ChildInfo& c : kept) c.split = false;
             b.children = std::move(kept);
         }
+        hp[2] += now_ms() - th;
+        th = now_ms();
         // groups of children that fit the frontier budget
         b.groups.clear();
         b.next_group = 0;
@@ -1424,6 +1447,7 @@ struct Miner {
             acc_ent += b.children[k].cap;
         }
         if (gs < b.children.size()) b.groups.push_back({gs, b.children.size()});
+        hp[3] += now_ms() - th;
         if (ctx->opts.verbose)
             std::fprintf(stderr, "[fsm] batch: classes=%zu entries=%llu freq=%llu children=%zu groups=%zu\n",
                          b.cls.size(), (unsigned long long)tot_ent, (unsigned long long)nfreq,
@@ -1433,6 +1457,7 @@ struct Miner {
     // emit child rows of group g of batch b into a new batch (k_emit1: one
     // pass, LDS join records, slab cursor; or the two-pass count/scan/write)
     void emit(Batch& b, size_t g, Batch& nb) {
+        const double th = now_ms();
         const auto [ga, gb] = b.groups[g];
         nb.cls.resize(gb - ga);
         std::vector<uint32_t> child_of(b.cbase_total, kNone);
@@ -1453,12 +1478,14 @@ struct Miner {
             total += ch.cap;
         }
         if (total >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch exceeds 2^32 entries");
+        const double th2 = now_ms();
+        hp[4] += th2 - th;
         nb.slab.alloc(total, W);
+        hp[5] += now_ms() - th2;
         nb.E = total;
         DevBuf d_child_of;
         upload(d_child_of, child_of);
         ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
-        uint64_t written = 0;
         if (b.E && !emit_twopass()) {
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
@@ -1477,7 +1504,7 @@ struct Miner {
             FSM_LAUNCHED("k_emit", s);
             // reads every parent entry once, writes every child entry once
             clk->end(tk, int64_t(b.E * entry_bytes() + total * entry_bytes()));
-            FSM_HIP(hipMemcpyAsync(&written, cursor.p, 8, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&pend[0], cursor.p, 8, hipMemcpyDeviceToHost, s));
         } else if (b.E) {
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
@@ -1502,13 +1529,23 @@ struct Miner {
 #undef FSM_EMIT_WRITE
 #undef FSM_EMIT_COUNT
 #undef FSM_EMIT
-            FSM_HIP(hipMemcpyAsync(&written, off.as<uint64_t>() + b.E, 8, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&pend[0], off.as<uint64_t>() + b.E, 8, hipMemcpyDeviceToHost, s));
+        } else {
+            pend[0] = 0;
         }
-        sync();
-        // the runs must add up exactly to the capacities (sum of child supports)
-        if (written != total)
+        // no sync: the host prepares the next count while the emit runs; the runs must add
+        // up exactly to the capacities (sum of child supports), checked at the next sync
+        pend_total = total;
+        pend_check = true;
+    }
+    // the deferred emit check (after a stream sync)
+    void check_emit() {
+        if (!pend_check) return;
+        pend_check = false;
+        const uint64_t written = pend[0];
+        if (written != pend_total)
             throw Error(FSM_EDEVICE, "SPADE emit: wrote " + std::to_string(written) + " child entries, expected " +
-                                         std::to_string(total));
+                                         std::to_string(pend_total));
     }
 
     void run_root(Batch& root, const std::vector<uint32_t>& freq_items, const std::vector<uint32_t>& f1) {
@@ -1706,6 +1743,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     size_t free_b = 0, total_b = 0;
     FSM_HIP(hipMemGetInfo(&free_b, &total_b));
     mn.budget = ctx->opts.mem_budget > 0 ? uint64_t(ctx->opts.mem_budget) : uint64_t(free_b / 2);
+    mn.pend = ctx->pinned_u64();
     mn.d_tests.alloc(8);
     FSM_HIP(hipMemsetAsync(mn.d_tests.p, 0, 8, ctx->stream));
 
@@ -1789,15 +1827,20 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         mn.count_and_freq(*nb);
         stack.push_back(std::move(nb));
     }
+    mn.sync();  // the last deferred emit check, before the agreement
     });
     mn.agree();
     {
         unsigned long long tests = 0;
         FSM_HIP(hipMemcpyAsync(&tests, mn.d_tests.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-        FSM_HIP(hipStreamSynchronize(ctx->stream));
+        mn.sync();
         ctx->stats.pair_tests = int64_t(tests);
     }
     ctx->stats.ms_lattice = now_ms() - t2;
+    if (const char* v = std::getenv("FSM_HOST_TRACE"); v && v[0] == '1')
+        std::fprintf(stderr, "[fsm host] f2 sort %.3f, kids %.3f, children %.3f, groups %.3f, emit tables %.3f, "
+                     "slab alloc %.3f, gpu wait %.3f ms\n", mn.hp[0], mn.hp[1], mn.hp[2], mn.hp[3], mn.hp[4], mn.hp[5],
+                     mn.wait_ms);
     clock.finish(ctx->kstats);
     for (const fsm_kernel_stat& k : ctx->kstats) {
         const std::string nm = k.name;
