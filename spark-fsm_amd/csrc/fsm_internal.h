@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -222,6 +223,19 @@ struct fsm_ctx {
     uint64_t* pinned_u64() {              // 8 u64 slots of pinned host memory
         if (!pin) pin = std::make_unique<fsm::PinnedBuf>(64);
         return static_cast<uint64_t*>(pin->host);
+    }
+    // mapped pinned host memory of at least `bytes` (kernels write results straight into it);
+    // grown on demand, kept for the context's lifetime
+    std::unique_ptr<fsm::PinnedBuf> pin_big;
+    size_t pin_big_bytes = 0;
+    fsm::PinnedBuf* pinned_big(size_t bytes) {
+        if (!pin_big || pin_big_bytes < bytes) {
+            const size_t nb = std::max<size_t>(bytes, std::max<size_t>(2 * pin_big_bytes, size_t(1) << 20));
+            pin_big.reset();
+            pin_big = std::make_unique<fsm::PinnedBuf>(nb);
+            pin_big_bytes = nb;
+        }
+        return pin_big.get();
     }
 };
 

@@ -502,47 +502,51 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ rows, uint32_t nrows,
-                                                       const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
-                                                       uint32_t minsup, uint32_t* __restrict__ rowcnt) {
+// One-pass frequent extraction: one wave per counter row ballots the frequent
+// candidates and appends FreqRec{row, slot, sup} at a block cursor reserved with
+// one global atomic per block (unordered; the host orders them, order_recs).
+// More than `cap` records: only counted (the host retries with the exact size).
+__global__ __launch_bounds__(kBlock) void k_freq_recs(const DRow* __restrict__ rows, uint32_t nrows,
+                                                      const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
+                                                      uint32_t minsup, uint32_t row_base, FreqRec* __restrict__ out,
+                                                      uint32_t cap, uint32_t* __restrict__ nout) {
+    __shared__ uint32_t w_n[kBlock / 64];
+    __shared__ uint32_t b_at;
     const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (g >= nrows) return;
-    const DRow r = rows[g];
-    const DClass c = cls[r.cls];
-    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const bool live = g < nrows;
+    DRow r{0, 0};
+    DClass c{0, 0, 0, 0, {0, 0, 0}};
+    const uint32_t* base = cnt;
     uint32_t n = 0;
-    for (uint32_t s = 0; s < c.D; s += 64) {
-        const uint32_t slot = s + lane_id();
-        const uint32_t v = slot < c.D ? base[slot] : 0u;
-        n += __popcll(__ballot(v >= minsup));
+    if (live) {
+        r = rows[g];
+        c = cls[r.cls];
+        base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
+        for (uint32_t s0 = 0; s0 < c.D; s0 += 64) {
+            const uint32_t slot = s0 + lane;
+            n += uint32_t(__popcll(__ballot(slot < c.D && base[slot] >= minsup)));
+        }
     }
-    if (lane_id() == 0) rowcnt[g] = n;
-}
-
-__global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ rows, uint32_t nrows,
-                                                       const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
-                                                       uint32_t minsup, const uint64_t* __restrict__ rowoff,
-                                                       uint32_t row_base, FreqRec* __restrict__ out) {
-    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (g >= nrows) return;
-    const DRow r = rows[g];
-    const DClass c = cls[r.cls];
-    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
-    uint64_t o = rowoff[g];
-    uint32_t nrank = 0;
-    const unsigned lane = lane_id();
-    const uint64_t lead_lt = (1ull << (lane & ~1u)) - 1ull;
-    for (uint32_t s = 0; s < c.D; s += 64) {
-        const uint32_t slot = s + lane;
+    if (lane == 0) w_n[wv] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; ++k) tot += w_n[k];
+        b_at = tot ? atomicAdd(nout, tot) : 0u;
+    }
+    __syncthreads();
+    if (!live || n == 0) return;
+    uint32_t at = b_at;
+    for (uint32_t k = 0; k < wv; ++k) at += w_n[k];
+    for (uint32_t s0 = 0; s0 < c.D; s0 += 64) {
+        const uint32_t slot = s0 + lane;
         const uint32_t v = slot < c.D ? base[slot] : 0u;
         const bool fr = slot < c.D && v >= minsup;
-        const bool partner = __shfl_xor(int(fr), 1, 64) != 0;
-        const uint64_t lead = __ballot((fr || partner) && !(lane & 1u));
-        const uint32_t crank = nrank + uint32_t(__popcll(lead & lead_lt));
         const uint64_t fb = __ballot(fr);
-        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{row_base + g, slot, v, crank << 1 | (slot & 1u)};
-        o += uint64_t(__popcll(fb));
-        nrank += uint32_t(__popcll(lead));
+        const uint32_t x = at + uint32_t(__popcll(fb & lanemask_lt()));
+        if (fr && x < cap) out[x] = FreqRec{row_base + g, slot, v, 0u};
+        at += uint32_t(__popcll(fb));
     }
 }
 
@@ -888,6 +892,33 @@ struct PNode {
     uint32_t support;
 };
 
+// Frequent-pair records in (row, slot) order with their child member ids: rank among
+// the row's slots with a frequent temporal or equality candidate, << 1 | type (the ids
+// k_freq_write assigns in-kernel).  Counting sort by row, then the few slots of a row.
+void order_recs(std::vector<FreqRec>& recs, uint32_t nrows) {
+    std::vector<uint32_t> off(size_t(nrows) + 1, 0);
+    for (const FreqRec& r : recs) ++off[size_t(r.row) + 1];
+    for (uint32_t x = 0; x < nrows; ++x) off[x + 1] += off[x];
+    std::vector<FreqRec> tmp(recs.size());
+    std::vector<uint32_t> at(off.begin(), off.end() - 1);
+    for (const FreqRec& r : recs) tmp[at[r.row]++] = r;
+    for (uint32_t x = 0; x < nrows; ++x)
+        if (off[x + 1] - off[x] > 1)
+            std::sort(tmp.begin() + off[x], tmp.begin() + off[x + 1],
+                      [](const FreqRec& a, const FreqRec& c) { return a.slot < c.slot; });
+    recs.swap(tmp);
+    for (size_t q = 0; q < recs.size();) {
+        size_t q2 = q;
+        uint32_t crank = 0;
+        while (q2 < recs.size() && recs[q2].row == recs[q].row) {
+            if (q2 > q && (recs[q2].slot >> 1) != (recs[q2 - 1].slot >> 1)) ++crank;
+            recs[q2].cid = crank << 1 | (recs[q2].slot & 1u);
+            ++q2;
+        }
+        q = q2;
+    }
+}
+
 struct Batch {
     Slab slab;
     std::vector<ClassMeta> cls;
@@ -1193,29 +1224,7 @@ struct Miner {
         // (row, slot) order and child member ids: rank among the row's slots with a frequent
         // temporal or equality candidate, << 1 | type (as k_freq_write assigns them)
         const double th0 = now_ms();
-        {  // (row, slot) order: counting sort by row, then the few slots of each row
-            std::vector<uint32_t> off(size_t(F) + 1, 0);
-            for (const FreqRec& r : recs) ++off[size_t(r.row) + 1];
-            for (uint32_t x = 0; x < F; ++x) off[x + 1] += off[x];
-            std::vector<FreqRec> tmp(recs.size());
-            std::vector<uint32_t> at(off.begin(), off.end() - 1);
-            for (const FreqRec& r : recs) tmp[at[r.row]++] = r;
-            for (uint32_t x = 0; x < F; ++x)
-                if (off[x + 1] - off[x] > 1)
-                    std::sort(tmp.begin() + off[x], tmp.begin() + off[x + 1],
-                              [](const FreqRec& a, const FreqRec& c) { return a.slot < c.slot; });
-            recs.swap(tmp);
-        }
-        for (size_t q = 0; q < recs.size();) {
-            size_t q2 = q;
-            uint32_t crank = 0;
-            while (q2 < recs.size() && recs[q2].row == recs[q].row) {
-                if (q2 > q && (recs[q2].slot >> 1) != (recs[q2 - 1].slot >> 1)) ++crank;
-                recs[q2].cid = crank << 1 | (recs[q2].slot & 1u);
-                ++q2;
-            }
-            q = q2;
-        }
+        order_recs(recs, F);
         hp[0] += now_ms() - th0;
         return true;
     }
@@ -1264,33 +1273,34 @@ struct Miner {
                 FSM_LAUNCHED("k_count", s);
                 clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));
             }
-            DevBuf d_rows, rowcnt((size_t(nrows) + 1) * 4), rowoff((size_t(nrows) + 1) * 8);
+            DevBuf d_rows;
             upload(d_rows, std::vector<DRow>(rows.begin() + rlo, rows.begin() + rhi));
             const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
-            if (nrows) {
-                const size_t tk = clk->begin("k_freq_count");
-                hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
-                                   b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
-                FSM_LAUNCHED("k_freq_count", s);
+            // one pass, unordered records at block cursors; rare overflow: extract again at the exact size
+            uint32_t cap_recs = uint32_t(std::min<uint64_t>(std::max<uint64_t>(uint64_t(nrows) * 4, 4096), b.n_cnt));
+            // the records land in mapped pinned host memory: one stream sync per batch
+            DevBuf d_n(4);
+            for (int attempt = 0; nrows; ++attempt) {
+                PinnedBuf* pb = ctx->pinned_big(size_t(std::max<uint32_t>(cap_recs, 1)) * sizeof(FreqRec));
+                FSM_HIP(hipMemsetAsync(d_n.p, 0, 4, s));
+                const size_t tk = clk->begin("k_freq_recs");
+                hipLaunchKernelGGL(k_freq_recs, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
+                                   b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rlo,
+                                   static_cast<FreqRec*>(pb->dev), cap_recs, d_n.as<uint32_t>());
+                FSM_LAUNCHED("k_freq_recs", s);
                 clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4));
-            }
-            scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
-            uint64_t nf = 0;
-            FSM_HIP(hipMemcpyAsync(&nf, rowoff.as<uint64_t>() + nrows, 8, hipMemcpyDeviceToHost, s));
-            sync();
-            recs.resize(nf);
-            if (nf) {
-                DevBuf d_recs(nf * sizeof(FreqRec));
-                const size_t tk = clk->begin("k_freq_write");
-                hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
-                                   b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
-                                   d_recs.as<FreqRec>());
-                FSM_LAUNCHED("k_freq_write", s);
-                clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
-                                     nf * sizeof(FreqRec)));
-                FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nf * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
+                FSM_HIP(hipMemcpyAsync(&pend[1], d_n.p, 4, hipMemcpyDeviceToHost, s));
                 sync();
+                const uint32_t nf = uint32_t(pend[1] & 0xFFFFFFFFu);
+                if (nf <= cap_recs) {
+                    const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
+                    recs.assign(hr, hr + nf);
+                    break;
+                }
+                if (attempt > 0) throw Error(FSM_EDEVICE, "SPADE: frequent candidate buffer overflow");
+                cap_recs = nf;
             }
+            order_recs(recs, rhi);
         }
         };
         if (shard) {  // a failure here or in run_root reaches every rank before the gather below
