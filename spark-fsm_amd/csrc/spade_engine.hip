@@ -924,7 +924,10 @@ struct Batch {
     std::vector<ClassMeta> cls;
     std::vector<DClass> h_cls;
     DevBuf d_cls;
-    DevBuf kid_off, kid_slot, kid_cid;  // frequent children of every member (CSR over cbase + mi)
+    DevBuf kid_tab;  // frequent children of every member (CSR over cbase + mi): offsets | slots | child ids
+    const uint32_t* kid_off = nullptr;
+    const uint32_t* kid_slot = nullptr;
+    const uint32_t* kid_cid = nullptr;
     uint64_t E = 0;                     // entries in the slab (runs of all classes, any order)
     uint64_t n_cnt = 0, cbase_total = 0;
     std::vector<uint32_t> rank_item;  // member tables of cls (see ClassMeta)
@@ -1322,22 +1325,31 @@ struct Miner {
         }
         double th = now_ms();
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
-        std::vector<uint32_t> koff(b.cbase_total + 1, 0), kslot(nfreq), kcid(nfreq);
+        // one table, one H2D copy: [koff: cbase_total + 1 | kslot: nfreq | kcid: nfreq]
+        const size_t nko = size_t(b.cbase_total) + 1;
+        std::vector<uint32_t> ktab(nko + 2 * size_t(nfreq), 0);
+        uint32_t* koff = ktab.data();
+        uint32_t* kslot = koff + nko;
+        uint32_t* kcid = kslot + nfreq;
         for (const FreqRec& fr : recs) koff[b.cls[rows[fr.row].cls].cbase + rows[fr.row].mi + 1] += 1;
         for (uint64_t x = 0; x < b.cbase_total; ++x) koff[x + 1] += koff[x];
         for (uint64_t q = 0; q < nfreq; ++q) {  // recs are ordered by (row, slot) = CSR order
             kslot[q] = recs[q].slot;
             kcid[q] = recs[q].cid;
         }
-        upload(b.kid_off, koff);
-        upload(b.kid_slot, kslot);
-        upload(b.kid_cid, kcid);
+        upload(b.kid_tab, ktab);
+        b.kid_off = b.kid_tab.as<uint32_t>();
+        b.kid_slot = b.kid_off + nko;
+        b.kid_cid = b.kid_slot + nfreq;
         hp[1] += now_ms() - th;
         th = now_ms();
         // children (new pattern nodes) in deterministic (row, slot) order
         b.children.clear();
         b.child_rank_item.clear();
         b.child_node_of.clear();
+        b.children.reserve(recs.size());
+        b.child_rank_item.reserve(recs.size() + 16);
+        b.child_node_of.reserve(2 * recs.size() + 16);
         for (size_t q = 0; q < recs.size();) {
             const uint32_t row = recs[q].row;
             const DRow pr = rows[row];
@@ -1506,8 +1518,8 @@ struct Miner {
             const size_t tk = clk->begin("k_emit");
 #define FSM_EMIT1(WW)                                                                                               \
     hipLaunchKernelGGL(k_emit1<WW>, dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),     \
-                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),       \
-                       b.kid_cid.as<uint32_t>(), d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
+                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                                         \
+                       b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
                        nb.slab.cap, emit_cap())
             FSM_W_DISPATCH(W, FSM_EMIT1)
 #undef FSM_EMIT1
@@ -1522,8 +1534,8 @@ struct Miner {
             const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, emit_grid_cap()));
 #define FSM_EMIT(WW, WR)                                                                                            \
     hipLaunchKernelGGL((k_emit<WW, WR>), dim3(grid), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
-                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off.as<uint32_t>(), b.kid_slot.as<uint32_t>(),        \
-                       b.kid_cid.as<uint32_t>(), d_child_of.as<uint32_t>(), ncnt.as<uint32_t>(),                   \
+                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                                          \
+                       b.kid_cid, d_child_of.as<uint32_t>(), ncnt.as<uint32_t>(),                   \
                        off.as<uint64_t>(), op, nb.slab.cap)
 #define FSM_EMIT_COUNT(WW) FSM_EMIT(WW, false)
 #define FSM_EMIT_WRITE(WW) FSM_EMIT(WW, true)
