@@ -266,6 +266,53 @@ struct F2Ent {
 };
 constexpr uint32_t kF2MaxRows = 4096;  // rows per block of k_f2_keys (row offsets staged in LDS)
 
+// Root rows fused with the F2 plan: block b builds the root runs of its row block
+// (rpb rows, one wave per row in turn, as k_root_write) and histograms the key
+// capacity of every entry it writes by rank group (k_f2_plan's numbers) in LDS.
+template <int W>
+__global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* __restrict__ row_off,
+                                                               const uint32_t* __restrict__ item,
+                                                               const uint64_t* __restrict__ mask,
+                                                               const uint32_t* __restrict__ rank, uint32_t R,
+                                                               uint32_t rpb, const uint64_t* __restrict__ off,
+                                                               SlabPtrs o, uint32_t pm, uint32_t G, uint32_t nblk,
+                                                               uint32_t mlo, uint32_t mhi, int bg,
+                                                               uint32_t* __restrict__ cap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+    for (uint32_t r = r0 + wave; r < r1; r += kF2Waves) {
+        const uint64_t ob = off[r];
+        const uint32_t len = uint32_t(off[r + 1] - ob);
+        const uint32_t e1 = row_off[r + 1];
+        uint32_t k = 0;
+        for (uint32_t b0 = row_off[r]; b0 < e1; b0 += 64) {
+            const uint32_t e = b0 + lane;
+            const uint32_t rk = e < e1 ? rank[item[e]] : kNone;
+            const bool fr = rk != kNone;
+            const uint64_t bal = __ballot(fr);
+            if (fr) {
+                const uint32_t p = k + uint32_t(__popcll(bal & lanemask_lt()));
+                uint64_t m[W];
+                load_mask<W>(mask + size_t(e) * W, m);
+                const uint64_t d = ob + p;
+                o.mem[d] = rk << 1 | kSeq;
+                o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+                o.pos[d] = (p << 16) | len;
+                store_mask<W>(o.mask + size_t(d) * W, m);
+                if ((rk << 1) - mlo < mhi - mlo) atomicAdd(&h[group_of(rk, pm)], 2 * len - 1 - p);
+            }
+            k += uint32_t(__popcll(bal));
+        }
+    }
+    __syncthreads();
+    // regions start on 16-byte boundaries (8 keys): k_f2_count reads them in aligned chunks
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+        cap[f2_region(g, blockIdx.x, G, nblk, bg)] = (h[g] + 7u) & ~7u;
+}
+
 template <int W>
 __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restrict__ roff, uint32_t R, uint32_t rpb,
                                                         const uint32_t* __restrict__ mem,
@@ -941,6 +988,10 @@ struct Batch {
     bool root = false;
     DevBuf root_rows;   // root batch: u64 [R+1] slab offset of every DB row's run
     uint64_t R = 0;
+    // root batch: F2 plan made by k_root_write_plan (region bases scanned, slot total read back)
+    bool f2_planned = false;
+    DevBuf f2_base;
+    uint64_t f2_nslots = 0;
 };
 
 struct Miner {
@@ -1126,6 +1177,11 @@ struct Miner {
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kChunk;
     }
     // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
+    // FSM_F2_FUSED=0: the F2 plan as its own kernel after the root rows (A/B knob)
+    static bool f2_fused() {
+        const char* v = std::getenv("FSM_F2_FUSED");
+        return !(v && v[0] == '0');
+    }
     // FSM_F2_LAYOUT=bg: key regions block-major instead of group-major (A/B knob)
     static bool f2_block_major() {
         const char* v = std::getenv("FSM_F2_LAYOUT");
@@ -1141,37 +1197,65 @@ struct Miner {
     // with their child member ids.  Returns false when a counter row does not
     // fit the LDS group tile, the groups are too many or the key slots exceed
     // 2^32 (the caller then takes the global-atomic path).
+    // root F2 geometry: rank groups of `per` counter rows (128 KiB of LDS), row blocks of
+    // rpb rows; ok = false when the group path does not apply (the atomic path runs)
+    struct F2Geo {
+        bool ok = false;
+        uint32_t D = 0, F = 0, per = 0, G = 0, pm = 0, mlo = 0, mhi = 0, R = 0, rpb = 0, nblk = 0;
+        uint64_t nd = 0;
+    };
+    F2Geo f2_geometry(const Batch& b, uint32_t D, uint64_t nent, uint64_t Rrows) const {
+        F2Geo g;
+        const uint32_t F = D / 2;
+        if (nent == 0 || D > kGroupCounters || Rrows == 0 || F >= (1u << 15) || root_atomic()) return g;
+        g.D = D;
+        g.F = F;
+        g.per = kGroupCounters / D;
+        g.G = (F + g.per - 1) / g.per;
+        if (g.G > kMaxGroups) return g;
+        g.pm = uint32_t(((uint64_t(1) << 32) + g.per - 1) / g.per);  // group_of multiplier
+        g.mlo = member_lo(b);
+        g.mhi = member_hi(b);
+        g.R = uint32_t(Rrows);
+        const uint32_t nb_want = std::min<uint32_t>(f2_blocks(), kF2MaxBlocks);
+        g.rpb = std::min<uint32_t>(kF2MaxRows, std::max<uint32_t>(16u, (g.R + nb_want - 1) / nb_want));
+        if (uint64_t(g.rpb) * kF2MaxBlocks < g.R) return g;  // more rows than the LDS-indexed blocks cover
+        g.nblk = (g.R + g.rpb - 1) / g.rpb;
+        g.nd = uint64_t(g.G) * g.nblk;
+        g.ok = true;
+        return g;
+    }
+
     bool root_f2(Batch& b, std::vector<FreqRec>& recs) {
         const ClassMeta& m = b.cls[0];
-        const uint32_t D = m.D, F = m.D / 2;
-        if (m.nent == 0 || D > kGroupCounters || b.root_rows.p == nullptr || b.R == 0 || F >= (1u << 15)) return false;
-        const uint32_t per = kGroupCounters / D;
-        const uint32_t G = (F + per - 1) / per;
-        if (G > kMaxGroups) return false;
-        const uint32_t pm = uint32_t(((uint64_t(1) << 32) + per - 1) / per);  // group_of multiplier
-        const uint32_t mlo = member_lo(b), mhi = member_hi(b);
+        if (b.root_rows.p == nullptr) return false;
+        const F2Geo geo = f2_geometry(b, m.D, m.nent, b.R);
+        if (!geo.ok) return false;
+        const uint32_t D = geo.D, F = geo.F, per = geo.per, G = geo.G, pm = geo.pm, mlo = geo.mlo, mhi = geo.mhi;
         const uint32_t rlo = comm ? slice_lo : 0u, rhi = comm ? std::min(slice_hi, F) : F;
-        const uint32_t R = uint32_t(b.R);
-        const uint32_t nb_want = std::min<uint32_t>(f2_blocks(), kF2MaxBlocks);
-        const uint32_t rpb = std::min<uint32_t>(kF2MaxRows, std::max<uint32_t>(16u, (R + nb_want - 1) / nb_want));
-        if (uint64_t(rpb) * kF2MaxBlocks < R) return false;  // more rows than the LDS-indexed blocks cover
-        const uint32_t nblk = (R + rpb - 1) / rpb;
-        const uint64_t nd = uint64_t(G) * nblk;
+        const uint32_t R = geo.R, rpb = geo.rpb, nblk = geo.nblk;
+        const uint64_t nd = geo.nd;
         const int bg = f2_block_major() ? 1 : 0;
         const SlabPtrs sp = b.slab.ptrs();
         const int64_t E0 = int64_t(m.nent);
-        // plan: region capacities -> bases
-        DevBuf cap(nd * 4), base((nd + 1) * 8), fill(nd * 4);
-        size_t tk = clk->begin("k_f2_plan");
-        hipLaunchKernelGGL(k_f2_plan, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, b.root_rows.as<uint64_t>(), R, rpb,
-                           sp.mem, sp.pos, pm, G, nblk, mlo, mhi, bg, cap.as<uint32_t>());
-        FSM_LAUNCHED("k_f2_plan", s);
-        clk->end(tk, E0 * 8 + int64_t(nd) * 4);
-        scan_exclusive(cap.as<uint32_t>(), base.as<uint64_t>(), nd, s);
+        DevBuf base, fill(nd * 4);
         uint64_t nslots = 0;
-        FSM_HIP(hipMemcpyAsync(&nslots, base.as<uint64_t>() + nd, 8, hipMemcpyDeviceToHost, s));
-        sync();
-        cap.release();
+        size_t tk = 0;
+        if (b.f2_planned) {  // planned while the root rows were written (k_root_write_plan)
+            base = std::move(b.f2_base);
+            nslots = b.f2_nslots;
+        } else {  // plan: region capacities -> bases
+            DevBuf cap(nd * 4);
+            base.alloc((nd + 1) * 8);
+            tk = clk->begin("k_f2_plan");
+            hipLaunchKernelGGL(k_f2_plan, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, b.root_rows.as<uint64_t>(), R,
+                               rpb, sp.mem, sp.pos, pm, G, nblk, mlo, mhi, bg, cap.as<uint32_t>());
+            FSM_LAUNCHED("k_f2_plan", s);
+            clk->end(tk, E0 * 8 + int64_t(nd) * 4);
+            scan_exclusive(cap.as<uint32_t>(), base.as<uint64_t>(), nd, s);
+            FSM_HIP(hipMemcpyAsync(&nslots, base.as<uint64_t>() + nd, 8, hipMemcpyDeviceToHost, s));
+            sync();
+        }
         if (nslots >= (uint64_t(1) << 32) - 4096) return false;  // region cursors are u32
         // the one enumeration (keys padded: k_f2_count reads whole 16-byte words past a region's end)
         DevBuf keys((nslots + 1024) * 2), nk(8);
@@ -1599,7 +1683,30 @@ struct Miner {
         root.E = E0;
         ctx->stats.root_entries = int64_t(E0);
         FSM_HIP(hipMemsetAsync(root.slab.cid.p, 0, E0 * 4, s));
-        if (r1 > r0) {
+        // the root batch's F2 geometry (its slab is this root slab): plan fused into the write
+        const uint32_t F = uint32_t(freq_items.size());
+        root.root = true;
+        const F2Geo geo = f2_geometry(root, 2 * F, E0, r1 - r0);
+        if (r1 > r0 && geo.ok && f2_fused()) {
+            const SlabPtrs op = root.slab.ptrs();
+            const int bg = f2_block_major() ? 1 : 0;
+            DevBuf cap(geo.nd * 4);
+            root.f2_base.alloc((geo.nd + 1) * 8);
+            const size_t tk = clk->begin("k_root_write");
+#define FSM_ROOTWP(WW)                                                                                            \
+    hipLaunchKernelGGL(k_root_write_plan<WW>, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,              \
+                       db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), db->mask.as<uint64_t>(),               \
+                       d_rank.as<uint32_t>(), geo.R, geo.rpb, roff.as<uint64_t>(), op, geo.pm, geo.G, geo.nblk,    \
+                       geo.mlo, geo.mhi, bg, cap.as<uint32_t>())
+            FSM_W_DISPATCH(W, FSM_ROOTWP)
+#undef FSM_ROOTWP
+            FSM_LAUNCHED("k_root_write", s);
+            clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W)) + E0 * (16 + 8 * uint64_t(W)) +
+                                 geo.nd * 4));
+            scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), geo.nd, s);
+            FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + geo.nd, 8, hipMemcpyDeviceToHost, s));
+            root.f2_planned = true;
+        } else if (r1 > r0) {
             const SlabPtrs op = root.slab.ptrs();
             const unsigned grid = unsigned(((r1 - r0) * 64 + kBlock - 1) / kBlock);
             const size_t tk = clk->begin("k_root_write");
@@ -1613,7 +1720,6 @@ struct Miner {
             clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W)) + E0 * (16 + 8 * uint64_t(W))));
         }
         ClassMeta m;
-        const uint32_t F = uint32_t(freq_items.size());
         m.D = 2 * F;
         m.mshift = 1;  // root members are all sequence-extensions: counter rows by rank
         m.ri_off = 0;
@@ -1630,6 +1736,7 @@ struct Miner {
         root.root_rows = std::move(roff);
         root.R = r1 - r0;
         sync();
+        if (root.f2_planned) root.f2_nslots = pend[2];
     }
 
 };

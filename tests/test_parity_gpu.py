@@ -355,7 +355,7 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["group", "group-few-blocks", "block-major", "atomic"])
+@pytest.mark.parametrize("path", ["group", "group-few-blocks", "block-major", "plan-unfused", "atomic"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
     """The root F2 implementations (key runs counted per rank group, at the
     default and at a small block chunk; global atomics) give the oracle's
@@ -368,6 +368,8 @@ def test_root_f2_paths_agree(eng, path, monkeypatch):
         monkeypatch.setenv("FSM_F2_BLOCKS", "3")
     if path == "block-major":
         monkeypatch.setenv("FSM_F2_LAYOUT", "bg")
+    if path == "plan-unfused":
+        monkeypatch.setenv("FSM_F2_FUSED", "0")
     ds = gen.quest(20000, seed=4)
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
     pats, meta, st = gpu_spade(eng, None, 0.003, tokens=ds)
