@@ -45,6 +45,7 @@ namespace fsm {
 namespace {
 
 constexpr uint32_t kSeq = 0, kItm = 1;
+constexpr uint32_t kFreqOnePassRows = 16384;  // counter rows of a batch up to which k_freq_recs extracts in one pass
 constexpr uint32_t kChunk = 512;         // class entries per k_count block (FSM_COUNT_CHUNK; swept on MI355X)
 constexpr uint32_t kGroupCounters = 32768;  // root F2: u32 LDS counters of one rank group (128 KiB)
 constexpr uint32_t kMaxGroups = 16384;      // root F2 rank groups: LDS cursors of k_f2_keys (64 KiB)
@@ -549,6 +550,52 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
     }
 }
 
+// Ordered frequent extraction (large batches): k_freq_count -> scan -> k_freq_write
+// gives the records in (row, slot) order with their child ids, no host ordering.
+__global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ rows, uint32_t nrows,
+                                                       const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
+                                                       uint32_t minsup, uint32_t* __restrict__ rowcnt) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (g >= nrows) return;
+    const DRow r = rows[g];
+    const DClass c = cls[r.cls];
+    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
+    uint32_t n = 0;
+    for (uint32_t s = 0; s < c.D; s += 64) {
+        const uint32_t slot = s + lane_id();
+        const uint32_t v = slot < c.D ? base[slot] : 0u;
+        n += __popcll(__ballot(v >= minsup));
+    }
+    if (lane_id() == 0) rowcnt[g] = n;
+}
+
+__global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ rows, uint32_t nrows,
+                                                       const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
+                                                       uint32_t minsup, const uint64_t* __restrict__ rowoff,
+                                                       uint32_t row_base, FreqRec* __restrict__ out) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (g >= nrows) return;
+    const DRow r = rows[g];
+    const DClass c = cls[r.cls];
+    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
+    uint64_t o = rowoff[g];
+    uint32_t nrank = 0;
+    const unsigned lane = lane_id();
+    const uint64_t lead_lt = (1ull << (lane & ~1u)) - 1ull;
+    for (uint32_t s = 0; s < c.D; s += 64) {
+        const uint32_t slot = s + lane;
+        const uint32_t v = slot < c.D ? base[slot] : 0u;
+        const bool fr = slot < c.D && v >= minsup;
+        const bool partner = __shfl_xor(int(fr), 1, 64) != 0;
+        const uint64_t lead = __ballot((fr || partner) && !(lane & 1u));
+        const uint32_t crank = nrank + uint32_t(__popcll(lead & lead_lt));
+        const uint64_t fb = __ballot(fr);
+        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{row_base + g, slot, v, crank << 1 | (slot & 1u)};
+        o += uint64_t(__popcll(fb));
+        nrank += uint32_t(__popcll(lead));
+    }
+}
+
 // One-pass frequent extraction: one wave per counter row ballots the frequent
 // candidates and appends FreqRec{row, slot, sup} at a block cursor reserved with
 // one global atomic per block (unordered; the host orders them, order_recs).
@@ -1013,7 +1060,7 @@ struct Miner {
 
     double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
     // FSM_HOST_TRACE=1: host time of the bookkeeping phases, printed at the end of the mine
-    double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f2 sort, kids CSR+upload, children, plan/groups, emit tables, slab alloc
+    double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f2 sort, kids, children, groups, emit tables, slab alloc, count prep, count
 
     // Sharded mining: a failure on one rank must not leave its peers blocked in
     // a collective.  The work between two collectives runs through
@@ -1317,6 +1364,7 @@ struct Miner {
     }
     // count kernel + frequent-candidate extraction; fills b.children / b.groups / kids
     void count_and_freq(Batch& b) {
+        const double tc0 = now_ms();
         dump(b);
         prepare(b);
         const bool shard = comm && b.root;  // root rows split over ranks, frequent pairs all-gathered
@@ -1340,6 +1388,8 @@ struct Miner {
         const uint32_t nrows = rhi - rlo;
         std::vector<FreqRec> recs;
         DevBuf cnt;
+        hp[6] += now_ms() - tc0;  // prepare + stats + rows
+        const double tc1 = now_ms();
         auto compute = [&] {
         // the root: pairs counted per rank group, only the frequent ones leave the device
         const bool root_done = b.E && b.root && !root_atomic() && root_f2(b, recs);
@@ -1363,6 +1413,36 @@ struct Miner {
             DevBuf d_rows;
             upload(d_rows, std::vector<DRow>(rows.begin() + rlo, rows.begin() + rhi));
             const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
+            if (nrows > kFreqOnePassRows) {
+                // large batches: ordered extraction (the host ordering and the mapped-memory
+                // reads of millions of records cost more than the extra sync)
+                DevBuf rowcnt((size_t(nrows) + 1) * 4), rowoff((size_t(nrows) + 1) * 8);
+                {
+                    const size_t tk = clk->begin("k_freq_count");
+                    hipLaunchKernelGGL(k_freq_count, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
+                                       b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowcnt.as<uint32_t>());
+                    FSM_LAUNCHED("k_freq_count", s);
+                    clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4));
+                }
+                scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nrows, s);
+                FSM_HIP(hipMemcpyAsync(&pend[1], rowoff.as<uint64_t>() + nrows, 8, hipMemcpyDeviceToHost, s));
+                sync();
+                const uint64_t nf = pend[1];
+                recs.resize(nf);
+                if (nf) {
+                    DevBuf d_recs(nf * sizeof(FreqRec));
+                    const size_t tk = clk->begin("k_freq_write");
+                    hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
+                                       b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
+                                       d_recs.as<FreqRec>());
+                    FSM_LAUNCHED("k_freq_write", s);
+                    clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
+                                         nf * sizeof(FreqRec)));
+                    FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nf * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
+                    sync();
+                }
+                return;
+            }
             // one pass, unordered records at block cursors; rare overflow: extract again at the exact size
             uint32_t cap_recs = uint32_t(std::min<uint64_t>(std::max<uint64_t>(uint64_t(nrows) * 4, 4096), b.n_cnt));
             // the records land in mapped pinned host memory: one stream sync per batch
@@ -1398,6 +1478,7 @@ struct Miner {
         }
         uint64_t nfreq = recs.size();
         cnt.release();
+        hp[7] += now_ms() - tc1;  // device count + extraction + ordering (incl. waits)
         if (shard) {  // every rank gets every frequent pair, in row order (slices ascend with the rank)
             std::vector<uint8_t> mine(recs.size() * sizeof(FreqRec));
             if (!recs.empty()) std::memcpy(mine.data(), recs.data(), mine.size());
@@ -1968,8 +2049,8 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     ctx->stats.ms_lattice = now_ms() - t2;
     if (const char* v = std::getenv("FSM_HOST_TRACE"); v && v[0] == '1')
         std::fprintf(stderr, "[fsm host] f2 sort %.3f, kids %.3f, children %.3f, groups %.3f, emit tables %.3f, "
-                     "slab alloc %.3f, gpu wait %.3f ms\n", mn.hp[0], mn.hp[1], mn.hp[2], mn.hp[3], mn.hp[4], mn.hp[5],
-                     mn.wait_ms);
+                     "slab alloc %.3f, count prep %.3f, count+extract %.3f, gpu wait %.3f ms\n", mn.hp[0], mn.hp[1],
+                     mn.hp[2], mn.hp[3], mn.hp[4], mn.hp[5], mn.hp[6], mn.hp[7], mn.wait_ms);
     clock.finish(ctx->kstats);
     for (const fsm_kernel_stat& k : ctx->kstats) {
         const std::string nm = k.name;

@@ -181,15 +181,16 @@ def load():
     L.fsm_tsr_mine.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_double, P(P(Rules))]
     L.fsm_rules_free.argtypes = [P(Rules)]
     L.fsm_rules_free.restype = None
-    L.fsm_ingest.argtypes = [ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, P(P(TokenDb))]
-    L.fsm_token_db_free.argtypes = [P(TokenDb)]
-    L.fsm_token_db_free.restype = None
-    for fn, st in (("fsm_patterns_serialize", Patterns), ("fsm_patterns_json", Patterns), ("fsm_rules_json", Rules)):
-        getattr(L, fn).argtypes = [P(st), P(vp), P(ctypes.c_int64)]
-    L.fsm_buffer_free.argtypes = [vp]
-    L.fsm_buffer_free.restype = None
-    L.fsm_rules_query.argtypes = [P(Rules), ctypes.c_int32, P(ctypes.c_int32), ctypes.c_int64, P(ctypes.c_int64),
-                                  P(ctypes.c_int64)]
+    if hasattr(L, "fsm_ingest"):  # (absent only from older builds loaded through FSM_LIB_PATH for A/B runs)
+        L.fsm_ingest.argtypes = [ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, P(P(TokenDb))]
+        L.fsm_token_db_free.argtypes = [P(TokenDb)]
+        L.fsm_token_db_free.restype = None
+        for fn, st in (("fsm_patterns_serialize", Patterns), ("fsm_patterns_json", Patterns), ("fsm_rules_json", Rules)):
+            getattr(L, fn).argtypes = [P(st), P(vp), P(ctypes.c_int64)]
+        L.fsm_buffer_free.argtypes = [vp]
+        L.fsm_buffer_free.restype = None
+        L.fsm_rules_query.argtypes = [P(Rules), ctypes.c_int32, P(ctypes.c_int32), ctypes.c_int64,
+                                      P(ctypes.c_int64), P(ctypes.c_int64)]
     _lib = L
     return L
 

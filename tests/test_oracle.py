@@ -148,3 +148,4 @@ def test_tsr_negative_item_only_fails_in_closed_itemsets():
     assert r["rules"] == [((1,), (2,), 2, 2 / 3)]
     with pytest.raises(oracle.OracleError):
         oracle.tsr([(0, "1 -1 -5 -1")], 3, 0.5)
+
