@@ -293,7 +293,14 @@ int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_pa
     return guarded(ctx, [&] {
         FSM_HIP(hipSetDevice(ctx->opts.device));
         reset_stats(ctx);
-        fsm::spade_mine(ctx, db, support, out);
+        const bool prof = fsm::host_prof_start();
+        try {
+            fsm::spade_mine(ctx, db, support, out);
+        } catch (...) {
+            if (prof) fsm::host_prof_stop();
+            throw;
+        }
+        if (prof) fsm::host_prof_stop();
     });
 }
 
@@ -306,7 +313,14 @@ int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules*
     return guarded(ctx, [&] {
         FSM_HIP(hipSetDevice(ctx->opts.device));
         reset_stats(ctx);
-        fsm::tsr_mine(ctx, db, k, minconf, out);
+        const bool prof = fsm::host_prof_start();
+        try {
+            fsm::tsr_mine(ctx, db, k, minconf, out);
+        } catch (...) {
+            if (prof) fsm::host_prof_stop();
+            throw;
+        }
+        if (prof) fsm::host_prof_stop();
     });
 }
 

@@ -256,4 +256,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out);
 void tsr_upload(fsm_ctx* ctx, fsm_db* db);
 void tsr_release(fsm_db* db);
 void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** out);
+// FSM_HOST_PROF=<file>: SIGPROF sampling of the host side of a mine (host_prof.cpp)
+bool host_prof_start();
+void host_prof_stop();
 }  // namespace fsm
