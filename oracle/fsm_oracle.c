@@ -248,7 +248,7 @@ static int first_bit(const uint64_t* m, int W) {
  * after the first bit of a (P x -> y), equality keeps a & b (P (x y)). */
 static void join(const ilist* a, const ilist* b, int W, int temporal, ilist* out) {
     int64_t i = 0, j = 0;
-    uint64_t res[64];
+    uint64_t res[1024]; /* W <= 1024: 65,536 distinct timestamps per sequence */
     out->n = 0;
     while (i < a->n && j < b->n) {
         int32_t sa = a->sid[i], sb = b->sid[j];
@@ -503,8 +503,8 @@ static int spade_core(regvec* regsp, int64_t n, double support, double time_limi
         }
         int W = (maxE + 63) / 64;
         if (W < 1) W = 1;
-        if (W > 64) {
-            set_err(err, errlen, "SPADE oracle: sequence with %d distinct timestamps exceeds 4096", maxE);
+        if (W > 1024) {
+            set_err(err, errlen, "SPADE oracle: sequence with %d distinct timestamps exceeds 65536", maxE);
             free(eid);
             free(sidx);
             rc = -1;
@@ -519,7 +519,7 @@ static int spade_core(regvec* regsp, int64_t n, double support, double time_limi
         for (int64_t q = 0; q < nreg; q++)
             if (q == 0 || uitems[q] != uitems[q - 1]) uitems[nitems++] = uitems[q];
         ilist* vert = calloc((size_t)(nitems ? nitems : 1), sizeof(ilist));
-        uint64_t m[64];
+        uint64_t m[1024];
         /* F1 vertical build (SPADE.scala:53-106): one id-list per distinct item */
         for (int64_t a = 0; a < nreg;) {
             int64_t b = a;

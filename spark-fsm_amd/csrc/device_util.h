@@ -87,6 +87,50 @@ template <int W> __device__ __forceinline__ void mask_clear_upto(uint64_t (&m)[W
     }
 }
 
+// --- runtime-width masks (W == 0: more than 64 words, up to kMaxMaskWords) --
+// Sequences with more than 4,096 distinct timestamps take the W = 0 kernel
+// instantiations: masks are not held in registers but read from HBM (L1/L2)
+// word by word, `wd` words each.  mask_words<W>(wd) is the per-entry stride.
+template <int W> __device__ __forceinline__ uint32_t mask_words(uint32_t wd) { return W ? uint32_t(W) : wd; }
+
+// a mask operand: in registers (W > 0) or by address (W == 0)
+template <int W> struct MaskV {
+    uint64_t w[W];
+    __device__ __forceinline__ void load(const uint64_t* __restrict__ p, uint32_t) { load_mask<W>(p, w); }
+    __device__ __forceinline__ bool and_any(const uint64_t* __restrict__ b, uint32_t) const {
+        uint64_t bm[W];
+        load_mask<W>(b, bm);
+        uint64_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) acc |= w[k] & bm[k];
+        return acc != 0;
+    }
+};
+template <> struct MaskV<0> {
+    const uint64_t* p;
+    __device__ __forceinline__ void load(const uint64_t* __restrict__ q, uint32_t) { p = q; }
+    __device__ __forceinline__ bool and_any(const uint64_t* __restrict__ b, uint32_t wd) const {
+        for (uint32_t k = 0; k < wd; ++k)
+            if (p[k] & b[k]) return true;
+        return false;
+    }
+};
+
+// copy src -> dst (wd words), returning first | last set eid << 16 (src non-zero)
+__device__ __forceinline__ uint32_t mask_copy_lohi_dyn(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                                       uint32_t wd) {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t k = 0; k < wd; ++k) {
+        const uint64_t v = src[k];
+        dst[k] = v;
+        if (v) {
+            if (lo == 0xFFFFFFFFu) lo = k * 64 + uint32_t(__builtin_ctzll(v));
+            hi = k * 64 + 63 - uint32_t(__builtin_clzll(v));
+        }
+    }
+    return (lo == 0xFFFFFFFFu ? 0u : lo) | (hi << 16);
+}
+
 // ---------------------------------------------------------------- scans
 // exclusive scan in[0..n) -> out[0..n], out[n] = total (u64 offsets)
 void scan_exclusive(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s);

@@ -276,11 +276,11 @@ void flatten_spade(const Source& src, FlatSpade& out) {
     std::vector<std::vector<int32_t>> ent_val(static_cast<size_t>(T2));
     std::vector<std::vector<uint64_t>> ent_msk(static_cast<size_t>(T2));   // row_words words per entry
     std::vector<std::vector<uint32_t>> row_len(static_cast<size_t>(T2));
-    std::vector<std::vector<uint8_t>> row_words(static_cast<size_t>(T2));
+    std::vector<std::vector<uint16_t>> row_words(static_cast<size_t>(T2));
     std::vector<int> maxE(size_t(T2), 0);
     std::vector<int64_t> maxOcc(size_t(T2), 0);
     parallel_chunks(R, T2, [&](int t, int64_t a, int64_t b) {
-        std::vector<uint64_t> buf;
+        std::vector<uint64_t> buf, m;
         std::vector<std::pair<int32_t, int32_t>> ie;  // (item, eid)
         auto& ev = ent_val[size_t(t)];
         auto& em = ent_msk[size_t(t)];
@@ -306,31 +306,32 @@ void flatten_spade(const Source& src, FlatSpade& out) {
             }
             maxE[size_t(t)] = std::max(maxE[size_t(t)], e + 1);
             maxOcc[size_t(t)] = std::max<int64_t>(maxOcc[size_t(t)], int64_t(ie.size()));
-            const int wr = std::max(1, std::min(64, (e + 1 + 63) / 64));
+            const int wr = std::max(1, std::min(int(kMaxMaskWords), (e + 1 + 63) / 64));
             std::sort(ie.begin(), ie.end());
             uint32_t len = 0;
             for (size_t q = 0; q < ie.size();) {
                 size_t s = q;
-                uint64_t m[64] = {0};
+                m.assign(size_t(wr), 0);
                 while (q < ie.size() && ie[q].first == ie[s].first) {
                     const int32_t ee = ie[q].second;
-                    if (ee < 4096) m[ee >> 6] |= 1ull << (ee & 63);
+                    if (ee < int32_t(64 * kMaxMaskWords)) m[size_t(ee >> 6)] |= 1ull << (ee & 63);
                     ++q;
                 }
                 ev.push_back(ie[s].first);
-                em.insert(em.end(), m, m + wr);
+                em.insert(em.end(), m.begin(), m.end());
                 ++len;
             }
             rl.push_back(len);
-            rw.push_back(uint8_t(wr - 1));
+            rw.push_back(uint16_t(wr - 1));
         }
     });
     int mE = 0;
     for (int v : maxE) mE = std::max(mE, v);
     for (int64_t v : maxOcc) out.max_occ = std::max(out.max_occ, v);
-    if (mE > 4096)
+    if (mE > int(64 * kMaxMaskWords))
         throw Error(FSM_ELIMIT, "SPADE: a sequence has " + std::to_string(mE) +
-                                    " distinct timestamps; the engine supports up to 4096");
+                                    " distinct timestamps; the engine supports up to " +
+                                    std::to_string(64 * kMaxMaskWords));
     int W = 1;
     while (W * 64 < mE) W *= 2;
     out.W = W;

@@ -37,6 +37,10 @@ bool debug_sync();
 void check_launch(const char* what, hipStream_t s, const char* file, int line);
 #define FSM_LAUNCHED(name, stream) ::fsm::check_launch(name, stream, __FILE__, __LINE__)
 
+// eid-mask words per SPADE entry at most: 65,536 distinct timestamps per sequence
+// (the first / last eid of an entry are 16-bit fields of the slab's lohi word)
+constexpr uint32_t kMaxMaskWords = 1024;
+
 inline double now_ms() {
     using namespace std::chrono;
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();

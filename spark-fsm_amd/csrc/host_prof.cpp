@@ -1,11 +1,14 @@
 // host_prof.cpp — a small SIGPROF sampler for the host side of a mine
 // (FSM_HOST_PROF=<file>: diagnostics only, off by default).  Every 50 us of
-// process CPU time the interrupted instruction pointer of the mining thread is
-// recorded; at the end each sample is written as "<object> <offset>" so the
+// wall time (a CLOCK_MONOTONIC POSIX timer aimed at the mining thread) the
+// interrupted instruction pointer of that thread is recorded; at the end each sample is written as "<object> <offset>" so the
 // offsets can be symbolized offline (llvm-symbolizer --obj=libfsm.so).
 #include <dlfcn.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <sys/time.h>
+#include <time.h>
+#include <unistd.h>
 #include <ucontext.h>
 
 #include <atomic>
@@ -24,6 +27,7 @@ constexpr size_t kMaxSamples = 1u << 20;
 uintptr_t g_ip[kMaxSamples];
 std::atomic<size_t> g_n{0};
 std::atomic<bool> g_on{false};
+timer_t g_timer;
 
 void on_prof(int, siginfo_t*, void* uc) {
     if (!g_on.load(std::memory_order_relaxed)) return;
@@ -41,16 +45,20 @@ bool host_prof_start() {
     sa.sa_flags = SA_SIGINFO | SA_RESTART;
     sigemptyset(&sa.sa_mask);
     sigaction(SIGPROF, &sa, nullptr);
+    sigevent sev{};
+    sev.sigev_notify = SIGEV_THREAD_ID;
+    sev.sigev_signo = SIGPROF;
+    sev._sigev_un._tid = pid_t(syscall(SYS_gettid));
+    if (timer_create(CLOCK_MONOTONIC, &sev, &g_timer) != 0) return false;
     g_on = true;
-    itimerval tv{{0, 50}, {0, 50}};
-    setitimer(ITIMER_PROF, &tv, nullptr);
+    itimerspec ts{{0, 50000}, {0, 50000}};
+    timer_settime(g_timer, 0, &ts, nullptr);
     return true;
 }
 
 void host_prof_stop() {
-    itimerval tv{{0, 0}, {0, 0}};
-    setitimer(ITIMER_PROF, &tv, nullptr);
     g_on = false;
+    timer_delete(g_timer);
     const char* path = std::getenv("FSM_HOST_PROF");
     if (!path) return;
     std::FILE* f = std::fopen(path, "a");

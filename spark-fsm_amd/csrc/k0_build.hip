@@ -489,7 +489,7 @@ bool k0_build(fsm_ctx* ctx, int mode, const Source& src, fsm_db* db) {
     FSM_HIP(hipMemcpyAsync(&st, d_st.p, sizeof(st), hipMemcpyDeviceToHost, s));
     FSM_HIP(hipStreamSynchronize(s));
     if (E >= (uint64_t(1) << 32)) return false;                    // host reports the limit
-    if (mode == FSM_MODE_SPADE && st.max_eids > 4096) return false;  // host reports the limit
+    if (mode == FSM_MODE_SPADE && st.max_eids > 4096) return false;  // wider masks: the host flatten (or its limit)
     if (mode == FSM_MODE_TSR && st.neg_item) return false;           // host reports the negative item
     std::vector<int32_t> ival(U);
     DevBuf d_ival(std::max<uint64_t>(U, 1) * 4);

@@ -57,7 +57,8 @@ struct DClass {
     uint32_t D;           // member id space (2 * ranks)
     uint32_t cbase;       // offset of the class's members in per-member arrays
     uint32_t mshift;      // counter row of member mi = mi >> mshift (root: 1, only SEQ members)
-    uint32_t pad[3];
+    uint32_t rstride;     // counters between consecutive rows (D, or a power of two >= D in keyed batches)
+    uint32_t pad[2];
 };
 struct DRow {
     uint32_t cls, mi;
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void k_root_write(const uint32_t* __restric
                                                        const uint32_t* __restrict__ item,
                                                        const uint64_t* __restrict__ mask,
                                                        const uint32_t* __restrict__ rank, uint64_t r0, uint64_t r1,
-                                                       const uint64_t* __restrict__ off, SlabPtrs o) {
+                                                       const uint64_t* __restrict__ off, SlabPtrs o, uint32_t wd) {
     const uint64_t r = r0 + ((uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
     if (r >= r1) return;
     const uint64_t ob = off[r - r0];
@@ -130,13 +131,17 @@ __global__ __launch_bounds__(kBlock) void k_root_write(const uint32_t* __restric
         const uint64_t bal = __ballot(fr);
         if (fr) {
             const uint32_t p = k + uint32_t(__popcll(bal & lanemask_lt()));
-            uint64_t m[W];
-            load_mask<W>(mask + size_t(e) * W, m);
             const uint64_t d = ob + p;
             o.mem[d] = rk << 1 | kSeq;
-            o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
             o.pos[d] = (p << 16) | len;
-            store_mask<W>(o.mask + size_t(d) * W, m);
+            if constexpr (W == 0) {
+                o.lohi[d] = mask_copy_lohi_dyn(mask + size_t(e) * wd, o.mask + size_t(d) * wd, wd);
+            } else {
+                uint64_t m[W];
+                load_mask<W>(mask + size_t(e) * W, m);
+                o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+                store_mask<W>(o.mask + size_t(d) * W, m);
+            }
         }
         k += uint32_t(__popcll(bal));
     }
@@ -159,7 +164,8 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
                                                   const uint32_t* __restrict__ pos, const uint64_t* __restrict__ mask,
                                                   uint32_t mlo, uint32_t mhi, uint32_t chunk,
                                                   uint32_t* __restrict__ cnt,
-                                                  unsigned long long* __restrict__ tests) {
+                                                  unsigned long long* __restrict__ tests, uint32_t wd) {
+    const uint32_t mw = mask_words<W>(wd);
     __shared__ uint32_t blk_tests;
     if (threadIdx.x == 0) blk_tests = 0;
     __syncthreads();
@@ -173,9 +179,9 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
         const uint32_t lo_i = lohi[e] & 0xFFFFu;
         const uint32_t ti = mi & 1u, ri = mi >> 1;
         const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
-        uint64_t mk[W];
-        load_mask<W>(mask + size_t(e) * W, mk);
-        uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi >> c.mshift) * c.D;
+        MaskV<W> mk;
+        mk.load(mask + size_t(e) * mw, wd);
+        uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
         for (uint32_t q = 0; q < rl; ++q) {
             const uint32_t f = rb + q;
             const uint32_t mj = mem[f];
@@ -184,9 +190,9 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
                 // P x -> y  /  P->x -> y : bits of L(j) strictly after first bit of L(i)
                 if ((lohi[f] >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
                 // P->(x y), y > x : L(i) & L(j)
-                if (ti == kSeq && rj > ri && and_nonzero<W>(mk, mask + size_t(f) * W))
+                if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * mw, wd))
                     atomicAdd(rowc + (rj << 1 | 1u), 1u);
-            } else if (ti == kItm && rj > ri && and_nonzero<W>(mk, mask + size_t(f) * W)) {
+            } else if (ti == kItm && rj > ri && mk.and_any(mask + size_t(f) * mw, wd)) {
                 // P(x y), y > x
                 atomicAdd(rowc + (rj << 1 | 1u), 1u);
             }
@@ -194,6 +200,130 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
     }
     atomicAdd(&blk_tests, my_tests);
     __syncthreads();
+    if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
+}
+
+// Keyed class counting (batches of >= kKeyedMinEntries entries; FSM_COUNT_PATH
+// selects): k_count's device-scope atomics execute at the memory side (15.5M of
+// them at D1M, 92 % of wave cycles waiting: profiles/r2/atomics).  Here the
+// batch's counters are laid out in groups of kGroupCounters (rows never straddle
+// a group) and counted like the root F2: k_cnt_plan histograms each entry's key
+// capacity by group per entry block, k_cnt_keys writes every successful join as
+// a u16 key (the counter's offset in its group) into region (group, block), and
+// k_f2_count<true> streams a group's regions into LDS counters and writes the
+// group's counters out whole (no memset, no global atomics).
+constexpr uint32_t kKeyedMinEntries = 1u << 20;
+constexpr uint32_t kGroupShift = 15;  // kGroupCounters = 1 << kGroupShift
+
+__device__ __forceinline__ uint64_t row_base(const DClass& c, uint32_t mi) {
+    return c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
+}
+
+__global__ __launch_bounds__(1024) void k_cnt_plan(uint32_t E, uint32_t epb, const uint32_t* __restrict__ cid,
+                                                   const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                   const uint32_t* __restrict__ pos, uint32_t mlo, uint32_t mhi,
+                                                   uint32_t G, uint32_t nblk, uint32_t* __restrict__ cap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
+    __syncthreads();
+    const uint32_t e0 = blockIdx.x * epb, e1 = min(E, e0 + epb);
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const uint32_t mi = mem[e];
+        if (mi - mlo >= mhi - mlo) continue;
+        const uint32_t p = pos[e], rl = p & 0xFFFFu, off = p >> 16;
+        // temporal: any partner (itself included); equality: partners of higher rank (after it)
+        atomicAdd(&h[uint32_t(row_base(cls[cid[e]], mi) >> kGroupShift)], 2 * rl - 1 - off);
+    }
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[uint64_t(g) * nblk + blockIdx.x] = (h[g] + 7u) & ~7u;
+}
+
+// the join tests of k_count for entry i against partner f; calls key(col) per successful join
+template <int W, class K>
+__device__ __forceinline__ void class_joins(uint32_t ti, uint32_t ri, uint32_t lo_i, const MaskV<W>& mk,
+                                            uint32_t f, const uint32_t* __restrict__ mem,
+                                            const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask,
+                                            uint32_t wd, K&& key) {
+    const uint32_t mw = mask_words<W>(wd);
+    const uint32_t mj = mem[f];
+    const uint32_t tj = mj & 1u, rj = mj >> 1;
+    if (tj == kSeq) {
+        if ((lohi[f] >> 16) > lo_i) key(rj << 1);
+        if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * mw, wd)) key(rj << 1 | 1u);
+    } else if (ti == kItm && rj > ri && mk.and_any(mask + size_t(f) * mw, wd)) {
+        key(rj << 1 | 1u);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(1024) void k_cnt_keys(uint32_t E, uint32_t epb, const uint32_t* __restrict__ cid,
+                                                   const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                   const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                                   const uint64_t* __restrict__ mask, uint32_t mlo, uint32_t mhi,
+                                                   uint32_t G, uint32_t nblk, const uint64_t* __restrict__ base,
+                                                   uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
+                                                   unsigned long long* __restrict__ tests, uint32_t wd) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];  // region cursors [G]
+    __shared__ uint32_t blk_tests;
+    const uint32_t b = blockIdx.x;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[uint64_t(g) * nblk + b]);
+    if (threadIdx.x == 0) blk_tests = 0;
+    __syncthreads();
+    uint32_t my_tests = 0;
+    const uint32_t e0 = b * epb, e1 = min(E, e0 + epb);
+    const uint32_t lane = lane_id();
+    for (uint32_t b0 = e0; b0 < e1; b0 += blockDim.x) {  // wave-uniform trip count (ballots below)
+        const uint32_t e = b0 + threadIdx.x;
+        uint32_t mi = e < e1 ? mem[e] : 0u;
+        const bool live = e < e1 && mi - mlo < mhi - mlo;
+        uint32_t n = 0, g = 0, kb = 0, rl = 0, rb = 0, lo_i = 0, ti = 0, ri = 0;
+        MaskV<W> mk;
+        if (live) {
+            const uint32_t p = pos[e];
+            rl = p & 0xFFFFu;
+            rb = e - (p >> 16);
+            my_tests += rl;
+            const uint64_t rbase = row_base(cls[cid[e]], mi);
+            g = uint32_t(rbase >> kGroupShift);
+            kb = uint32_t(rbase) & (kGroupCounters - 1u);
+            lo_i = lohi[e] & 0xFFFFu;
+            ti = mi & 1u;
+            ri = mi >> 1;
+            mk.load(mask + size_t(e) * mask_words<W>(wd), wd);
+            for (uint32_t q = 0; q < rl; ++q)
+                class_joins<W>(ti, ri, lo_i, mk, rb + q, mem, lohi, mask, wd, [&](uint32_t) { ++n; });
+        }
+        // region slots: with few groups every lane of a wave would hit the same LDS
+        // cursors, so the wave reserves once per distinct group among its lanes
+        uint32_t at = 0;
+        if (G <= 64) {
+            for (uint64_t todo = __ballot(n > 0); todo;) {
+                const int lead = __ffsll((unsigned long long)todo) - 1;
+                const uint32_t lg = uint32_t(__shfl(int(g), lead, 64));
+                const bool in = n > 0 && g == lg;
+                const uint64_t m = __ballot(in);
+                const uint32_t v = in ? n : 0u;
+                const uint32_t incl = wave_incl_scan(v);
+                const uint32_t tot = uint32_t(__shfl(int(incl), 63, 64));
+                uint32_t base = 0;
+                if (int(lane) == lead) base = atomicAdd(&cur[lg], tot);
+                base = uint32_t(__shfl(int(base), lead, 64));
+                if (in) at = base + incl - v;
+                todo &= ~m;
+            }
+        } else if (n) {
+            at = atomicAdd(&cur[g], n);
+        }
+        if (n) {
+            for (uint32_t q = 0; q < rl; ++q)
+                class_joins<W>(ti, ri, lo_i, mk, rb + q, mem, lohi, mask, wd,
+                               [&](uint32_t col) { keys[at++] = uint16_t(kb + col); });
+        }
+    }
+    atomicAdd(&blk_tests, my_tests);
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+        fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[uint64_t(g) * nblk + b]);
     if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
 }
 
@@ -278,7 +408,7 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
                                                                uint32_t rpb, const uint64_t* __restrict__ off,
                                                                SlabPtrs o, uint32_t pm, uint32_t G, uint32_t nblk,
                                                                uint32_t mlo, uint32_t mhi, int bg,
-                                                               uint32_t* __restrict__ cap) {
+                                                               uint32_t* __restrict__ cap, uint32_t wd) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
     __syncthreads();
@@ -296,13 +426,17 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
             const uint64_t bal = __ballot(fr);
             if (fr) {
                 const uint32_t p = k + uint32_t(__popcll(bal & lanemask_lt()));
-                uint64_t m[W];
-                load_mask<W>(mask + size_t(e) * W, m);
                 const uint64_t d = ob + p;
                 o.mem[d] = rk << 1 | kSeq;
-                o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
                 o.pos[d] = (p << 16) | len;
-                store_mask<W>(o.mask + size_t(d) * W, m);
+                if constexpr (W == 0) {
+                    o.lohi[d] = mask_copy_lohi_dyn(mask + size_t(e) * wd, o.mask + size_t(d) * wd, wd);
+                } else {
+                    uint64_t m[W];
+                    load_mask<W>(mask + size_t(e) * W, m);
+                    o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+                    store_mask<W>(o.mask + size_t(d) * W, m);
+                }
                 if ((rk << 1) - mlo < mhi - mlo) atomicAdd(&h[group_of(rk, pm)], 2 * len - 1 - p);
             }
             k += uint32_t(__popcll(bal));
@@ -322,7 +456,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                                                         uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
                                                         uint32_t mhi, const uint64_t* __restrict__ base, int bg,
                                                         uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
-                                                        unsigned long long* __restrict__ nkeys_total) {
+                                                        unsigned long long* __restrict__ nkeys_total, uint32_t wd) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     F2Ent* stage_all = reinterpret_cast<F2Ent*>(smem);  // kF2Waves x 64 entries
     uint32_t* srow = smem + kF2Waves * 64 * (sizeof(F2Ent) / 4);  // row offsets of the block [rpb + 1]
@@ -416,11 +550,15 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                 const uint32_t ri = me >> 1, g = group_of(ri, pm);
                 const uint32_t li = rfl(lohi[rb + i]) & 0xFFFFu;
                 const uint32_t kb = (ri - g * per) * D;
-                uint64_t mi[W];
+                MaskV<W> mi;  // entry i's mask, wave-uniform (by address when W == 0)
+                if constexpr (W == 0) {
+                    mi.load(mask + size_t(rb + i) * wd, wd);
+                } else {
 #pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    const uint64_t v = mask[size_t(rb + i) * W + w];
-                    mi[w] = uint64_t(rfl(uint32_t(v))) | (uint64_t(rfl(uint32_t(v >> 32))) << 32);
+                    for (int w = 0; w < W; ++w) {
+                        const uint64_t v = mask[size_t(rb + i) * W + w];
+                        mi.w[w] = uint64_t(rfl(uint32_t(v))) | (uint64_t(rfl(uint32_t(v >> 32))) << 32);
+                    }
                 }
                 for (uint32_t c0 = 0; c0 < rl; c0 += 64) {
                     const uint32_t q = c0 + lane;
@@ -430,7 +568,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                     if (v) {
                         rq = mem[rb + q] >> 1;
                         t_ok = (lohi[rb + q] >> 16) > li;
-                        if (q > i) e_ok = and_nonzero<W>(mi, mask + size_t(rb + q) * W);
+                        if (q > i) e_ok = mi.and_any(mask + size_t(rb + q) * mask_words<W>(wd), wd);
                     }
                     const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
                     const uint32_t nt = uint32_t(__popcll(tb)), n = nt + uint32_t(__popcll(eb));
@@ -462,31 +600,39 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
 // counters.  Then the frequent pairs of the group's counter rows
 // [max(g*per, rlo), min((g+1)*per, rhi)) are balloted out with one atomic per
 // wave; records come out unordered and the host sorts them.
+// kOut (the keyed class count): the group's kGroupCounters counters are written
+// out to cnt_out[g * kGroupCounters ...] instead of extracted.
 constexpr uint32_t kF2MaxBlocks = 2048;  // row blocks (regions per group) k_f2_count can index in LDS
+template <bool kOut>
 __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base, uint32_t G, int bg,
                                                          const uint32_t* __restrict__ fill, uint32_t nblk,
                                                          const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
                                                          uint32_t g0, uint32_t rlo, uint32_t rhi, uint32_t minsup,
                                                          FreqRec* __restrict__ recs, uint32_t cap,
-                                                         uint32_t* __restrict__ nrec) {
+                                                         uint32_t* __restrict__ nrec, uint32_t* __restrict__ cnt_out,
+                                                         uint32_t parts) {
     __shared__ uint32_t h[kGroupCounters];
     __shared__ uint32_t cpre[kF2MaxBlocks + 1];  // first logical chunk of each region
     __shared__ uint32_t cst[kF2MaxBlocks];       // first physical chunk of each region
     __shared__ uint32_t sfill[kF2MaxBlocks];     // keys in each region
     __shared__ uint32_t wsum[kF2Waves];
-    const uint32_t g = g0 + blockIdx.x;
+    // kOut with parts > 1: `parts` blocks share a group, each over its own range of regions
+    const uint32_t g = g0 + blockIdx.x / parts, part = blockIdx.x % parts;
+    const uint32_t rb0 = uint32_t(uint64_t(nblk) * part / parts), rb1 = uint32_t(uint64_t(nblk) * (part + 1) / parts);
+    const uint32_t nr = rb1 - rb0;
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    for (uint32_t t = threadIdx.x; t < per * D; t += blockDim.x) h[t] = 0;
+    const uint32_t nz = kOut ? kGroupCounters : per * D;
+    for (uint32_t t = threadIdx.x; t < nz; t += blockDim.x) h[t] = 0;
     // region chunk counts -> exclusive prefix (nblk <= 2 * blockDim.x: two per thread)
-    const uint64_t gi = uint64_t(g) * nblk;
+    const uint64_t gi = uint64_t(g) * nblk + rb0;
     const uint32_t s0 = 2 * threadIdx.x;
-    const uint32_t f0 = s0 < nblk ? fill[gi + s0] : 0u, f1 = s0 + 1 < nblk ? fill[gi + s0 + 1] : 0u;
-    if (s0 < nblk) {
-        cst[s0] = uint32_t(base[f2_region(g, s0, G, nblk, bg)]) >> 3;
+    const uint32_t f0 = s0 < nr ? fill[gi + s0] : 0u, f1 = s0 + 1 < nr ? fill[gi + s0 + 1] : 0u;
+    if (s0 < nr) {
+        cst[s0] = uint32_t(base[f2_region(g, rb0 + s0, G, nblk, bg)]) >> 3;
         sfill[s0] = f0;
     }
-    if (s0 + 1 < nblk) {
-        cst[s0 + 1] = uint32_t(base[f2_region(g, s0 + 1, G, nblk, bg)]) >> 3;
+    if (s0 + 1 < nr) {
+        cst[s0 + 1] = uint32_t(base[f2_region(g, rb0 + s0 + 1, G, nblk, bg)]) >> 3;
         sfill[s0 + 1] = f1;
     }
     const uint32_t c0 = (f0 + 7) >> 3, c1 = (f1 + 7) >> 3;
@@ -500,9 +646,9 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
         total += wsum[w];
     }
     const uint32_t ex = woff + incl - pair;
-    if (s0 < nblk) cpre[s0] = ex;
-    if (s0 + 1 < nblk) cpre[s0 + 1] = ex + c0;
-    if (threadIdx.x == 0) cpre[nblk] = total;
+    if (s0 < nr) cpre[s0] = ex;
+    if (s0 + 1 < nr) cpre[s0 + 1] = ex + c0;
+    if (threadIdx.x == 0) cpre[nr] = total;
     __syncthreads();
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
     constexpr uint32_t kU = 4;  // chunks per thread per round
@@ -514,7 +660,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
             const uint32_t c = q0 + u * kF2Threads;
             nv[u] = 0;
             if (c < total) {
-                uint32_t lo = 0, hi = nblk;  // region of c: the last s with cpre[s] <= c
+                uint32_t lo = 0, hi = nr;  // region of c: the last s with cpre[s] <= c
                 while (hi - lo > 1) {
                     const uint32_t mid = (lo + hi) >> 1;
                     if (cpre[mid] <= c) lo = mid; else hi = mid;
@@ -533,6 +679,17 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
         }
     }
     __syncthreads();
+    if constexpr (kOut) {
+        uint32_t* o = cnt_out + uint64_t(g) * kGroupCounters;
+        if (parts == 1) {  // the group's only block: every counter written (no memset)
+            const uint4* hv = reinterpret_cast<const uint4*>(h);
+            for (uint32_t t = threadIdx.x; t < kGroupCounters / 4; t += blockDim.x) reinterpret_cast<uint4*>(o)[t] = hv[t];
+        } else {  // shared group (zeroed beforehand): contiguous adds of the non-zero counters
+            for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x)
+                if (h[t]) atomicAdd(o + t, h[t]);
+        }
+        return;
+    }
     const uint32_t ra = max(g * per, rlo), rz = min((g + 1) * per, rhi);
     for (uint32_t row = ra; row < rz; ++row) {
         const uint32_t* hr = h + (row - g * per) * D;
@@ -559,7 +716,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ 
     if (g >= nrows) return;
     const DRow r = rows[g];
     const DClass c = cls[r.cls];
-    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
+    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.rstride;
     uint32_t n = 0;
     for (uint32_t s = 0; s < c.D; s += 64) {
         const uint32_t slot = s + lane_id();
@@ -577,7 +734,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
     if (g >= nrows) return;
     const DRow r = rows[g];
     const DClass c = cls[r.cls];
-    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
+    const uint32_t* base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.rstride;
     uint64_t o = rowoff[g];
     uint32_t nrank = 0;
     const unsigned lane = lane_id();
@@ -610,13 +767,13 @@ __global__ __launch_bounds__(kBlock) void k_freq_recs(const DRow* __restrict__ r
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const bool live = g < nrows;
     DRow r{0, 0};
-    DClass c{0, 0, 0, 0, {0, 0, 0}};
+    DClass c{0, 0, 0, 0, 0, {0, 0}};
     const uint32_t* base = cnt;
     uint32_t n = 0;
     if (live) {
         r = rows[g];
         c = cls[r.cls];
-        base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.D;
+        base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.rstride;
         for (uint32_t s0 = 0; s0 < c.D; s0 += 64) {
             const uint32_t slot = s0 + lane;
             n += uint32_t(__popcll(__ballot(slot < c.D && base[slot] >= minsup)));
@@ -694,7 +851,7 @@ __device__ __forceinline__ EmitEnt emit_ent(uint64_t e64, uint32_t E, const uint
 template <int W, class OnOk>
 __device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, const uint32_t* __restrict__ mem,
                                                const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask,
-                                               const uint32_t* __restrict__ kid_slot, OnOk&& on_ok) {
+                                               const uint32_t* __restrict__ kid_slot, uint32_t wd, OnOk&& on_ok) {
     const uint32_t lane = lane_id();
     const uint32_t incl = wave_incl_scan(t.nk), excl = incl - t.nk;
     const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
@@ -732,9 +889,9 @@ __device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, co
                 if (ct == kSeq) {
                     ok = (lohi[f] >> 16) > (o_lt & 0xFFFFu);
                 } else {
-                    uint64_t mk[W];
-                    load_mask<W>(mask + size_t(o_e) * W, mk);
-                    ok = and_nonzero<W>(mk, mask + size_t(f) * W);
+                    MaskV<W> mk;
+                    mk.load(mask + size_t(o_e) * mask_words<W>(wd), wd);
+                    ok = mk.and_any(mask + size_t(f) * mask_words<W>(wd), wd);
                 }
             }
         }
@@ -753,8 +910,39 @@ __device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, co
 template <int W>
 __device__ __forceinline__ void emit_write(const SlabPtrs& o, uint64_t cap, uint64_t d, uint32_t cc, uint32_t kidc, uint32_t k,
                                            uint32_t n, uint64_t o_e, uint32_t o_lt, uint32_t f, uint32_t slot,
-                                           const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask) {
+                                           const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask,
+                                           uint32_t wd) {
     if (d >= cap) return;  // a count mismatch: the host reports it, nothing lands past the slab
+    if constexpr (W == 0) {  // runtime width: word by word through HBM
+        const uint64_t* src = mask + size_t(f) * wd;
+        uint64_t* dst = o.mask + d * wd;
+        uint32_t lo2 = 0xFFFFFFFFu, hi2 = 0;
+        if ((slot & 1u) == kSeq) {
+            hi2 = lohi[f] >> 16;
+            const int lo = int(o_lt & 0xFFFFu);
+            for (uint32_t k = 0; k < wd; ++k) {
+                const int sh = lo + 1 - int(k) * 64;  // bits [0, sh) of word k are cleared
+                const uint64_t v = src[k] & (sh <= 0 ? ~0ull : (sh >= 64 ? 0ull : (~0ull << sh)));
+                dst[k] = v;
+                if (v && lo2 == 0xFFFFFFFFu) lo2 = k * 64 + uint32_t(__builtin_ctzll(v));
+            }
+        } else {
+            const uint64_t* mk = mask + size_t(o_e) * wd;
+            for (uint32_t k = 0; k < wd; ++k) {
+                const uint64_t v = src[k] & mk[k];
+                dst[k] = v;
+                if (v) {
+                    if (lo2 == 0xFFFFFFFFu) lo2 = k * 64 + uint32_t(__builtin_ctzll(v));
+                    hi2 = k * 64 + 63 - uint32_t(__builtin_clzll(v));
+                }
+            }
+        }
+        o.cid[d] = cc;
+        o.mem[d] = kidc;
+        o.lohi[d] = (lo2 == 0xFFFFFFFFu ? 0u : lo2) | (hi2 << 16);
+        o.pos[d] = (k << 16) | n;
+        return;
+    } else {
     uint64_t m[W];
     load_mask<W>(mask + size_t(f) * W, m);
     uint32_t lo2, hi2;
@@ -775,6 +963,7 @@ __device__ __forceinline__ void emit_write(const SlabPtrs& o, uint64_t cap, uint
     o.lohi[d] = lo2 | (hi2 << 16);
     o.pos[d] = (k << 16) | n;
     store_mask<W>(o.mask + d * W, m);
+    }
 }
 
 // Two-pass emission (FSM_EMIT_PATH=twopass): count pass -> exclusive scan of
@@ -788,7 +977,8 @@ __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __r
                                                  const uint32_t* __restrict__ kid_slot,
                                                  const uint32_t* __restrict__ kid_cid,
                                                  const uint32_t* __restrict__ child_of, uint32_t* __restrict__ ncnt,
-                                                 const uint64_t* __restrict__ off, SlabPtrs o, uint64_t cap) {
+                                                 const uint64_t* __restrict__ off, SlabPtrs o, uint64_t cap,
+                                                 uint32_t wd) {
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wstride = uint64_t(gridDim.x) * wpb * 64;  // 64-bit: no wrap for E near 2^32
@@ -804,14 +994,14 @@ __global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __r
             }
         }
         const uint32_t done = emit_pairs<W>(
-            t, w0, mem, lohi, mask, kid_slot,
+            t, w0, mem, lohi, mask, kid_slot, wd,
             [&](bool ok, uint32_t ow, uint64_t o_e, uint32_t o_lt, uint32_t q, uint32_t f, uint32_t slot, uint32_t k) {
                 if constexpr (kWrite) {
                     // shuffles stay outside the branch: a source lane must be active
                     const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
                     const uint64_t o_base = __shfl(base, int(ow), 64);
                     const uint32_t o_cc = uint32_t(__shfl(int(t.cc), int(ow), 64));
-                    if (ok) emit_write<W>(o, cap, o_base + k, o_cc, kid_cid[q], k, o_n, o_e, o_lt, f, slot, lohi, mask);
+                    if (ok) emit_write<W>(o, cap, o_base + k, o_cc, kid_cid[q], k, o_n, o_e, o_lt, f, slot, lohi, mask, wd);
                 }
             });
         if constexpr (!kWrite) {
@@ -851,7 +1041,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
                                                   const uint32_t* __restrict__ kid_cid,
                                                   const uint32_t* __restrict__ child_of,
                                                   unsigned long long* __restrict__ cursor, SlabPtrs o,
-                                                  uint64_t cap, uint32_t rcap) {
+                                                  uint64_t cap, uint32_t rcap, uint32_t wd) {
     constexpr uint32_t kWaves = kEmitBlock / 64;
     constexpr uint32_t kPer = 64 * kEmitRounds;  // entries of one wave per chunk
     __shared__ uint32_t r_f[kWaves][kEmitCap], r_q[kWaves][kEmitCap], r_ek[kWaves][kEmitCap];
@@ -866,7 +1056,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
             const uint64_t w0 = c0 + uint64_t(r) * kEmitBlock + uint64_t(w) * 64;
             const EmitEnt t = emit_ent(w0 + lane, E, cid, cls, mem, lohi, pos, kid_off, child_of);
             const uint32_t done = emit_pairs<W>(
-                t, w0, mem, lohi, mask, kid_slot,
+                t, w0, mem, lohi, mask, kid_slot, wd,
                 [&](bool ok, uint32_t ow, uint64_t, uint32_t, uint32_t q, uint32_t f, uint32_t, uint32_t k) {
                     const uint64_t b = __ballot(ok);
                     if (ok) {
@@ -903,7 +1093,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
                 const uint32_t el = ek >> 16, k = ek & 0xFFFFu;
                 const uint64_t o_e = c0 + uint64_t(el >> 6) * kEmitBlock + uint64_t(w) * 64 + (el & 63u);
                 emit_write<W>(o, cap, wb + i_off[w][el] + k, i_cc[w][el], kid_cid[q], k, i_n[w][el], o_e, i_lt[w][el], f,
-                              kid_slot[q], lohi, mask);
+                              kid_slot[q], lohi, mask, wd);
             }
         } else {
             for (int r = 0; r < kEmitRounds; ++r) {
@@ -913,7 +1103,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
                 const uint64_t base = wb + i_off[w][el];
                 const uint32_t n_run = i_n[w][el];
                 if (n_run == 0) t.nk = 0;
-                emit_pairs<W>(t, w0, mem, lohi, mask, kid_slot,
+                emit_pairs<W>(t, w0, mem, lohi, mask, kid_slot, wd,
                               [&](bool ok, uint32_t ow, uint64_t o_e, uint32_t o_lt, uint32_t q, uint32_t f,
                                   uint32_t slot, uint32_t k) {
                                   const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
@@ -921,7 +1111,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
                                   const uint32_t o_cc = uint32_t(__shfl(int(t.cc), int(ow), 64));
                                   if (ok)
                                       emit_write<W>(o, cap, o_base + k, o_cc, kid_cid[q], k, o_n, o_e, o_lt, f, slot, lohi,
-                                                    mask);
+                                                    mask, wd);
                               });
             }
         }
@@ -939,7 +1129,8 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
         case 8: MACRO(8); break;  \
         case 16: MACRO(16); break; \
         case 32: MACRO(32); break; \
-        default: MACRO(64); break; \
+        case 64: MACRO(64); break; \
+        default: MACRO(0); break;  \
     }
 
 struct Slab {
@@ -961,29 +1152,63 @@ struct Slab {
 
 // Per-class member tables live in flat per-batch arrays (no per-class heap
 // vectors: deep lattices have millions of small classes).
+// One record per prefix class.  A batch's children (the classes its frequent
+// candidates open) are the next batch's classes: the same record, so an emit of
+// a batch's only group hands the whole array over (no per-class copy).
 struct ClassMeta {
     uint64_t ri_off = 0;  // rank -> dense item id:        Batch::rank_item[ri_off + rank]
     uint64_t no_off = 0;  // member -> pattern node or -1:  Batch::node_of[no_off + member]
+    uint64_t cnt_off = 0;
+    uint64_t cap = 0;     // entries of the class in its batch slab (= sum of member supports)
+    uint64_t sS = 0, sI = 0;  // summed supports of the members by type (sequence / itemset extension)
     uint32_t D = 0;
     uint32_t mshift = 0;
-    uint64_t cnt_off = 0;
-    uint32_t nent = 0, cbase = 0;  // entries of the class in the batch slab (= sum of member supports)
+    uint32_t cbase = 0;
+    uint32_t nS = 0, nI = 0;  // members by type
+    uint32_t psup = 0;    // support of the class prefix P: an upper bound of the class's runs
+    uint32_t pcls = 0, pmi = 0;  // as a child: the parent class and member that open it
     bool split = false;  // sharded: a heavy first-level class every rank counts; its sub-classes are split
 };
+using ChildInfo = ClassMeta;
 
-struct ChildInfo {
-    uint32_t pcls = 0, pmi = 0;
-    uint64_t ri_off = 0, no_off = 0;  // into the parent batch's child_rank_item / child_node_of
-    uint32_t D = 0;
-    uint64_t cap = 0;
-    bool split = false;
+// append-only array in fixed chunks: growth never copies (or faults in again) what
+// is already there (pattern nodes: millions in deep lattices)
+template <class T, int kShift = 20> struct ChunkedVec {
+    std::vector<std::unique_ptr<T[]>> ch;
+    size_t n = 0;
+    static constexpr size_t kMask = (size_t(1) << kShift) - 1;
+    size_t size() const { return n; }
+    T& operator[](size_t i) { return ch[i >> kShift][i & kMask]; }
+    const T& operator[](size_t i) const { return ch[i >> kShift][i & kMask]; }
+    void push_back(const T& v) {
+        if ((n >> kShift) == ch.size()) ch.emplace_back(new T[size_t(1) << kShift]);
+        ch[n >> kShift][n & kMask] = v;
+        ++n;
+    }
+    void grow(size_t m) {  // size n + m; the new elements are written by index afterwards
+        while (((n + m + kMask) >> kShift) > ch.size()) ch.emplace_back(new T[size_t(1) << kShift]);
+        n += m;
+    }
 };
+
+// fn(t, i0, i1) over nthr contiguous slices of [0, n), one host thread each
+template <class F> void par_slices(int64_t nthr, int64_t n, F&& fn) {
+    if (nthr <= 1) {
+        fn(int64_t(0), int64_t(0), n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nthr; ++t) th.emplace_back([&fn, t, nthr, n] { fn(t, n * t / nthr, n * (t + 1) / nthr); });
+    for (auto& x : th) x.join();
+}
+int64_t host_threads() { return int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)); }
 
 struct PNode {
     int32_t parent;
     uint32_t item;
     uint32_t type;
     uint32_t support;
+    uint32_t len_sets;  // items << 16 | itemsets of the pattern (both < 2^16)
 };
 
 // Frequent-pair records in (row, slot) order with their child member ids: rank among
@@ -1039,6 +1264,32 @@ struct Batch {
     bool f2_planned = false;
     DevBuf f2_base;
     uint64_t f2_nslots = 0;
+
+    // back to an empty batch: device buffers released, host vectors cleared with their
+    // capacity kept (the DFS reuses popped batches: no fresh pages per batch)
+    void recycle() {
+        slab = Slab{};
+        cls.clear();
+        h_cls.clear();
+        d_cls.release();
+        kid_tab.release();
+        kid_off = kid_slot = kid_cid = nullptr;
+        E = n_cnt = cbase_total = 0;
+        rank_item.clear();
+        node_of.clear();
+        children.clear();
+        child_rank_item.clear();
+        child_node_of.clear();
+        groups.clear();
+        next_group = 0;
+        depth = 1;
+        root = false;
+        root_rows.release();
+        R = 0;
+        f2_planned = false;
+        f2_base.release();
+        f2_nslots = 0;
+    }
 };
 
 struct Miner {
@@ -1048,7 +1299,7 @@ struct Miner {
     int W;
     uint32_t minsup;
     uint64_t budget;
-    std::vector<PNode> nodes;
+    ChunkedVec<PNode> nodes;
     KernelClock* clk = nullptr;
     DevBuf d_tests;  // u64: (entry, partner) join tests of the class count kernels
     // sharded mining (nranks > 1): this rank counts the root rows of ranks
@@ -1057,6 +1308,11 @@ struct Miner {
     uint32_t slice_lo = 0, slice_hi = kNone;
     size_t n_shared = 0;  // pattern nodes every rank holds (root + its frequent children)
     std::vector<uint8_t> node_dup;  // sharded: nodes of split classes, output by rank 0 only
+
+    // host scratch reused by every batch (capacity kept: no fresh pages per batch)
+    std::vector<DRow> rows_s;
+    std::vector<FreqRec> recs_s;
+    std::vector<uint32_t> ktab_s, child_of_s;
 
     double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
     // FSM_HOST_TRACE=1: host time of the bookkeeping phases, printed at the end of the mine
@@ -1129,33 +1385,125 @@ struct Miner {
     }
 
 
-    // class descriptors (counter matrix offsets, member bases) of a batch
-    void prepare(Batch& b) {
+    // class descriptors (counter matrix offsets, member bases) of a batch.  keyed:
+    // counters laid out for the keyed count (a class matrix that fits one group of
+    // kGroupCounters is not cut by a group boundary; larger ones start on a group
+    // boundary with a power-of-two row stride, so no counter row straddles a
+    // group).  Returns false (plain layout) when a row exceeds a group.
+    bool prepare(Batch& b, bool keyed) {
         b.h_cls.resize(b.cls.size());
-        uint64_t off = 0, cb = 0;
-        for (size_t c = 0; c < b.cls.size(); ++c) {
-            ClassMeta& m = b.cls[c];
-            m.cnt_off = off;
-            m.cbase = uint32_t(cb);
-            off += uint64_t(m.D >> m.mshift) * m.D;
-            cb += m.D;
-            b.h_cls[c] = DClass{m.cnt_off, m.D, m.cbase, m.mshift, {0, 0, 0}};
+        for (int pass = keyed ? 0 : 1; pass < 2; ++pass) {
+            const bool kl = pass == 0;
+            uint64_t off = 0, cb = 0;
+            bool ok = true;
+            for (size_t c = 0; c < b.cls.size() && ok; ++c) {
+                ClassMeta& m = b.cls[c];
+                const uint64_t rows = m.D >> m.mshift;
+                uint32_t stride = m.D;
+                if (kl) {
+                    if (rows * m.D <= kGroupCounters) {
+                        if ((off & (kGroupCounters - 1)) + rows * m.D > kGroupCounters)
+                            off = (off + kGroupCounters - 1) & ~uint64_t(kGroupCounters - 1);
+                    } else if (m.D <= kGroupCounters) {
+                        stride = m.D <= 1 ? 1u : 1u << (32 - __builtin_clz(m.D - 1));
+                        off = (off + kGroupCounters - 1) & ~uint64_t(kGroupCounters - 1);
+                    } else {
+                        ok = false;
+                    }
+                }
+                m.cnt_off = off;
+                m.cbase = uint32_t(cb);
+                off += rows * stride;
+                cb += m.D;
+                b.h_cls[c] = DClass{m.cnt_off, m.D, m.cbase, m.mshift, stride, {0, 0}};
+            }
+            if (!ok) continue;
+            if (cb >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
+            b.n_cnt = off;
+            b.cbase_total = cb;
+            upload(b.d_cls, b.h_cls);
+            return kl;
         }
-        if (cb >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
-        b.n_cnt = off;
-        b.cbase_total = cb;
-        upload(b.d_cls, b.h_cls);
+        return false;
+    }
+
+    // FSM_COUNT_PATH=atomic|keys: force the class count path (default: keyed for
+    // batches of >= kKeyedMinEntries entries; tests, profiling)
+    static int count_path() {
+        const char* v = std::getenv("FSM_COUNT_PATH");
+        if (!v) return 0;
+        return !std::strcmp(v, "keys") ? 2 : (!std::strcmp(v, "atomic") ? 1 : 0);
+    }
+    // Keyed counting pays one group pass per kGroupCounters counters and a key pass
+    // over the entries, atomics one memory-side atomic per join: keyed when the
+    // batch's joins (estimated as sum cap^2 / runs, runs <= the prefix support)
+    // reach both its counters and twice its entries.
+    bool want_keyed(const Batch& b) const {
+        const int cp = count_path();
+        if (b.root || b.E == 0 || b.E >= kNone || cp == 1) return false;
+        if (cp == 2) return true;
+        if (b.E < kKeyedMinEntries) return false;
+        double est = 0, ncnt = 0;
+        for (const ClassMeta& m : b.cls) {
+            est += double(m.cap) * double(m.cap) / double(std::max<uint32_t>(m.psup, 1));
+            ncnt += double(m.D >> m.mshift) * double(m.D);
+        }
+        if (ctx->opts.verbose)
+            std::fprintf(stderr, "[fsm] batch entries %llu: estimated joins %.3g, counters %.3g\n",
+                         (unsigned long long)b.E, est, ncnt);
+        // measured on MI355X: keyed wins on long runs (BIBLE/SIGN-shaped batches, >= 2 joins
+        // per entry); at about one join per entry (Quest D1M) the atomics are as fast
+        return est >= ncnt && est >= 2.0 * double(b.E);
+    }
+
+    // Keyed count of a (non-root) batch laid out by prepare(b, true): plan ->
+    // scan -> keys -> per-group LDS count writing the counters out.  Returns
+    // false when the geometry does not apply (the atomic path then runs).
+    bool keyed_count(Batch& b, DevBuf& cnt) {
+        const uint64_t G64 = (b.n_cnt + kGroupCounters - 1) >> kGroupShift;
+        if (G64 == 0 || G64 > kMaxGroups) return false;
+        const uint32_t G = uint32_t(G64), E = uint32_t(b.E);
+        const uint32_t nblk = uint32_t(std::min<uint64_t>(kF2MaxBlocks, std::max<uint64_t>(1, (b.E + 8191) / 8192)));
+        const uint32_t epb = (E + nblk - 1) / nblk;
+        const uint64_t nd = uint64_t(G) * nblk;
+        const SlabPtrs sp = b.slab.ptrs();
+        const uint32_t mlo = member_lo(b), mhi = member_hi(b);
+        DevBuf cap(nd * 4), base((nd + 1) * 8), fill(nd * 4);
+        size_t tk = clk->begin("k_cnt_plan");
+        hipLaunchKernelGGL(k_cnt_plan, dim3(nblk), dim3(kF2Threads), size_t(G) * 4, s, E, epb, sp.cid,
+                           b.d_cls.as<DClass>(), sp.mem, sp.pos, mlo, mhi, G, nblk, cap.as<uint32_t>());
+        FSM_LAUNCHED("k_cnt_plan", s);
+        clk->end(tk, int64_t(b.E * 12 + nd * 4));
+        scan_exclusive(cap.as<uint32_t>(), base.as<uint64_t>(), nd, s);
+        FSM_HIP(hipMemcpyAsync(&pend[3], base.as<uint64_t>() + nd, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        const uint64_t nslots = pend[3];
+        if (nslots >= (uint64_t(1) << 32) - 4096) return false;  // region cursors are u32
+        DevBuf keys((nslots + 1024) * 2);
+        tk = clk->begin("k_cnt_keys");
+#define FSM_CK(WW)                                                                                                   \
+    hipLaunchKernelGGL(k_cnt_keys<WW>, dim3(nblk), dim3(kF2Threads), size_t(G) * 4, s, E, epb, sp.cid,                \
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, mlo, mhi, G, nblk, base.as<uint64_t>(), \
+                       fill.as<uint32_t>(), keys.as<uint16_t>(), d_tests.as<unsigned long long>(), uint32_t(W))
+        FSM_W_DISPATCH(W, FSM_CK)
+#undef FSM_CK
+        FSM_LAUNCHED("k_cnt_keys", s);
+        clk->end(tk, int64_t(b.E * entry_bytes() + nd * 12));
+        cnt.alloc(std::max<uint64_t>(G64 << kGroupShift, 1) * 4);
+        // few groups: several blocks per group (each over a range of the regions) keep the CUs busy
+        const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>({64u, 512u / G, nblk}));
+        if (parts > 1) FSM_HIP(hipMemsetAsync(cnt.p, 0, (G64 << kGroupShift) * 4, s));
+        tk = clk->begin("k_cnt_count");
+        hipLaunchKernelGGL(k_f2_count<true>, dim3(G * parts), dim3(kF2Threads), 0, s, base.as<uint64_t>(), G, 0,
+                           fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), 0u, 0u, 0u, 0u, 0u, 0u,
+                           (FreqRec*)nullptr, 0u, (uint32_t*)nullptr, cnt.as<uint32_t>(), parts);
+        FSM_LAUNCHED("k_cnt_count", s);
+        clk->end(tk, int64_t(G64 << kGroupShift) * 4 + int64_t(nd) * 12);
+        return true;
     }
 
     void stats_for_class(const Batch& b, const ClassMeta& m) {
-        uint64_t S = 0, I = 0, sS = 0, sI = 0;
-        const int32_t* node_of = b.node_of.data() + m.no_off;
-        for (uint32_t mi = 0; mi < m.D; ++mi) {
-            const int32_t nd = node_of[mi];
-            if (nd < 0) continue;
-            const uint64_t sup = nodes[size_t(nd)].support;
-            if ((mi & 1u) == kSeq) { ++S; sS += sup; } else { ++I; sI += sup; }
-        }
+        const uint64_t S = m.nS, I = m.nI, sS = m.sS, sI = m.sI;
         fsm_stats& st = ctx->stats;
         const int64_t j = int64_t(S * S + I * S + (S ? S * (S - 1) / 2 : 0) + (I ? I * (I - 1) / 2 : 0));
         st.joins += j;
@@ -1276,7 +1624,7 @@ struct Miner {
     bool root_f2(Batch& b, std::vector<FreqRec>& recs) {
         const ClassMeta& m = b.cls[0];
         if (b.root_rows.p == nullptr) return false;
-        const F2Geo geo = f2_geometry(b, m.D, m.nent, b.R);
+        const F2Geo geo = f2_geometry(b, m.D, m.cap, b.R);
         if (!geo.ok) return false;
         const uint32_t D = geo.D, F = geo.F, per = geo.per, G = geo.G, pm = geo.pm, mlo = geo.mlo, mhi = geo.mhi;
         const uint32_t rlo = comm ? slice_lo : 0u, rhi = comm ? std::min(slice_hi, F) : F;
@@ -1284,7 +1632,7 @@ struct Miner {
         const uint64_t nd = geo.nd;
         const int bg = f2_block_major() ? 1 : 0;
         const SlabPtrs sp = b.slab.ptrs();
-        const int64_t E0 = int64_t(m.nent);
+        const int64_t E0 = int64_t(m.cap);
         DevBuf base, fill(nd * 4);
         uint64_t nslots = 0;
         size_t tk = 0;
@@ -1312,7 +1660,7 @@ struct Miner {
 #define FSM_F2K(WW)                                                                                                   \
     hipLaunchKernelGGL(k_f2_keys<WW>, dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(), R, rpb,      \
                        sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(), bg,               \
-                       fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>())
+                       fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>(), uint32_t(W))
         FSM_W_DISPATCH(W, FSM_F2K)
 #undef FSM_F2K
         FSM_LAUNCHED("k_f2_keys", s);
@@ -1332,9 +1680,9 @@ struct Miner {
             FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
             tk_cnt = clk->begin("k_f2_count");
             if (g1 > g0)
-                hipLaunchKernelGGL(k_f2_count, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(), G, bg,
+                hipLaunchKernelGGL(k_f2_count<false>, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(), G, bg,
                                    fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), D, per, g0, rlo, rhi, minsup,
-                                   d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>());
+                                   d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u);
             FSM_LAUNCHED("k_f2_count", s);
             clk->end(tk_cnt, int64_t(g1 - g0) * nblk * 12);
             uint32_t nrec = 0;
@@ -1362,15 +1710,112 @@ struct Miner {
         hp[0] += now_ms() - th0;
         return true;
     }
+    // The children loop of count_and_freq split over host threads (unsharded, large
+    // batches; same tables, same node ids: node of record q = first + q).  Rows of
+    // records -> per-row sizes (parallel) -> table offsets (prefix) -> fill (parallel).
+    void children_parallel(Batch& b, const FreqRec* R, uint64_t nfreq, const std::vector<DRow>& rows) {
+        std::vector<uint64_t> gs;  // first record of each row group
+        gs.reserve(nfreq / 2 + 2);
+        for (uint64_t q = 0; q < nfreq; ++q)
+            if (q == 0 || R[q].row != R[q - 1].row) gs.push_back(q);
+        const int64_t ng = int64_t(gs.size());
+        gs.push_back(nfreq);
+        const int64_t nthr = host_threads();
+        std::vector<uint32_t> r2(size_t(ng) + 1, 0);
+        std::vector<uint8_t> keep(size_t(ng), 0);
+        par_slices(nthr, ng, [&](int64_t, int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {
+                uint32_t maxcid = 0;
+                for (uint64_t q = gs[size_t(i)]; q < gs[size_t(i) + 1]; ++q) maxcid = std::max(maxcid, R[q].cid);
+                r2[size_t(i)] = (maxcid >> 1) + 1;
+                const uint64_t nch = gs[size_t(i) + 1] - gs[size_t(i)];
+                keep[size_t(i)] = !(nch == 1 && (R[gs[size_t(i)]].slot & 1u) == kItm);
+            }
+        });
+        std::vector<uint64_t> ri(size_t(ng) + 1, 0);
+        std::vector<uint32_t> kidx(size_t(ng) + 1, 0);
+        for (int64_t i = 0; i < ng; ++i) {
+            ri[size_t(i) + 1] = ri[size_t(i)] + r2[size_t(i)];
+            kidx[size_t(i) + 1] = kidx[size_t(i)] + keep[size_t(i)];
+        }
+        b.child_rank_item.assign(ri[size_t(ng)], 0u);
+        b.child_node_of.assign(2 * ri[size_t(ng)], -1);
+        b.children.resize(kidx[size_t(ng)]);
+        const size_t node0 = nodes.size();
+        nodes.grow(nfreq);
+        std::vector<int64_t> jb(size_t(nthr), 0);
+        std::vector<int> bad(size_t(nthr), 0);
+        par_slices(nthr, ng, [&](int64_t t, int64_t i0, int64_t i1) {
+            int64_t acc = 0;
+            for (int64_t i = i0; i < i1; ++i) {
+                const uint64_t q0 = gs[size_t(i)], q1 = gs[size_t(i) + 1];
+                const DRow pr = rows[R[q0].row];
+                const ClassMeta& pm = b.cls[pr.cls];
+                const int32_t parent = b.node_of[pm.no_off + pr.mi];
+                const uint32_t pls = nodes[size_t(parent)].len_sets;
+                if ((pls >> 16) >= 0xFFFFu) bad[size_t(t)] |= 1;
+                if (q1 - q0 > 0xFFFFu) bad[size_t(t)] |= 2;
+                ChildInfo ch;
+                ch.pcls = pr.cls;
+                ch.pmi = pr.mi;
+                ch.D = 2 * r2[size_t(i)];
+                ch.ri_off = ri[size_t(i)];
+                ch.no_off = 2 * ri[size_t(i)];
+                ch.psup = nodes[size_t(parent)].support;
+                for (uint64_t q = q0; q < q1; ++q) {
+                    const FreqRec& fr = R[q];
+                    const uint32_t item = b.rank_item[pm.ri_off + (fr.slot >> 1)];
+                    const size_t node = node0 + q;
+                    nodes[node] = PNode{parent, item, fr.slot & 1u, fr.sup, pls + (1u << 16) + ((fr.slot & 1u) == kSeq)};
+                    b.child_rank_item[ch.ri_off + (fr.cid >> 1)] = item;
+                    b.child_node_of[ch.no_off + fr.cid] = int32_t(node);
+                    ch.cap += fr.sup;
+                    if ((fr.slot & 1u) == kSeq) { ++ch.nS; ch.sS += fr.sup; } else { ++ch.nI; ch.sI += fr.sup; }
+                    acc += int64_t(12ull * fr.sup);
+                }
+                if (keep[size_t(i)]) b.children[kidx[size_t(i)]] = ch;
+            }
+            jb[size_t(t)] = acc;
+        });
+        for (int64_t t = 0; t < nthr; ++t) {
+            if (bad[size_t(t)] & 1) throw Error(FSM_ELIMIT, "SPADE: a pattern exceeds 65534 items");
+            if (bad[size_t(t)] & 2) throw Error(FSM_ELIMIT, "SPADE: a prefix class has more than 65535 frequent children");
+            ctx->stats.bytes_join_equiv += jb[size_t(t)];
+        }
+    }
+
     // count kernel + frequent-candidate extraction; fills b.children / b.groups / kids
     void count_and_freq(Batch& b) {
         const double tc0 = now_ms();
         dump(b);
-        prepare(b);
+        const bool keyed_layout = prepare(b, want_keyed(b));
         const bool shard = comm && b.root;  // root rows split over ranks, frequent pairs all-gathered
+        const int64_t ncls = int64_t(b.cls.size());
+        const int64_t nthr = ncls >= (int64_t(1) << 15) ? host_threads() : 1;
         // the root and split classes are counted by every rank: their stats come from rank 0
-        for (auto& m : b.cls)
-            if (!comm || (!shard && !m.split) || comm->rank() == 0) stats_for_class(b, m);
+        if (comm || nthr == 1) {
+            for (auto& m : b.cls)
+                if (!comm || (!shard && !m.split) || comm->rank() == 0) stats_for_class(b, m);
+        } else {  // unsharded, many classes: the same sums over host threads
+            std::vector<int64_t> sj(size_t(nthr), 0), sb(size_t(nthr), 0);
+            par_slices(nthr, ncls, [&](int64_t t, int64_t c0, int64_t c1) {
+                int64_t j = 0, bb = 0;
+                for (int64_t c = c0; c < c1; ++c) {
+                    const ClassMeta& m = b.cls[size_t(c)];
+                    const uint64_t S = m.nS, I = m.nI, sS = m.sS, sI = m.sI;
+                    j += int64_t(S * S + I * S + (S ? S * (S - 1) / 2 : 0) + (I ? I * (I - 1) / 2 : 0));
+                    bb += int64_t(12 * (2 * S * sS + S * sI + I * sS + (S ? (S - 1) * sS : 0) + (I ? (I - 1) * sI : 0)));
+                }
+                sj[size_t(t)] = j;
+                sb[size_t(t)] = bb;
+            });
+            for (int64_t t = 0; t < nthr; ++t) {
+                ctx->stats.joins += sj[size_t(t)];
+                if (b.root) ctx->stats.joins_root += sj[size_t(t)];
+                ctx->stats.bytes_join_equiv += sb[size_t(t)];
+            }
+            ctx->stats.classes += ncls;
+        }
         fsm_stats& st = ctx->stats;
         st.batches += 1;
         const uint64_t tot_ent = b.E;
@@ -1378,15 +1823,33 @@ struct Miner {
         st.bytes_streamed += int64_t(tot_ent * entry_bytes());
         st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
         // member rows of the counter matrix
-        std::vector<DRow> rows;
-        for (size_t c = 0; c < b.cls.size(); ++c)
-            for (uint32_t mi = 0; mi < b.cls[c].D; ++mi)
-                if (b.node_of[b.cls[c].no_off + mi] >= 0) rows.push_back(DRow{uint32_t(c), mi});
+        std::vector<DRow>& rows = rows_s;
+        rows.clear();
+        if (nthr == 1) {
+            for (size_t c = 0; c < b.cls.size(); ++c)
+                for (uint32_t mi = 0; mi < b.cls[c].D; ++mi)
+                    if (b.node_of[b.cls[c].no_off + mi] >= 0) rows.push_back(DRow{uint32_t(c), mi});
+        } else {  // a class's rows are its members (nS + nI of them): offsets, then a parallel fill
+            std::vector<uint64_t> ro(size_t(ncls) + 1, 0);
+            for (int64_t c = 0; c < ncls; ++c) ro[size_t(c) + 1] = ro[size_t(c)] + b.cls[size_t(c)].nS + b.cls[size_t(c)].nI;
+            rows.resize(ro[size_t(ncls)]);
+            par_slices(nthr, ncls, [&](int64_t, int64_t c0, int64_t c1) {
+                for (int64_t c = c0; c < c1; ++c) {
+                    const ClassMeta& m = b.cls[size_t(c)];
+                    uint64_t at = ro[size_t(c)];
+                    for (uint32_t mi = 0; mi < m.D; ++mi)
+                        if (b.node_of[m.no_off + mi] >= 0) rows[at++] = DRow{uint32_t(c), mi};
+                }
+            });
+        }
         // root rows are rows[r] = rank r: a shard extracts its own slice of them
         const uint32_t rlo = shard ? std::min<uint32_t>(slice_lo, uint32_t(rows.size())) : 0u;
         const uint32_t rhi = shard ? std::min<uint32_t>(slice_hi, uint32_t(rows.size())) : uint32_t(rows.size());
         const uint32_t nrows = rhi - rlo;
-        std::vector<FreqRec> recs;
+        std::vector<FreqRec>& recs = recs_s;
+        recs.clear();
+        const FreqRec* ext = nullptr;  // ordered extraction: the records in pinned host memory
+        uint64_t ext_n = 0;
         DevBuf cnt;
         hp[6] += now_ms() - tc0;  // prepare + stats + rows
         const double tc1 = now_ms();
@@ -1394,16 +1857,20 @@ struct Miner {
         // the root: pairs counted per rank group, only the frequent ones leave the device
         const bool root_done = b.E && b.root && !root_atomic() && root_f2(b, recs);
         if (b.E) st.count_launches += 1;
-        if (!root_done) {
+        const bool keyed_done = !root_done && keyed_layout && keyed_count(b, cnt);
+        if (!root_done && !keyed_done) {
             cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
             FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
-            if (b.E) {
+        }
+        if (!root_done) {
+            if (b.E && !keyed_done) {
                 const SlabPtrs sp = b.slab.ptrs();
                 const uint32_t cchunk = count_chunk();
 #define FSM_COUNT(WW)                                                                                   \
     hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + cchunk - 1) / cchunk)), dim3(kBlock), 0, s,   \
                        uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
-                       member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>(), d_tests.as<unsigned long long>())
+                       member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>(), d_tests.as<unsigned long long>(),    \
+                       uint32_t(W))
                 const size_t tk = clk->begin("k_count");
                 FSM_W_DISPATCH(W, FSM_COUNT)
 #undef FSM_COUNT
@@ -1411,7 +1878,10 @@ struct Miner {
                 clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));
             }
             DevBuf d_rows;
-            upload(d_rows, std::vector<DRow>(rows.begin() + rlo, rows.begin() + rhi));
+            d_rows.alloc(std::max<size_t>(nrows, 1) * sizeof(DRow));
+            if (nrows)
+                FSM_HIP(hipMemcpyAsync(d_rows.p, rows.data() + rlo, size_t(nrows) * sizeof(DRow), hipMemcpyHostToDevice,
+                                       s));
             const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
             if (nrows > kFreqOnePassRows) {
                 // large batches: ordered extraction (the host ordering and the mapped-memory
@@ -1428,18 +1898,18 @@ struct Miner {
                 FSM_HIP(hipMemcpyAsync(&pend[1], rowoff.as<uint64_t>() + nrows, 8, hipMemcpyDeviceToHost, s));
                 sync();
                 const uint64_t nf = pend[1];
-                recs.resize(nf);
-                if (nf) {
-                    DevBuf d_recs(nf * sizeof(FreqRec));
+                if (nf) {  // records straight into mapped pinned host memory, read there after the sync
+                    PinnedBuf* pb = ctx->pinned_big(nf * sizeof(FreqRec));
                     const size_t tk = clk->begin("k_freq_write");
                     hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
                                        b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
-                                       d_recs.as<FreqRec>());
+                                       static_cast<FreqRec*>(pb->dev));
                     FSM_LAUNCHED("k_freq_write", s);
                     clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
                                          nf * sizeof(FreqRec)));
-                    FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nf * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
                     sync();
+                    ext = static_cast<const FreqRec*>(pb->host);
+                    ext_n = nf;
                 }
                 return;
             }
@@ -1476,32 +1946,51 @@ struct Miner {
         } else {
             compute();
         }
-        uint64_t nfreq = recs.size();
+        const FreqRec* R = ext ? ext : recs.data();
+        uint64_t nfreq = ext ? ext_n : recs.size();
         cnt.release();
         hp[7] += now_ms() - tc1;  // device count + extraction + ordering (incl. waits)
         if (shard) {  // every rank gets every frequent pair, in row order (slices ascend with the rank)
-            std::vector<uint8_t> mine(recs.size() * sizeof(FreqRec));
-            if (!recs.empty()) std::memcpy(mine.data(), recs.data(), mine.size());
+            std::vector<uint8_t> mine(nfreq * sizeof(FreqRec));
+            if (nfreq) std::memcpy(mine.data(), R, mine.size());
             std::vector<size_t> sizes;
             const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s);
             nfreq = all.size() / sizeof(FreqRec);
             recs.resize(nfreq);
             if (nfreq) std::memcpy(recs.data(), all.data(), all.size());
+            R = recs.data();
         }
         double th = now_ms();
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
         // one table, one H2D copy: [koff: cbase_total + 1 | kslot: nfreq | kcid: nfreq]
         const size_t nko = size_t(b.cbase_total) + 1;
-        std::vector<uint32_t> ktab(nko + 2 * size_t(nfreq), 0);
+        std::vector<uint32_t>& ktab = ktab_s;
+        ktab.resize(nko + 2 * size_t(nfreq));
         uint32_t* koff = ktab.data();
         uint32_t* kslot = koff + nko;
         uint32_t* kcid = kslot + nfreq;
-        for (const FreqRec& fr : recs) koff[b.cls[rows[fr.row].cls].cbase + rows[fr.row].mi + 1] += 1;
-        for (uint64_t x = 0; x < b.cbase_total; ++x) koff[x + 1] += koff[x];
-        for (uint64_t q = 0; q < nfreq; ++q) {  // recs are ordered by (row, slot) = CSR order
-            kslot[q] = recs[q].slot;
-            kcid[q] = recs[q].cid;
-        }
+        // records are in (row, slot) order, and a row's member slot cbase + mi ascends
+        // with the row: koff[x] = records of slots < x, by a merge (threads split x)
+        auto slot_of = [&](uint64_t q) { return uint64_t(b.cls[rows[R[q].row].cls].cbase) + rows[R[q].row].mi; };
+        const int64_t nthk = nfreq >= (uint64_t(1) << 16) ? host_threads() : 1;
+        par_slices(nthk, int64_t(nko), [&](int64_t, int64_t x0, int64_t x1) {
+            uint64_t lo = 0, hi = nfreq;  // first record with slot >= x0
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) / 2;
+                if (slot_of(mid) < uint64_t(x0)) lo = mid + 1; else hi = mid;
+            }
+            uint64_t q = lo;
+            for (int64_t x = x0; x < x1; ++x) {
+                while (q < nfreq && slot_of(q) < uint64_t(x)) ++q;
+                koff[x] = uint32_t(q);
+            }
+        });
+        par_slices(nthk, int64_t(nfreq), [&](int64_t, int64_t q0, int64_t q1) {
+            for (int64_t q = q0; q < q1; ++q) {  // recs are ordered by (row, slot) = CSR order
+                kslot[q] = R[q].slot;
+                kcid[q] = R[q].cid;
+            }
+        });
         upload(b.kid_tab, ktab);
         b.kid_off = b.kid_tab.as<uint32_t>();
         b.kid_slot = b.kid_off + nko;
@@ -1512,16 +2001,19 @@ struct Miner {
         b.children.clear();
         b.child_rank_item.clear();
         b.child_node_of.clear();
-        b.children.reserve(recs.size());
-        b.child_rank_item.reserve(recs.size() + 16);
-        b.child_node_of.reserve(2 * recs.size() + 16);
-        for (size_t q = 0; q < recs.size();) {
-            const uint32_t row = recs[q].row;
+        b.children.reserve(nfreq);
+        b.child_rank_item.reserve(nfreq + 16);
+        b.child_node_of.reserve(2 * nfreq + 16);
+        if (!comm && nfreq >= (uint64_t(1) << 16)) {
+            children_parallel(b, R, nfreq, rows);
+        } else
+        for (size_t q = 0; q < nfreq;) {
+            const uint32_t row = R[q].row;
             const DRow pr = rows[row];
             const ClassMeta& pm = b.cls[pr.cls];
             size_t q2 = q;
             uint32_t maxcid = 0;
-            while (q2 < recs.size() && recs[q2].row == row) { maxcid = std::max(maxcid, recs[q2].cid); ++q2; }
+            while (q2 < nfreq && R[q2].row == row) { maxcid = std::max(maxcid, R[q2].cid); ++q2; }
             ChildInfo ch;
             ch.pcls = pr.cls;
             ch.pmi = pr.mi;
@@ -1532,13 +2024,16 @@ struct Miner {
             b.child_rank_item.resize(ch.ri_off + R2, 0);
             b.child_node_of.resize(ch.no_off + ch.D, -1);
             const int32_t parent = b.node_of[pm.no_off + pr.mi];
+            const uint32_t pls = nodes[size_t(parent)].len_sets;
+            ch.psup = nodes[size_t(parent)].support;
+            if ((pls >> 16) >= 0xFFFFu) throw Error(FSM_ELIMIT, "SPADE: a pattern exceeds 65534 items");
             const bool dup = comm && pm.split && comm->rank() != 0;  // a split class's nodes: rank 0 outputs them
             uint32_t last_type = 0;
             for (size_t k = q; k < q2; ++k) {
-                const FreqRec& fr = recs[k];
+                const FreqRec& fr = R[k];
                 const uint32_t item = b.rank_item[pm.ri_off + (fr.slot >> 1)];
                 const int32_t node = int32_t(nodes.size());
-                nodes.push_back(PNode{parent, item, fr.slot & 1u, fr.sup});
+                nodes.push_back(PNode{parent, item, fr.slot & 1u, fr.sup, pls + (1u << 16) + ((fr.slot & 1u) == kSeq)});
                 if (dup) {
                     node_dup.resize(nodes.size(), 0);
                     node_dup[size_t(node)] = 1;
@@ -1546,6 +2041,7 @@ struct Miner {
                 b.child_rank_item[ch.ri_off + (fr.cid >> 1)] = item;
                 b.child_node_of[ch.no_off + fr.cid] = node;
                 ch.cap += fr.sup;
+                if ((fr.slot & 1u) == kSeq) { ++ch.nS; ch.sS += fr.sup; } else { ++ch.nI; ch.sI += fr.sup; }
                 if (!dup) st.bytes_join_equiv += int64_t(12ull * fr.sup);
                 last_type = fr.slot & 1u;
             }
@@ -1646,23 +2142,49 @@ struct Miner {
     void emit(Batch& b, size_t g, Batch& nb) {
         const double th = now_ms();
         const auto [ga, gb] = b.groups[g];
-        nb.cls.resize(gb - ga);
-        std::vector<uint32_t> child_of(b.cbase_total, kNone);
+        std::vector<uint32_t>& child_of = child_of_s;
+        child_of.assign(b.cbase_total, kNone);
         uint64_t total = 0;
-        for (size_t k = ga; k < gb; ++k) {
-            ChildInfo& ch = b.children[k];
-            ClassMeta& m = nb.cls[k - ga];
-            m.ri_off = nb.rank_item.size();
-            m.no_off = nb.node_of.size();
-            nb.rank_item.insert(nb.rank_item.end(), b.child_rank_item.begin() + int64_t(ch.ri_off),
-                                b.child_rank_item.begin() + int64_t(ch.ri_off + ch.D / 2));
-            nb.node_of.insert(nb.node_of.end(), b.child_node_of.begin() + int64_t(ch.no_off),
-                              b.child_node_of.begin() + int64_t(ch.no_off + ch.D));
-            m.D = ch.D;
-            m.nent = uint32_t(ch.cap);
-            m.split = ch.split;
-            child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
-            total += ch.cap;
+        // the only group: the children and their member tables move over whole (swapped:
+        // the parent, released after this emit and recycled, keeps nb's old capacity)
+        const bool whole = ga == 0 && gb == b.children.size() && b.groups.size() == 1;
+        if (whole) {
+            nb.cls.clear();
+            nb.rank_item.clear();
+            nb.node_of.clear();
+            std::swap(nb.cls, b.children);
+            std::swap(nb.rank_item, b.child_rank_item);
+            std::swap(nb.node_of, b.child_node_of);
+            const int64_t n = int64_t(nb.cls.size());
+            const ClassMeta* pc = b.cls.data();
+            ClassMeta* cc = nb.cls.data();
+            uint32_t* co = child_of.data();
+            std::vector<uint64_t> tt(16, 0);
+            const int64_t nthr = n >= (int64_t(1) << 16) ? host_threads() : 1;
+            par_slices(nthr, n, [&](int64_t t, int64_t k0, int64_t k1) {
+                uint64_t acc = 0;
+                for (int64_t k = k0; k < k1; ++k) {
+                    co[pc[cc[k].pcls].cbase + cc[k].pmi] = uint32_t(k);
+                    acc += cc[k].cap;
+                }
+                tt[size_t(t)] = acc;
+            });
+            for (uint64_t v : tt) total += v;
+        } else {
+            nb.cls.resize(gb - ga);
+            for (size_t k = ga; k < gb; ++k) {
+                const ChildInfo& ch = b.children[k];
+                ClassMeta& m = nb.cls[k - ga];
+                m = ch;
+                m.ri_off = nb.rank_item.size();
+                m.no_off = nb.node_of.size();
+                nb.rank_item.insert(nb.rank_item.end(), b.child_rank_item.begin() + int64_t(ch.ri_off),
+                                    b.child_rank_item.begin() + int64_t(ch.ri_off + ch.D / 2));
+                nb.node_of.insert(nb.node_of.end(), b.child_node_of.begin() + int64_t(ch.no_off),
+                                  b.child_node_of.begin() + int64_t(ch.no_off + ch.D));
+                child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
+                total += ch.cap;
+            }
         }
         if (total >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch exceeds 2^32 entries");
         const double th2 = now_ms();
@@ -1685,7 +2207,7 @@ struct Miner {
     hipLaunchKernelGGL(k_emit1<WW>, dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),     \
                        sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                                         \
                        b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
-                       nb.slab.cap, emit_cap())
+                       nb.slab.cap, emit_cap(), uint32_t(W))
             FSM_W_DISPATCH(W, FSM_EMIT1)
 #undef FSM_EMIT1
             FSM_LAUNCHED("k_emit", s);
@@ -1701,7 +2223,7 @@ struct Miner {
     hipLaunchKernelGGL((k_emit<WW, WR>), dim3(grid), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
                        sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                                          \
                        b.kid_cid, d_child_of.as<uint32_t>(), ncnt.as<uint32_t>(),                   \
-                       off.as<uint64_t>(), op, nb.slab.cap)
+                       off.as<uint64_t>(), op, nb.slab.cap, uint32_t(W))
 #define FSM_EMIT_COUNT(WW) FSM_EMIT(WW, false)
 #define FSM_EMIT_WRITE(WW) FSM_EMIT(WW, true)
             size_t tk = clk->begin("k_emit<count>");
@@ -1778,7 +2300,7 @@ struct Miner {
     hipLaunchKernelGGL(k_root_write_plan<WW>, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,              \
                        db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), db->mask.as<uint64_t>(),               \
                        d_rank.as<uint32_t>(), geo.R, geo.rpb, roff.as<uint64_t>(), op, geo.pm, geo.G, geo.nblk,    \
-                       geo.mlo, geo.mhi, bg, cap.as<uint32_t>())
+                       geo.mlo, geo.mhi, bg, cap.as<uint32_t>(), uint32_t(W))
             FSM_W_DISPATCH(W, FSM_ROOTWP)
 #undef FSM_ROOTWP
             FSM_LAUNCHED("k_root_write", s);
@@ -1794,7 +2316,7 @@ struct Miner {
 #define FSM_ROOTW(WW)                                                                                         \
     hipLaunchKernelGGL(k_root_write<WW>, dim3(grid), dim3(kBlock), 0, s, db->row_off.as<uint32_t>(),           \
                        db->item.as<uint32_t>(), db->mask.as<uint64_t>(), d_rank.as<uint32_t>(), r0, r1,       \
-                       roff.as<uint64_t>(), op)
+                       roff.as<uint64_t>(), op, uint32_t(W))
             FSM_W_DISPATCH(W, FSM_ROOTW)
 #undef FSM_ROOTW
             FSM_LAUNCHED("k_root_write", s);
@@ -1809,9 +2331,11 @@ struct Miner {
         root.node_of.assign(m.D, -1);
         for (uint32_t r = 0; r < F; ++r) {
             root.node_of[2 * r] = int32_t(nodes.size());
-            nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]]});
+            nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]], (1u << 16) | 1u});
         }
-        m.nent = uint32_t(E0);
+        m.cap = E0;
+        m.nS = F;
+        for (uint32_t r = 0; r < F; ++r) m.sS += f1[freq_items[r]];
         root.cls.push_back(std::move(m));
         root.root = true;
         root.root_rows = std::move(roff);
@@ -2016,14 +2540,26 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     // sharded: rank-local, failures agreed on before the pattern gather
     mn.run_or_defer([&] {
     mn.maybe_inject("lattice");
+    std::vector<std::unique_ptr<Batch>> spare;  // popped batches, recycled
+    auto pop = [&] {
+        stack.back()->recycle();
+        spare.push_back(std::move(stack.back()));
+        stack.pop_back();
+    };
     while (!stack.empty()) {
         Batch& top = *stack.back();
         if (top.next_group >= top.groups.size()) {
-            stack.pop_back();
+            pop();
             continue;
         }
         const size_t g = top.next_group++;
-        auto nb = std::make_unique<Batch>();
+        std::unique_ptr<Batch> nb;
+        if (spare.empty()) {
+            nb = std::make_unique<Batch>();
+        } else {
+            nb = std::move(spare.back());
+            spare.pop_back();
+        }
         nb->depth = top.depth + 1;
         // a pattern cannot hold more items than the longest sequence has (item, eid) occurrences
         if (nb->depth > db->spade.max_occ)
@@ -2032,7 +2568,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         mn.emit(top, g, *nb);
         if (top.next_group >= top.groups.size()) {
             // parent fully emitted: release it before descending
-            stack.pop_back();
+            pop();
         }
         mn.count_and_freq(*nb);
         stack.push_back(std::move(nb));
@@ -2060,9 +2596,10 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
 
     // ---- output CSR in discovery order (the reference's order is discovery order too);
     // sharded: rank 0 holds the shared root levels, every rank its own classes.
-    // A node's parent precedes it, so item / itemset counts are one forward
-    // pass, and every pattern then fills its own slice by walking its parents
-    // (independent slices: split over host threads).
+    // Every node carries its pattern's item and itemset counts, so the output is
+    // split over host threads in two passes: per-thread totals, then each thread
+    // writes its offsets and fills its patterns by walking their parents (the
+    // fresh output pages are first touched by the threads that fill them).
     const double to0 = now_ms();
     ctx->stats.ms_gpu_wait = mn.wait_ms;
     const auto& nodes = mn.nodes;
@@ -2078,45 +2615,54 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     }
     auto node_at = [&](int64_t k) -> int64_t { return any_dup ? int64_t(outn[size_t(k)]) : first + k; };
     int64_t n = any_dup ? int64_t(outn.size()) : NN - first;
-    std::vector<uint32_t> plen(static_cast<size_t>(NN)), pset(static_cast<size_t>(NN));
-    for (int64_t k = 0; k < NN; ++k) {
-        const int32_t q = nodes[size_t(k)].parent;
-        plen[size_t(k)] = (q < 0 ? 0u : plen[size_t(q)]) + 1u;
-        pset[size_t(k)] = (q < 0 ? 0u : pset[size_t(q)]) + ((q < 0 || nodes[size_t(k)].type == kSeq) ? 1u : 0u);
+    const int64_t nthr = n >= (int64_t(1) << 16) ? int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)) : 1;
+    auto par = [&](auto&& fn) {  // fn(t, k0, k1) over nthr slices of [0, n)
+        if (nthr == 1) return fn(int64_t(0), int64_t(0), n);
+        std::vector<std::thread> th;
+        for (int64_t t = 0; t < nthr; ++t) th.emplace_back(fn, t, n * t / nthr, n * (t + 1) / nthr);
+        for (auto& x : th) x.join();
+    };
+    std::vector<int64_t> tsets(size_t(nthr) + 1, 0), titems(size_t(nthr) + 1, 0);
+    par([&](int64_t t, int64_t k0, int64_t k1) {
+        int64_t a = 0, c = 0;
+        for (int64_t k = k0; k < k1; ++k) {
+            const uint32_t ls = nodes[size_t(node_at(k))].len_sets;
+            a += ls & 0xFFFFu;
+            c += ls >> 16;
+        }
+        tsets[size_t(t) + 1] = a;
+        titems[size_t(t) + 1] = c;
+    });
+    for (int64_t t = 0; t < nthr; ++t) {
+        tsets[size_t(t) + 1] += tsets[size_t(t)];
+        titems[size_t(t) + 1] += titems[size_t(t)];
     }
     // the output arrays are filled in place (malloc'd, handed to the caller:
     // no zero-fill and no second copy of multi-hundred-MB pattern sets)
     MallocArr<int32_t> sup{static_cast<size_t>(n)};
     MallocArr<int64_t> pat_off{static_cast<size_t>(n) + 1};
-    std::vector<int64_t> item_off(size_t(n) + 1, 0);
-    pat_off[0] = 0;
-    for (int64_t k = 0; k < n; ++k) {
-        pat_off[size_t(k) + 1] = pat_off[size_t(k)] + pset[size_t(node_at(k))];
-        item_off[size_t(k) + 1] = item_off[size_t(k)] + plen[size_t(node_at(k))];
-    }
-    MallocArr<int64_t> set_off{static_cast<size_t>(pat_off[size_t(n)]) + 1};
-    MallocArr<int32_t> items{static_cast<size_t>(item_off[size_t(n)])};
-    set_off[set_off.n - 1] = item_off[size_t(n)];
+    MallocArr<int64_t> set_off{static_cast<size_t>(tsets[size_t(nthr)]) + 1};
+    MallocArr<int32_t> items{static_cast<size_t>(titems[size_t(nthr)])};
+    pat_off[size_t(n)] = tsets[size_t(nthr)];
+    set_off[set_off.n - 1] = titems[size_t(nthr)];
     const int32_t* ival = db->spade.item_val.data();
-    auto fill = [&](int64_t k0, int64_t k1) {
+    par([&](int64_t t, int64_t k0, int64_t k1) {
+        int64_t ps = tsets[size_t(t)], pi = titems[size_t(t)];
         for (int64_t k = k0; k < k1; ++k) {
-            int64_t pos = item_off[size_t(k) + 1], sidx = pat_off[size_t(k) + 1];
-            for (int32_t q = int32_t(node_at(k)); q >= 0; q = nodes[size_t(q)].parent) {
+            const int64_t nk = node_at(k);
+            const uint32_t ls = nodes[size_t(nk)].len_sets;
+            pat_off[size_t(k)] = ps;
+            ps += ls & 0xFFFFu;
+            pi += ls >> 16;
+            int64_t pos = pi, sidx = ps;
+            for (int32_t q = int32_t(nk); q >= 0; q = nodes[size_t(q)].parent) {
                 const PNode& nd = nodes[size_t(q)];
                 items[size_t(--pos)] = ival[nd.item];
                 if (nd.parent < 0 || nd.type == kSeq) set_off[size_t(--sidx)] = pos;
             }
-            sup[size_t(k)] = int32_t(nodes[size_t(node_at(k))].support);
+            sup[size_t(k)] = int32_t(nodes[size_t(nk)].support);
         }
-    };
-    const int64_t nthr = n >= (int64_t(1) << 17) ? int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)) : 1;
-    if (nthr > 1) {
-        std::vector<std::thread> th;
-        for (int64_t t = 0; t < nthr; ++t) th.emplace_back(fill, n * t / nthr, n * (t + 1) / nthr);
-        for (auto& x : th) x.join();
-    } else {
-        fill(0, n);
-    }
+    });
     ctx->stats.ms_output = now_ms() - to0;
     auto* p = static_cast<fsm_patterns*>(std::calloc(1, sizeof(fsm_patterns)));
     if (!p) throw Error(FSM_ENOMEM, "calloc failed");

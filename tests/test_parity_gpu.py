@@ -176,13 +176,16 @@ def test_long_sequences_multiword_masks(eng):
             assert st["mask_words"] >= 2 and len(pats) > 5
 
 
-@pytest.mark.parametrize("nsets,W", [(1000, 16), (4000, 64)])
-def test_very_long_sequences_wide_masks(eng, nsets, W):
-    """~1,000 and ~4,000 distinct timestamps per sequence: W = 16 and W = 64
-    mask words (the widest the engine instantiates; more than 4,096 distinct
-    timestamps in one sequence is FSM_ELIMIT).  Planted patterns
+@pytest.mark.parametrize("nsets,W", [(1000, 16), (4000, 64), (5000, 128), (30000, 512)])
+@pytest.mark.parametrize("count_path", ["default", "keys"])
+def test_very_long_sequences_wide_masks(eng, nsets, W, count_path, monkeypatch):
+    """~1,000 to 30,000 distinct timestamps per sequence: W = 16 and W = 64
+    mask words (the widest register-held width) and W = 128 / 512 (the
+    runtime-width kernels, masks read word by word; up to 65,536 distinct
+    timestamps, SPADE.scala:74,90 registers any timestamp).  Planted patterns
     across the whole eid range, unique noise items elsewhere; the text path
-    (host flatten) and the token path (K0 on the device) against the oracle."""
+    (host flatten) and the token path (K0 on the device, or the host flatten
+    for more than 4,096 timestamps) against the oracle."""
     import numpy as np
     from oracle import oracle
     rng = random.Random(nsets)
@@ -201,6 +204,8 @@ def test_very_long_sequences_wide_masks(eng, nsets, W):
         tokens = np.array([x for t in toks for x in t], dtype=np.int64)
         sids = np.arange(len(toks), dtype=np.int32)
 
+    if count_path != "default":
+        monkeypatch.setenv("FSM_COUNT_PATH", count_path)
     for sup in (0.5, 0.75):
         o = oracle.spade(recs, sup)
         pats, _, st = gpu_spade(eng, recs, sup)
@@ -400,6 +405,43 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
+
+
+def test_timestamp_limit(eng, fsm):
+    """More than 65,536 distinct timestamps in one sequence (the 16-bit eid
+    fields of the slab) is FSM_ELIMIT with a message, never a wrong answer."""
+    recs = [(0, " ".join("%d -1" % (10 + k) for k in range(65537)) + " -2"), (1, "1 -1 2 -1 -2")]
+    with pytest.raises(fsm.FsmError) as ei:
+        gpu_spade(eng, recs, 0.5)
+    assert ei.value.code == fsm.FSM_ELIMIT and "65536" in str(ei.value)
+
+
+@pytest.mark.parametrize("path", ["keys", "atomic", "default"])
+@pytest.mark.parametrize("shape", ["quest", "sign", "bible", "sign-low"])
+def test_count_paths_agree(eng, path, shape, monkeypatch):
+    """Class counting: the keyed count (group-aligned counter layout, u16 keys
+    in (group, block) regions, LDS counting, counters written out), forced on
+    every batch, the global-atomic k_count, and the default size switch give
+    the oracle's patterns and joins, and the same executed pair tests."""
+    from oracle import oracle
+    from tools import gen
+    if path != "default":
+        monkeypatch.setenv("FSM_COUNT_PATH", path)
+    if shape == "quest":
+        ds, sup = gen.quest(20000, seed=9), 0.003
+    elif shape == "sign":
+        ds, sup = gen.sign(seed=2).head(400), 0.3
+    elif shape == "bible":
+        ds, sup = gen.bible(seed=2).head(1500), 0.03
+    else:  # low support: first-level classes whose counter matrix spans several groups
+        ds, sup = gen.sign(seed=3).head(60), 0.05
+    o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
+    pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
+    assert pats == o["patterns"] and st["joins"] == o["joins"]
+    if path == "keys":
+        monkeypatch.setenv("FSM_COUNT_PATH", "atomic")
+        _, _, st2 = gpu_spade(eng, None, sup, tokens=ds)
+        assert st2["pair_tests"] == st["pair_tests"]
 
 
 # ------------------------------------------------------ sharded (N > 1)

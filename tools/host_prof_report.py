@@ -21,6 +21,7 @@ def main():
     lib = args[1] if len(args) > 1 else os.path.join(ROOT, "spark-fsm_amd", "spark_fsm_amd", "libfsm.so")
     per_obj = collections.Counter()
     fsm_off = collections.Counter()
+    other = collections.defaultdict(collections.Counter)
     total = 0
     for ln in open(prof):
         if ln.startswith("#"):
@@ -31,6 +32,8 @@ def main():
         per_obj[os.path.basename(obj)] += n
         if obj.endswith("libfsm.so"):
             fsm_off[off] += n
+        elif os.path.exists(obj):
+            other[obj][off] += n
     print(f"samples {total}")
     for o, n in per_obj.most_common(12):
         print(f"{100.0 * n / total:6.1f}%  {o}")
@@ -46,6 +49,16 @@ def main():
     print("--- libfsm")
     for k, n in agg.most_common(40):
         print(f"{100.0 * n / total:6.1f}%  {k}")
+    for obj, cnt in other.items():
+        offs = list(cnt)
+        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-symbolizer", f"--obj={obj}", "--inlining=false",
+                              "--demangle"] + offs, capture_output=True, text=True).stdout.strip().split("\n\n")
+        a2 = collections.Counter()
+        for off, s in zip(offs, out):
+            a2[s.strip().split("\n")[0][:90]] += cnt[off]
+        print("---", os.path.basename(obj))
+        for k, n in a2.most_common(8):
+            print(f"{100.0 * n / total:6.1f}%  {k}")
 
 
 if __name__ == "__main__":
