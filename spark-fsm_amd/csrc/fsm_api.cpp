@@ -173,6 +173,8 @@ void fsm_ctx_destroy(fsm_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (hipEvent_t e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->stage_ev)
+        if (e) (void)hipEventDestroy(e);
     delete ctx->comm;
     if (ctx->pool) ctx->pool->trim();  // this context's cached blocks only; live DBs keep their pool alive
     ctx->pool.reset();

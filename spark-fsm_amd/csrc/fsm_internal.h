@@ -241,6 +241,33 @@ struct fsm_ctx {
         }
         return pin_big.get();
     }
+    // H2D staging slots (pinned, grown on demand, kept for the context's lifetime): a
+    // slot is rewritten only after the copy that last read it has completed (its event)
+    static constexpr int kStageSlots = 4;
+    std::unique_ptr<fsm::PinnedBuf> stage[kStageSlots];
+    size_t stage_bytes[kStageSlots] = {0, 0, 0, 0};
+    hipEvent_t stage_ev[kStageSlots] = {nullptr, nullptr, nullptr, nullptr};
+    bool stage_pending[kStageSlots] = {false, false, false, false};
+    void* stage_host(int i, size_t bytes) {
+        if (stage_pending[i]) {
+            FSM_HIP(hipEventSynchronize(stage_ev[i]));
+            stage_pending[i] = false;
+        }
+        if (!stage[i] || stage_bytes[i] < bytes) {
+            const size_t nb = std::max<size_t>(bytes, std::max<size_t>(2 * stage_bytes[i], size_t(1) << 20));
+            stage[i].reset();
+            stage[i] = std::make_unique<fsm::PinnedBuf>(nb);
+            stage_bytes[i] = nb;
+        }
+        return stage[i]->host;
+    }
+    void stage_copy(int i, void* dst, size_t bytes) {  // async H2D of the slot's first `bytes`
+        if (!bytes) return;
+        if (!stage_ev[i]) FSM_HIP(hipEventCreateWithFlags(&stage_ev[i], hipEventDisableTiming));
+        FSM_HIP(hipMemcpyAsync(dst, stage[i]->host, bytes, hipMemcpyHostToDevice, stream));
+        FSM_HIP(hipEventRecord(stage_ev[i], stream));
+        stage_pending[i] = true;
+    }
 };
 
 struct fsm_db {

@@ -34,6 +34,10 @@
 #include <cstdlib>
 #include <memory>
 #include <numeric>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 #include "comm.h"
@@ -1191,15 +1195,91 @@ template <class T, int kShift = 20> struct ChunkedVec {
     }
 };
 
-// fn(t, i0, i1) over nthr contiguous slices of [0, n), one host thread each
+// A persistent pool of host threads for the per-batch bookkeeping (deep lattices
+// run dozens of parallel sections per mine: creating threads for each cost more
+// than the work).  One section at a time; a caller that finds the pool busy (a
+// concurrent mine on another context) runs its section inline.  Never destroyed:
+// the workers are detached and idle between sections.
+class HostPool {
+  public:
+    static HostPool& get() {
+        static HostPool* p = new HostPool();
+        return *p;
+    }
+    // fn(t) for t in [0, n): task 0 and any unclaimed ones on the caller, the rest on workers
+    bool run(int64_t n, const std::function<void(int64_t)>& fn) {
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (!busy.owns_lock()) return false;
+        while (int64_t(workers_) < n - 1) {
+            std::thread(&HostPool::work, this).detach();
+            ++workers_;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &fn;
+            n_ = n;
+            next_.store(1);
+            left_ = n;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        finish_one();
+        for (int64_t t; (t = next_.fetch_add(1)) < n;) {
+            fn(t);
+            finish_one();
+        }
+        std::unique_lock<std::mutex> g(mu_);
+        // every worker that joined this section has left it before the next can start
+        done_cv_.wait(g, [&] { return left_ == 0 && active_ == 0; });
+        job_ = nullptr;
+        return true;
+    }
+
+  private:
+    void finish_one() {
+        std::lock_guard<std::mutex> g(mu_);
+        if (--left_ == 0 && active_ == 0) done_cv_.notify_all();
+    }
+    void work() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int64_t)>* job;
+            int64_t n;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return gen_ != seen && job_ != nullptr; });
+                seen = gen_;
+                job = job_;
+                n = n_;
+                ++active_;
+            }
+            for (int64_t t; (t = next_.fetch_add(1)) < n;) {
+                (*job)(t);
+                finish_one();
+            }
+            std::lock_guard<std::mutex> g(mu_);
+            if (--active_ == 0 && left_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int64_t)>* job_ = nullptr;
+    int64_t n_ = 0, left_ = 0, active_ = 0;
+    uint64_t gen_ = 0;
+    std::atomic<int64_t> next_{0};
+    size_t workers_ = 0;
+};
+
+// fn(t, i0, i1) over nthr contiguous slices of [0, n) on the host pool
 template <class F> void par_slices(int64_t nthr, int64_t n, F&& fn) {
     if (nthr <= 1) {
         fn(int64_t(0), int64_t(0), n);
         return;
     }
-    std::vector<std::thread> th;
-    for (int64_t t = 0; t < nthr; ++t) th.emplace_back([&fn, t, nthr, n] { fn(t, n * t / nthr, n * (t + 1) / nthr); });
-    for (auto& x : th) x.join();
+    const std::function<void(int64_t)> task = [&fn, nthr, n](int64_t t) { fn(t, n * t / nthr, n * (t + 1) / nthr); };
+    if (!HostPool::get().run(nthr, task))
+        for (int64_t t = 0; t < nthr; ++t) task(t);
 }
 int64_t host_threads() { return int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)); }
 
@@ -1377,6 +1457,19 @@ struct Miner {
 
     uint64_t entry_bytes() const { return 16ull + 8ull * uint64_t(W); }  // cid, mem, lohi, pos, mask
 
+    // large per-batch tables: copied into a pinned staging slot (over the host pool
+    // when large) and DMA'd asynchronously (pageable copies run at a fraction of that)
+    void upload_staged(int slot, DevBuf& d, const void* src, size_t bytes) {
+        d.alloc(std::max<size_t>(bytes, 4));
+        if (!bytes) return;
+        char* dst = static_cast<char*>(ctx->stage_host(slot, bytes));
+        const char* sp = static_cast<const char*>(src);
+        const int64_t nthr = bytes >= (size_t(8) << 20) ? host_threads() : 1;
+        par_slices(nthr, int64_t(bytes), [&](int64_t, int64_t a, int64_t z) {
+            if (z > a) std::memcpy(dst + a, sp + a, size_t(z - a));
+        });
+        ctx->stage_copy(slot, d.p, bytes);
+    }
     // pageable H2D copies are staged before hipMemcpyAsync returns; callers keep
     // the host vectors alive until the next synchronization anyway.
     template <class T> void upload(DevBuf& d, const std::vector<T>& h) {
@@ -1421,7 +1514,7 @@ struct Miner {
             if (cb >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
             b.n_cnt = off;
             b.cbase_total = cb;
-            upload(b.d_cls, b.h_cls);
+            upload_staged(0, b.d_cls, b.h_cls.data(), b.h_cls.size() * sizeof(DClass));
             return kl;
         }
         return false;
@@ -1878,10 +1971,7 @@ struct Miner {
                 clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));
             }
             DevBuf d_rows;
-            d_rows.alloc(std::max<size_t>(nrows, 1) * sizeof(DRow));
-            if (nrows)
-                FSM_HIP(hipMemcpyAsync(d_rows.p, rows.data() + rlo, size_t(nrows) * sizeof(DRow), hipMemcpyHostToDevice,
-                                       s));
+            upload_staged(1, d_rows, rows.data() + rlo, size_t(nrows) * sizeof(DRow));
             const unsigned grid = unsigned((uint64_t(nrows) * 64 + kBlock - 1) / kBlock);
             if (nrows > kFreqOnePassRows) {
                 // large batches: ordered extraction (the host ordering and the mapped-memory
@@ -1991,7 +2081,7 @@ struct Miner {
                 kcid[q] = R[q].cid;
             }
         });
-        upload(b.kid_tab, ktab);
+        upload_staged(2, b.kid_tab, ktab.data(), ktab.size() * 4);
         b.kid_off = b.kid_tab.as<uint32_t>();
         b.kid_slot = b.kid_off + nko;
         b.kid_cid = b.kid_slot + nfreq;
@@ -2193,7 +2283,7 @@ struct Miner {
         hp[5] += now_ms() - th2;
         nb.E = total;
         DevBuf d_child_of;
-        upload(d_child_of, child_of);
+        upload_staged(3, d_child_of, child_of.data(), child_of.size() * 4);
         ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
         if (b.E && !emit_twopass()) {
             const SlabPtrs sp = b.slab.ptrs();
@@ -2615,13 +2705,8 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     }
     auto node_at = [&](int64_t k) -> int64_t { return any_dup ? int64_t(outn[size_t(k)]) : first + k; };
     int64_t n = any_dup ? int64_t(outn.size()) : NN - first;
-    const int64_t nthr = n >= (int64_t(1) << 16) ? int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)) : 1;
-    auto par = [&](auto&& fn) {  // fn(t, k0, k1) over nthr slices of [0, n)
-        if (nthr == 1) return fn(int64_t(0), int64_t(0), n);
-        std::vector<std::thread> th;
-        for (int64_t t = 0; t < nthr; ++t) th.emplace_back(fn, t, n * t / nthr, n * (t + 1) / nthr);
-        for (auto& x : th) x.join();
-    };
+    const int64_t nthr = n >= (int64_t(1) << 16) ? host_threads() : 1;
+    auto par = [&](auto&& fn) { par_slices(nthr, n, fn); };  // fn(t, k0, k1) over nthr slices of [0, n)
     std::vector<int64_t> tsets(size_t(nthr) + 1, 0), titems(size_t(nthr) + 1, 0);
     par([&](int64_t t, int64_t k0, int64_t k1) {
         int64_t a = 0, c = 0;

@@ -434,7 +434,7 @@ def test_count_paths_agree(eng, path, shape, monkeypatch):
     elif shape == "bible":
         ds, sup = gen.bible(seed=2).head(1500), 0.03
     else:  # low support: first-level classes whose counter matrix spans several groups
-        ds, sup = gen.sign(seed=3).head(60), 0.05
+        ds, sup = gen.sign(seed=3).head(60), 0.08
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
