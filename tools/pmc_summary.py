@@ -18,7 +18,7 @@ import sys
 
 
 def kernel_name(demangled):
-    m = re.search(r"\b(k_\w+)(<([^>]*)>)?", demangled)
+    m = re.search(r"\b(k0?_\w+)(<([^>]*)>)?", demangled)
     if not m:
         return demangled.split("(")[0][:40]
     base, targs = m.group(1), m.group(3) or ""
