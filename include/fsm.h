@@ -45,7 +45,7 @@ extern "C" {
 #define FSM_EDEVICE 3   /* HIP runtime / kernel failure, or no usable gfx950 device */
 #define FSM_ENOMEM 4    /* host or device allocation failed */
 #define FSM_ECOMM 5     /* RCCL failure (multi-GPU) */
-#define FSM_ELIMIT 6    /* input exceeds an engine limit (e.g. > 4096 eids per sequence) */
+#define FSM_ELIMIT 6    /* input exceeds an engine limit (e.g. > 65536 eids per sequence) */
 
 typedef struct fsm_ctx fsm_ctx;
 typedef struct fsm_db fsm_db;

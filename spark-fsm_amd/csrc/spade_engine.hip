@@ -418,14 +418,27 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
     const uint32_t r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+    // the next row's bounds and first 64 ranks are loaded while the current row is
+    // written (each row is a chain of dependent loads: bounds -> items -> ranks)
+    uint64_t nob = 0;
+    uint32_t nlen = 0, nrb = 0, ne1 = 0, nrk = kNone;
+    auto fetch = [&](uint32_t rr) {
+        if (rr >= r1) return;
+        nob = off[rr];
+        nlen = uint32_t(off[rr + 1] - nob);
+        nrb = row_off[rr];
+        ne1 = row_off[rr + 1];
+        nrk = nrb + lane < ne1 ? rank[item[nrb + lane]] : kNone;
+    };
+    fetch(r0 + wave);
     for (uint32_t r = r0 + wave; r < r1; r += kF2Waves) {
-        const uint64_t ob = off[r];
-        const uint32_t len = uint32_t(off[r + 1] - ob);
-        const uint32_t e1 = row_off[r + 1];
+        const uint64_t ob = nob;
+        const uint32_t len = nlen, rb = nrb, e1 = ne1, rk0 = nrk;
+        fetch(r + kF2Waves);
         uint32_t k = 0;
-        for (uint32_t b0 = row_off[r]; b0 < e1; b0 += 64) {
+        for (uint32_t b0 = rb; b0 < e1; b0 += 64) {
             const uint32_t e = b0 + lane;
-            const uint32_t rk = e < e1 ? rank[item[e]] : kNone;
+            const uint32_t rk = b0 == rb ? rk0 : (e < e1 ? rank[item[e]] : kNone);
             const bool fr = rk != kNone;
             const uint64_t bal = __ballot(fr);
             if (fr) {
@@ -2365,21 +2378,20 @@ struct Miner {
             clk->end(tk, int64_t((r1 - r0) * 12 + uint64_t(db->E) * 8));
         }
         scan_exclusive(rcnt.as<uint32_t>(), roff.as<uint64_t>(), r1 - r0, s);
-        uint64_t E0 = 0;
-        uint32_t fl = 0;
-        FSM_HIP(hipMemcpyAsync(&E0, roff.as<uint64_t>() + (r1 - r0), 8, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipMemcpyAsync(&fl, flag.p, 4, hipMemcpyDeviceToHost, s));
-        sync();
-        if (fl) throw Error(FSM_ELIMIT, "SPADE: a sequence has more than 65535 distinct frequent items");
-        if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
-        root.slab.alloc(E0, W);
-        root.E = E0;
-        ctx->stats.root_entries = int64_t(E0);
-        FSM_HIP(hipMemsetAsync(root.slab.cid.p, 0, E0 * 4, s));
+        // the root entry count and the row-length flag are read back with the F2 plan's
+        // slot total at the one sync below: the root slab is sized by the DB's entries
+        pend[4] = 0;
+        pend[5] = 0;
+        FSM_HIP(hipMemcpyAsync(&pend[4], roff.as<uint64_t>() + (r1 - r0), 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(&pend[5], flag.p, 4, hipMemcpyDeviceToHost, s));
+        const uint64_t Ecap = uint64_t(std::max<int64_t>(db->E, 1));
+        root.slab.alloc(Ecap, W);
+        FSM_HIP(hipMemsetAsync(root.slab.cid.p, 0, Ecap * 4, s));
         // the root batch's F2 geometry (its slab is this root slab): plan fused into the write
         const uint32_t F = uint32_t(freq_items.size());
+        size_t tk_rw = size_t(-1);
         root.root = true;
-        const F2Geo geo = f2_geometry(root, 2 * F, E0, r1 - r0);
+        const F2Geo geo = f2_geometry(root, 2 * F, Ecap, r1 - r0);
         if (r1 > r0 && geo.ok && f2_fused()) {
             const SlabPtrs op = root.slab.ptrs();
             const int bg = f2_block_major() ? 1 : 0;
@@ -2394,8 +2406,8 @@ struct Miner {
             FSM_W_DISPATCH(W, FSM_ROOTWP)
 #undef FSM_ROOTWP
             FSM_LAUNCHED("k_root_write", s);
-            clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W)) + E0 * (16 + 8 * uint64_t(W)) +
-                                 geo.nd * 4));
+            clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W)) + geo.nd * 4));
+            tk_rw = tk;
             scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), geo.nd, s);
             FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + geo.nd, 8, hipMemcpyDeviceToHost, s));
             root.f2_planned = true;
@@ -2410,7 +2422,8 @@ struct Miner {
             FSM_W_DISPATCH(W, FSM_ROOTW)
 #undef FSM_ROOTW
             FSM_LAUNCHED("k_root_write", s);
-            clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W)) + E0 * (16 + 8 * uint64_t(W))));
+            clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W))));
+            tk_rw = tk;
         }
         ClassMeta m;
         m.D = 2 * F;
@@ -2423,7 +2436,7 @@ struct Miner {
             root.node_of[2 * r] = int32_t(nodes.size());
             nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]], (1u << 16) | 1u});
         }
-        m.cap = E0;
+        m.cap = 0;  // set from the read-back count below
         m.nS = F;
         for (uint32_t r = 0; r < F; ++r) m.sS += f1[freq_items[r]];
         root.cls.push_back(std::move(m));
@@ -2431,6 +2444,13 @@ struct Miner {
         root.root_rows = std::move(roff);
         root.R = r1 - r0;
         sync();
+        const uint64_t E0 = pend[4];
+        if (pend[5] & 0xFFFFFFFFu) throw Error(FSM_ELIMIT, "SPADE: a sequence has more than 65535 distinct frequent items");
+        if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
+        root.E = E0;
+        root.cls[0].cap = E0;
+        ctx->stats.root_entries = int64_t(E0);
+        if (tk_rw != size_t(-1)) clk->add_bytes(tk_rw, int64_t(E0 * (16 + 8 * uint64_t(W))));
         if (root.f2_planned) root.f2_nslots = pend[2];
     }
 
