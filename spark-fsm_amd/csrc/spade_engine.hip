@@ -331,6 +331,59 @@ __global__ __launch_bounds__(1024) void k_cnt_keys(uint32_t E, uint32_t epb, con
     if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
 }
 
+// Group-privatized class counting (FSM_COUNT_PATH=grp; measured slower than the
+// atomics at D1M, DESIGN.md §9, so opt-in; batches whose counters span at most
+// kGrpMax groups, e.g. the D1M first level: 8 groups): block (chunk, g) counts the joins
+// of the chunk's entries whose counter row lies in group g into an LDS copy of
+// that group, then adds its non-zero counters to HBM.  The join atomics stay in
+// LDS; each entry's group is computed once (k_entry_group).
+constexpr uint32_t kGrpMax = 16;
+
+__global__ __launch_bounds__(kBlock) void k_entry_group(uint32_t E, const uint32_t* __restrict__ cid,
+                                                        const DClass* __restrict__ cls,
+                                                        const uint32_t* __restrict__ mem, uint32_t mlo, uint32_t mhi,
+                                                        uint8_t* __restrict__ grp) {
+    for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += uint64_t(gridDim.x) * blockDim.x) {
+        const uint32_t mi = mem[e];
+        grp[e] = mi - mlo < mhi - mlo ? uint8_t(row_base(cls[cid[e]], mi) >> kGroupShift) : uint8_t(0xFF);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(1024) void k_count_grp(uint32_t E, uint32_t chunk, uint32_t G,
+                                                    const uint8_t* __restrict__ grp, const uint32_t* __restrict__ cid,
+                                                    const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                    const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                                    const uint64_t* __restrict__ mask, uint32_t* __restrict__ cnt,
+                                                    unsigned long long* __restrict__ tests, uint32_t wd) {
+    __shared__ uint32_t h[kGroupCounters];
+    __shared__ uint32_t blk_tests;
+    const uint32_t g = blockIdx.x % G, c = blockIdx.x / G;
+    for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x) h[t] = 0;
+    if (threadIdx.x == 0) blk_tests = 0;
+    __syncthreads();
+    uint32_t my_tests = 0;
+    const uint64_t e0 = uint64_t(c) * chunk, e1 = min(uint64_t(E), e0 + chunk);
+    for (uint64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        if (grp[e] != g) continue;
+        const uint32_t mi = mem[e], p = pos[e];
+        const uint32_t rl = p & 0xFFFFu, rb = uint32_t(e) - (p >> 16);
+        my_tests += rl;
+        const uint32_t kb = uint32_t(row_base(cls[cid[e]], mi)) & (kGroupCounters - 1u);
+        const uint32_t lo_i = lohi[e] & 0xFFFFu, ti = mi & 1u, ri = mi >> 1;
+        MaskV<W> mk;
+        mk.load(mask + size_t(e) * mask_words<W>(wd), wd);
+        for (uint32_t q = 0; q < rl; ++q)
+            class_joins<W>(ti, ri, lo_i, mk, rb + q, mem, lohi, mask, wd, [&](uint32_t col) { atomicAdd(&h[kb + col], 1u); });
+    }
+    atomicAdd(&blk_tests, my_tests);
+    __syncthreads();
+    uint32_t* o = cnt + uint64_t(g) * kGroupCounters;
+    for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x)
+        if (h[t]) atomicAdd(o + t, h[t]);
+    if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
+}
+
 __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bits [a, b), 0 <= a <= b <= 64
     const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
     const uint64_t lo = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
@@ -1533,22 +1586,25 @@ struct Miner {
         return false;
     }
 
-    // FSM_COUNT_PATH=atomic|keys: force the class count path (default: keyed for
-    // batches of >= kKeyedMinEntries entries; tests, profiling)
+    // FSM_COUNT_PATH=atomic|keys|grp: force the class count path (default: keyed or
+    // group-privatized for batches of >= kKeyedMinEntries entries; tests, profiling)
     static int count_path() {
         const char* v = std::getenv("FSM_COUNT_PATH");
         if (!v) return 0;
+        if (!std::strcmp(v, "grp")) return 3;
         return !std::strcmp(v, "keys") ? 2 : (!std::strcmp(v, "atomic") ? 1 : 0);
     }
     // Keyed counting pays one group pass per kGroupCounters counters and a key pass
     // over the entries, atomics one memory-side atomic per join: keyed when the
     // batch's joins (estimated as sum cap^2 / runs, runs <= the prefix support)
     // reach both its counters and twice its entries.
-    bool want_keyed(const Batch& b) const {
+    // 0: global atomics (k_count), 1: keyed, 2: group-privatized (k_count_grp)
+    int count_mode(const Batch& b) const {
         const int cp = count_path();
-        if (b.root || b.E == 0 || b.E >= kNone || cp == 1) return false;
-        if (cp == 2) return true;
-        if (b.E < kKeyedMinEntries) return false;
+        if (b.root || b.E == 0 || b.E >= kNone || cp == 1) return 0;
+        if (cp == 2) return 1;
+        if (cp == 3) return 2;
+        if (b.E < kKeyedMinEntries) return 0;
         double est = 0, ncnt = 0;
         for (const ClassMeta& m : b.cls) {
             est += double(m.cap) * double(m.cap) / double(std::max<uint32_t>(m.psup, 1));
@@ -1558,8 +1614,40 @@ struct Miner {
             std::fprintf(stderr, "[fsm] batch entries %llu: estimated joins %.3g, counters %.3g\n",
                          (unsigned long long)b.E, est, ncnt);
         // measured on MI355X: keyed wins on long runs (BIBLE/SIGN-shaped batches, >= 2 joins
-        // per entry); at about one join per entry (Quest D1M) the atomics are as fast
-        return est >= ncnt && est >= 2.0 * double(b.E);
+        // per entry); at about one join per entry (Quest D1M) its key pass costs as much as the
+        // atomics, and the group-privatized count is slower still (2.27 vs 0.9 ms: one 128 KiB
+        // LDS group per CU, same-address LDS atomics on the popular pairs), so it is opt-in
+        return est >= ncnt && est >= 2.0 * double(b.E) ? 1 : 0;
+    }
+
+    // group-privatized count of a batch laid out by prepare(b, true); false when it
+    // spans more than kGrpMax groups (the atomic path runs)
+    bool grp_count(Batch& b, DevBuf& cnt) {
+        const uint64_t G64 = (b.n_cnt + kGroupCounters - 1) >> kGroupShift;
+        if (G64 == 0 || G64 > kGrpMax) return false;
+        const uint32_t G = uint32_t(G64), E = uint32_t(b.E);
+        const SlabPtrs sp = b.slab.ptrs();
+        cnt.alloc((G64 << kGroupShift) * 4);
+        FSM_HIP(hipMemsetAsync(cnt.p, 0, (G64 << kGroupShift) * 4, s));
+        DevBuf grp(std::max<uint64_t>(b.E, 1));
+        size_t tk = clk->begin("k_entry_group");
+        hipLaunchKernelGGL(k_entry_group, dim3(unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 16384))),
+                           dim3(kBlock), 0, s, E, sp.cid, b.d_cls.as<DClass>(), sp.mem, member_lo(b), member_hi(b),
+                           grp.as<uint8_t>());
+        FSM_LAUNCHED("k_entry_group", s);
+        clk->end(tk, int64_t(b.E * 9));
+        const uint32_t nchunk = std::max<uint32_t>(1, std::min<uint32_t>(512 / G, uint32_t((b.E + 4095) / 4096)));
+        const uint32_t chunk = uint32_t((b.E + nchunk - 1) / nchunk);
+        tk = clk->begin("k_count_grp");
+#define FSM_CG(WW)                                                                                                  \
+    hipLaunchKernelGGL(k_count_grp<WW>, dim3(nchunk * G), dim3(1024), 0, s, E, chunk, G, grp.as<uint8_t>(), sp.cid, \
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, cnt.as<uint32_t>(),                   \
+                       d_tests.as<unsigned long long>(), uint32_t(W))
+        FSM_W_DISPATCH(W, FSM_CG)
+#undef FSM_CG
+        FSM_LAUNCHED("k_count_grp", s);
+        clk->end(tk, int64_t(b.E * (G + entry_bytes()) + (G64 << kGroupShift) * 4 * nchunk));
+        return true;
     }
 
     // Keyed count of a (non-root) batch laid out by prepare(b, true): plan ->
@@ -1894,7 +1982,8 @@ struct Miner {
     void count_and_freq(Batch& b) {
         const double tc0 = now_ms();
         dump(b);
-        const bool keyed_layout = prepare(b, want_keyed(b));
+        const int cmode = count_mode(b);
+        const bool keyed_layout = prepare(b, cmode != 0);
         const bool shard = comm && b.root;  // root rows split over ranks, frequent pairs all-gathered
         const int64_t ncls = int64_t(b.cls.size());
         const int64_t nthr = ncls >= (int64_t(1) << 15) ? host_threads() : 1;
@@ -1963,7 +2052,8 @@ struct Miner {
         // the root: pairs counted per rank group, only the frequent ones leave the device
         const bool root_done = b.E && b.root && !root_atomic() && root_f2(b, recs);
         if (b.E) st.count_launches += 1;
-        const bool keyed_done = !root_done && keyed_layout && keyed_count(b, cnt);
+        const bool keyed_done = !root_done && keyed_layout &&
+                                (cmode == 1 ? keyed_count(b, cnt) : grp_count(b, cnt));
         if (!root_done && !keyed_done) {
             cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
             FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));

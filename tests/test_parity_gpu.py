@@ -416,13 +416,15 @@ def test_timestamp_limit(eng, fsm):
     assert ei.value.code == fsm.FSM_ELIMIT and "65536" in str(ei.value)
 
 
-@pytest.mark.parametrize("path", ["keys", "atomic", "default"])
+@pytest.mark.parametrize("path", ["keys", "grp", "atomic", "default"])
 @pytest.mark.parametrize("shape", ["quest", "sign", "bible", "sign-low"])
 def test_count_paths_agree(eng, path, shape, monkeypatch):
     """Class counting: the keyed count (group-aligned counter layout, u16 keys
-    in (group, block) regions, LDS counting, counters written out), forced on
-    every batch, the global-atomic k_count, and the default size switch give
-    the oracle's patterns and joins, and the same executed pair tests."""
+    in (group, block) regions, LDS counting, counters written out) and the
+    group-privatized count (one LDS group per block, falls back to the atomics
+    beyond 16 groups), each forced on every batch, the global-atomic k_count,
+    and the default size switch give the oracle's patterns and joins, and the
+    same executed pair tests."""
     from oracle import oracle
     from tools import gen
     if path != "default":
@@ -438,7 +440,7 @@ def test_count_paths_agree(eng, path, shape, monkeypatch):
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
-    if path == "keys":
+    if path in ("keys", "grp"):
         monkeypatch.setenv("FSM_COUNT_PATH", "atomic")
         _, _, st2 = gpu_spade(eng, None, sup, tokens=ds)
         assert st2["pair_tests"] == st["pair_tests"]
