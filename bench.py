@@ -65,12 +65,37 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_share():
-    """CPUs this process may run on (the GPU box gives each GPU a share of the host)."""
+def cgroup_cpu_quota():
+    """CPUs granted by a cgroup CPU quota (v2 cpu.max, v1 cfs quota/period), or None."""
+    import math
     try:
-        return len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                return max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0 and per > 0:
+            return max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_share():
+    """CPUs this process may run on (the GPU box gives each GPU a share of the host):
+    the affinity mask, capped by a cgroup CPU quota when one is set."""
+    try:
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cgroup_cpu_quota()
+    return min(n, q) if q else n
 
 
 def cpu_baseline(ds, support, seconds, threads, reps):
