@@ -172,8 +172,8 @@ def tsr_leg(fsm, gen, cpu_seconds, cpu_reps, cpu):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--sequences", type=int, default=1000000)
     ap.add_argument("--support", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=1)
