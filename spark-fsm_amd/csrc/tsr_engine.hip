@@ -32,6 +32,7 @@
 #include <queue>
 #include <set>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "comm.h"
 #include "dev_db.h"
@@ -1155,40 +1156,66 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         return v ? uint32_t(std::clamp<long>(std::strtol(v, nullptr, 10), 1, kMaxBatch)) : uint32_t(kExpBatch);
     }();
     const uint64_t SU = uint64_t(B) * std::max<uint32_t>(U, 1);
-    DevBuf TL(SU * 4), DL(SU * 4), TR(SU * 4), seen(SU * 4), list(SU * 4), ctl(B * sizeof(ExpCtl));
-    FSM_HIP(hipMemsetAsync(TL.p, 0, SU * 4, s));
-    FSM_HIP(hipMemsetAsync(DL.p, 0, SU * 4, s));
-    FSM_HIP(hipMemsetAsync(TR.p, 0, SU * 4, s));
-    FSM_HIP(hipMemsetAsync(seen.p, 0, SU * 4, s));
-    FSM_HIP(hipMemsetAsync(ctl.p, 0, B * sizeof(ExpCtl), s));
-    // per-launch rule descriptors: staged in pinned host memory, one H2D copy
     const size_t kSidesB = B * sizeof(Side), kOffB = (B + 1) * 8;
-    PinnedBuf stage(kSidesB + 2 * kOffB);
-    DevBuf d_stage(kSidesB + 2 * kOffB);
-    Side* h_sides = static_cast<Side*>(stage.host);
-    uint64_t* h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(stage.host) + kSidesB);
-    uint64_t* h_wave = h_drv + (B + 1);
-    Side* d_sides = d_stage.as<Side>();
-    uint64_t* d_drv = reinterpret_cast<uint64_t*>(d_stage.as<char>() + kSidesB);
-    uint64_t* d_wave = d_drv + (B + 1);
     const bool use_bm = d->bm.p != nullptr;
-    DevBuf d_dlw, d_ndlw(16);
-    if (use_bm) {
-        d_dlw.alloc(SU * sizeof(uint4));
-    }
-    // expansion results land in mapped pinned host memory (at most one record per item per slot)
     const uint32_t ecap = std::max<uint32_t>(U, 1);
-    PinnedBuf pin(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
-    ExpHdr* h_hdr = static_cast<ExpHdr*>(pin.host);
-    ExpRec* h_rec = reinterpret_cast<ExpRec*>(h_hdr + B);
-    ExpHdr* d_hdr = static_cast<ExpHdr*>(pin.dev);
-    ExpRec* d_rec = reinterpret_cast<ExpRec*>(d_hdr + B);
+    // One set of launch buffers: per-slot histograms and control, the rule descriptors
+    // (pinned stage + device copy, one H2D copy per launch) and the results (mapped pinned
+    // host memory, at most one record per item per slot).  Set 0 serves the synchronous
+    // launches; set 1 the lookahead batch that runs while the host commits (below).
+    struct ExpSet {
+        DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw;
+        std::unique_ptr<PinnedBuf> stage, pin;
+        Side* h_sides = nullptr;
+        uint64_t *h_drv = nullptr, *h_wave = nullptr;
+        Side* d_sides = nullptr;
+        uint64_t *d_drv = nullptr, *d_wave = nullptr;
+        ExpHdr *h_hdr = nullptr, *d_hdr = nullptr;
+        ExpRec *h_rec = nullptr, *d_rec = nullptr;
+        std::vector<Rule*> batch;
+        std::vector<char> drv_in_x;
+        bool busy = false, timed = false;
+    };
+    auto make_set = [&](ExpSet& x) {
+        x.TL.alloc(SU * 4);
+        x.DL.alloc(SU * 4);
+        x.TR.alloc(SU * 4);
+        x.seen.alloc(SU * 4);
+        x.list.alloc(SU * 4);
+        x.ctl.alloc(B * sizeof(ExpCtl));
+        FSM_HIP(hipMemsetAsync(x.TL.p, 0, SU * 4, s));
+        FSM_HIP(hipMemsetAsync(x.DL.p, 0, SU * 4, s));
+        FSM_HIP(hipMemsetAsync(x.TR.p, 0, SU * 4, s));
+        FSM_HIP(hipMemsetAsync(x.seen.p, 0, SU * 4, s));
+        FSM_HIP(hipMemsetAsync(x.ctl.p, 0, B * sizeof(ExpCtl), s));
+        x.stage = std::make_unique<PinnedBuf>(kSidesB + 2 * kOffB);
+        x.d_stage.alloc(kSidesB + 2 * kOffB);
+        x.h_sides = static_cast<Side*>(x.stage->host);
+        x.h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(x.stage->host) + kSidesB);
+        x.h_wave = x.h_drv + (B + 1);
+        x.d_sides = x.d_stage.as<Side>();
+        x.d_drv = reinterpret_cast<uint64_t*>(x.d_stage.as<char>() + kSidesB);
+        x.d_wave = x.d_drv + (B + 1);
+        x.d_ndlw.alloc(16);
+        if (use_bm) x.d_dlw.alloc(SU * sizeof(uint4));
+        x.pin = std::make_unique<PinnedBuf>(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
+        x.h_hdr = static_cast<ExpHdr*>(x.pin->host);
+        x.h_rec = reinterpret_cast<ExpRec*>(x.h_hdr + B);
+        x.d_hdr = static_cast<ExpHdr*>(x.pin->dev);
+        x.d_rec = reinterpret_cast<ExpRec*>(x.d_hdr + B);
+    };
+    // FSM_TSR_LOOKAHEAD=1 enables the lookahead batch (opt-in: measured on MI355X at c4 it
+    // multiplied the pushed-back and child-speculated rules, 20K -> 121K launches, 8.5 -> 37 s)
+    const bool lookahead_on = [] { const char* v = std::getenv("FSM_TSR_LOOKAHEAD"); return v && v[0] == '1'; }();
+    ExpSet sets[2];
+    make_set(sets[0]);
+    if (lookahead_on) make_set(sets[1]);
     struct ExpResult {
         std::vector<ExpRec> recs;
         std::vector<Rule*> preL, preR;  // children created (and expanded) ahead of the commit, by record
     };
     std::unordered_map<Rule*, ExpResult> cache;
-    int64_t expansions = 0, launches = 0, spec_pushback = 0;
+    int64_t expansions = 0, launches = 0, spec_pushback = 0, la_launches = 0, la_rules = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     double last_log_ms = now_ms();  // verbose progress line every 20 s
     double prep_ms = 0, post_ms = 0, commit_ms = 0, pop_ms = 0;  // host time split (verbose summary)
@@ -1200,8 +1227,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const char* v = std::getenv("FSM_TSR_SPB");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
     }();
-    // per-kernel device time: every launch ends in a stream sync, so one set
-    // of events is recorded and read back per launch (ctx->kstats rows)
+    // per-kernel device time: every 16th synchronous launch records one set of events
+    // and reads them back at its sync (ctx->kstats rows)
     struct Seg {
         double ms = 0;  // over the timed launches
         int64_t n = 0, timed = 0, bytes = 0;
@@ -1210,13 +1237,15 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     for (hipEvent_t& e : ctx->ev)
         if (!e) FSM_HIP(hipEventCreate(&e));
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0;
-    auto launch = [&](const std::vector<Rule*>& batch) {
+    // enqueue the expansions of `batch` on set x (no sync)
+    auto launch_async = [&](ExpSet& x, const std::vector<Rule*>& batch, bool may_time) {
         const double tl0 = now_ms();
         const uint32_t nb = uint32_t(batch.size());
+        x.batch = batch;
         sides.assign(nb, Side{});
         drv_off.assign(nb + 1, 0);
         wave_off.assign(nb + 1, 0);
-        std::vector<char> drv_in_x(nb, 1);
+        x.drv_in_x.assign(nb, 1);
         for (uint32_t k = 0; k < nb; ++k) {
             const Rule* r = batch[k];
             const uint32_t *rx = rp.st.X(r), *ry = rp.st.Y(r);
@@ -1233,7 +1262,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             uint32_t drv = rx[0];
             for (uint32_t q = 0; q < r->nx; ++q) if (sup[rx[q]] < sup[drv]) drv = rx[q];
             if (!r->expandLR)
-                for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < sup[drv]) { drv = ry[q]; drv_in_x[k] = 0; }
+                for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < sup[drv]) { drv = ry[q]; x.drv_in_x[k] = 0; }
             drv_off[k] = voff[drv];
             // list path: one wave per driver sid; bitmap path: blocks sized by the
             // expected domain (about twice the rule's support: sids holding X u Y
@@ -1242,57 +1271,63 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                                                              grid.expand)
                                                     : (voff[drv + 1] - voff[drv]));
         }
-        std::memcpy(h_sides, sides.data(), nb * sizeof(Side));
-        std::memcpy(h_drv, drv_off.data(), (nb + 1) * 8);
-        std::memcpy(h_wave, wave_off.data(), (nb + 1) * 8);
-        FSM_HIP(hipMemcpyAsync(d_stage.p, stage.host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
+        std::memcpy(x.h_sides, sides.data(), nb * sizeof(Side));
+        std::memcpy(x.h_drv, drv_off.data(), (nb + 1) * 8);
+        std::memcpy(x.h_wave, wave_off.data(), (nb + 1) * 8);
+        FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
         const uint64_t waves = use_bm ? 0 : wave_off[nb];
-        const bool timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
-        if (timed) FSM_HIP(hipEventRecord(ctx->ev[0], s));
+        x.timed = may_time && (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
+        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[0], s));
         if (use_bm) {
-            hipLaunchKernelGGL(k_expand_bm, dim3(unsigned(wave_off[nb])), dim3(kBlock), 0, s, d_sides, d_wave, nb,
+            hipLaunchKernelGGL(k_expand_bm, dim3(unsigned(wave_off[nb])), dim3(kBlock), 0, s, x.d_sides, x.d_wave, nb,
                                d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), k_item.as<uint32_t>(),
                                k_first.as<uint32_t>(), k_last.as<uint32_t>(), k_sup.as<uint32_t>(), U,
-                               TL.as<uint32_t>(), TR.as<uint32_t>(), ctl.as<ExpCtl>(), d_ndlw.as<uint32_t>(),
+                               x.TL.as<uint32_t>(), x.TR.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_ndlw.as<uint32_t>(),
                                rp.minsup);
             FSM_LAUNCHED("k_expand_bm", s);
         }
         if (waves) {
             hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               d_sides, d_drv, d_wave, nb,
+                               x.d_sides, x.d_drv, x.d_wave, nb,
                                d->vert_sid.as<uint32_t>(), k_off.as<uint32_t>(), k_item.as<uint32_t>(),
-                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, TL.as<uint32_t>(),
-                               DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
-                               ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
+                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, x.TL.as<uint32_t>(),
+                               x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
+                               x.ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
             FSM_LAUNCHED("k_expand", s);
         }
-        if (timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
-        hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, TL.as<uint32_t>(),
-                           DL.as<uint32_t>(), TR.as<uint32_t>(), seen.as<uint32_t>(), list.as<uint32_t>(),
-                           ctl.as<ExpCtl>(), U, rp.minsup, d_rec, d_hdr, ecap,
-                           use_bm ? d_dlw.as<uint4>() : nullptr, d_ndlw.as<uint32_t>(),
+        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
+        hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, x.TL.as<uint32_t>(),
+                           x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
+                           x.ctl.as<ExpCtl>(), U, rp.minsup, x.d_rec, x.d_hdr, ecap,
+                           use_bm ? x.d_dlw.as<uint4>() : nullptr, x.d_ndlw.as<uint32_t>(),
                            use_bm ? d_kept.as<uint32_t>() : nullptr, uint32_t(kept_items.size()));
         FSM_LAUNCHED("k_expand_collect", s);
-        if (timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
+        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
         if (use_bm) {
-            hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, d_sides, d->bm.as<uint32_t>(),
-                               d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), d_dlw.as<uint4>(),
-                               d_ndlw.as<uint32_t>(), d_rec, ecap, ctl.as<ExpCtl>(), d_hdr, nb);
+            hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
+                               d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), x.d_dlw.as<uint4>(),
+                               x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
             FSM_LAUNCHED("k_dl", s);
         } else {
-            hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, ctl.as<ExpCtl>(), d_hdr, nb);
+            hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
             FSM_LAUNCHED("k_publish", s);
         }
-        if (timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
+        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
+        x.busy = true;
+        prep_ms += now_ms() - tl0;
+    };
+    // wait for every enqueued launch (one stream: in order) and take in set x's results
+    auto finish = [&](ExpSet& x) {
         const double tw0 = now_ms();
-        prep_ms += tw0 - tl0;
         FSM_HIP(hipStreamSynchronize(s));
         const double tw1 = now_ms();
         wait_ms += tw1 - tw0;
         ++launches;
+        const std::vector<Rule*>& batch = x.batch;
+        const uint32_t nb = uint32_t(batch.size());
         for (int q = 0; q < 3; ++q) {
             float ms = 0;
-            if (timed && hipEventElapsedTime(&ms, ctx->ev[q], ctx->ev[q + 1]) == hipSuccess) {
+            if (x.timed && hipEventElapsedTime(&ms, ctx->ev[q], ctx->ev[q + 1]) == hipSuccess) {
                 seg[q].ms += ms;
                 seg[q].timed += 1;
             }
@@ -1300,7 +1335,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
         uint64_t nout_all = 0;
         for (uint32_t k = 0; k < nb; ++k) {
-            const ExpHdr h = h_hdr[k];
+            const ExpHdr h = x.h_hdr[k];
             nout_all += h.nout;
             if (use_bm) {  // algorithmic bytes: the |X|+|Y| bitmap operands + the domain's row entries
                 const uint64_t bmb = uint64_t(batch[k]->nx + batch[k]->ny) * d->NW * 4;
@@ -1310,18 +1345,31 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 seg[0].bytes += int64_t(bmb + 12ull * h.nent + 8ull * h.nsid);
             }
             if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
-            if (!use_bm && drv_in_x[k] && h.nx != batch[k]->nX)
+            if (!use_bm && x.drv_in_x[k] && h.nx != batch[k]->nX)
                 throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(h.nx) + " vs " +
                                              std::to_string(batch[k]->nX) + ")");
             ExpResult& res = cache[batch[k]];
-            const ExpRec* rec = h_rec + size_t(k) * ecap;
+            const ExpRec* rec = x.h_rec + size_t(k) * ecap;
             res.recs.assign(rec, rec + h.nout);
-            std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& x, const ExpRec& y) { return x.c < y.c; });
+            std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
         }
         seg[1].bytes += int64_t(nout_all * sizeof(ExpRec));
+        x.busy = false;
+        x.timed = false;
         post_ms += now_ms() - tw1;
     };
-
+    std::unordered_set<const Rule*> flying;  // rules of the lookahead batch in flight
+    auto finish_lookahead = [&] {
+        if (!sets[1].busy) return;
+        finish(sets[1]);
+        for (const Rule* r : sets[1].batch) flying.erase(r);
+    };
+    // synchronous launch on set 0 (a lookahead in flight finishes at the same sync)
+    auto launch = [&](const std::vector<Rule*>& batch) {
+        launch_async(sets[0], batch, !sets[1].busy);
+        finish(sets[0]);
+        finish_lookahead();
+    };
     // Speculated rules wait in `pending` (ordered like the heap, results
     // cached) instead of going back to the heap: the next rule to commit is
     // always the larger of the heap top and the pending front, which is
@@ -1445,6 +1493,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const bool from_p = have_p && (!have_h || rule_cmp(rp.st, *pending.begin(), rp.cand.top().r) > 0);
         Rule* r = from_p ? *pending.begin() : rp.cand.top().r;
         if (r->sup < rp.minsup) break;
+        if (flying.count(r)) {  // its results are still being computed by the lookahead batch
+            finish_lookahead();
+            continue;
+        }
         auto ci = cache.find(r);
         if (from_p || ci != cache.end()) {  // results at hand (speculated earlier): commit now
             if (from_p) pending.erase(pending.begin());
@@ -1475,7 +1527,29 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         spec_pushback += int64_t(batch.size()) - 1;
         for (Rule* c : batch) pending.insert(c);
         if (spec_on) speculate(batch);
+        // Lookahead: the next heap rules are expanded on the second buffer set while the
+        // host commits this batch's results (their commit order is unchanged: they wait in
+        // `pending`, and a commit that reaches one in flight first waits for the batch)
+        if (lookahead_on && !sets[1].busy) {
+            std::vector<Rule*> la;
+            while (la.size() < size_t(B) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
+                Rule* x = rp.cand.top().r;
+                rp.cand.pop();
+                if (cache.count(x)) pending.insert(x);
+                else la.push_back(x);
+            }
+            if (!la.empty()) {
+                launch_async(sets[1], la, false);
+                for (Rule* c : la) {
+                    flying.insert(c);
+                    pending.insert(c);
+                }
+                ++la_launches;
+                la_rules += int64_t(la.size());
+            }
+        }
     }
+    finish_lookahead();  // a lookahead still in flight at the end: its results are not needed
     if (ctx->opts.verbose)
         std::fprintf(stderr,
                      "[fsm tsr] expansions %lld in %lld launches (%lld pushed back), %.0f ms waiting on the GPU; "
@@ -1483,8 +1557,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      (long long)expansions, (long long)launches, (long long)spec_pushback, wait_ms, prep_ms, post_ms,
                      commit_ms, pop_ms, rp.st.rules.size());
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches\n", (long long)spec_made,
-                     (long long)spec_launches);
+        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; lookahead: %lld rules in %lld launches\n",
+                     (long long)spec_made, (long long)spec_launches, (long long)la_rules, (long long)la_launches);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {

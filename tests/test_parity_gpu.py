@@ -541,13 +541,16 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
 
 
 @pytest.mark.parametrize("batch", ["1", "7", "128"])
-def test_tsr_batch_sizes_agree(eng, batch, monkeypatch):
-    """Rules expanded per launch (FSM_TSR_BATCH) change only how much runs
-    ahead speculatively: the rules and final minsup stay the oracle's."""
+@pytest.mark.parametrize("lookahead", ["1", "0"])
+def test_tsr_batch_sizes_agree(eng, batch, lookahead, monkeypatch):
+    """Rules expanded per launch (FSM_TSR_BATCH) and the lookahead batch on the
+    second buffer set (FSM_TSR_LOOKAHEAD) change only how much runs ahead
+    speculatively: the rules and final minsup stay the oracle's."""
     from oracle import oracle
     from tools import gen
     from spark_fsm_amd import MODE_TSR
     monkeypatch.setenv("FSM_TSR_BATCH", batch)
+    monkeypatch.setenv("FSM_TSR_LOOKAHEAD", lookahead)
     ds = gen.kosarak(D=5000, seed=6)
     o = oracle.tsr(ds.records(), 150, 0.5)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)
