@@ -1604,7 +1604,11 @@ struct Miner {
         if (b.root || b.E == 0 || b.E >= kNone || cp == 1) return 0;
         if (cp == 2) return 1;
         if (cp == 3) return 2;
-        if (b.E < kKeyedMinEntries) return 0;
+        static const uint64_t min_e = [] {  // FSM_KEYED_MIN overrides kKeyedMinEntries (tuning)
+            const char* v = std::getenv("FSM_KEYED_MIN");
+            return v ? uint64_t(std::strtoull(v, nullptr, 10)) : uint64_t(kKeyedMinEntries);
+        }();
+        if (b.E < min_e) return 0;
         double est = 0, ncnt = 0;
         for (const ClassMeta& m : b.cls) {
             est += double(m.cap) * double(m.cap) / double(std::max<uint32_t>(m.psup, 1));
