@@ -693,7 +693,7 @@ typedef struct {
     int64_t* item_off;          /* [nsets+1] into items */
     int32_t* items;             /* dense item ids */
     heap krules, cand;
-    VEC(rule*) all;
+    int64_t purge_at;           /* candidate count that triggers the next purge */
     int64_t expansions;
     /* scratch for expansions */
     int32_t* cnt_last_tid;
@@ -709,6 +709,38 @@ static void rule_release_state(rule* r) {
     r->common = NULL;
 }
 
+/* A rule is freed as soon as neither kRules nor the candidates (nor the
+ * expansion in progress, which holds in_cand) reference it: memory then
+ * follows the live rules, not every rule ever made (the 100K-sequence
+ * Kosarak prefix makes ~10^8 of them while minsup is still low). */
+static void rule_maybe_free(rule* r) {
+    if (r->in_k || r->in_cand) return;
+    rule_release_state(r);
+    free(r->X);
+    free(r->Y);
+    free(r);
+}
+
+/* Candidates with sup < minsup can never be expanded (the expansion loop
+ * stops at the first such pop, and minsup only rises), so dropping them
+ * changes nothing: the remaining pop order is the comparator's total order. */
+static void tsr_purge(tsr_ctx* c) {
+    heap old = c->cand;
+    c->cand.a = NULL;
+    c->cand.n = c->cand.cap = 0;
+    for (int64_t q = 0; q < old.n; q++) {
+        rule* r = old.a[q];
+        if (r->sup >= c->minsup) {
+            heap_push(&c->cand, r);
+        } else {
+            r->in_cand = 0;
+            rule_maybe_free(r);
+        }
+    }
+    free(old.a);
+    c->purge_at = 2 * c->cand.n > (1 << 20) ? 2 * c->cand.n : (1 << 20);
+}
+
 /* AlgoTopSeqRules.save [EXT, SURVEY A.3] */
 static void tsr_save(tsr_ctx* c, rule* r) {
     heap_push(&c->krules, r);
@@ -719,6 +751,7 @@ static void tsr_save(tsr_ctx* c, rule* r) {
                 rule* lower = heap_pop(&c->krules);
                 if (!lower) break;
                 lower->in_k = 0;
+                if (lower != r) rule_maybe_free(lower);  /* r itself is registered next */
             } while (c->krules.n > c->k);
         }
         c->minsup = c->krules.a[0]->sup;
@@ -729,6 +762,7 @@ static void tsr_register(tsr_ctx* c, rule* r, int lr) {
     r->expandLR = lr;
     r->in_cand = 1;
     heap_push(&c->cand, r);
+    if (c->cand.n > c->purge_at) tsr_purge(c);
 }
 
 static rule* rule_new(tsr_ctx* c, const int32_t* X, int32_t nx, int32_t xadd, const int32_t* Y,
@@ -742,7 +776,6 @@ static rule* rule_new(tsr_ctx* c, const int32_t* X, int32_t nx, int32_t xadd, co
     memcpy(r->Y, Y, (size_t)ny * sizeof(int32_t));
     if (xadd >= 0) r->X[nx] = xadd;
     if (yadd >= 0) r->Y[ny] = yadd;
-    VPUSH(c->all, r);
     return r;
 }
 
@@ -783,9 +816,31 @@ static int contains_lex(const int32_t* s, int32_t n, int32_t c) {
     return 0;
 }
 
+/* tidsIJ of a pair-phase rule, made when the rule is first expanded (the pair
+ * phase keeps no per-rule sid lists: at minsup 1 there are ~10^8 such rules on
+ * the 100K-sequence Kosarak prefix): the sids of I (sids(X), firstX) and J
+ * (sids(Y), lastY) with firstX < lastY, ascending. */
+static void ensure_common(rule* r) {
+    if (r->common) return;
+    const tidpos *I = r->I, *J = r->J;
+    r->common = malloc((size_t)(I->n < J->n ? I->n : J->n) * sizeof(int32_t) + 4);
+    r->ncommon = 0;
+    int64_t a = 0, b = 0;
+    while (a < I->n && b < J->n) {
+        if (I->sid[a] < J->sid[b]) a++;
+        else if (J->sid[b] < I->sid[a]) b++;
+        else {
+            if (I->pos[a] < J->pos[b]) r->common[r->ncommon++] = I->sid[a];
+            a++;
+            b++;
+        }
+    }
+}
+
 /* expandL: rules X U {c} => Y, c > max(X), c not in Y, c before lastY(s). */
 static void tsr_expand_left(tsr_ctx* c, rule* r) {
     c->expansions++;
+    ensure_common(r);
     scan_reset(c);
     for (int64_t q = 0; q < r->ncommon; q++) {
         int32_t tid = r->common[q];
@@ -834,6 +889,7 @@ static void tsr_expand_left(tsr_ctx* c, rule* r) {
 /* expandR: rules X => Y U {c}, c > max(Y), c not in X, c after firstX(s). */
 static void tsr_expand_right(tsr_ctx* c, rule* r) {
     c->expansions++;
+    ensure_common(r);
     scan_reset(c);
     for (int64_t q = 0; q < r->ncommon; q++) {
         int32_t tid = r->common[q];
@@ -960,6 +1016,7 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
         c.minsup = 1;
         c.krules.max = 0;
         c.cand.max = 1;
+        c.purge_at = 1 << 20;
         c.nseq = n;
         c.set_off = set_off.a;
         c.item_off = item_off.a;
@@ -1024,14 +1081,12 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
                 if (fj->n < c.minsup) continue;
                 pairs++;
                 int64_t a = 0, b = 0, nij = 0, nji = 0;
-                int32_t* tij = malloc((size_t)(fi->n < fj->n ? fi->n : fj->n) * sizeof(int32_t) + 4);
-                int32_t* tji = malloc((size_t)(fi->n < fj->n ? fi->n : fj->n) * sizeof(int32_t) + 4);
                 while (a < fi->n && b < fj->n) {
                     if (fi->sid[a] < fj->sid[b]) a++;
                     else if (fj->sid[b] < fi->sid[a]) b++;
                     else {
-                        if (fi->pos[a] < lj->pos[b]) tij[nij++] = fi->sid[a];
-                        if (fj->pos[b] < li->pos[a]) tji[nji++] = fi->sid[a];
+                        nij += fi->pos[a] < lj->pos[b];
+                        nji += fj->pos[b] < li->pos[a];
                         a++;
                         b++;
                     }
@@ -1043,7 +1098,7 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
                     r->conf = (double)nij / (double)fi->n;
                     r->I = c.first[i]; r->I->refs++;
                     r->J = c.last[j]; r->J->refs++;
-                    r->common = tij; r->ncommon = nij; tij = NULL;
+                    /* tidsIJ: made by ensure_common if r is ever expanded */
                     if (r->conf >= c.minconf) tsr_save(&c, r);
                     tsr_register(&c, r, 1);
                 }
@@ -1053,27 +1108,29 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
                     r->conf = (double)nji / (double)fj->n;
                     r->I = c.first[j]; r->I->refs++;
                     r->J = c.last[i]; r->J->refs++;
-                    r->common = tji; r->ncommon = nji; tji = NULL;
+                    /* tidsJI: likewise */
                     if (r->conf >= c.minconf) tsr_save(&c, r);
                     tsr_register(&c, r, 1);
                 }
-                free(tij);
-                free(tji);
             }
         }
         /* Expansion loop */
         while (complete && c.cand.n > 0) {
             if (deadline > 0 && mono_s() > deadline) { complete = 0; break; }
-            rule* r = heap_pop(&c.cand);
-            r->in_cand = 0;
-            if (r->sup < c.minsup) break;
+            rule* r = heap_pop(&c.cand);  /* in_cand stays set while r is expanded */
+            if (r->sup < c.minsup) {
+                r->in_cand = 0;
+                rule_maybe_free(r);
+                break;
+            }
             if (r->expandLR) {
                 tsr_expand_left(&c, r);
                 tsr_expand_right(&c, r);
             } else {
                 tsr_expand_right(&c, r);
             }
-            rule_release_state(r);
+            r->in_cand = 0;
+            rule_maybe_free(r);
         }
         /* result = kRules */
         oracle_rules* o = calloc(1, sizeof(*o));
@@ -1105,14 +1162,14 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
         }
         *out = o;
         /* cleanup */
-        for (int64_t q = 0; q < c.all.n; q++) {
-            rule* r = c.all.a[q];
-            rule_release_state(r);
-            free(r->X);
-            free(r->Y);
-            free(r);
+        for (int64_t q = 0; q < c.krules.n; q++) {
+            c.krules.a[q]->in_k = 0;
+            rule_maybe_free(c.krules.a[q]);
         }
-        VFREE(c.all);
+        for (int64_t q = 0; q < c.cand.n; q++) {
+            c.cand.a[q]->in_cand = 0;
+            rule_maybe_free(c.cand.a[q]);
+        }
         for (int64_t q = 0; q < nu; q++) {
             tidpos_release(c.first[q]);
             tidpos_release(c.last[q]);

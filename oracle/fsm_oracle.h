@@ -76,6 +76,12 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
                      int32_t k, double minconf, double time_limit_s, oracle_rules** out, char* err, int errlen);
 void oracle_rules_free(oracle_rules* r);
 
+/* Every valid rule (conf >= minconf) with support >= t, by definition at a fixed
+ * threshold (oracle/tsr_exhaustive.c; seed subtrees on nthreads OpenMP threads).
+ * expansions = rule nodes with sup >= t visited, pairs = seed pairs, final_minsup = t. */
+int oracle_tsr_all(const int64_t* seq_off, const int64_t* tokens, int64_t n, int32_t t, double minconf,
+                   int nthreads, oracle_rules** out, char* err, int errlen);
+
 /* Definitional point checks over a token stream (-1 / -2 separators). */
 int64_t oracle_pattern_support(const int64_t* seq_off, const int64_t* tokens, int64_t n,
                                const int32_t* items, const int64_t* set_off, int64_t nsets);

@@ -102,6 +102,9 @@ def lib():
             ctypes.POINTER(ctypes.POINTER(_Rules)), ctypes.c_char_p, ctypes.c_int]
         L.oracle_tsr_timed.restype = ctypes.c_int
         L.oracle_rules_free.argtypes = [ctypes.POINTER(_Rules)]
+        L.oracle_tsr_all.argtypes = [I64P, I64P, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.POINTER(_Rules)), ctypes.c_char_p, ctypes.c_int]
+        L.oracle_tsr_all.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -244,5 +247,34 @@ def tsr(records, k, minconf, time_limit_s=0.0):
     rules.sort(key=lambda t: (-t[2], t[0], t[1]))
     res = {"rules": rules, "total": r.total, "expansions": r.expansions,
            "final_minsup": r.final_minsup, "complete": bool(r.complete), "seconds": r.seconds, "pairs": r.pairs}
+    L.oracle_rules_free(out)
+    return res
+
+
+def _rules_out(r):
+    rules = []
+    for i in range(r.n):
+        x = tuple(r.ante[q] for q in range(r.ante_off[i], r.ante_off[i + 1]))
+        y = tuple(r.cons[q] for q in range(r.cons_off[i], r.cons_off[i + 1]))
+        rules.append((x, y, r.support[i], r.confidence[i]))
+    rules.sort(key=lambda t: (-t[2], t[0], t[1]))
+    return rules
+
+
+def tsr_all(seq_off, tokens, t, minconf, threads=1):
+    """Every valid rule with support >= t, by definition at a fixed threshold
+    (oracle/tsr_exhaustive.c): the completeness pin of SURVEY §8(c)(ii).
+    Token stream: -1 closes an itemset, -2 is ignored, sid = record index."""
+    L = lib()
+    so, so_p = _np64(seq_off)
+    tk, tk_p = _np64(tokens)
+    out = ctypes.POINTER(_Rules)()
+    err = ctypes.create_string_buffer(512)
+    rc = L.oracle_tsr_all(so_p, tk_p, len(so) - 1, int(t), float(minconf), int(threads), ctypes.byref(out), err, 512)
+    if rc != 0:
+        raise OracleError(err.value.decode())
+    r = out.contents
+    res = {"rules": _rules_out(r), "total": r.total, "explored": r.expansions, "seeds": r.pairs,
+           "t": r.final_minsup, "seconds": r.seconds}
     L.oracle_rules_free(out)
     return res

@@ -11,6 +11,11 @@
 //             Device buffers are staged through host memory around the callback.
 #include <dlfcn.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
 #include <mutex>
 
 #include <rccl/rccl.h>
@@ -186,6 +191,31 @@ void shard_plan(const uint64_t* volume, int64_t n, int32_t nranks, int32_t* owne
         owner[i] = best;
         load[size_t(best)] += volume[i];
     }
+}
+
+}  // namespace fsm
+
+namespace fsm {
+
+void Agreement::agree(hipStream_t s) {
+    if (!comm) return;
+    std::vector<uint32_t> v(8, 0u);
+    if (code) v[size_t(std::clamp(code, 1, 7))] = 1u;
+    comm->host_allreduce_u32(v.data(), v.size(), s);
+    if (code) throw Error(code, msg);
+    for (int c = 1; c < 8; ++c)
+        if (v[size_t(c)])
+            throw Error(c, std::string(what) + ": a peer rank failed (FSM error " + std::to_string(c) +
+                               "); the sharded mine is aborted on every rank");
+}
+
+void Agreement::maybe_inject(const char* phase) const {
+    const char* v = std::getenv("FSM_INJECT_FAIL");
+    if (!v || !comm) return;
+    char ph[16] = {0};
+    int r = -1;
+    if (std::sscanf(v, "%d,%15s", &r, ph) == 2 && r == comm->rank() && !std::strcmp(ph, phase))
+        throw Error(FSM_ELIMIT, std::string(what) + ": injected failure (FSM_INJECT_FAIL, " + phase + ")");
 }
 
 }  // namespace fsm

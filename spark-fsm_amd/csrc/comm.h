@@ -2,6 +2,7 @@
 #pragma once
 
 #include <memory>
+#include <string>
 
 #include "fsm_internal.h"
 
@@ -25,6 +26,41 @@ class Comm {
 
   private:
     int nranks_, rank_;
+};
+
+// Failure agreement of a sharded phase: a failure on one rank must not leave
+// its peers blocked in a collective.  The work between two collectives runs
+// through run(), which records a throw instead of unwinding when there is a
+// communicator; agree(), called by every rank before the next collective,
+// all-reduces the failure flags and throws the same FSM_E* code on every rank.
+struct Agreement {
+    Comm* comm = nullptr;
+    const char* what = "";  // "SPADE" / "TSR", for the peer message
+    int code = 0;
+    std::string msg;
+    template <class F> void run(F&& f) {
+        if (!comm) {
+            f();
+            return;
+        }
+        if (code) return;
+        try {
+            f();
+        } catch (const Error& e) {
+            code = e.code;
+            msg = e.what();
+        } catch (const std::bad_alloc&) {
+            code = FSM_ENOMEM;
+            msg = "host allocation failed";
+        } catch (const std::exception& e) {
+            code = FSM_EDEVICE;
+            msg = e.what();
+        }
+    }
+    void agree(hipStream_t s);
+    // FSM_INJECT_FAIL="<rank>,<phase>": throw FSM_ELIMIT on that rank at that phase
+    // (test hook for the agreement)
+    void maybe_inject(const char* phase) const;
 };
 
 std::unique_ptr<Comm> make_comm(const fsm_opts& o);

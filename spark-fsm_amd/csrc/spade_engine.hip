@@ -36,6 +36,7 @@
 #include <numeric>
 #include <atomic>
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -331,59 +332,6 @@ __global__ __launch_bounds__(1024) void k_cnt_keys(uint32_t E, uint32_t epb, con
     if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
 }
 
-// Group-privatized class counting (FSM_COUNT_PATH=grp; measured slower than the
-// atomics at D1M, DESIGN.md §9, so opt-in; batches whose counters span at most
-// kGrpMax groups, e.g. the D1M first level: 8 groups): block (chunk, g) counts the joins
-// of the chunk's entries whose counter row lies in group g into an LDS copy of
-// that group, then adds its non-zero counters to HBM.  The join atomics stay in
-// LDS; each entry's group is computed once (k_entry_group).
-constexpr uint32_t kGrpMax = 16;
-
-__global__ __launch_bounds__(kBlock) void k_entry_group(uint32_t E, const uint32_t* __restrict__ cid,
-                                                        const DClass* __restrict__ cls,
-                                                        const uint32_t* __restrict__ mem, uint32_t mlo, uint32_t mhi,
-                                                        uint8_t* __restrict__ grp) {
-    for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += uint64_t(gridDim.x) * blockDim.x) {
-        const uint32_t mi = mem[e];
-        grp[e] = mi - mlo < mhi - mlo ? uint8_t(row_base(cls[cid[e]], mi) >> kGroupShift) : uint8_t(0xFF);
-    }
-}
-
-template <int W>
-__global__ __launch_bounds__(1024) void k_count_grp(uint32_t E, uint32_t chunk, uint32_t G,
-                                                    const uint8_t* __restrict__ grp, const uint32_t* __restrict__ cid,
-                                                    const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
-                                                    const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
-                                                    const uint64_t* __restrict__ mask, uint32_t* __restrict__ cnt,
-                                                    unsigned long long* __restrict__ tests, uint32_t wd) {
-    __shared__ uint32_t h[kGroupCounters];
-    __shared__ uint32_t blk_tests;
-    const uint32_t g = blockIdx.x % G, c = blockIdx.x / G;
-    for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x) h[t] = 0;
-    if (threadIdx.x == 0) blk_tests = 0;
-    __syncthreads();
-    uint32_t my_tests = 0;
-    const uint64_t e0 = uint64_t(c) * chunk, e1 = min(uint64_t(E), e0 + chunk);
-    for (uint64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-        if (grp[e] != g) continue;
-        const uint32_t mi = mem[e], p = pos[e];
-        const uint32_t rl = p & 0xFFFFu, rb = uint32_t(e) - (p >> 16);
-        my_tests += rl;
-        const uint32_t kb = uint32_t(row_base(cls[cid[e]], mi)) & (kGroupCounters - 1u);
-        const uint32_t lo_i = lohi[e] & 0xFFFFu, ti = mi & 1u, ri = mi >> 1;
-        MaskV<W> mk;
-        mk.load(mask + size_t(e) * mask_words<W>(wd), wd);
-        for (uint32_t q = 0; q < rl; ++q)
-            class_joins<W>(ti, ri, lo_i, mk, rb + q, mem, lohi, mask, wd, [&](uint32_t col) { atomicAdd(&h[kb + col], 1u); });
-    }
-    atomicAdd(&blk_tests, my_tests);
-    __syncthreads();
-    uint32_t* o = cnt + uint64_t(g) * kGroupCounters;
-    for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x)
-        if (h[t]) atomicAdd(o + t, h[t]);
-    if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
-}
-
 __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bits [a, b), 0 <= a <= b <= 64
     const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
     const uint64_t lo = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
@@ -395,9 +343,10 @@ __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bit
 // Every key of a root entry lies in the counter row of its own rank, so the
 // matrix is cut into rank groups of `per` ranks whose per*D counters fit
 // 128 KiB of LDS, and the pairs are partitioned by group on the way out:
-//   k_f2_plan   per (group, row block): key capacity = sum of the entries'
+//   plan        per (group, row block): key capacity = sum of the entries'
 //               upper bounds (temporal <= row length, equality <= partners of
-//               higher rank); exclusive scan -> region bases, group-major
+//               higher rank), made by k_root_write_plan while it writes the
+//               root rows; exclusive scan -> region bases, group-major
 //   k_f2_keys   THE one partner enumeration: row block b writes the keys of
 //               group g (u16, local to the group's counter tile) into region
 //               (g, b) through an LDS cursor per group.  Rows of <= 64 entries
@@ -414,33 +363,10 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return uint32_t(__builtin_
 // rank -> group by multiply-high (exact for rank < 2^16, per < 2^15)
 __device__ __forceinline__ uint32_t group_of(uint32_t rank, uint32_t pm) { return __umulhi(rank, pm); }
 
-// region (group g, row block b) in scan order: group-major [g][b] (each group's keys one
-// contiguous stream for k_f2_count) or block-major [b][g] (each block's keys one contiguous
-// stretch: region boundary lines are written by one block, in one XCD's L2)
-__device__ __forceinline__ uint64_t f2_region(uint32_t g, uint32_t b, uint32_t G, uint32_t nblk, int bg) {
-    return bg ? uint64_t(b) * G + g : uint64_t(g) * nblk + b;
-}
-
-__global__ __launch_bounds__(kBlock) void k_f2_plan(const uint64_t* __restrict__ roff, uint32_t R, uint32_t rpb,
-                                                    const uint32_t* __restrict__ mem, const uint32_t* __restrict__ pos,
-                                                    uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo, uint32_t mhi,
-                                                    int bg, uint32_t* __restrict__ cap) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
-    __syncthreads();
-    const uint32_t r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
-    const uint64_t e0 = roff[r0], e1 = roff[r1];
-    for (uint64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-        const uint32_t mi = mem[e];
-        if (mi - mlo < mhi - mlo) {
-            const uint32_t p = pos[e], rl = p & 0xFFFFu, off = p >> 16;
-            atomicAdd(&h[group_of(mi >> 1, pm)], 2 * rl - 1 - off);
-        }
-    }
-    __syncthreads();
-    // regions start on 16-byte boundaries (8 keys): k_f2_count reads them in aligned chunks
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
-        cap[f2_region(g, blockIdx.x, G, nblk, bg)] = (h[g] + 7u) & ~7u;
+// region (group g, row block b) in scan order: group-major [g][b], each group's keys one
+// contiguous stream for k_f2_count (block-major measured no faster)
+__device__ __forceinline__ uint64_t f2_region(uint32_t g, uint32_t b, uint32_t nblk) {
+    return uint64_t(g) * nblk + b;
 }
 
 constexpr uint32_t kF2Threads = 1024;  // k_f2_keys / k_f2_count block
@@ -456,7 +382,7 @@ constexpr uint32_t kF2MaxRows = 4096;  // rows per block of k_f2_keys (row offse
 
 // Root rows fused with the F2 plan: block b builds the root runs of its row block
 // (rpb rows, one wave per row in turn, as k_root_write) and histograms the key
-// capacity of every entry it writes by rank group (k_f2_plan's numbers) in LDS.
+// capacity of every entry it writes by rank group (the F2 plan) in LDS.
 template <int W>
 __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* __restrict__ row_off,
                                                                const uint32_t* __restrict__ item,
@@ -464,7 +390,7 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
                                                                const uint32_t* __restrict__ rank, uint32_t R,
                                                                uint32_t rpb, const uint64_t* __restrict__ off,
                                                                SlabPtrs o, uint32_t pm, uint32_t G, uint32_t nblk,
-                                                               uint32_t mlo, uint32_t mhi, int bg,
+                                                               uint32_t mlo, uint32_t mhi,
                                                                uint32_t* __restrict__ cap, uint32_t wd) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
@@ -515,7 +441,7 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
     __syncthreads();
     // regions start on 16-byte boundaries (8 keys): k_f2_count reads them in aligned chunks
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
-        cap[f2_region(g, blockIdx.x, G, nblk, bg)] = (h[g] + 7u) & ~7u;
+        cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + 7u) & ~7u;
 }
 
 template <int W>
@@ -524,7 +450,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                                                         const uint32_t* __restrict__ lohi,
                                                         const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
                                                         uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
-                                                        uint32_t mhi, const uint64_t* __restrict__ base, int bg,
+                                                        uint32_t mhi, const uint64_t* __restrict__ base,
                                                         uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
                                                         unsigned long long* __restrict__ nkeys_total, uint32_t wd) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -535,7 +461,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     __shared__ uint32_t blk_keys;
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[f2_region(g, b, G, nblk, bg)]);
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[f2_region(g, b, nblk)]);
     for (uint32_t r = r0 + threadIdx.x; r <= r1; r += blockDim.x) srow[r - r0] = uint32_t(roff[r]);
     if (threadIdx.x == 0) blk_keys = 0;
     __syncthreads();
@@ -657,7 +583,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     atomicAdd(&blk_keys, my_keys);
     __syncthreads();
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
-        fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[f2_region(g, b, G, nblk, bg)]);
+        fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[f2_region(g, b, nblk)]);
     if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
@@ -674,7 +600,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
 // out to cnt_out[g * kGroupCounters ...] instead of extracted.
 constexpr uint32_t kF2MaxBlocks = 2048;  // row blocks (regions per group) k_f2_count can index in LDS
 template <bool kOut>
-__global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base, uint32_t G, int bg,
+__global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base,
                                                          const uint32_t* __restrict__ fill, uint32_t nblk,
                                                          const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
                                                          uint32_t g0, uint32_t rlo, uint32_t rhi, uint32_t minsup,
@@ -698,11 +624,11 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
     const uint32_t s0 = 2 * threadIdx.x;
     const uint32_t f0 = s0 < nr ? fill[gi + s0] : 0u, f1 = s0 + 1 < nr ? fill[gi + s0 + 1] : 0u;
     if (s0 < nr) {
-        cst[s0] = uint32_t(base[f2_region(g, rb0 + s0, G, nblk, bg)]) >> 3;
+        cst[s0] = uint32_t(base[f2_region(g, rb0 + s0, nblk)]) >> 3;
         sfill[s0] = f0;
     }
     if (s0 + 1 < nr) {
-        cst[s0 + 1] = uint32_t(base[f2_region(g, rb0 + s0 + 1, G, nblk, bg)]) >> 3;
+        cst[s0 + 1] = uint32_t(base[f2_region(g, rb0 + s0 + 1, nblk)]) >> 3;
         sfill[s0 + 1] = f1;
     }
     const uint32_t c0 = (f0 + 7) >> 3, c1 = (f1 + 7) >> 3;
@@ -1036,50 +962,6 @@ __device__ __forceinline__ void emit_write(const SlabPtrs& o, uint64_t cap, uint
     }
 }
 
-// Two-pass emission (FSM_EMIT_PATH=twopass): count pass -> exclusive scan of
-// the run lengths -> write pass that joins again; runs in parent-entry order.
-template <int W, bool kWrite>
-__global__ __launch_bounds__(kBlock) void k_emit(uint32_t E, const uint32_t* __restrict__ cid,
-                                                 const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
-                                                 const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
-                                                 const uint64_t* __restrict__ mask,
-                                                 const uint32_t* __restrict__ kid_off,
-                                                 const uint32_t* __restrict__ kid_slot,
-                                                 const uint32_t* __restrict__ kid_cid,
-                                                 const uint32_t* __restrict__ child_of, uint32_t* __restrict__ ncnt,
-                                                 const uint64_t* __restrict__ off, SlabPtrs o, uint64_t cap,
-                                                 uint32_t wd) {
-    const uint32_t lane = lane_id();
-    const uint32_t wpb = blockDim.x >> 6;
-    const uint64_t wstride = uint64_t(gridDim.x) * wpb * 64;  // 64-bit: no wrap for E near 2^32
-    for (uint64_t w0 = (uint64_t(blockIdx.x) * wpb + (threadIdx.x >> 6)) * 64; w0 < E; w0 += wstride) {
-        EmitEnt t = emit_ent(w0 + lane, E, cid, cls, mem, lohi, pos, kid_off, child_of);
-        uint64_t base = 0;
-        uint32_t n_run = 0;
-        if constexpr (kWrite) {
-            if (w0 + lane < E) {
-                base = off[w0 + lane];
-                n_run = uint32_t(off[w0 + lane + 1] - base);
-                if (n_run == 0) t.nk = 0;
-            }
-        }
-        const uint32_t done = emit_pairs<W>(
-            t, w0, mem, lohi, mask, kid_slot, wd,
-            [&](bool ok, uint32_t ow, uint64_t o_e, uint32_t o_lt, uint32_t q, uint32_t f, uint32_t slot, uint32_t k) {
-                if constexpr (kWrite) {
-                    // shuffles stay outside the branch: a source lane must be active
-                    const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
-                    const uint64_t o_base = __shfl(base, int(ow), 64);
-                    const uint32_t o_cc = uint32_t(__shfl(int(t.cc), int(ow), 64));
-                    if (ok) emit_write<W>(o, cap, o_base + k, o_cc, kid_cid[q], k, o_n, o_e, o_lt, f, slot, lohi, mask, wd);
-                }
-            });
-        if constexpr (!kWrite) {
-            if (w0 + lane < E) ncnt[w0 + lane] = done;
-        }
-    }
-}
-
 // One-pass emission (default).  A block takes a chunk of kEmitRounds x 256
 // parent entries; each wave joins its entries once, keeping every non-empty
 // join (partner, kid, owner, rank in run) in LDS, then the block reserves its
@@ -1265,7 +1147,10 @@ template <class T, int kShift = 20> struct ChunkedVec {
 // run dozens of parallel sections per mine: creating threads for each cost more
 // than the work).  One section at a time; a caller that finds the pool busy (a
 // concurrent mine on another context) runs its section inline.  Never destroyed:
-// the workers are detached and idle between sections.
+// the workers are detached and idle between sections.  A task that throws
+// (bad_alloc in a fill, FSM_ELIMIT) never unwinds past a running section: the
+// first exception is kept, the section drains (no worker is left inside the
+// caller's frame), then it is rethrown on the caller's thread.
 class HostPool {
   public:
     static HostPool& get() {
@@ -1289,20 +1174,31 @@ class HostPool {
             ++gen_;
         }
         cv_.notify_all();
-        fn(0);
-        finish_one();
-        for (int64_t t; (t = next_.fetch_add(1)) < n;) {
-            fn(t);
-            finish_one();
+        guarded(fn, 0);
+        for (int64_t t; (t = next_.fetch_add(1)) < n;) guarded(fn, t);
+        std::exception_ptr ex;
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            // every worker that joined this section has left it before the next can start
+            done_cv_.wait(g, [&] { return left_ == 0 && active_ == 0; });
+            job_ = nullptr;
+            std::swap(ex, err_);
         }
-        std::unique_lock<std::mutex> g(mu_);
-        // every worker that joined this section has left it before the next can start
-        done_cv_.wait(g, [&] { return left_ == 0 && active_ == 0; });
-        job_ = nullptr;
+        if (ex) std::rethrow_exception(ex);
         return true;
     }
 
   private:
+    // one task: a throw is recorded (the first one wins) instead of unwinding
+    void guarded(const std::function<void(int64_t)>& fn, int64_t t) {
+        try {
+            fn(t);
+        } catch (...) {
+            std::lock_guard<std::mutex> g(mu_);
+            if (!err_) err_ = std::current_exception();
+        }
+        finish_one();
+    }
     void finish_one() {
         std::lock_guard<std::mutex> g(mu_);
         if (--left_ == 0 && active_ == 0) done_cv_.notify_all();
@@ -1320,10 +1216,7 @@ class HostPool {
                 n = n_;
                 ++active_;
             }
-            for (int64_t t; (t = next_.fetch_add(1)) < n;) {
-                (*job)(t);
-                finish_one();
-            }
+            for (int64_t t; (t = next_.fetch_add(1)) < n;) guarded(*job, t);
             std::lock_guard<std::mutex> g(mu_);
             if (--active_ == 0 && left_ == 0) done_cv_.notify_all();
         }
@@ -1331,6 +1224,7 @@ class HostPool {
     std::mutex run_mu_, mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(int64_t)>* job_ = nullptr;
+    std::exception_ptr err_;
     int64_t n_ = 0, left_ = 0, active_ = 0;
     uint64_t gen_ = 0;
     std::atomic<int64_t> next_{0};
@@ -1464,53 +1358,12 @@ struct Miner {
     // FSM_HOST_TRACE=1: host time of the bookkeeping phases, printed at the end of the mine
     double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f2 sort, kids, children, groups, emit tables, slab alloc, count prep, count
 
-    // Sharded mining: a failure on one rank must not leave its peers blocked in
-    // a collective.  The work between two collectives runs through
-    // run_or_defer, which records a throw instead of unwinding (nranks > 1);
-    // agree(), called by every rank before the next collective, all-reduces
-    // the failure flags and throws the same FSM_E* code on every rank.
-    int err_code = 0;
-    std::string err_msg;
-    template <class F> void run_or_defer(F&& f) {
-        if (!comm) {
-            f();
-            return;
-        }
-        if (err_code) return;
-        try {
-            f();
-        } catch (const Error& e) {
-            err_code = e.code;
-            err_msg = e.what();
-        } catch (const std::bad_alloc&) {
-            err_code = FSM_ENOMEM;
-            err_msg = "host allocation failed";
-        } catch (const std::exception& e) {
-            err_code = FSM_EDEVICE;
-            err_msg = e.what();
-        }
-    }
-    // FSM_INJECT_FAIL="<rank>,<root|lattice>": throw FSM_ELIMIT on that rank at
-    // that phase (test hook for the failure agreement of sharded mining)
-    void maybe_inject(const char* phase) const {
-        const char* v = std::getenv("FSM_INJECT_FAIL");
-        if (!v || !comm) return;
-        char ph[16] = {0};
-        int r = -1;
-        if (std::sscanf(v, "%d,%15s", &r, ph) == 2 && r == comm->rank() && !std::strcmp(ph, phase))
-            throw Error(FSM_ELIMIT, std::string("SPADE: injected failure (FSM_INJECT_FAIL, ") + phase + ")");
-    }
-    void agree() {
-        if (!comm) return;
-        std::vector<uint32_t> v(8, 0u);
-        if (err_code) v[size_t(std::clamp(err_code, 1, 7))] = 1u;
-        comm->host_allreduce_u32(v.data(), v.size(), s);
-        if (err_code) throw Error(err_code, err_msg);
-        for (int c = 1; c < 8; ++c)
-            if (v[size_t(c)])
-                throw Error(c, "SPADE: a peer rank failed (FSM error " + std::to_string(c) +
-                                   "); the sharded mine is aborted on every rank");
-    }
+    // Sharded mining: the work between two collectives runs through
+    // run_or_defer; agree() before the next collective (comm.h Agreement)
+    Agreement agr;
+    template <class F> void run_or_defer(F&& f) { agr.run(std::forward<F>(f)); }
+    void maybe_inject(const char* phase) const { agr.maybe_inject(phase); }
+    void agree() { agr.agree(s); }
     void sync() {
         const double t = now_ms();
         FSM_HIP(hipStreamSynchronize(s));
@@ -1586,24 +1439,22 @@ struct Miner {
         return false;
     }
 
-    // FSM_COUNT_PATH=atomic|keys|grp: force the class count path (default: keyed or
-    // group-privatized for batches of >= kKeyedMinEntries entries; tests, profiling)
+    // FSM_COUNT_PATH=atomic|keys: force the class count path (default: keyed for
+    // join-dense batches of >= kKeyedMinEntries entries; tests, profiling)
     static int count_path() {
         const char* v = std::getenv("FSM_COUNT_PATH");
         if (!v) return 0;
-        if (!std::strcmp(v, "grp")) return 3;
         return !std::strcmp(v, "keys") ? 2 : (!std::strcmp(v, "atomic") ? 1 : 0);
     }
     // Keyed counting pays one group pass per kGroupCounters counters and a key pass
     // over the entries, atomics one memory-side atomic per join: keyed when the
     // batch's joins (estimated as sum cap^2 / runs, runs <= the prefix support)
     // reach both its counters and twice its entries.
-    // 0: global atomics (k_count), 1: keyed, 2: group-privatized (k_count_grp)
+    // 0: global atomics (k_count), 1: keyed
     int count_mode(const Batch& b) const {
         const int cp = count_path();
         if (b.root || b.E == 0 || b.E >= kNone || cp == 1) return 0;
         if (cp == 2) return 1;
-        if (cp == 3) return 2;
         static const uint64_t min_e = [] {  // FSM_KEYED_MIN overrides kKeyedMinEntries (tuning)
             const char* v = std::getenv("FSM_KEYED_MIN");
             return v ? uint64_t(std::strtoull(v, nullptr, 10)) : uint64_t(kKeyedMinEntries);
@@ -1619,39 +1470,8 @@ struct Miner {
                          (unsigned long long)b.E, est, ncnt);
         // measured on MI355X: keyed wins on long runs (BIBLE/SIGN-shaped batches, >= 2 joins
         // per entry); at about one join per entry (Quest D1M) its key pass costs as much as the
-        // atomics, and the group-privatized count is slower still (2.27 vs 0.9 ms: one 128 KiB
-        // LDS group per CU, same-address LDS atomics on the popular pairs), so it is opt-in
+        // atomics
         return est >= ncnt && est >= 2.0 * double(b.E) ? 1 : 0;
-    }
-
-    // group-privatized count of a batch laid out by prepare(b, true); false when it
-    // spans more than kGrpMax groups (the atomic path runs)
-    bool grp_count(Batch& b, DevBuf& cnt) {
-        const uint64_t G64 = (b.n_cnt + kGroupCounters - 1) >> kGroupShift;
-        if (G64 == 0 || G64 > kGrpMax) return false;
-        const uint32_t G = uint32_t(G64), E = uint32_t(b.E);
-        const SlabPtrs sp = b.slab.ptrs();
-        cnt.alloc((G64 << kGroupShift) * 4);
-        FSM_HIP(hipMemsetAsync(cnt.p, 0, (G64 << kGroupShift) * 4, s));
-        DevBuf grp(std::max<uint64_t>(b.E, 1));
-        size_t tk = clk->begin("k_entry_group");
-        hipLaunchKernelGGL(k_entry_group, dim3(unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 16384))),
-                           dim3(kBlock), 0, s, E, sp.cid, b.d_cls.as<DClass>(), sp.mem, member_lo(b), member_hi(b),
-                           grp.as<uint8_t>());
-        FSM_LAUNCHED("k_entry_group", s);
-        clk->end(tk, int64_t(b.E * 9));
-        const uint32_t nchunk = std::max<uint32_t>(1, std::min<uint32_t>(512 / G, uint32_t((b.E + 4095) / 4096)));
-        const uint32_t chunk = uint32_t((b.E + nchunk - 1) / nchunk);
-        tk = clk->begin("k_count_grp");
-#define FSM_CG(WW)                                                                                                  \
-    hipLaunchKernelGGL(k_count_grp<WW>, dim3(nchunk * G), dim3(1024), 0, s, E, chunk, G, grp.as<uint8_t>(), sp.cid, \
-                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, cnt.as<uint32_t>(),                   \
-                       d_tests.as<unsigned long long>(), uint32_t(W))
-        FSM_W_DISPATCH(W, FSM_CG)
-#undef FSM_CG
-        FSM_LAUNCHED("k_count_grp", s);
-        clk->end(tk, int64_t(b.E * (G + entry_bytes()) + (G64 << kGroupShift) * 4 * nchunk));
-        return true;
     }
 
     // Keyed count of a (non-root) batch laid out by prepare(b, true): plan ->
@@ -1692,7 +1512,7 @@ struct Miner {
         const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>({64u, 512u / G, nblk}));
         if (parts > 1) FSM_HIP(hipMemsetAsync(cnt.p, 0, (G64 << kGroupShift) * 4, s));
         tk = clk->begin("k_cnt_count");
-        hipLaunchKernelGGL(k_f2_count<true>, dim3(G * parts), dim3(kF2Threads), 0, s, base.as<uint64_t>(), G, 0,
+        hipLaunchKernelGGL(k_f2_count<true>, dim3(G * parts), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
                            fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), 0u, 0u, 0u, 0u, 0u, 0u,
                            (FreqRec*)nullptr, 0u, (uint32_t*)nullptr, cnt.as<uint32_t>(), parts);
         FSM_LAUNCHED("k_cnt_count", s);
@@ -1754,11 +1574,6 @@ struct Miner {
         const double f = v ? std::atof(v) : 0.5;
         return f > 0.0 ? f : 1e300;
     }
-    // FSM_EMIT_PATH=twopass: count pass + scan + write pass instead of k_emit1 (tests, profiling)
-    static bool emit_twopass() {
-        const char* v = std::getenv("FSM_EMIT_PATH");
-        return v && !std::strcmp(v, "twopass");
-    }
     // LDS join records per wave of k_emit1 (FSM_EMIT_CAP lowers it: tests of the overflow path)
     static uint32_t emit_cap() {
         const char* v = std::getenv("FSM_EMIT_CAP");
@@ -1770,22 +1585,12 @@ struct Miner {
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kChunk;
     }
     // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
-    // FSM_F2_FUSED=0: the F2 plan as its own kernel after the root rows (A/B knob)
-    static bool f2_fused() {
-        const char* v = std::getenv("FSM_F2_FUSED");
-        return !(v && v[0] == '0');
-    }
-    // FSM_F2_LAYOUT=bg: key regions block-major instead of group-major (A/B knob)
-    static bool f2_block_major() {
-        const char* v = std::getenv("FSM_F2_LAYOUT");
-        return v && !std::strcmp(v, "bg");
-    }
     static uint32_t f2_blocks() {
         const char* v = std::getenv("FSM_F2_BLOCKS");
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, kF2MaxBlocks)) : 1024u;
     }
 
-    // Root F2 by rank groups (k_f2_plan / k_f2_keys / k_f2_count): the
+    // Root F2 by rank groups (plan / k_f2_keys / k_f2_count): the
     // frequent (rank, slot) pairs of this rank's slice, sorted by (row, slot),
     // with their child member ids.  Returns false when a counter row does not
     // fit the LDS group tile, the groups are too many or the key slots exceed
@@ -1828,27 +1633,12 @@ struct Miner {
         const uint32_t rlo = comm ? slice_lo : 0u, rhi = comm ? std::min(slice_hi, F) : F;
         const uint32_t R = geo.R, rpb = geo.rpb, nblk = geo.nblk;
         const uint64_t nd = geo.nd;
-        const int bg = f2_block_major() ? 1 : 0;
         const SlabPtrs sp = b.slab.ptrs();
         const int64_t E0 = int64_t(m.cap);
-        DevBuf base, fill(nd * 4);
-        uint64_t nslots = 0;
+        if (!b.f2_planned) return false;  // the plan is made while the root rows are written
+        DevBuf base = std::move(b.f2_base), fill(nd * 4);
+        const uint64_t nslots = b.f2_nslots;
         size_t tk = 0;
-        if (b.f2_planned) {  // planned while the root rows were written (k_root_write_plan)
-            base = std::move(b.f2_base);
-            nslots = b.f2_nslots;
-        } else {  // plan: region capacities -> bases
-            DevBuf cap(nd * 4);
-            base.alloc((nd + 1) * 8);
-            tk = clk->begin("k_f2_plan");
-            hipLaunchKernelGGL(k_f2_plan, dim3(nblk), dim3(kBlock), size_t(G) * 4, s, b.root_rows.as<uint64_t>(), R,
-                               rpb, sp.mem, sp.pos, pm, G, nblk, mlo, mhi, bg, cap.as<uint32_t>());
-            FSM_LAUNCHED("k_f2_plan", s);
-            clk->end(tk, E0 * 8 + int64_t(nd) * 4);
-            scan_exclusive(cap.as<uint32_t>(), base.as<uint64_t>(), nd, s);
-            FSM_HIP(hipMemcpyAsync(&nslots, base.as<uint64_t>() + nd, 8, hipMemcpyDeviceToHost, s));
-            sync();
-        }
         if (nslots >= (uint64_t(1) << 32) - 4096) return false;  // region cursors are u32
         // the one enumeration (keys padded: k_f2_count reads whole 16-byte words past a region's end)
         DevBuf keys((nslots + 1024) * 2), nk(8);
@@ -1857,7 +1647,7 @@ struct Miner {
         const size_t kshm = size_t(kF2Waves) * 64 * (sizeof(F2Ent) + 4) + (size_t(kF2MaxRows) + 1) * 4 + size_t(G) * 4;
 #define FSM_F2K(WW)                                                                                                   \
     hipLaunchKernelGGL(k_f2_keys<WW>, dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(), R, rpb,      \
-                       sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(), bg,               \
+                       sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(),                   \
                        fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>(), uint32_t(W))
         FSM_W_DISPATCH(W, FSM_F2K)
 #undef FSM_F2K
@@ -1878,7 +1668,7 @@ struct Miner {
             FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
             tk_cnt = clk->begin("k_f2_count");
             if (g1 > g0)
-                hipLaunchKernelGGL(k_f2_count<false>, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(), G, bg,
+                hipLaunchKernelGGL(k_f2_count<false>, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
                                    fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), D, per, g0, rlo, rhi, minsup,
                                    d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u);
             FSM_LAUNCHED("k_f2_count", s);
@@ -2056,8 +1846,7 @@ struct Miner {
         // the root: pairs counted per rank group, only the frequent ones leave the device
         const bool root_done = b.E && b.root && !root_atomic() && root_f2(b, recs);
         if (b.E) st.count_launches += 1;
-        const bool keyed_done = !root_done && keyed_layout &&
-                                (cmode == 1 ? keyed_count(b, cnt) : grp_count(b, cnt));
+        const bool keyed_done = !root_done && keyed_layout && keyed_count(b, cnt);
         if (!root_done && !keyed_done) {
             cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
             FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
@@ -2335,7 +2124,7 @@ struct Miner {
     }
 
     // emit child rows of group g of batch b into a new batch (k_emit1: one
-    // pass, LDS join records, slab cursor; or the two-pass count/scan/write)
+    // pass, LDS join records, slab cursor)
     void emit(Batch& b, size_t g, Batch& nb) {
         const double th = now_ms();
         const auto [ga, gb] = b.groups[g];
@@ -2392,7 +2181,7 @@ struct Miner {
         DevBuf d_child_of;
         upload_staged(3, d_child_of, child_of.data(), child_of.size() * 4);
         ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
-        if (b.E && !emit_twopass()) {
+        if (b.E) {
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
             DevBuf cursor(8);
@@ -2411,31 +2200,6 @@ struct Miner {
             // reads every parent entry once, writes every child entry once
             clk->end(tk, int64_t(b.E * entry_bytes() + total * entry_bytes()));
             FSM_HIP(hipMemcpyAsync(&pend[0], cursor.p, 8, hipMemcpyDeviceToHost, s));
-        } else if (b.E) {
-            const SlabPtrs sp = b.slab.ptrs();
-            const SlabPtrs op = nb.slab.ptrs();
-            DevBuf ncnt(std::max<uint64_t>(b.E, 1) * 4), off((b.E + 1) * 8);
-            const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, emit_grid_cap()));
-#define FSM_EMIT(WW, WR)                                                                                            \
-    hipLaunchKernelGGL((k_emit<WW, WR>), dim3(grid), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
-                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                                          \
-                       b.kid_cid, d_child_of.as<uint32_t>(), ncnt.as<uint32_t>(),                   \
-                       off.as<uint64_t>(), op, nb.slab.cap, uint32_t(W))
-#define FSM_EMIT_COUNT(WW) FSM_EMIT(WW, false)
-#define FSM_EMIT_WRITE(WW) FSM_EMIT(WW, true)
-            size_t tk = clk->begin("k_emit<count>");
-            FSM_W_DISPATCH(W, FSM_EMIT_COUNT)
-            FSM_LAUNCHED("k_emit<count>", s);
-            clk->end(tk, int64_t(b.E * (entry_bytes() + 4)));
-            scan_exclusive(ncnt.as<uint32_t>(), off.as<uint64_t>(), b.E, s);
-            tk = clk->begin("k_emit<write>");
-            FSM_W_DISPATCH(W, FSM_EMIT_WRITE)
-            FSM_LAUNCHED("k_emit<write>", s);
-            clk->end(tk, int64_t(b.E * (entry_bytes() + 8) + total * entry_bytes()));
-#undef FSM_EMIT_WRITE
-#undef FSM_EMIT_COUNT
-#undef FSM_EMIT
-            FSM_HIP(hipMemcpyAsync(&pend[0], off.as<uint64_t>() + b.E, 8, hipMemcpyDeviceToHost, s));
         } else {
             pend[0] = 0;
         }
@@ -2486,9 +2250,8 @@ struct Miner {
         size_t tk_rw = size_t(-1);
         root.root = true;
         const F2Geo geo = f2_geometry(root, 2 * F, Ecap, r1 - r0);
-        if (r1 > r0 && geo.ok && f2_fused()) {
+        if (r1 > r0 && geo.ok) {
             const SlabPtrs op = root.slab.ptrs();
-            const int bg = f2_block_major() ? 1 : 0;
             DevBuf cap(geo.nd * 4);
             root.f2_base.alloc((geo.nd + 1) * 8);
             const size_t tk = clk->begin("k_root_write");
@@ -2496,7 +2259,7 @@ struct Miner {
     hipLaunchKernelGGL(k_root_write_plan<WW>, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,              \
                        db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), db->mask.as<uint64_t>(),               \
                        d_rank.as<uint32_t>(), geo.R, geo.rpb, roff.as<uint64_t>(), op, geo.pm, geo.G, geo.nblk,    \
-                       geo.mlo, geo.mhi, bg, cap.as<uint32_t>(), uint32_t(W))
+                       geo.mlo, geo.mhi, cap.as<uint32_t>(), uint32_t(W))
             FSM_W_DISPATCH(W, FSM_ROOTWP)
 #undef FSM_ROOTWP
             FSM_LAUNCHED("k_root_write", s);
@@ -2672,6 +2435,8 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     ClockScope clock_scope(&clock);
     mn.clk = &clock;
     mn.comm = ctx->comm;
+    mn.agr.comm = ctx->comm;
+    mn.agr.what = "SPADE";
     Comm* comm = ctx->comm;
     ctx->stats.mask_words = d->W;
     // minsupp = Math.ceil(support * total) (SPADE.scala:113), >= 1 for the lattice

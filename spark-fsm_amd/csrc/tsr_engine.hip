@@ -48,7 +48,7 @@ constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRI
 constexpr int kExpBatch = 256;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
 constexpr int kMaxBatch = 256;
 constexpr int kExpandBlocks = 64;   // bitmap path: at most this many expansion blocks per rule slot
-constexpr int kExpSpb = 12;         // bitmap path: expected domain sids per expansion block (swept: 1..96)
+constexpr int kExpSpb = 64;         // bitmap path: expected domain sids per expansion block (FSM_TSR_SPB)
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kDlUnroll = 8;        // k_dl: independent words / sids per thread per round
 constexpr int kSpecDepth = 3;       // child speculation: levels per launch
@@ -339,18 +339,14 @@ struct ExpHdr {
     uint32_t nout, nx, nsid, nent;
 };
 
-// Visit the candidate items of this expansion - the kept items (bitmap path:
-// the expansion bumps without any touched-item bookkeeping) or the touched
-// list (list path) - keep the counts >= t (records go to mapped pinned host
-// memory, any order; the host sorts them by item) and re-zero the counters.
+// List path: visit the items this expansion touched, keep the counts >= t
+// (records to mapped pinned host memory, any order; the host sorts them by
+// item) and re-zero the counters and the touched marks.
 __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict__ TLb, uint32_t* __restrict__ DLb,
                                                            uint32_t* __restrict__ TRb, uint32_t* __restrict__ seenb,
                                                            const uint32_t* __restrict__ listb,
                                                            ExpCtl* __restrict__ ctlb, uint32_t U, uint32_t t,
-                                                           ExpRec* __restrict__ outb, ExpHdr* __restrict__ hdrb,
-                                                           uint32_t cap, uint4* __restrict__ dlw,
-                                                           uint32_t* __restrict__ ndlw,
-                                                           const uint32_t* __restrict__ kept, uint32_t nkept) {
+                                                           ExpRec* __restrict__ outb, uint32_t cap) {
     const uint64_t b = blockIdx.y, U64 = U;
     uint32_t* TL = TLb + b * U64;
     uint32_t* DL = DLb + b * U64;
@@ -359,30 +355,17 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
     const uint32_t* list = listb + b * U64;
     ExpCtl* ctl = ctlb + b;
     ExpRec* out = outb + b * uint64_t(cap);
-    (void)hdrb;
-    // bitmap path: every item that can still be a candidate (kept), no touched list;
-    // list path: the items the expansion touched
-    const uint32_t n = kept ? nkept : ctl->nlist;
+    const uint32_t n = ctl->nlist;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t c = kept ? kept[i] : list[i];
-        const uint32_t tl = TL[c], dl = kept ? 0u : DL[c], tr = TR[c];
-        if (kept) {
-            if ((tl | tr) == 0u) continue;
-            TL[c] = 0;
-            TR[c] = 0;
-        } else {
-            TL[c] = 0;
-            DL[c] = 0;
-            TR[c] = 0;
-            seen[c] = 0;
-        }
+        const uint32_t c = list[i];
+        const uint32_t tl = TL[c], dl = DL[c], tr = TR[c];
+        TL[c] = 0;
+        DL[c] = 0;
+        TR[c] = 0;
+        seen[c] = 0;
         if (tl >= t || tr >= t) {
             const uint32_t idx = atomicAdd(&ctl->nout, 1u);
-            if (idx < cap) {
-                out[idx] = ExpRec{c, tl, dl, tr};
-                // bitmap path: |sids(X u {c})| of a left extension comes from k_dl
-                if (dlw && tl >= t) dlw[atomicAdd(ndlw, 1u)] = make_uint4(uint32_t(b), c, idx, 0u);
-            }
+            if (idx < cap) out[idx] = ExpRec{c, tl, dl, tr};
         }
     }
 }
@@ -427,25 +410,98 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_build(const uint32_t* __restr
     }
 }
 
-// Expansion of slot b (blockIdx.y) over the sids holding every item of X u Y.
-// Block x owns a contiguous range of bitmap words, one word per thread per
-// pass: the rule's |X|+|Y| item bitmaps are ANDed (operand loads issued
-// together), a block scan places the set sids and their row bounds in LDS
-// windows, and the waves take the window's sids kExpSids at a time: the row
-// loads of those sids are all in flight before any is examined (the domain
-// is sparse - a couple of sids per wave - so the per-sid load latency, not
-// bandwidth, bounds the kernel).  TL / TR histograms in HBM.
+// ---- bitmap path: expansion rows packed for the expansions.  After the pair
+// phase only the items with support >= its minsup (K "kept" items, dense kid
+// ascending with the item, so c > max(X) compares alike) can still be in a
+// rule; every row is cut to them and each entry packed into 8 bytes:
+//   x = kid, y = first | last << 16  (itemset indexes of the row, < 65536)
+// one load per lane per entry (the entry's support check is the alive bitmap).
+__global__ __launch_bounds__(kBlock) void k_rows_pack(const uint32_t* __restrict__ row_off,
+                                                      const uint32_t* __restrict__ item,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ last,
+                                                      const uint32_t* __restrict__ kid_of, uint64_t N,
+                                                      uint32_t* __restrict__ cnt, uint32_t* __restrict__ maxpos,
+                                                      const uint64_t* __restrict__ off, uint2* __restrict__ out) {
+    const uint64_t wstride = (uint64_t(gridDim.x) * blockDim.x) >> 6;
+    uint32_t mp = 0;
+    for (uint64_t r = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; r < N; r += wstride) {
+        const uint32_t rb = row_off[r], re = row_off[r + 1];
+        uint64_t o = off ? off[r] : 0;
+        uint32_t n = 0;
+        for (uint32_t e0 = rb; e0 < re; e0 += 64) {
+            const uint32_t e = e0 + lane_id();
+            const uint32_t k = e < re ? kid_of[item[e]] : kNone;
+            const bool keep = k != kNone;
+            const uint64_t b = __ballot(keep);
+            if (keep) {
+                const uint32_t la = last[e];
+                mp = max(mp, la);
+                if (off) out[o + uint32_t(__popcll(b & lanemask_lt()))] = make_uint2(k, first[e] | (la << 16));
+            }
+            o += uint32_t(__popcll(b));
+            n += uint32_t(__popcll(b));
+        }
+        if (!off && lane_id() == 0) cnt[r] = n;
+    }
+    if (!off) {
+        mp = wave_max(mp);
+        if (lane_id() == 0 && mp) atomicMax(maxpos, mp);
+    }
+}
+
+// alive[w] bit j: kid 32w + j still has support >= the launch minsup t (t only
+// rises, so a dead kid never comes back; run when t changes)
+__global__ __launch_bounds__(kBlock) void k_alive(const uint32_t* __restrict__ ksup, uint32_t K, uint32_t t,
+                                                  uint32_t* __restrict__ alive) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= (K + 31) / 32) return;
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 32; ++j) {
+        const uint32_t k = w * 32 + j;
+        if (k < K && ksup[k] >= t) v |= 1u << j;
+    }
+    alive[w] = v;
+}
+
+// Expansion of rule slot b over the sids holding every item of X u Y, with
+// the expandL / expandR histograms of a kid range [kid_lo, kid_lo + KP) in LDS
+// (the per-entry device-scope atomics of the HBM histograms - 26.7 G
+// per c4 mine, all executed at the memory side - are gone).  A slot's blocks
+// own contiguous ranges of bitmap words (one word per thread per pass): the
+// rule's |X|+|Y| item bitmaps are ANDed (operand loads issued together), a
+// block scan places the set sids and their row bounds in LDS windows, and the
+// waves take the window's sids kExpSids at a time with all their row loads in
+// flight.  Each block writes its whole histogram as one dense partial row
+// (plain coalesced stores); k_expand_reduce sums a slot's rows.
 #ifndef FSM_TSR_SIDS
 #define FSM_TSR_SIDS 4
 #endif
-constexpr int kExpSids = FSM_TSR_SIDS;  // sids per wave step
-constexpr uint32_t kExpWin = 1024;      // sids per LDS window
-constexpr int kExpGrp = 4;              // rows > 64 entries: 64-entry chunks of loads in flight per round
-__device__ __forceinline__ void expand_short(uint32_t c, uint32_t fi, uint32_t la, uint32_t sp,
-                                             const uint32_t* sX, uint32_t nx, const uint32_t* sY, uint32_t ny,
-                                             uint32_t maxX, uint32_t maxY, uint32_t doL, uint32_t doR, uint32_t t,
-                                             uint32_t* __restrict__ TL, uint32_t* __restrict__ TR) {
-    // every item of X u Y is in the row (s came from the bitmap AND): found by ballot
+#ifndef FSM_TSR_XBLOCK
+#define FSM_TSR_XBLOCK 512
+#endif
+constexpr int kExpSids = FSM_TSR_SIDS;      // sids per wave step
+constexpr int kXBlock = FSM_TSR_XBLOCK;     // threads of an expansion block
+constexpr uint32_t kExpWin = 1024;          // sids per LDS window
+constexpr int kExpGrp = 4;                  // rows > 64 entries: 64-entry chunks of loads in flight per round
+constexpr uint32_t kPassKids = 4096;        // kids per LDS histogram pass (2 x 16 KiB)
+constexpr uint32_t kMaxKids = 65536;        // bitmap path: kept items (alive bitmap 8 KiB of LDS)
+
+struct ExpGeo {       // kernel view of one launch's geometry
+    uint32_t K, KP;   // kept items, kids per pass
+    uint32_t nblk;    // expansion blocks of the launch (partial rows per pass)
+    uint32_t t;       // launch minsup
+};
+
+__device__ __forceinline__ uint32_t alive_bit(const uint32_t* al, uint32_t c) { return (al[c >> 5] >> (c & 31u)) & 1u; }
+
+// one short row (<= 64 entries; lane = entry): every item of X u Y is in it
+// (s came from the bitmap AND), found by ballot
+__device__ __forceinline__ void expand_short(uint32_t c, uint32_t fl, const uint32_t* sX, uint32_t nx,
+                                             const uint32_t* sY, uint32_t ny, uint32_t maxX, uint32_t maxY,
+                                             uint32_t doL, uint32_t doR, const uint32_t* al, uint32_t kid_lo,
+                                             uint32_t KP, uint32_t* hL, uint32_t* hR) {
+    const uint32_t fi = fl & 0xFFFFu, la = fl >> 16;
     uint32_t fX = 0, lY = 0xFFFFFFFFu;
     bool inX = false, inY = false;
     for (uint32_t k = 0; k < nx; ++k) {
@@ -461,49 +517,60 @@ __device__ __forceinline__ void expand_short(uint32_t c, uint32_t fi, uint32_t l
         lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(la), int(__ffsll((long long)hb) - 1))));
     }
     if (fX >= lY) return;  // X => Y does not hold in s
-    // a candidate whose own support is below the launch's minsup can never reach it
-    const bool fq = sp >= t && c != 0xFFFFFFFFu;
-    if (doL && fq && c > maxX && fi < lY && !inY) atomicAdd(&TL[c], 1u);
-    if (doR && fq && c > maxY && la > fX && !inX) atomicAdd(&TR[c], 1u);
+    const uint32_t rel = c - kid_lo;
+    if (c == kNone || rel >= KP || !alive_bit(al, c)) return;
+    if (doL && c > maxX && fi < lY && !inY) atomicAdd(&hL[rel], 1u);
+    if (doR && c > maxY && la > fX && !inX) atomicAdd(&hR[rel], 1u);
 }
 
-__global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ sides,
-                                                      const uint64_t* __restrict__ blk_off, uint32_t nslot,
-                                                      const uint32_t* __restrict__ bm,
-                                                      uint32_t NW, const uint32_t* __restrict__ row_off,
-                                                      const uint32_t* __restrict__ item,
-                                                      const uint32_t* __restrict__ first,
-                                                      const uint32_t* __restrict__ last,
-                                                      const uint32_t* __restrict__ esup, uint32_t U,
-                                                      uint32_t* __restrict__ TLb, uint32_t* __restrict__ TRb,
-                                                      ExpCtl* __restrict__ ctlb, uint32_t* __restrict__ ndlw,
-                                                      uint32_t t) {
+__global__ __launch_bounds__(kXBlock) void k_expand_bm(const Side* __restrict__ sides,
+                                                       const uint64_t* __restrict__ blk_off, uint32_t nslot,
+                                                       const uint32_t* __restrict__ bm, uint32_t NW,
+                                                       const uint32_t* __restrict__ row_off,
+                                                       const uint2* __restrict__ ent,
+                                                       const uint32_t* __restrict__ kid_of,
+                                                       const uint32_t* __restrict__ alive, ExpGeo geo,
+                                                       uint32_t* __restrict__ part, ExpCtl* __restrict__ ctlb,
+                                                       uint32_t* __restrict__ ndlw) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];  // hist L [KP] | hist R [KP] | alive
     __shared__ uint32_t lrb[kExpWin], lre[kExpWin];
-    __shared__ uint32_t sXY[2 * kMaxSide];  // X then Y
-    __shared__ uint32_t wsum[kBlock / 64];
+    __shared__ uint32_t sXY[2 * kMaxSide];  // X then Y, as kids
+    __shared__ uint32_t sIt[2 * kMaxSide];  // X then Y, as items (bitmap rows)
+    __shared__ uint32_t wsum[kXBlock / 64];
+    const uint32_t KP = geo.KP, pass = blockIdx.y, kid_lo = pass * KP;
+    uint32_t* hL = dsm;
+    uint32_t* hR = dsm + KP;
+    uint32_t* al = dsm + 2 * KP;
     // slot of this block: the last b with blk_off[b] <= blockIdx.x (blocks per slot sized by its domain)
     uint32_t b = 0;
     for (uint32_t step = kMaxBatch / 2; step > 0; step >>= 1)
         if (b + step < nslot && blk_off[b + step] <= blockIdx.x) b += step;
-    const uint64_t U64 = U;
     const uint32_t bx = uint32_t(blockIdx.x - blk_off[b]), nbx = uint32_t(blk_off[b + 1] - blk_off[b]);
     const Side& side = sides[b];
-    uint32_t* TL = TLb + b * U64;
-    uint32_t* TR = TRb + b * U64;
     ExpCtl* ctl = ctlb + b;
-    // k_expand_collect (next on the stream) appends the k_dl work list
-    if (blockIdx.x == 0 && threadIdx.x == 0) *ndlw = 0u;
+    // k_expand_reduce (next on the stream) appends the k_dl work list
+    if (blockIdx.x == 0 && pass == 0 && threadIdx.x == 0) *ndlw = 0u;
     const uint32_t nx = side.nx, ny = side.ny, nxy = nx + ny;
-    const uint32_t maxX = side.maxX, maxY = side.maxY, doL = side.doL, doR = side.doR;
-    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) sXY[k] = k < nx ? side.X[k] : side.Y[k - nx];
+    const uint32_t doL = side.doL, doR = side.doR;
+    for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) dsm[k] = 0;
+    for (uint32_t k = threadIdx.x; k < (geo.K + 31) / 32; k += blockDim.x) al[k] = alive[k];
+    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) {
+        const uint32_t it = k < nx ? side.X[k] : side.Y[k - nx];
+        sIt[k] = it;
+        sXY[k] = kid_of[it];
+    }
     __syncthreads();
     const uint32_t* sX = sXY;
     const uint32_t* sY = sXY + nx;
+    const uint32_t maxX = sX[nx - 1], maxY = sY[ny - 1];  // sides ascend by item, so by kid
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     uint32_t my_ent = 0, my_sid = 0;  // row entries / domain sids this wave / thread saw
     const uint32_t w0 = uint32_t(uint64_t(bx) * NW / nbx);
     const uint32_t w1 = uint32_t(uint64_t(bx + 1) * NW / nbx);
+    // bumps of this pass start past min(max X, max Y) (both extensions need c above one of them)
+    const uint32_t mlo = max(doL ? (doR ? min(maxX, maxY) : maxX) : maxY, kid_lo == 0 ? 0u : kid_lo - 1u);
+    const uint32_t mhi = kid_lo + KP;  // and stop at the pass end
     for (uint32_t c0 = w0; c0 < w1; c0 += blockDim.x) {
         const uint32_t w = c0 + threadIdx.x;
         uint32_t v = 0;
@@ -512,7 +579,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
             for (uint32_t k0 = 0; k0 < nxy && v; k0 += 8) {  // 8 operand loads in flight per round
                 uint32_t o[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) o[j] = k0 + j < nxy ? bm[uint64_t(sXY[k0 + j]) * NW + w] : ~0u;
+                for (int j = 0; j < 8; ++j)
+                    o[j] = k0 + j < nxy ? bm[uint64_t(sIt[k0 + j]) * NW + w] : ~0u;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v &= o[j];
             }
@@ -543,82 +611,73 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
             __syncthreads();
             const uint32_t n = min(kExpWin, tot - win);
             for (uint32_t q0 = wv; q0 < n; q0 += wpb * kExpSids) {
-                uint32_t rb[kExpSids], re[kExpSids], c[kExpSids], fi[kExpSids], la[kExpSids], sp[kExpSids];
+                uint32_t rb[kExpSids], re[kExpSids];
+                uint2 e[kExpSids];
 #pragma unroll
                 for (int j = 0; j < kExpSids; ++j) {  // all kExpSids rows in flight
                     const uint32_t q = q0 + uint32_t(j) * wpb;
                     rb[j] = q < n ? lrb[q] : 0u;
                     re[j] = q < n ? lre[q] : 0u;
-                    const uint32_t e = rb[j] + lane;
-                    const bool ok = e < re[j] && re[j] - rb[j] <= 64u;
-                    c[j] = ok ? item[e] : 0xFFFFFFFFu;
-                    fi[j] = ok ? first[e] : 0u;
-                    la[j] = ok ? last[e] : 0u;
-                    sp[j] = ok ? esup[e] : 0u;
+                    const uint32_t x = rb[j] + lane;
+                    e[j] = x < re[j] && re[j] - rb[j] <= 64u ? ent[x] : make_uint2(kNone, 0u);
                 }
 #pragma unroll
                 for (int j = 0; j < kExpSids; ++j) {
                     if (q0 + uint32_t(j) * wpb >= n) break;
                     const uint32_t len = re[j] - rb[j];
-                    if (lane == 0) my_ent += len;
+                    if (lane == 0 && pass == 0) my_ent += len;
                     if (len <= 64u) {
-                        expand_short(c[j], fi[j], la[j], sp[j], sX, nx, sY, ny, maxX, maxY, doL, doR, t, TL, TR);
+                        expand_short(e[j].x, e[j].y, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP, hL, hR);
                         continue;
                     }
                     // longer rows: two ballot passes over 64-entry chunks, kExpGrp chunks of
                     // loads in flight per round (no dependent searches): pass 1 finds the X / Y
-                    // items (firstX, lastY) and the first entry past min(maxX, maxY); pass 2
-                    // bumps from there
+                    // items (firstX, lastY) and the first entry past mlo; pass 2 bumps from
+                    // there up to the end of this kid pass
                     const uint32_t rbj = rb[j], rej = re[j];
-                    const uint32_t mlo = doL ? (doR ? min(maxX, maxY) : maxX) : maxY;
                     uint32_t fX = 0, lY = 0xFFFFFFFFu, qs = rej;
                     for (uint32_t g0 = rbj; g0 < rej; g0 += 64u * kExpGrp) {
-                        uint32_t cg[kExpGrp], fg[kExpGrp], lg[kExpGrp];
+                        uint2 eg[kExpGrp];
 #pragma unroll
                         for (int h = 0; h < kExpGrp; ++h) {
-                            const uint32_t e = g0 + uint32_t(h) * 64u + lane;
-                            const bool v = e < rej;
-                            cg[h] = v ? item[e] : 0xFFFFFFFFu;
-                            fg[h] = v ? first[e] : 0u;
-                            lg[h] = v ? last[e] : 0u;
+                            const uint32_t x = g0 + uint32_t(h) * 64u + lane;
+                            eg[h] = x < rej ? ent[x] : make_uint2(kNone, 0u);
                         }
 #pragma unroll
                         for (int h = 0; h < kExpGrp; ++h) {
-                            const uint64_t gt = __ballot(cg[h] != 0xFFFFFFFFu && cg[h] > mlo);
+                            const uint32_t ce = eg[h].x;
+                            const uint64_t gt = __ballot(ce != kNone && ce > mlo);
                             if (gt && qs == rej) qs = g0 + uint32_t(h) * 64u + uint32_t(__ffsll((long long)gt)) - 1u;
                             for (uint32_t k = 0; k < nx; ++k) {
-                                const uint64_t hb = __ballot(cg[h] == sX[k]);
-                                if (hb) fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(fg[h]), int(__ffsll((long long)hb) - 1))));
+                                const uint64_t hb = __ballot(ce == sX[k]);
+                                if (hb) fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(eg[h].y & 0xFFFFu), int(__ffsll((long long)hb) - 1))));
                             }
                             for (uint32_t k = 0; k < ny; ++k) {
-                                const uint64_t hb = __ballot(cg[h] == sY[k]);
-                                if (hb) lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(lg[h]), int(__ffsll((long long)hb) - 1))));
+                                const uint64_t hb = __ballot(ce == sY[k]);
+                                if (hb) lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(eg[h].y >> 16), int(__ffsll((long long)hb) - 1))));
                             }
                         }
                     }
                     if (fX >= lY) continue;  // X => Y does not hold in s
-                    // expandL (c > max(X), c not in Y, c before lastY(s)) and expandR
-                    // (c > max(Y), c not in X, c after firstX(s)); each entry read once more
-                    for (uint32_t g0 = qs; g0 < rej; g0 += 64u * kExpGrp) {
-                        uint32_t cg[kExpGrp], fg[kExpGrp], lg[kExpGrp], sg[kExpGrp];
+                    bool past = false;
+                    for (uint32_t g0 = qs; g0 < rej && !past; g0 += 64u * kExpGrp) {
+                        uint2 eg[kExpGrp];
 #pragma unroll
                         for (int h = 0; h < kExpGrp; ++h) {
-                            const uint32_t e = g0 + uint32_t(h) * 64u + lane;
-                            const bool v = e < rej;
-                            cg[h] = v ? item[e] : 0xFFFFFFFFu;
-                            fg[h] = v ? first[e] : 0u;
-                            lg[h] = v ? last[e] : 0u;
-                            sg[h] = v ? esup[e] : 0u;
+                            const uint32_t x = g0 + uint32_t(h) * 64u + lane;
+                            eg[h] = x < rej ? ent[x] : make_uint2(kNone, 0u);
                         }
 #pragma unroll
                         for (int h = 0; h < kExpGrp; ++h) {
-                            const uint32_t ce = cg[h];
-                            if (sg[h] < t || ce == 0xFFFFFFFFu) continue;
+                            const uint32_t ce = eg[h].x;
+                            past |= __ballot(ce != kNone && ce >= mhi) != 0ull;  // wave-uniform: the pass ends here
+                            const uint32_t rel = ce - kid_lo;
+                            if (ce == kNone || rel >= KP || !alive_bit(al, ce)) continue;
                             bool inX = false, inY = false;
                             for (uint32_t k = 0; k < nx; ++k) inX |= ce == sX[k];
                             for (uint32_t k = 0; k < ny; ++k) inY |= ce == sY[k];
-                            if (doL && ce > maxX && fg[h] < lY && !inY) atomicAdd(&TL[ce], 1u);
-                            if (doR && ce > maxY && lg[h] > fX && !inX) atomicAdd(&TR[ce], 1u);
+                            if (doL && ce > maxX && (eg[h].y & 0xFFFFu) < lY && !inY) atomicAdd(&hL[rel], 1u);
+                            if (doR && ce > maxY && (eg[h].y >> 16) > fX && !inX) atomicAdd(&hR[rel], 1u);
                         }
                     }
                 }
@@ -626,10 +685,47 @@ __global__ __launch_bounds__(kBlock) void k_expand_bm(const Side* __restrict__ s
             __syncthreads();  // the window's LDS is rewritten next
         }
     }
-    // domain and entry counters (one atomic per wave)
-    my_sid = uint32_t(__shfl(int(wave_incl_scan(my_sid)), 63, 64));
-    if (lane == 0 && my_sid) atomicAdd(&ctl->nsid, my_sid);
-    if (lane == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
+    // the block's histograms -> its dense partial rows [L | R] (k_expand_reduce sums a slot's)
+    uint32_t* prow = part + (uint64_t(pass) * geo.nblk + blockIdx.x) * 2 * KP;
+    for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) prow[k] = dsm[k];
+    // domain and entry counters (one atomic per wave, first pass only)
+    if (pass == 0) {
+        my_sid = uint32_t(__shfl(int(wave_incl_scan(my_sid)), 63, 64));
+        if (lane == 0 && my_sid) atomicAdd(&ctl->nsid, my_sid);
+        if (lane == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
+    }
+}
+
+// Sum each slot's partial rows per kid; keep the counts >= t (records to mapped
+// pinned host memory, any order: the host sorts them by item) and queue the
+// left extensions for k_dl.  grid = (blocks per slot, slots, kid passes).
+__global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __restrict__ part,
+                                                          const uint64_t* __restrict__ blk_off, ExpGeo geo,
+                                                          const uint32_t* __restrict__ kept,
+                                                          ExpCtl* __restrict__ ctlb, ExpRec* __restrict__ outb,
+                                                          uint32_t cap, uint4* __restrict__ dlw,
+                                                          uint32_t* __restrict__ ndlw) {
+    const uint32_t b = blockIdx.y, pass = blockIdx.z, KP = geo.KP, kid_lo = pass * KP;
+    const uint64_t r0 = blk_off[b], r1 = blk_off[b + 1];
+    ExpCtl* ctl = ctlb + b;
+    ExpRec* out = outb + uint64_t(b) * cap;
+    const uint32_t* rows = part + uint64_t(pass) * geo.nblk * 2 * KP;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < KP && kid_lo + c < geo.K; c += gridDim.x * blockDim.x) {
+        uint32_t tl = 0, tr = 0;
+        for (uint64_t r = r0; r < r1; ++r) {
+            tl += rows[r * 2 * KP + c];
+            tr += rows[r * 2 * KP + KP + c];
+        }
+        if (tl >= geo.t || tr >= geo.t) {
+            const uint32_t it = kept[kid_lo + c];
+            const uint32_t idx = atomicAdd(&ctl->nout, 1u);
+            if (idx < cap) {
+                out[idx] = ExpRec{it, tl, 0u, tr};
+                // |sids(X u {c})| of a left extension comes from k_dl
+                if (tl >= geo.t) dlw[atomicAdd(ndlw, 1u)] = make_uint4(b, it, idx, 0u);
+            }
+        }
+    }
 }
 
 // |sids(X u {c})| for the kept left-extension candidates: AND + popcount
@@ -968,15 +1064,26 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // ---------------- pair phase (i ascending, j > i; IJ then JI)
     // nranks > 1: each rank counts the pairs of its own sequence range; the candidate
     // keys are exchanged and their partial counts summed.  The
-    // expansions then run on every rank alike (replicated, no exchange).
+    // expansions then run on every rank alike (replicated, no exchange).  A failure
+    // on one rank is agreed on before each collective, so no peer is left blocked.
     Comm* comm = ctx->comm;
     const bool shard = comm && comm->nranks() > 1;
+    Agreement agr;
+    agr.comm = shard ? comm : nullptr;
+    agr.what = "TSR";
     const int R = shard ? comm->nranks() : 1;
     const uint32_t slo = shard ? uint32_t(uint64_t(d->N) * uint64_t(comm->rank()) / uint64_t(R)) : 0u;
     const uint32_t shi = shard ? uint32_t(uint64_t(d->N) * uint64_t(comm->rank() + 1) / uint64_t(R))
                                : uint32_t(d->N);
     uint64_t rp_pair_exchanged = 0;  // union keys exchanged (verbose)
     uint32_t nb_items = 16;
+    // the batch grows while a batch's candidate records stay below pair_recs and
+    // shrinks above 4 x pair_recs (FSM_TSR_PAIR_RECS lowers it: test hook for the
+    // sharded batch agreement)
+    const uint64_t pair_recs = [] {
+        const char* v = std::getenv("FSM_TSR_PAIR_RECS");
+        return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, uint64_t(1) << 30) : uint64_t(1) << 20;
+    }();
     const uint64_t scr_cap_items = std::max<uint64_t>(1, (uint64_t(256) << 20) / (uint64_t(std::max<uint32_t>(U, 1)) * 8));
     DevBuf scr;
     uint64_t scr_items = 0;
@@ -985,52 +1092,53 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const uint32_t t = rp.minsup;
         const uint32_t nb = uint32_t(std::min<uint64_t>({uint64_t(nb_items), uint64_t(U - a), scr_cap_items}));
         const uint32_t b = a + nb;
-        if (scr_items < nb) {
-            scr.alloc(uint64_t(nb) * U * 8);
-            FSM_HIP(hipMemsetAsync(scr.p, 0, uint64_t(nb) * U * 8, s));
-            scr_items = nb;
-        }
-        const uint64_t v0 = voff[a], v1 = voff[b];
-        if (v1 > v0) {
-            hipLaunchKernelGGL(k_pairs, dim3(unsigned((v1 - v0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               d->vert_sid.as<uint32_t>(), d->vert_item.as<uint32_t>(), v0, v1, a, U, t, slo, shi,
-                               d_sup.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
-                               d->first.as<uint32_t>(), d->last.as<uint32_t>(), scr.as<uint32_t>());
-            FSM_LAUNCHED("k_pairs", s);
-        }
         // compaction threshold: t, or ceil(t / R) for a rank's partial counts (a pair whose
         // total reaches t has a partial >= t / R on some rank)
         const uint32_t tq = shard ? (t + uint32_t(R) - 1) / uint32_t(R) : t;
-        DevBuf rowcnt(size_t(nb) * 4 + 4), rowoff((size_t(nb) + 1) * 8);
         const unsigned grid = unsigned((uint64_t(nb) * 64 + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, tq,
-                           rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), (PairRec*)nullptr, 0);
-        FSM_LAUNCHED("k_pairs_compact", s);
-        scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nb, s);
-        std::vector<uint64_t> hoff(size_t(nb) + 1);
-        FSM_HIP(hipMemcpyAsync(hoff.data(), rowoff.p, (size_t(nb) + 1) * 8, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipStreamSynchronize(s));
-        const uint64_t nrec = hoff[nb];
-        DevBuf d_recs(std::max<uint64_t>(nrec, 1) * sizeof(PairRec));
-        if (!shard) {  // the compaction also re-zeroes the counters it visits
-            hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, t,
-                               rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>(), 1);
+        std::vector<uint64_t> hoff(size_t(nb) + 1, 0);
+        std::vector<PairRec> mine;
+        uint64_t nrec = 0;
+        // this rank's counts of the batch (rank-local work: deferred on failure when sharded)
+        agr.run([&] {
+            if (shard) agr.maybe_inject("pairs");
+            if (scr_items < nb) {
+                scr.alloc(uint64_t(nb) * U * 8);
+                FSM_HIP(hipMemsetAsync(scr.p, 0, uint64_t(nb) * U * 8, s));
+                scr_items = nb;
+            }
+            const uint64_t v0 = voff[a], v1 = voff[b];
+            if (v1 > v0) {
+                hipLaunchKernelGGL(k_pairs, dim3(unsigned((v1 - v0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                                   d->vert_sid.as<uint32_t>(), d->vert_item.as<uint32_t>(), v0, v1, a, U, t, slo, shi,
+                                   d_sup.as<uint32_t>(), d->row_off.as<uint32_t>(), d->item.as<uint32_t>(),
+                                   d->first.as<uint32_t>(), d->last.as<uint32_t>(), scr.as<uint32_t>());
+                FSM_LAUNCHED("k_pairs", s);
+            }
+            DevBuf rowcnt(size_t(nb) * 4 + 4), rowoff((size_t(nb) + 1) * 8);
+            hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, tq,
+                               rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), (PairRec*)nullptr, 0);
             FSM_LAUNCHED("k_pairs_compact", s);
-            recs.resize(nrec);
-            if (nrec)
-                FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
+            scan_exclusive(rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), nb, s);
+            FSM_HIP(hipMemcpyAsync(hoff.data(), rowoff.p, (size_t(nb) + 1) * 8, hipMemcpyDeviceToHost, s));
             FSM_HIP(hipStreamSynchronize(s));
-        } else {
+            nrec = hoff[nb];
+            DevBuf d_recs(std::max<uint64_t>(nrec, 1) * sizeof(PairRec));
+            // unsharded: the compaction also re-zeroes the counters it visits; sharded: the
+            // counters are read again for the union's partials
+            hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, tq,
+                               rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>(), shard ? 0 : 1);
+            FSM_LAUNCHED("k_pairs_compact", s);
+            std::vector<PairRec>& dst = shard ? mine : recs;
+            dst.resize(nrec);
+            if (nrec) FSM_HIP(hipMemcpyAsync(dst.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipStreamSynchronize(s));
+        });
+        uint64_t nadapt = nrec;  // drives the next batch size (must be alike on every rank)
+        if (shard) {
             // candidate keys of this rank -> union over ranks -> every rank's partials of
             // the union summed -> the exact counts, kept at t like the one-rank compaction
-            std::vector<PairRec> mine(nrec);
-            if (nrec) {
-                hipLaunchKernelGGL(k_pairs_compact, dim3(grid), dim3(kBlock), 0, s, scr.as<uint32_t>(), a, nb, U, tq,
-                                   rowcnt.as<uint32_t>(), rowoff.as<uint64_t>(), d_recs.as<PairRec>(), 0);
-                FSM_LAUNCHED("k_pairs_compact", s);
-                FSM_HIP(hipMemcpyAsync(mine.data(), d_recs.p, nrec * sizeof(PairRec), hipMemcpyDeviceToHost, s));
-                FSM_HIP(hipStreamSynchronize(s));
-            }
+            agr.agree(s);
             std::vector<uint8_t> blob(mine.size() * 8);
             for (size_t q = 0; q < mine.size(); ++q) {
                 std::memcpy(blob.data() + q * 8, &mine[q].i, 4);
@@ -1046,18 +1154,24 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                    [](const uint2& x, const uint2& y) { return x.x == y.x && x.y == y.y; }),
                        keys.end());
             std::vector<uint32_t> part(keys.size() * 2, 0u);
-            if (!keys.empty()) {
-                DevBuf d_keys(keys.size() * 8), d_part(keys.size() * 8);
-                FSM_HIP(hipMemcpyAsync(d_keys.p, keys.data(), keys.size() * 8, hipMemcpyHostToDevice, s));
-                hipLaunchKernelGGL(k_pairs_gather, dim3(unsigned((keys.size() + kBlock - 1) / kBlock)), dim3(kBlock),
-                                   0, s, scr.as<uint32_t>(), a, U, d_keys.as<uint2>(), uint32_t(keys.size()),
-                                   d_part.as<uint32_t>());
-                FSM_LAUNCHED("k_pairs_gather", s);
-                FSM_HIP(hipMemcpyAsync(part.data(), d_part.p, keys.size() * 8, hipMemcpyDeviceToHost, s));
+            agr.run([&] {
+                for (const uint2& kk : keys)  // every rank batched [a, b) alike
+                    if (kk.x < a || kk.x >= b || kk.y >= U)
+                        throw Error(FSM_EDEVICE, "TSR sharded pair phase: exchanged key outside the batch");
+                if (!keys.empty()) {
+                    DevBuf d_keys(keys.size() * 8), d_part(keys.size() * 8);
+                    FSM_HIP(hipMemcpyAsync(d_keys.p, keys.data(), keys.size() * 8, hipMemcpyHostToDevice, s));
+                    hipLaunchKernelGGL(k_pairs_gather, dim3(unsigned((keys.size() + kBlock - 1) / kBlock)),
+                                       dim3(kBlock), 0, s, scr.as<uint32_t>(), a, U, d_keys.as<uint2>(),
+                                       uint32_t(keys.size()), d_part.as<uint32_t>());
+                    FSM_LAUNCHED("k_pairs_gather", s);
+                    FSM_HIP(hipMemcpyAsync(part.data(), d_part.p, keys.size() * 8, hipMemcpyDeviceToHost, s));
+                }
+                FSM_HIP(hipMemsetAsync(scr.p, 0, uint64_t(nb) * U * 8, s));
                 FSM_HIP(hipStreamSynchronize(s));
-            }
+            });
+            agr.agree(s);
             comm->host_allreduce_u32(part.data(), part.size(), s);
-            FSM_HIP(hipMemsetAsync(scr.p, 0, uint64_t(nb) * U * 8, s));
             recs.clear();
             std::fill(hoff.begin(), hoff.end(), 0);
             for (size_t q = 0; q < keys.size(); ++q) {
@@ -1068,6 +1182,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             }
             for (uint32_t g = 0; g < nb; ++g) hoff[g + 1] += hoff[g];
             rp_pair_exchanged += keys.size();
+            nadapt = keys.size();  // the union: the same number on every rank
         }
         for (uint32_t g = 0; g < nb; ++g) {
             const uint32_t i = a + g;
@@ -1088,22 +1203,73 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 }
             }
         }
-        if (nrec < (1u << 20)) nb_items = std::min<uint32_t>(nb_items * 2, 4096);
-        else if (nrec > (4u << 20) && nb_items > 1) nb_items /= 2;
+        if (nadapt < pair_recs) nb_items = std::min<uint32_t>(nb_items * 2, 4096);
+        else if (nadapt > 4 * pair_recs && nb_items > 1) nb_items /= 2;
         a = b;
     }
     scr.release();
-    // The expansions scan rows restricted to the items that can still be in a
-    // rule: support >= the pair phase's minsup, which only rises from here
-    // (the first / last itemset indexes of the kept items are unchanged).
-    DevBuf k_off, k_item, k_first, k_last, k_sup;
+    // The expansions see only the items that can still be in a rule: support >=
+    // the pair phase's minsup, which only rises from here (K "kept" items).
+    std::vector<uint32_t> kept_items;
+    for (uint32_t c = 0; c < U; ++c)
+        if (sup[c] >= rp.minsup) kept_items.push_back(c);
+    const uint32_t K = uint32_t(kept_items.size());
+    const uint64_t N = uint64_t(d->N);
+    // bitmap path: sid bitmaps built, K <= kMaxKids, itemset indexes < 2^16 (packed rows)
+    bool use_bm = d->bm.p != nullptr && K > 0 && K <= kMaxKids;
+    DevBuf k_off, k_item, k_first, k_last, k_sup;  // list path rows (SoA)
+    DevBuf k_ent, d_kidof, d_kept, d_ksup, d_alive;  // bitmap path rows (packed) and kid tables
     uint64_t E2 = 0;
-    {
-        const uint64_t N = uint64_t(d->N);
-        DevBuf rc(std::max<uint64_t>(N, 1) * 4), off64((N + 1) * 8);
-        const unsigned g = unsigned(std::min<uint64_t>((N * 64 + kBlock - 1) / kBlock, 65536));
+    const unsigned rows_grid = unsigned(std::min<uint64_t>((N * 64 + kBlock - 1) / kBlock, 65536));
+    if (use_bm) {
+        std::vector<uint32_t> kid_of(U, kNone), ksup(K);
+        for (uint32_t q = 0; q < K; ++q) {
+            kid_of[kept_items[q]] = q;
+            ksup[q] = sup[kept_items[q]];
+        }
+        d_kidof.alloc(size_t(std::max<uint32_t>(U, 1)) * 4);
+        d_kept.alloc(size_t(K) * 4);
+        d_ksup.alloc(size_t(K) * 4);
+        d_alive.alloc(size_t((K + 31) / 32) * 4);
+        FSM_HIP(hipMemcpyAsync(d_kidof.p, kid_of.data(), size_t(U) * 4, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipMemcpyAsync(d_kept.p, kept_items.data(), size_t(K) * 4, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipMemcpyAsync(d_ksup.p, ksup.data(), size_t(K) * 4, hipMemcpyHostToDevice, s));
+        DevBuf rc(std::max<uint64_t>(N, 1) * 4), off64((N + 1) * 8), mpos(4);
+        FSM_HIP(hipMemsetAsync(mpos.p, 0, 4, s));
         if (N) {
-            hipLaunchKernelGGL(k_rows_keep, dim3(g), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
+            hipLaunchKernelGGL(k_rows_pack, dim3(rows_grid), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
+                               d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
+                               d_kidof.as<uint32_t>(), N, rc.as<uint32_t>(), mpos.as<uint32_t>(),
+                               (const uint64_t*)nullptr, (uint2*)nullptr);
+            FSM_LAUNCHED("k_rows_pack", s);
+        }
+        scan_exclusive(rc.as<uint32_t>(), off64.as<uint64_t>(), N, s);
+        uint32_t maxpos = 0;
+        FSM_HIP(hipMemcpyAsync(&E2, off64.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(&maxpos, mpos.p, 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        if (maxpos > 0xFFFFu || E2 >= kNone) {
+            use_bm = false;  // an itemset index past 2^16: the list path takes it
+        } else {
+            k_off.alloc((N + 1) * 4);
+            k_ent.alloc(std::max<uint64_t>(E2, 1) * 8);
+            hipLaunchKernelGGL(k_off32, dim3(unsigned(std::min<uint64_t>((N + 256) / 256, 4096))), dim3(256), 0, s,
+                               off64.as<uint64_t>(), N, k_off.as<uint32_t>());
+            FSM_LAUNCHED("k_off32", s);
+            if (N) {
+                hipLaunchKernelGGL(k_rows_pack, dim3(rows_grid), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
+                                   d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
+                                   d_kidof.as<uint32_t>(), N, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                   off64.as<uint64_t>(), k_ent.as<uint2>());
+                FSM_LAUNCHED("k_rows_pack", s);
+            }
+            FSM_HIP(hipStreamSynchronize(s));
+        }
+    }
+    if (!use_bm) {  // list path: rows restricted to the kept items, SoA with each entry's item support
+        DevBuf rc(std::max<uint64_t>(N, 1) * 4), off64((N + 1) * 8);
+        if (N) {
+            hipLaunchKernelGGL(k_rows_keep, dim3(rows_grid), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
                                d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
                                d_sup.as<uint32_t>(), rp.minsup, N, rc.as<uint32_t>(), (const uint64_t*)nullptr,
                                (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
@@ -1121,7 +1287,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                            off64.as<uint64_t>(), N, k_off.as<uint32_t>());
         FSM_LAUNCHED("k_off32", s);
         if (N) {
-            hipLaunchKernelGGL(k_rows_keep, dim3(g), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
+            hipLaunchKernelGGL(k_rows_keep, dim3(rows_grid), dim3(kBlock), 0, s, d->row_off.as<uint32_t>(),
                                d->item.as<uint32_t>(), d->first.as<uint32_t>(), d->last.as<uint32_t>(),
                                d_sup.as<uint32_t>(), rp.minsup, N, (uint32_t*)nullptr, off64.as<uint64_t>(),
                                k_item.as<uint32_t>(), k_first.as<uint32_t>(), k_last.as<uint32_t>(),
@@ -1130,18 +1296,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
         FSM_HIP(hipStreamSynchronize(s));
     }
-    // candidate items of every later expansion (support >= the pair phase's minsup)
-    std::vector<uint32_t> kept_items;
-    for (uint32_t c = 0; c < U; ++c)
-        if (sup[c] >= rp.minsup) kept_items.push_back(c);
-    DevBuf d_kept(std::max<size_t>(kept_items.size(), 1) * 4);
-    if (!kept_items.empty())
-        FSM_HIP(hipMemcpyAsync(d_kept.p, kept_items.data(), kept_items.size() * 4, hipMemcpyHostToDevice, s));
-    FSM_HIP(hipStreamSynchronize(s));
     const double t1 = now_ms();
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] pair phase %.0f ms: minsup %u, candidates %zu, rules %zu (ranks %d, keys exchanged %llu)\n",
-                     t1 - t0, rp.minsup, rp.cand.size(), rp.krules.size(), R, (unsigned long long)rp_pair_exchanged);
+        std::fprintf(stderr, "[fsm tsr] pair phase %.0f ms: minsup %u, candidates %zu, rules %zu, kept items %u, "
+                     "row entries %llu, %s path (ranks %d, keys exchanged %llu)\n",
+                     t1 - t0, rp.minsup, rp.cand.size(), rp.krules.size(), K, (unsigned long long)E2,
+                     use_bm ? "bitmap" : "list", R, (unsigned long long)rp_pair_exchanged);
 
     // ---------------- expansions
     // Batched speculation, committed in the exact sequential order: the next
@@ -1157,14 +1317,26 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     }();
     const uint64_t SU = uint64_t(B) * std::max<uint32_t>(U, 1);
     const size_t kSidesB = B * sizeof(Side), kOffB = (B + 1) * 8;
-    const bool use_bm = d->bm.p != nullptr;
-    const uint32_t ecap = std::max<uint32_t>(U, 1);
-    // One set of launch buffers: per-slot histograms and control, the rule descriptors
-    // (pinned stage + device copy, one H2D copy per launch) and the results (mapped pinned
-    // host memory, at most one record per item per slot).  Set 0 serves the synchronous
-    // launches; set 1 the lookahead batch that runs while the host commits (below).
+    // records per slot: at most one per candidate item (bitmap path: the kept items)
+    const uint32_t ecap = use_bm ? std::max<uint32_t>(K, 1) : std::max<uint32_t>(U, 1);
+    // bitmap path geometry: LDS histogram passes of KP kids; dense partial rows of
+    // 2 * KP counters per expansion block, at most max_blocks blocks per launch
+    const uint32_t pass_kids = [] {  // FSM_TSR_PASS_KIDS lowers the pass width (test hook: several passes)
+        const char* v = std::getenv("FSM_TSR_PASS_KIDS");
+        return v ? std::clamp<uint32_t>(uint32_t(std::strtoul(v, nullptr, 10)), 1, kPassKids) : kPassKids;
+    }();
+    const uint32_t KP = use_bm ? std::min<uint32_t>(K, pass_kids) : 0u;
+    const uint32_t P = use_bm ? (K + KP - 1) / KP : 0u;
+    const uint64_t row_bytes = uint64_t(P) * 2 * KP * 4;
+    const uint64_t part_budget = std::max<uint64_t>(uint64_t(32) << 20, uint64_t(B) * row_bytes);
+    const uint64_t max_blocks = use_bm ? part_budget / row_bytes : 0;
+    const size_t xlds = use_bm ? (size_t(2) * KP + (K + 31) / 32) * 4 : 0;
+    // One set of launch buffers: the rule descriptors (pinned stage + device copy, one
+    // H2D copy per launch), the per-slot control blocks, the histograms (list path:
+    // per-slot HBM arrays; bitmap path: per-block partial rows) and the results (mapped
+    // pinned host memory, at most ecap records per slot).
     struct ExpSet {
-        DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw;
+        DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part;
         std::unique_ptr<PinnedBuf> stage, pin;
         Side* h_sides = nullptr;
         uint64_t *h_drv = nullptr, *h_wave = nullptr;
@@ -1174,48 +1346,44 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         ExpRec *h_rec = nullptr, *d_rec = nullptr;
         std::vector<Rule*> batch;
         std::vector<char> drv_in_x;
-        bool busy = false, timed = false;
-    };
-    auto make_set = [&](ExpSet& x) {
+        bool timed = false;
+    } x;
+    x.ctl.alloc(B * sizeof(ExpCtl));
+    FSM_HIP(hipMemsetAsync(x.ctl.p, 0, B * sizeof(ExpCtl), s));
+    if (use_bm) {
+        x.part.alloc(max_blocks * row_bytes);
+        x.d_dlw.alloc(uint64_t(B) * ecap * sizeof(uint4));
+    } else {
         x.TL.alloc(SU * 4);
         x.DL.alloc(SU * 4);
         x.TR.alloc(SU * 4);
         x.seen.alloc(SU * 4);
         x.list.alloc(SU * 4);
-        x.ctl.alloc(B * sizeof(ExpCtl));
         FSM_HIP(hipMemsetAsync(x.TL.p, 0, SU * 4, s));
         FSM_HIP(hipMemsetAsync(x.DL.p, 0, SU * 4, s));
         FSM_HIP(hipMemsetAsync(x.TR.p, 0, SU * 4, s));
         FSM_HIP(hipMemsetAsync(x.seen.p, 0, SU * 4, s));
-        FSM_HIP(hipMemsetAsync(x.ctl.p, 0, B * sizeof(ExpCtl), s));
-        x.stage = std::make_unique<PinnedBuf>(kSidesB + 2 * kOffB);
-        x.d_stage.alloc(kSidesB + 2 * kOffB);
-        x.h_sides = static_cast<Side*>(x.stage->host);
-        x.h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(x.stage->host) + kSidesB);
-        x.h_wave = x.h_drv + (B + 1);
-        x.d_sides = x.d_stage.as<Side>();
-        x.d_drv = reinterpret_cast<uint64_t*>(x.d_stage.as<char>() + kSidesB);
-        x.d_wave = x.d_drv + (B + 1);
-        x.d_ndlw.alloc(16);
-        if (use_bm) x.d_dlw.alloc(SU * sizeof(uint4));
-        x.pin = std::make_unique<PinnedBuf>(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
-        x.h_hdr = static_cast<ExpHdr*>(x.pin->host);
-        x.h_rec = reinterpret_cast<ExpRec*>(x.h_hdr + B);
-        x.d_hdr = static_cast<ExpHdr*>(x.pin->dev);
-        x.d_rec = reinterpret_cast<ExpRec*>(x.d_hdr + B);
-    };
-    // FSM_TSR_LOOKAHEAD=1 enables the lookahead batch (opt-in: measured on MI355X at c4 it
-    // multiplied the pushed-back and child-speculated rules, 20K -> 121K launches, 8.5 -> 37 s)
-    const bool lookahead_on = [] { const char* v = std::getenv("FSM_TSR_LOOKAHEAD"); return v && v[0] == '1'; }();
-    ExpSet sets[2];
-    make_set(sets[0]);
-    if (lookahead_on) make_set(sets[1]);
+    }
+    x.stage = std::make_unique<PinnedBuf>(kSidesB + 2 * kOffB);
+    x.d_stage.alloc(kSidesB + 2 * kOffB);
+    x.h_sides = static_cast<Side*>(x.stage->host);
+    x.h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(x.stage->host) + kSidesB);
+    x.h_wave = x.h_drv + (B + 1);
+    x.d_sides = x.d_stage.as<Side>();
+    x.d_drv = reinterpret_cast<uint64_t*>(x.d_stage.as<char>() + kSidesB);
+    x.d_wave = x.d_drv + (B + 1);
+    x.d_ndlw.alloc(16);
+    x.pin = std::make_unique<PinnedBuf>(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
+    x.h_hdr = static_cast<ExpHdr*>(x.pin->host);
+    x.h_rec = reinterpret_cast<ExpRec*>(x.h_hdr + B);
+    x.d_hdr = static_cast<ExpHdr*>(x.pin->dev);
+    x.d_rec = reinterpret_cast<ExpRec*>(x.d_hdr + B);
     struct ExpResult {
         std::vector<ExpRec> recs;
         std::vector<Rule*> preL, preR;  // children created (and expanded) ahead of the commit, by record
     };
     std::unordered_map<Rule*, ExpResult> cache;
-    int64_t expansions = 0, launches = 0, spec_pushback = 0, la_launches = 0, la_rules = 0;
+    int64_t expansions = 0, launches = 0, spec_pushback = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     double last_log_ms = now_ms();  // verbose progress line every 20 s
     double prep_ms = 0, post_ms = 0, commit_ms = 0, pop_ms = 0;  // host time split (verbose summary)
@@ -1227,18 +1395,20 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const char* v = std::getenv("FSM_TSR_SPB");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
     }();
-    // per-kernel device time: every 16th synchronous launch records one set of events
+    // per-kernel device time: every 16th launch records one set of events
     // and reads them back at its sync (ctx->kstats rows)
     struct Seg {
         double ms = 0;  // over the timed launches
         int64_t n = 0, timed = 0, bytes = 0;
-    } seg[3];  // expansion, collect, k_dl / k_publish
-    const char* seg_name[3] = {use_bm ? "k_expand_bm" : "k_expand", "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
+    } seg[3];  // expansion, reduce / collect, k_dl / k_publish
+    const char* seg_name[3] = {use_bm ? "k_expand_bm" : "k_expand", use_bm ? "k_expand_reduce" : "k_expand_collect",
+                               use_bm ? "k_dl" : "k_publish"};
     for (hipEvent_t& e : ctx->ev)
         if (!e) FSM_HIP(hipEventCreate(&e));
-    int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0;
-    // enqueue the expansions of `batch` on set x (no sync)
-    auto launch_async = [&](ExpSet& x, const std::vector<Rule*>& batch, bool may_time) {
+    int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
+    uint32_t alive_t = 0;  // minsup the alive bitmap was built for
+    // expand `batch`: one launch, one stream sync; results into the cache
+    auto launch = [&](const std::vector<Rule*>& batch) {
         const double tl0 = now_ms();
         const uint32_t nb = uint32_t(batch.size());
         x.batch = batch;
@@ -1258,73 +1428,87 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             sd.maxY = ry[r->ny - 1];
             std::copy(rx, rx + r->nx, sd.X);
             std::copy(ry, ry + r->ny, sd.Y);
-            // driver list: rarest item of X (expandL needs all of sids(X)), else of X u Y
-            uint32_t drv = rx[0];
-            for (uint32_t q = 0; q < r->nx; ++q) if (sup[rx[q]] < sup[drv]) drv = rx[q];
-            if (!r->expandLR)
-                for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < sup[drv]) { drv = ry[q]; x.drv_in_x[k] = 0; }
-            drv_off[k] = voff[drv];
-            // list path: one wave per driver sid; bitmap path: blocks sized by the
-            // expected domain (about twice the rule's support: sids holding X u Y
-            // in either order), exp_spb sids per block, at most grid.expand
-            wave_off[k + 1] = wave_off[k] + (use_bm ? std::clamp<uint64_t>((2ull * r->sup + exp_spb - 1) / exp_spb, 1,
-                                                                             grid.expand)
-                                                    : (voff[drv + 1] - voff[drv]));
+            if (use_bm) {
+                // bitmap path: blocks sized by the expected domain (about twice the rule's
+                // support: sids holding X u Y in either order), exp_spb sids per block
+                wave_off[k + 1] = wave_off[k] + std::clamp<uint64_t>((2ull * r->sup + exp_spb - 1) / exp_spb, 1,
+                                                                     grid.expand);
+            } else {
+                // list path: one wave per sid of the driver list: the rarest item of X
+                // (expandL needs all of sids(X)), else of X u Y
+                uint32_t drv = rx[0];
+                for (uint32_t q = 0; q < r->nx; ++q) if (sup[rx[q]] < sup[drv]) drv = rx[q];
+                if (!r->expandLR)
+                    for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < sup[drv]) { drv = ry[q]; x.drv_in_x[k] = 0; }
+                drv_off[k] = voff[drv];
+                wave_off[k + 1] = wave_off[k] + (voff[drv + 1] - voff[drv]);
+            }
+        }
+        if (use_bm && wave_off[nb] > max_blocks) {  // partial rows over budget: fewer, larger blocks
+            const uint64_t tot = wave_off[nb];
+            uint64_t prev = 0;  // the original prefix at k
+            for (uint32_t k = 0; k < nb; ++k) {
+                const uint64_t n0 = wave_off[k + 1] - prev;
+                prev = wave_off[k + 1];
+                wave_off[k + 1] = wave_off[k] + std::max<uint64_t>(1, n0 * (max_blocks - nb) / tot);
+            }
         }
         std::memcpy(x.h_sides, sides.data(), nb * sizeof(Side));
         std::memcpy(x.h_drv, drv_off.data(), (nb + 1) * 8);
         std::memcpy(x.h_wave, wave_off.data(), (nb + 1) * 8);
         FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
-        const uint64_t waves = use_bm ? 0 : wave_off[nb];
-        x.timed = may_time && (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
+        x.timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
+        const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
+        if (use_bm && alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
+            hipLaunchKernelGGL(k_alive, dim3(unsigned(((K + 31) / 32 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                               d_ksup.as<uint32_t>(), K, rp.minsup, d_alive.as<uint32_t>());
+            FSM_LAUNCHED("k_alive", s);
+            alive_t = rp.minsup;
+        }
         if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[0], s));
         if (use_bm) {
-            hipLaunchKernelGGL(k_expand_bm, dim3(unsigned(wave_off[nb])), dim3(kBlock), 0, s, x.d_sides, x.d_wave, nb,
-                               d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), k_item.as<uint32_t>(),
-                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), k_sup.as<uint32_t>(), U,
-                               x.TL.as<uint32_t>(), x.TR.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_ndlw.as<uint32_t>(),
-                               rp.minsup);
+            hipLaunchKernelGGL(k_expand_bm, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
+                               x.d_wave, nb, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), k_ent.as<uint2>(),
+                               d_kidof.as<uint32_t>(), d_alive.as<uint32_t>(), geo, x.part.as<uint32_t>(),
+                               x.ctl.as<ExpCtl>(), x.d_ndlw.as<uint32_t>());
             FSM_LAUNCHED("k_expand_bm", s);
-        }
-        if (waves) {
-            hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               x.d_sides, x.d_drv, x.d_wave, nb,
-                               d->vert_sid.as<uint32_t>(), k_off.as<uint32_t>(), k_item.as<uint32_t>(),
-                               k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, x.TL.as<uint32_t>(),
-                               x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
-                               x.ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
-            FSM_LAUNCHED("k_expand", s);
-        }
-        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
-        hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, x.TL.as<uint32_t>(),
-                           x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
-                           x.ctl.as<ExpCtl>(), U, rp.minsup, x.d_rec, x.d_hdr, ecap,
-                           use_bm ? x.d_dlw.as<uint4>() : nullptr, x.d_ndlw.as<uint32_t>(),
-                           use_bm ? d_kept.as<uint32_t>() : nullptr, uint32_t(kept_items.size()));
-        FSM_LAUNCHED("k_expand_collect", s);
-        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
-        if (use_bm) {
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
+            hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
+                               x.d_wave, geo, d_kept.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_rec, ecap,
+                               x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>());
+            FSM_LAUNCHED("k_expand_reduce", s);
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
             hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
                                d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), x.d_dlw.as<uint4>(),
                                x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
             FSM_LAUNCHED("k_dl", s);
         } else {
+            const uint64_t waves = wave_off[nb];
+            if (waves) {
+                hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                                   x.d_sides, x.d_drv, x.d_wave, nb,
+                                   d->vert_sid.as<uint32_t>(), k_off.as<uint32_t>(), k_item.as<uint32_t>(),
+                                   k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, x.TL.as<uint32_t>(),
+                                   x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(),
+                                   x.list.as<uint32_t>(), x.ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
+                FSM_LAUNCHED("k_expand", s);
+            }
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
+            hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, x.TL.as<uint32_t>(),
+                               x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
+                               x.ctl.as<ExpCtl>(), U, rp.minsup, x.d_rec, ecap);
+            FSM_LAUNCHED("k_expand_collect", s);
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
             hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
             FSM_LAUNCHED("k_publish", s);
         }
         if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
-        x.busy = true;
-        prep_ms += now_ms() - tl0;
-    };
-    // wait for every enqueued launch (one stream: in order) and take in set x's results
-    auto finish = [&](ExpSet& x) {
         const double tw0 = now_ms();
+        prep_ms += tw0 - tl0;
         FSM_HIP(hipStreamSynchronize(s));
         const double tw1 = now_ms();
         wait_ms += tw1 - tw0;
         ++launches;
-        const std::vector<Rule*>& batch = x.batch;
-        const uint32_t nb = uint32_t(batch.size());
         for (int q = 0; q < 3; ++q) {
             float ms = 0;
             if (x.timed && hipEventElapsedTime(&ms, ctx->ev[q], ctx->ev[q + 1]) == hipSuccess) {
@@ -1333,6 +1517,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             }
             seg[q].n += 1;
         }
+        if (use_bm) exp_part_bytes += int64_t(wave_off[nb] * row_bytes);
         uint64_t nout_all = 0;
         for (uint32_t k = 0; k < nb; ++k) {
             const ExpHdr h = x.h_hdr[k];
@@ -1342,7 +1527,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 exp_domain += h.nsid;
                 exp_entries += h.nent;
                 exp_bitmap_bytes += int64_t(bmb);
-                seg[0].bytes += int64_t(bmb + 12ull * h.nent + 8ull * h.nsid);
+                seg[0].bytes += int64_t(bmb + 8ull * h.nent + 8ull * h.nsid);
             }
             if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
             if (!use_bm && x.drv_in_x[k] && h.nx != batch[k]->nX)
@@ -1354,21 +1539,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
         }
         seg[1].bytes += int64_t(nout_all * sizeof(ExpRec));
-        x.busy = false;
         x.timed = false;
         post_ms += now_ms() - tw1;
-    };
-    std::unordered_set<const Rule*> flying;  // rules of the lookahead batch in flight
-    auto finish_lookahead = [&] {
-        if (!sets[1].busy) return;
-        finish(sets[1]);
-        for (const Rule* r : sets[1].batch) flying.erase(r);
-    };
-    // synchronous launch on set 0 (a lookahead in flight finishes at the same sync)
-    auto launch = [&](const std::vector<Rule*>& batch) {
-        launch_async(sets[0], batch, !sets[1].busy);
-        finish(sets[0]);
-        finish_lookahead();
     };
     // Speculated rules wait in `pending` (ordered like the heap, results
     // cached) instead of going back to the heap: the next rule to commit is
@@ -1493,10 +1665,6 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const bool from_p = have_p && (!have_h || rule_cmp(rp.st, *pending.begin(), rp.cand.top().r) > 0);
         Rule* r = from_p ? *pending.begin() : rp.cand.top().r;
         if (r->sup < rp.minsup) break;
-        if (flying.count(r)) {  // its results are still being computed by the lookahead batch
-            finish_lookahead();
-            continue;
-        }
         auto ci = cache.find(r);
         if (from_p || ci != cache.end()) {  // results at hand (speculated earlier): commit now
             if (from_p) pending.erase(pending.begin());
@@ -1527,29 +1695,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         spec_pushback += int64_t(batch.size()) - 1;
         for (Rule* c : batch) pending.insert(c);
         if (spec_on) speculate(batch);
-        // Lookahead: the next heap rules are expanded on the second buffer set while the
-        // host commits this batch's results (their commit order is unchanged: they wait in
-        // `pending`, and a commit that reaches one in flight first waits for the batch)
-        if (lookahead_on && !sets[1].busy) {
-            std::vector<Rule*> la;
-            while (la.size() < size_t(B) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
-                Rule* x = rp.cand.top().r;
-                rp.cand.pop();
-                if (cache.count(x)) pending.insert(x);
-                else la.push_back(x);
-            }
-            if (!la.empty()) {
-                launch_async(sets[1], la, false);
-                for (Rule* c : la) {
-                    flying.insert(c);
-                    pending.insert(c);
-                }
-                ++la_launches;
-                la_rules += int64_t(la.size());
-            }
-        }
     }
-    finish_lookahead();  // a lookahead still in flight at the end: its results are not needed
     if (ctx->opts.verbose)
         std::fprintf(stderr,
                      "[fsm tsr] expansions %lld in %lld launches (%lld pushed back), %.0f ms waiting on the GPU; "
@@ -1557,8 +1703,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      (long long)expansions, (long long)launches, (long long)spec_pushback, wait_ms, prep_ms, post_ms,
                      commit_ms, pop_ms, rp.st.rules.size());
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; lookahead: %lld rules in %lld launches\n",
-                     (long long)spec_made, (long long)spec_launches, (long long)la_rules, (long long)la_launches);
+        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB\n",
+                     (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {

@@ -79,7 +79,9 @@ class Engine:
             m = out.contents
 
             def arr(ptr, n):
-                return np.ctypeslib.as_array(ptr, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0)
+                # an empty field keeps its ctypes element type (uint32 / uint64 / int32)
+                dt = np.dtype(ptr._type_)
+                return np.ctypeslib.as_array(ptr, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0, dtype=dt)
 
             img = {"mode": m.mode, "mask_words": m.mask_words, "rows": m.rows, "entries": m.entries,
                    "items": m.items, "max_occ": m.max_occ, "row_off": arr(m.row_off, m.rows + 1),

@@ -7,6 +7,7 @@ tests/test_parity_gpu.py as a plain child process).
   mode spade_fail D sup : the same with a failure injected on one rank (FSM_INJECT_FAIL)
   mode spade_digest shape D sup : sharded SPADE, digest of the result (full-size configs)
   mode tsr D k minconf : TSR with the pair phase sharded by sequence range
+  mode tsr_fail D k minconf : the same with a failure injected on one rank (FSM_INJECT_FAIL)
 Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (torch.distributed, gloo).
 """
 import json
@@ -67,6 +68,19 @@ def main():
             db.free()
         res.update(rules=sorted([list(x), list(y), s, c] for x, y, s, c in rules),
                    final_minsup=meta["final_minsup"])
+    elif mode == "tsr_fail":
+        # sharded TSR pair phase with FSM_INJECT_FAIL set for one rank: every rank fails, none hangs
+        from tools import gen
+        D, k, mc = int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5])
+        ds = gen.kosarak(D=D, seed=3)
+        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc) as eng:
+            db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
+            try:
+                eng.tsr(db, k, mc)
+                res.update(code=0, msg="")
+            except fsm.FsmError as e:
+                res.update(code=e.code, msg=e.msg)
+            db.free()
     elif mode == "spade_fail":
         # sharded SPADE with FSM_INJECT_FAIL set for one rank: every rank must fail, none may hang
         from tools import gen

@@ -35,6 +35,7 @@ CONFIGS = {
     "c5-bible": ("spade", "bible", {}, 0.004),
     "c5-sign": ("spade", "sign", {}, 0.015),
     "c4-prefix": ("tsr", "kosarak", {"D": 990002, "prefix": 20000}, (1000, 0.5)),
+    "c4-prefix100k": ("tsr", "kosarak", {"D": 990002, "prefix": 100000}, (1000, 0.5)),
 }
 
 

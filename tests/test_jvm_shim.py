@@ -80,29 +80,33 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 
 
 @pytest.mark.gpu
-def test_shim_spade_matches_engine(harness):
-    import spark_fsm_amd as fsm
-    cases = json.load(open(os.path.join(GOLD, "spade_cases.json")))[:12]
-    for case in cases:
+def test_shim_spade_matches_golden(harness):
+    """The JNI shim's Pattern.serialize() lines (SPADEActor.scala:49-50) equal
+    the committed fixtures' patterns rendered the same way: every golden case,
+    not a comparison with the engine's own Python path."""
+    from spark_fsm_amd.api import Pattern
+    for case in json.load(open(os.path.join(GOLD, "spade_cases.json"))):
         recs = [tuple(r) for r in case["records"]]
         got = call(harness, "harness_spade", recs, case["support"], 0)
-        exp = "".join(p.serialize() + "\n" for p in fsm.extract_rdd_patterns(recs, case["support"], stats=False))
-        assert sorted(got.splitlines()) == sorted(exp.splitlines()), case["name"]
+        exp = [Pattern([list(x) for x in sets], sup).serialize() for sets, sup in case["patterns"]]
+        assert sorted(got.splitlines()) == sorted(exp), case["name"]
     err = json.load(open(os.path.join(GOLD, "error_cases.json")))["spade"][0]
     assert call(harness, "harness_spade", [tuple(r) for r in err["records"]], 0.5, 0).startswith(
         "EXCEPTION java/lang/Exception: libfsm fsm_db_from_spmf failed (FSM error 2)")
 
 
 @pytest.mark.gpu
-def test_shim_tsr_matches_engine(harness):
-    import spark_fsm_amd as fsm
-    cases = json.load(open(os.path.join(GOLD, "tsr_cases.json")))[:12]
-    for case in cases:
+def test_shim_tsr_matches_golden(harness):
+    """The JNI shim's Rule accessors (TSRActor.scala:55-59) equal the committed
+    fixtures' rules: antecedent, consequent, support and the confidence as the
+    same IEEE double (the shim prints Double.toString's shortest form)."""
+    for case in json.load(open(os.path.join(GOLD, "tsr_cases.json"))):
         recs = [tuple(r) for r in case["records"]]
         got = call(harness, "harness_tsr", recs, case["k"], case["minconf"], 0)
-        exp = "".join("%s ==> %s #SUP: %d #CONF: %s\n" % (",".join(map(str, r.getItemset1())),
-                                                           ",".join(map(str, r.getItemset2())),
-                                                           r.getAbsoluteSupport(), repr(r.getConfidence()))
-                      for r in fsm.extract_rdd_rules(recs, case["k"], case["minconf"]))
-        norm = lambda s: sorted((l.rsplit(" ", 1)[0], float(l.rsplit(" ", 1)[1])) for l in s.splitlines())
-        assert norm(got) == norm(exp), case["name"]
+        exp = ["%s ==> %s #SUP: %d #CONF: %s" % (",".join(map(str, x)), ",".join(map(str, y)), sup, repr(float(c)))
+               for x, y, sup, c in case["rules"]]
+        norm = lambda lines: sorted((l.rsplit(" ", 1)[0], float(l.rsplit(" ", 1)[1])) for l in lines)
+        assert norm(got.splitlines()) == norm(exp), case["name"]
+    for err in json.load(open(os.path.join(GOLD, "error_cases.json")))["tsr"]:
+        out = call(harness, "harness_tsr", [tuple(r) for r in err["records"]], 3, 0.5, 0)
+        assert out.startswith("EXCEPTION java/lang/Exception: libfsm ") and "(FSM error 2)" in out, err["name"]

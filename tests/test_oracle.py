@@ -4,6 +4,7 @@ import json
 import os
 import random
 
+import numpy as np
 import pytest
 from hypothesis import given, settings, strategies as st
 
@@ -149,3 +150,44 @@ def test_tsr_negative_item_only_fails_in_closed_itemsets():
     with pytest.raises(oracle.OracleError):
         oracle.tsr([(0, "1 -1 -5 -1")], 3, 0.5)
 
+
+
+def _tokens(db):
+    so, tk = [0], []
+    for seq in db:
+        for iset in seq:
+            tk += list(iset) + [-1]
+        tk.append(-2)
+        so.append(len(tk))
+    return np.array(so, dtype=np.int64), np.array(tk, dtype=np.int64)
+
+
+@settings(max_examples=80, deadline=None)
+@given(records_st, st.integers(1, 3), st.sampled_from([0.0, 0.3, 0.5, 1.0]))
+def test_tsr_exhaustive_matches_brute(db, t, minconf):
+    """oracle/tsr_exhaustive.c (the c4 completeness pin) is the definitional
+    set: every valid rule with sup >= t, exactly as brute force enumerates it."""
+    if not any(db):
+        return
+    so, tk = _tokens(db)
+    got = oracle.tsr_all(so, tk, t, minconf, threads=2)["rules"]
+    valid = brute.brute_tsr_valid(_render(db), minconf)
+    exp = sorted([(x, y, s, c) for (x, y), (s, c) in valid.items() if s >= t], key=lambda r: (-r[2], r[0], r[1]))
+    assert got == exp
+
+
+def test_tsr_exhaustive_pins_the_topk_result_on_a_prefix():
+    """On the 5,000-sequence Kosarak prefix the top-k restatement's result R and
+    the fixed-threshold enumeration at R's final minsup m agree as SURVEY
+    §8(c)(ii) requires: the valid rules with sup > m are exactly R's, and every
+    rule of R is valid with the definitional sup / conf."""
+    from tools import gen
+    ds = gen.kosarak(D=990002, seed=1).head(5000)
+    r = oracle.tsr(ds.records(), 1000, 0.5)
+    m = r["final_minsup"]
+    a = oracle.tsr_all(ds.seq_off, ds.tokens, m, 0.5, threads=4)
+    R = {(x, y): (s, c) for x, y, s, c in r["rules"]}
+    A = {(x, y): (s, c) for x, y, s, c in a["rules"]}
+    assert {k: v for k, v in A.items() if v[0] > m} == {k: v for k, v in R.items() if v[0] > m}
+    assert all(A.get(k) == v for k, v in R.items())
+    assert len(R) >= 1000

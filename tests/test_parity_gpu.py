@@ -360,7 +360,7 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["group", "group-few-blocks", "block-major", "plan-unfused", "atomic"])
+@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
     """The root F2 implementations (key runs counted per rank group, at the
     default and at a small block chunk; global atomics) give the oracle's
@@ -371,28 +371,21 @@ def test_root_f2_paths_agree(eng, path, monkeypatch):
         monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
     if path == "group-few-blocks":
         monkeypatch.setenv("FSM_F2_BLOCKS", "3")
-    if path == "block-major":
-        monkeypatch.setenv("FSM_F2_LAYOUT", "bg")
-    if path == "plan-unfused":
-        monkeypatch.setenv("FSM_F2_FUSED", "0")
     ds = gen.quest(20000, seed=4)
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
     pats, meta, st = gpu_spade(eng, None, 0.003, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
 
 
-@pytest.mark.parametrize("path", ["onepass", "twopass", "overflow-all", "overflow-some"])
+@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some"])
 @pytest.mark.parametrize("shape", ["quest", "sign", "bible"])
 def test_emit_paths_agree(eng, path, shape, monkeypatch):
     """Child-run emission: the one-pass k_emit1 (LDS join records, slab
-    cursor), its overflow path (records capped at 0 / 17 per wave, so waves
-    join again while writing) and the two-pass count/scan/write give the
-    oracle's patterns and joins."""
+    cursor) and its overflow path (records capped at 0 / 17 per wave, so waves
+    join again while writing) give the oracle's patterns and joins."""
     from oracle import oracle
     from tools import gen
-    if path == "twopass":
-        monkeypatch.setenv("FSM_EMIT_PATH", "twopass")
-    elif path == "overflow-all":
+    if path == "overflow-all":
         monkeypatch.setenv("FSM_EMIT_CAP", "0")
     elif path == "overflow-some":
         monkeypatch.setenv("FSM_EMIT_CAP", "17")
@@ -416,15 +409,13 @@ def test_timestamp_limit(eng, fsm):
     assert ei.value.code == fsm.FSM_ELIMIT and "65536" in str(ei.value)
 
 
-@pytest.mark.parametrize("path", ["keys", "grp", "atomic", "default"])
+@pytest.mark.parametrize("path", ["keys", "atomic", "default"])
 @pytest.mark.parametrize("shape", ["quest", "sign", "bible", "sign-low"])
 def test_count_paths_agree(eng, path, shape, monkeypatch):
     """Class counting: the keyed count (group-aligned counter layout, u16 keys
-    in (group, block) regions, LDS counting, counters written out) and the
-    group-privatized count (one LDS group per block, falls back to the atomics
-    beyond 16 groups), each forced on every batch, the global-atomic k_count,
-    and the default size switch give the oracle's patterns and joins, and the
-    same executed pair tests."""
+    in (group, block) regions, LDS counting, counters written out) forced on
+    every batch, the global-atomic k_count, and the default size switch give
+    the oracle's patterns and joins, and the same executed pair tests."""
     from oracle import oracle
     from tools import gen
     if path != "default":
@@ -440,7 +431,7 @@ def test_count_paths_agree(eng, path, shape, monkeypatch):
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
-    if path in ("keys", "grp"):
+    if path == "keys":
         monkeypatch.setenv("FSM_COUNT_PATH", "atomic")
         _, _, st2 = gpu_spade(eng, None, sup, tokens=ds)
         assert st2["pair_tests"] == st["pair_tests"]
@@ -467,15 +458,19 @@ def test_sharded_heavy_class_split(eng, world, frac, tmp_path, monkeypatch):
     for r in res:
         assert r["digest"] == exp and r["joins"] == meta["joins"] and r["minsup"] == meta["minsup"]
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_tsr_pair_phase(eng, world, tmp_path):
+@pytest.mark.parametrize("world,recs", [(2, "default"), (3, "default"), (2, "64")])
+def test_sharded_tsr_pair_phase(eng, world, recs, tmp_path, monkeypatch):
     """TSR with `world` ranks on this GPU over gloo: each rank counts the pairs of
     its own sequence range, the candidate keys (partial >= ceil(t / world)) are
     exchanged and every rank's partials of their union summed.  Every rank must
-    return exactly the oracle's rules and final minsup."""
+    return exactly the oracle's rules and final minsup.  recs = 64 lowers the
+    batch-size thresholds (FSM_TSR_PAIR_RECS) so the item batches grow and
+    shrink during the phase: every rank must size them alike."""
     from oracle import oracle
     from test_dist import run_ranks
     from tools import gen
+    if recs != "default":
+        monkeypatch.setenv("FSM_TSR_PAIR_RECS", recs)
     res = run_ranks(world, ["tsr", "8000", "120", "0.4"], tmp_path, timeout=110)
     ds = gen.kosarak(D=8000, seed=3)
     o = oracle.tsr(ds.records(), 120, 0.4)
@@ -521,14 +516,30 @@ def test_sharded_spade_failure_reaches_every_rank(phase, tmp_path, monkeypatch):
     assert "injected" in res[1]["msg"] and "peer rank failed" in res[0]["msg"]
 
 
-@pytest.mark.parametrize("bitmap", ["1", "0"])
+def test_sharded_tsr_failure_reaches_every_rank(tmp_path, monkeypatch):
+    """A failure on one rank of the sharded TSR pair phase (injected FSM_ELIMIT
+    on rank 1) comes back as the same FSM_E* code on every rank instead of
+    leaving the peer blocked in the key exchange."""
+    from test_dist import run_ranks
+    from spark_fsm_amd import FSM_ELIMIT
+    monkeypatch.setenv("FSM_INJECT_FAIL", "1,pairs")
+    res = run_ranks(2, ["tsr_fail", "6000", "100", "0.4"], tmp_path, timeout=100)
+    assert [r["code"] for r in res] == [FSM_ELIMIT, FSM_ELIMIT]
+    assert "injected" in res[1]["msg"] and "peer rank failed" in res[0]["msg"]
+
+
+@pytest.mark.parametrize("bitmap", ["1", "0", "passes"])
 def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
-    """TSR expansions over sid bitmaps (default) and over the driver item's
-    sid list (FSM_TSR_BITMAP=0, the over-budget fallback) give the oracle's rules."""
+    """TSR expansions over sid bitmaps (default; "passes": the LDS histograms
+    cover 37 kids per pass, so every expansion runs several kid passes) and
+    over the driver item's sid list (FSM_TSR_BITMAP=0, the over-budget
+    fallback) give the oracle's rules."""
     from oracle import oracle
     from tools import gen
     from spark_fsm_amd import MODE_TSR
-    monkeypatch.setenv("FSM_TSR_BITMAP", bitmap)
+    monkeypatch.setenv("FSM_TSR_BITMAP", "0" if bitmap == "0" else "1")
+    if bitmap == "passes":
+        monkeypatch.setenv("FSM_TSR_PASS_KIDS", "37")
     ds = gen.kosarak(D=6000, seed=3)
     o = oracle.tsr(ds.records(), 300, 0.4)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)  # bitmaps are built at upload
@@ -541,16 +552,18 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
 
 
 @pytest.mark.parametrize("batch", ["1", "7", "128"])
-@pytest.mark.parametrize("lookahead", ["1", "0"])
-def test_tsr_batch_sizes_agree(eng, batch, lookahead, monkeypatch):
-    """Rules expanded per launch (FSM_TSR_BATCH) and the lookahead batch on the
-    second buffer set (FSM_TSR_LOOKAHEAD) change only how much runs ahead
-    speculatively: the rules and final minsup stay the oracle's."""
+@pytest.mark.parametrize("spb", ["default", "4", "100000"])
+def test_tsr_batch_sizes_agree(eng, batch, spb, monkeypatch):
+    """Rules expanded per launch (FSM_TSR_BATCH) and the domain sids per
+    expansion block (FSM_TSR_SPB: many small blocks, each slot in one block)
+    change only how much runs ahead speculatively and how the partial
+    histograms are split: the rules and final minsup stay the oracle's."""
     from oracle import oracle
     from tools import gen
     from spark_fsm_amd import MODE_TSR
     monkeypatch.setenv("FSM_TSR_BATCH", batch)
-    monkeypatch.setenv("FSM_TSR_LOOKAHEAD", lookahead)
+    if spb != "default":
+        monkeypatch.setenv("FSM_TSR_SPB", spb)
     ds = gen.kosarak(D=5000, seed=6)
     o = oracle.tsr(ds.records(), 150, 0.5)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)
