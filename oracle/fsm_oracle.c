@@ -611,17 +611,22 @@ static void tidpos_release(tidpos* t) {
     }
 }
 
+/* A rule carries only its items, support and confidence while it waits in the
+ * candidate heap; its tid state (I, J, common) is built from the items'
+ * first / last lists when it is expanded and released right after (memory
+ * follows the live candidates, not their tid sets: the 100K-sequence Kosarak
+ * prefix registers ~10^8 candidates while minsup is still low). */
 typedef struct rule {
-    int32_t* X;
+    int32_t* X;       /* X and Y live in the same allocation, after the struct */
     int32_t nx;
     int32_t* Y;
     int32_t ny;
     int32_t sup;
     double conf;
     int expandLR;
-    tidpos* I;        /* sids(X) with firstX (occurencesIfirst) */
-    tidpos* J;        /* sids(Y) with lastY  (occurencesJlast)  */
-    int32_t* common;  /* tidsIJ, sorted */
+    tidpos* I;        /* sids(X) with firstX (occurencesIfirst), while expanded */
+    tidpos* J;        /* sids(Y) with lastY  (occurencesJlast), while expanded  */
+    int32_t* common;  /* tidsIJ, sorted, while expanded */
     int64_t ncommon;
     int in_k;         /* still referenced by kRules */
     int in_cand;      /* still referenced by candidates */
@@ -716,8 +721,6 @@ static void rule_release_state(rule* r) {
 static void rule_maybe_free(rule* r) {
     if (r->in_k || r->in_cand) return;
     rule_release_state(r);
-    free(r->X);
-    free(r->Y);
     free(r);
 }
 
@@ -767,11 +770,13 @@ static void tsr_register(tsr_ctx* c, rule* r, int lr) {
 
 static rule* rule_new(tsr_ctx* c, const int32_t* X, int32_t nx, int32_t xadd, const int32_t* Y,
                       int32_t ny, int32_t yadd) {
-    rule* r = calloc(1, sizeof(rule));
-    r->nx = nx + (xadd >= 0);
-    r->ny = ny + (yadd >= 0);
-    r->X = malloc((size_t)r->nx * sizeof(int32_t));
-    r->Y = malloc((size_t)r->ny * sizeof(int32_t));
+    (void)c;
+    const int32_t mx = nx + (xadd >= 0), my = ny + (yadd >= 0);
+    rule* r = calloc(1, sizeof(rule) + (size_t)(mx + my) * sizeof(int32_t));
+    r->nx = mx;
+    r->ny = my;
+    r->X = (int32_t*)(r + 1);
+    r->Y = r->X + mx;
     memcpy(r->X, X, (size_t)nx * sizeof(int32_t));
     memcpy(r->Y, Y, (size_t)ny * sizeof(int32_t));
     if (xadd >= 0) r->X[nx] = xadd;
@@ -820,7 +825,42 @@ static int contains_lex(const int32_t* s, int32_t n, int32_t c) {
  * phase keeps no per-rule sid lists: at minsup 1 there are ~10^8 such rules on
  * the 100K-sequence Kosarak prefix): the sids of I (sids(X), firstX) and J
  * (sids(Y), lastY) with firstX < lastY, ascending. */
-static void ensure_common(rule* r) {
+/* sids(S) with the max (first lists) or min (last lists) position over the items of S */
+static tidpos* tid_intersect(tidpos* const* lists, const int32_t* S, int32_t n, int take_max) {
+    tidpos* acc = lists[S[0]];
+    if (n == 1) {
+        acc->refs++;
+        return acc;
+    }
+    tidpos* cur = NULL;
+    for (int32_t k = 1; k < n; k++) {
+        const tidpos* o = lists[S[k]];
+        tidpos* nx = tidpos_new(acc->n < o->n ? acc->n : o->n);
+        nx->n = 0;
+        int64_t a = 0, b = 0;
+        while (a < acc->n && b < o->n) {
+            if (acc->sid[a] < o->sid[b]) a++;
+            else if (o->sid[b] < acc->sid[a]) b++;
+            else {
+                nx->sid[nx->n] = acc->sid[a];
+                nx->pos[nx->n] = take_max ? (acc->pos[a] > o->pos[b] ? acc->pos[a] : o->pos[b])
+                                          : (acc->pos[a] < o->pos[b] ? acc->pos[a] : o->pos[b]);
+                nx->n++;
+                a++;
+                b++;
+            }
+        }
+        tidpos_release(cur);
+        cur = acc = nx;
+    }
+    return cur;
+}
+
+/* I = sids(X) with firstX, J = sids(Y) with lastY (from the items' lists), and
+ * common = tidsIJ: the sids of both with firstX < lastY, ascending. */
+static void ensure_state(tsr_ctx* c, rule* r) {
+    if (!r->I) r->I = tid_intersect(c->first, r->X, r->nx, 1);
+    if (!r->J) r->J = tid_intersect(c->last, r->Y, r->ny, 0);
     if (r->common) return;
     const tidpos *I = r->I, *J = r->J;
     r->common = malloc((size_t)(I->n < J->n ? I->n : J->n) * sizeof(int32_t) + 4);
@@ -840,7 +880,7 @@ static void ensure_common(rule* r) {
 /* expandL: rules X U {c} => Y, c > max(X), c not in Y, c before lastY(s). */
 static void tsr_expand_left(tsr_ctx* c, rule* r) {
     c->expansions++;
-    ensure_common(r);
+    ensure_state(c, r);
     scan_reset(c);
     for (int64_t q = 0; q < r->ncommon; q++) {
         int32_t tid = r->common[q];
@@ -857,30 +897,21 @@ static void tsr_expand_left(tsr_ctx* c, rule* r) {
         int32_t it = c->touched.a[q];
         i32vec* tl = &c->tids_of[it];
         if (tl->n < c->minsup) continue;
-        /* tidsIC = sids(X) ∩ sids(c); firstIC = max(firstX, first_c) */
+        /* |tidsIC| = |sids(X) ∩ sids(c)| (the child's tid state is rebuilt if it is expanded) */
         const tidpos* fc = c->first[it];
-        tidpos* I2 = tidpos_new(r->I->n < fc->n ? r->I->n : fc->n);
-        int64_t a = 0, b = 0;
+        int64_t a = 0, b = 0, nI2 = 0;
         while (a < r->I->n && b < fc->n) {
             if (r->I->sid[a] < fc->sid[b]) a++;
             else if (fc->sid[b] < r->I->sid[a]) b++;
             else {
-                I2->sid[I2->n] = r->I->sid[a];
-                I2->pos[I2->n] = r->I->pos[a] > fc->pos[b] ? r->I->pos[a] : fc->pos[b];
-                I2->n++;
+                nI2++;
                 a++;
                 b++;
             }
         }
         rule* nr = rule_new(c, r->X, r->nx, it, r->Y, r->ny, -1);
         nr->sup = (int32_t)tl->n;
-        nr->conf = (double)tl->n / (double)I2->n;
-        nr->I = I2;
-        nr->J = r->J;
-        r->J->refs++;
-        nr->ncommon = tl->n;
-        nr->common = malloc((size_t)tl->n * sizeof(int32_t));
-        memcpy(nr->common, tl->a, (size_t)tl->n * sizeof(int32_t)); /* tids ascending */
+        nr->conf = (double)tl->n / (double)nI2;
         if (nr->conf >= c->minconf) tsr_save(c, nr);
         tsr_register(c, nr, 1);
     }
@@ -889,7 +920,7 @@ static void tsr_expand_left(tsr_ctx* c, rule* r) {
 /* expandR: rules X => Y U {c}, c > max(Y), c not in X, c after firstX(s). */
 static void tsr_expand_right(tsr_ctx* c, rule* r) {
     c->expansions++;
-    ensure_common(r);
+    ensure_state(c, r);
     scan_reset(c);
     for (int64_t q = 0; q < r->ncommon; q++) {
         int32_t tid = r->common[q];
@@ -906,30 +937,10 @@ static void tsr_expand_right(tsr_ctx* c, rule* r) {
         int32_t it = c->touched.a[q];
         i32vec* tl = &c->tids_of[it];
         if (tl->n < c->minsup) continue;
-        /* tidsJC = sids(Y) ∩ sids(c); lastJC = min(lastY, last_c) */
-        const tidpos* lc = c->last[it];
-        tidpos* J2 = tidpos_new(r->J->n < lc->n ? r->J->n : lc->n);
-        int64_t a = 0, b = 0;
-        while (a < r->J->n && b < lc->n) {
-            if (r->J->sid[a] < lc->sid[b]) a++;
-            else if (lc->sid[b] < r->J->sid[a]) b++;
-            else {
-                J2->sid[J2->n] = r->J->sid[a];
-                J2->pos[J2->n] = r->J->pos[a] < lc->pos[b] ? r->J->pos[a] : lc->pos[b];
-                J2->n++;
-                a++;
-                b++;
-            }
-        }
+        /* X => Y u {c}: conf over |sids(X)| (tid state rebuilt if it is expanded) */
         rule* nr = rule_new(c, r->X, r->nx, -1, r->Y, r->ny, it);
         nr->sup = (int32_t)tl->n;
         nr->conf = (double)tl->n / (double)r->I->n;
-        nr->I = r->I;
-        r->I->refs++;
-        nr->J = J2;
-        nr->ncommon = tl->n;
-        nr->common = malloc((size_t)tl->n * sizeof(int32_t));
-        memcpy(nr->common, tl->a, (size_t)tl->n * sizeof(int32_t));
         if (nr->conf >= c->minconf) tsr_save(c, nr);
         tsr_register(c, nr, 0);
     }
@@ -1130,6 +1141,7 @@ int oracle_tsr_timed(const int32_t* sids, const char* const* lines, const int64_
                 tsr_expand_right(&c, r);
             }
             r->in_cand = 0;
+            rule_release_state(r);
             rule_maybe_free(r);
         }
         /* result = kRules */

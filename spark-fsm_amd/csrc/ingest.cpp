@@ -246,9 +246,10 @@ extern "C" int fsm_ingest(int32_t format, const char* data, int64_t len, int64_t
             fsm_token_db_free(t);
             return FSM_ENOMEM;
         }
-        std::memcpy(t->sids, o.sids.data(), o.sids.size() * 4);
-        std::memcpy(t->seq_off, o.off.data(), o.off.size() * 8);
-        std::memcpy(t->tokens, o.tok.data(), o.tok.size() * 8);
+        // empty vectors may hand out a null data(): memcpy from null is undefined even for 0 bytes
+        if (!o.sids.empty()) std::memcpy(t->sids, o.sids.data(), o.sids.size() * 4);
+        if (!o.off.empty()) std::memcpy(t->seq_off, o.off.data(), o.off.size() * 8);
+        if (!o.tok.empty()) std::memcpy(t->tokens, o.tok.data(), o.tok.size() * 8);
         *out = t;
         return FSM_OK;
     } catch (const Error& e) {

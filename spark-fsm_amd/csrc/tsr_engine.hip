@@ -47,7 +47,7 @@ constexpr int kMaxSide = 64;
 constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRID sweep: 4-8 best)
 constexpr int kExpBatch = 256;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
 constexpr int kMaxBatch = 256;
-constexpr int kExpandBlocks = 64;   // bitmap path: at most this many expansion blocks per rule slot
+constexpr int kExpandBlocks = 4096; // bitmap path: at most this many expansion blocks per rule slot
 constexpr int kExpSpb = 64;         // bitmap path: expected domain sids per expansion block (FSM_TSR_SPB)
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kDlUnroll = 8;        // k_dl: independent words / sids per thread per round
@@ -483,7 +483,11 @@ __global__ __launch_bounds__(kBlock) void k_alive(const uint32_t* __restrict__ k
 constexpr int kExpSids = FSM_TSR_SIDS;      // sids per wave step
 constexpr int kXBlock = FSM_TSR_XBLOCK;     // threads of an expansion block
 constexpr uint32_t kExpWin = 1024;          // sids per LDS window
-constexpr int kExpGrp = 4;                  // rows > 64 entries: 64-entry chunks of loads in flight per round
+constexpr int kExpGrp = 4;                  // rows > 64 x kLongR entries: 64-entry chunks of loads in flight per round
+#ifndef FSM_TSR_LONGR
+#define FSM_TSR_LONGR 4
+#endif
+constexpr int kLongR = FSM_TSR_LONGR;       // rows of <= 64 x kLongR entries: loaded once, both passes in registers
 constexpr uint32_t kPassKids = 4096;        // kids per LDS histogram pass (2 x 16 KiB)
 constexpr uint32_t kMaxKids = 65536;        // bitmap path: kept items (alive bitmap 8 KiB of LDS)
 
@@ -495,32 +499,51 @@ struct ExpGeo {       // kernel view of one launch's geometry
 
 __device__ __forceinline__ uint32_t alive_bit(const uint32_t* al, uint32_t c) { return (al[c >> 5] >> (c & 31u)) & 1u; }
 
-// one short row (<= 64 entries; lane = entry): every item of X u Y is in it
-// (s came from the bitmap AND), found by ballot
-__device__ __forceinline__ void expand_short(uint32_t c, uint32_t fl, const uint32_t* sX, uint32_t nx,
-                                             const uint32_t* sY, uint32_t ny, uint32_t maxX, uint32_t maxY,
-                                             uint32_t doL, uint32_t doR, const uint32_t* al, uint32_t kid_lo,
-                                             uint32_t KP, uint32_t* hL, uint32_t* hR) {
-    const uint32_t fi = fl & 0xFFFFu, la = fl >> 16;
-    uint32_t fX = 0, lY = 0xFFFFFFFFu;
-    bool inX = false, inY = false;
-    for (uint32_t k = 0; k < nx; ++k) {
-        const bool hit = c == sX[k];
-        inX |= hit;
-        const uint64_t hb = __ballot(hit);
-        fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(fi), int(__ffsll((long long)hb) - 1))));
-    }
-    for (uint32_t k = 0; k < ny; ++k) {
-        const bool hit = c == sY[k];
-        inY |= hit;
-        const uint64_t hb = __ballot(hit);
-        lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(la), int(__ffsll((long long)hb) - 1))));
-    }
-    if (fX >= lY) return;  // X => Y does not hold in s
+// the bumps of one entry (kid c, first | last << 16) of a row where X => Y
+// holds (firstX fX < lastY lY): expandL when c > max X, c not in Y and c
+// occurs before lastY; expandR when c > max Y, c not in X and c occurs after
+// firstX; only kids of this pass that can still reach the launch minsup
+__device__ __forceinline__ void bump(uint32_t c, uint32_t fl, uint32_t fX, uint32_t lY, const uint32_t* sX,
+                                     uint32_t nx, const uint32_t* sY, uint32_t ny, uint32_t maxX, uint32_t maxY,
+                                     uint32_t doL, uint32_t doR, const uint32_t* al, uint32_t kid_lo, uint32_t KP,
+                                     uint32_t* hL, uint32_t* hR) {
     const uint32_t rel = c - kid_lo;
     if (c == kNone || rel >= KP || !alive_bit(al, c)) return;
-    if (doL && c > maxX && fi < lY && !inY) atomicAdd(&hL[rel], 1u);
-    if (doR && c > maxY && la > fX && !inX) atomicAdd(&hR[rel], 1u);
+    bool inX = false, inY = false;
+    for (uint32_t k = 0; k < nx; ++k) inX |= c == sX[k];
+    for (uint32_t k = 0; k < ny; ++k) inY |= c == sY[k];
+    if (doL && c > maxX && (fl & 0xFFFFu) < lY && !inY) atomicAdd(&hL[rel], 1u);
+    if (doR && c > maxY && (fl >> 16) > fX && !inX) atomicAdd(&hR[rel], 1u);
+}
+
+// one row of up to 64 x kLongR entries held in registers (lane + 64 h, nch
+// chunks, wave-uniform): every item of X u Y is in it (s came from the bitmap
+// AND), found by ballot; then the bumps from the same registers
+__device__ __forceinline__ void expand_row(const uint2 (&e)[kLongR], uint32_t nch, const uint32_t* sX, uint32_t nx,
+                                           const uint32_t* sY, uint32_t ny, uint32_t maxX, uint32_t maxY,
+                                           uint32_t doL, uint32_t doR, const uint32_t* al, uint32_t kid_lo,
+                                           uint32_t KP, uint32_t mlo, uint32_t* hL, uint32_t* hR) {
+    uint32_t fX = 0, lY = 0xFFFFFFFFu;
+#pragma unroll
+    for (int h = 0; h < kLongR; ++h) {
+        if (uint32_t(h) >= nch) break;
+        const uint32_t c = e[h].x;
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint64_t hb = __ballot(c == sX[k]);
+            if (hb) fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(e[h].y & 0xFFFFu), int(__ffsll((long long)hb) - 1))));
+        }
+        for (uint32_t k = 0; k < ny; ++k) {
+            const uint64_t hb = __ballot(c == sY[k]);
+            if (hb) lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(e[h].y >> 16), int(__ffsll((long long)hb) - 1))));
+        }
+    }
+    if (fX >= lY) return;  // X => Y does not hold in s
+#pragma unroll
+    for (int h = 0; h < kLongR; ++h) {
+        if (uint32_t(h) >= nch) break;
+        if (e[h].x != kNone && e[h].x > mlo)
+            bump(e[h].x, e[h].y, fX, lY, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP, hL, hR);
+    }
 }
 
 __global__ __launch_bounds__(kXBlock) void k_expand_bm(const Side* __restrict__ sides,
@@ -611,29 +634,36 @@ __global__ __launch_bounds__(kXBlock) void k_expand_bm(const Side* __restrict__ 
             __syncthreads();
             const uint32_t n = min(kExpWin, tot - win);
             for (uint32_t q0 = wv; q0 < n; q0 += wpb * kExpSids) {
+                // kExpSids rows per wave step, the first 64 x kLongR entries of each loaded
+                // at once into registers (lane + 64 h): one load round serves both passes of
+                // every row up to 64 x kLongR entries (most domain rows)
                 uint32_t rb[kExpSids], re[kExpSids];
-                uint2 e[kExpSids];
+                uint2 e[kExpSids][kLongR];
 #pragma unroll
-                for (int j = 0; j < kExpSids; ++j) {  // all kExpSids rows in flight
+                for (int j = 0; j < kExpSids; ++j) {
                     const uint32_t q = q0 + uint32_t(j) * wpb;
                     rb[j] = q < n ? lrb[q] : 0u;
                     re[j] = q < n ? lre[q] : 0u;
-                    const uint32_t x = rb[j] + lane;
-                    e[j] = x < re[j] && re[j] - rb[j] <= 64u ? ent[x] : make_uint2(kNone, 0u);
+#pragma unroll
+                    for (int h = 0; h < kLongR; ++h) {
+                        const uint32_t x = rb[j] + uint32_t(h) * 64u + lane;
+                        e[j][h] = x < re[j] ? ent[x] : make_uint2(kNone, 0u);
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < kExpSids; ++j) {
                     if (q0 + uint32_t(j) * wpb >= n) break;
                     const uint32_t len = re[j] - rb[j];
                     if (lane == 0 && pass == 0) my_ent += len;
-                    if (len <= 64u) {
-                        expand_short(e[j].x, e[j].y, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP, hL, hR);
+                    if (len <= 64u * kLongR) {
+                        expand_row(e[j], (len + 63u) >> 6, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP,
+                                   mlo, hL, hR);
                         continue;
                     }
                     // longer rows: two ballot passes over 64-entry chunks, kExpGrp chunks of
-                    // loads in flight per round (no dependent searches): pass 1 finds the X / Y
-                    // items (firstX, lastY) and the first entry past mlo; pass 2 bumps from
-                    // there up to the end of this kid pass
+                    // loads in flight per round: pass 1 finds the X / Y items (firstX, lastY)
+                    // and the first entry past mlo; pass 2 bumps from there up to the end of
+                    // this kid pass
                     const uint32_t rbj = rb[j], rej = re[j];
                     uint32_t fX = 0, lY = 0xFFFFFFFFu, qs = rej;
                     for (uint32_t g0 = rbj; g0 < rej; g0 += 64u * kExpGrp) {
@@ -671,13 +701,7 @@ __global__ __launch_bounds__(kXBlock) void k_expand_bm(const Side* __restrict__ 
                         for (int h = 0; h < kExpGrp; ++h) {
                             const uint32_t ce = eg[h].x;
                             past |= __ballot(ce != kNone && ce >= mhi) != 0ull;  // wave-uniform: the pass ends here
-                            const uint32_t rel = ce - kid_lo;
-                            if (ce == kNone || rel >= KP || !alive_bit(al, ce)) continue;
-                            bool inX = false, inY = false;
-                            for (uint32_t k = 0; k < nx; ++k) inX |= ce == sX[k];
-                            for (uint32_t k = 0; k < ny; ++k) inY |= ce == sY[k];
-                            if (doL && ce > maxX && (eg[h].y & 0xFFFFu) < lY && !inY) atomicAdd(&hL[rel], 1u);
-                            if (doR && ce > maxY && (eg[h].y >> 16) > fX && !inX) atomicAdd(&hR[rel], 1u);
+                            bump(ce, eg[h].y, fX, lY, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP, hL, hR);
                         }
                     }
                 }
@@ -1328,7 +1352,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     const uint32_t KP = use_bm ? std::min<uint32_t>(K, pass_kids) : 0u;
     const uint32_t P = use_bm ? (K + KP - 1) / KP : 0u;
     const uint64_t row_bytes = uint64_t(P) * 2 * KP * 4;
-    const uint64_t part_budget = std::max<uint64_t>(uint64_t(32) << 20, uint64_t(B) * row_bytes);
+    const uint64_t part_mb = [] {  // FSM_TSR_PART_MB: partial-row budget per launch (tuning)
+        const char* v = std::getenv("FSM_TSR_PART_MB");
+        return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 4096) : uint64_t(32);
+    }();
+    const uint64_t part_budget = std::max<uint64_t>(part_mb << 20, uint64_t(B) * row_bytes);
     const uint64_t max_blocks = use_bm ? part_budget / row_bytes : 0;
     const size_t xlds = use_bm ? (size_t(2) * KP + (K + 31) / 32) * 4 : 0;
     // One set of launch buffers: the rule descriptors (pinned stage + device copy, one
@@ -1444,7 +1472,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 wave_off[k + 1] = wave_off[k] + (voff[drv + 1] - voff[drv]);
             }
         }
-        if (use_bm && wave_off[nb] > max_blocks) {  // partial rows over budget: fewer, larger blocks
+        if (use_bm && wave_off[nb] > max_blocks) {
+            // partial rows over budget: the budget is shared in proportion to the slots'
+            // expected domains (the launch lasts as long as its largest slot's blocks), at
+            // least one block each
             const uint64_t tot = wave_off[nb];
             uint64_t prev = 0;  // the original prefix at k
             for (uint32_t k = 0; k < nb; ++k) {
