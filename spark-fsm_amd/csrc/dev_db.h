@@ -23,7 +23,7 @@ struct TsrDevDB {
     fsm::DevBuf vert_off, vert_sid, vert_item;
     fsm::DevBuf bm;                          // sid bitmaps: U x NW u32 (empty when over budget)
     int64_t N = 0, E = 0, U = 0;
-    uint32_t NW = 0;                         // u32 words per item bitmap = ceil(N / 32)
+    uint32_t NW = 0;                         // u32 words per item bitmap = ceil(N / 128) * 4 (16-byte rows)
     std::vector<uint32_t> sup;               // |sids(item)|
 };
 

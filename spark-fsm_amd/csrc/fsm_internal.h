@@ -219,7 +219,7 @@ struct fsm_ctx {
     std::string err;
     fsm_stats stats{};
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     fsm::Comm* comm = nullptr;  // nranks > 1 (owned)
     std::shared_ptr<fsm::Pool> pool;  // device blocks of this context (see fsm::Pool)
     std::vector<fsm_kernel_stat> kstats;  // of the last mine call

@@ -450,46 +450,38 @@ __global__ __launch_bounds__(kBlock) void k_rows_pack(const uint32_t* __restrict
     }
 }
 
-// alive[w] bit j: kid 32w + j still has support >= the launch minsup t (t only
-// rises, so a dead kid never comes back; run when t changes)
+// alive[w], 2 bits per kid (16 kids per word): code 1 when kid 16w + j still
+// has support >= the launch minsup t, else 0 (t only rises, so a dead kid
+// never comes back; run when t changes).  k_exp_rows marks X / Y on its copy.
 __global__ __launch_bounds__(kBlock) void k_alive(const uint32_t* __restrict__ ksup, uint32_t K, uint32_t t,
                                                   uint32_t* __restrict__ alive) {
     const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= (K + 31) / 32) return;
+    if (w >= (K + 15) / 16) return;
     uint32_t v = 0;
-    for (uint32_t j = 0; j < 32; ++j) {
-        const uint32_t k = w * 32 + j;
-        if (k < K && ksup[k] >= t) v |= 1u << j;
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t k = w * 16 + j;
+        if (k < K && ksup[k] >= t) v |= 1u << (2 * j);
     }
     alive[w] = v;
 }
 
-// Expansion of rule slot b over the sids holding every item of X u Y, with
-// the expandL / expandR histograms of a kid range [kid_lo, kid_lo + KP) in LDS
-// (the per-entry device-scope atomics of the HBM histograms - 26.7 G
-// per c4 mine, all executed at the memory side - are gone).  A slot's blocks
-// own contiguous ranges of bitmap words (one word per thread per pass): the
-// rule's |X|+|Y| item bitmaps are ANDed (operand loads issued together), a
-// block scan places the set sids and their row bounds in LDS windows, and the
-// waves take the window's sids kExpSids at a time with all their row loads in
-// flight.  Each block writes its whole histogram as one dense partial row
-// (plain coalesced stores); k_expand_reduce sums a slot's rows.
-#ifndef FSM_TSR_SIDS
-#define FSM_TSR_SIDS 4
-#endif
+// Expansions on the bitmap path (no device-scope atomics per
+// entry): k_exp_domain ANDs each rule's |X|+|Y| item bitmaps once and
+// compacts the sids holding X u Y into a per-slot domain list; k_exp_rows
+// counts the expandL / expandR candidates of the domain rows into LDS
+// histograms, one dense partial row per block; k_expand_reduce sums them.
 #ifndef FSM_TSR_XBLOCK
 #define FSM_TSR_XBLOCK 512
 #endif
-constexpr int kExpSids = FSM_TSR_SIDS;      // sids per wave step
 constexpr int kXBlock = FSM_TSR_XBLOCK;     // threads of an expansion block
-constexpr uint32_t kExpWin = 1024;          // sids per LDS window
-constexpr int kExpGrp = 4;                  // rows > 64 x kLongR entries: 64-entry chunks of loads in flight per round
-#ifndef FSM_TSR_LONGR
-#define FSM_TSR_LONGR 4
+constexpr uint32_t kExpWin = 2 * kXBlock;   // sids per LDS window (two per thread in the length scan)
+#ifndef FSM_TSR_EPT
+#define FSM_TSR_EPT 8
 #endif
-constexpr int kLongR = FSM_TSR_LONGR;       // rows of <= 64 x kLongR entries: loaded once, both passes in registers
+constexpr int kEpt = FSM_TSR_EPT;           // row entries per lane per chunk (registers)
+constexpr uint32_t kChunkEnt = uint32_t(kXBlock) * kEpt;  // entries of one flat chunk
 constexpr uint32_t kPassKids = 4096;        // kids per LDS histogram pass (2 x 16 KiB)
-constexpr uint32_t kMaxKids = 65536;        // bitmap path: kept items (alive bitmap 8 KiB of LDS)
+constexpr uint32_t kMaxKids = 65536;        // bitmap path: kept items (kid codes 16 KiB of LDS)
 
 struct ExpGeo {       // kernel view of one launch's geometry
     uint32_t K, KP;   // kept items, kids per pass
@@ -497,73 +489,131 @@ struct ExpGeo {       // kernel view of one launch's geometry
     uint32_t t;       // launch minsup
 };
 
-__device__ __forceinline__ uint32_t alive_bit(const uint32_t* al, uint32_t c) { return (al[c >> 5] >> (c & 31u)) & 1u; }
-
-// the bumps of one entry (kid c, first | last << 16) of a row where X => Y
-// holds (firstX fX < lastY lY): expandL when c > max X, c not in Y and c
-// occurs before lastY; expandR when c > max Y, c not in X and c occurs after
-// firstX; only kids of this pass that can still reach the launch minsup
-__device__ __forceinline__ void bump(uint32_t c, uint32_t fl, uint32_t fX, uint32_t lY, const uint32_t* sX,
-                                     uint32_t nx, const uint32_t* sY, uint32_t ny, uint32_t maxX, uint32_t maxY,
-                                     uint32_t doL, uint32_t doR, const uint32_t* al, uint32_t kid_lo, uint32_t KP,
+// the bumps of one candidate entry (kid c alive and not in X u Y; first |
+// last << 16) of a row where X => Y holds (firstX fX < lastY lY): expandL when
+// c > max X and c occurs before lastY; expandR when c > max Y and c occurs
+// after firstX; only kids of this pass [kid_lo, kid_lo + KP)
+__device__ __forceinline__ void bump(uint32_t c, uint32_t fl, uint32_t fX, uint32_t lY, bool, bool, uint32_t maxX,
+                                     uint32_t maxY, uint32_t doL, uint32_t doR, uint32_t kid_lo, uint32_t KP,
                                      uint32_t* hL, uint32_t* hR) {
     const uint32_t rel = c - kid_lo;
-    if (c == kNone || rel >= KP || !alive_bit(al, c)) return;
-    bool inX = false, inY = false;
-    for (uint32_t k = 0; k < nx; ++k) inX |= c == sX[k];
-    for (uint32_t k = 0; k < ny; ++k) inY |= c == sY[k];
-    if (doL && c > maxX && (fl & 0xFFFFu) < lY && !inY) atomicAdd(&hL[rel], 1u);
-    if (doR && c > maxY && (fl >> 16) > fX && !inX) atomicAdd(&hR[rel], 1u);
+    if (rel >= KP) return;
+    if (doL && c > maxX && (fl & 0xFFFFu) < lY) atomicAdd(&hL[rel], 1u);
+    if (doR && c > maxY && (fl >> 16) > fX) atomicAdd(&hR[rel], 1u);
 }
 
-// one row of up to 64 x kLongR entries held in registers (lane + 64 h, nch
-// chunks, wave-uniform): every item of X u Y is in it (s came from the bitmap
-// AND), found by ballot; then the bumps from the same registers
-__device__ __forceinline__ void expand_row(const uint2 (&e)[kLongR], uint32_t nch, const uint32_t* sX, uint32_t nx,
-                                           const uint32_t* sY, uint32_t ny, uint32_t maxX, uint32_t maxY,
-                                           uint32_t doL, uint32_t doR, const uint32_t* al, uint32_t kid_lo,
-                                           uint32_t KP, uint32_t mlo, uint32_t* hL, uint32_t* hR) {
-    uint32_t fX = 0, lY = 0xFFFFFFFFu;
+// Domain of rule slot k (grid.y): its |X|+|Y| item bitmaps ANDed over this
+// block's kDomWords words (4 consecutive words per thread, 16-byte operand
+// loads, 8 operands in flight), the set sids compacted into the slot's domain
+// list at dom_off[k] (one cursor atomic per block: ExpCtl::nsid) as (row start,
+// row length) pairs of the packed kept rows.  Every pass of the row kernel
+// reads this list; the bitmaps are ANDed once per rule.
+constexpr uint32_t kDomThreads = 256;
+constexpr uint32_t kDomWords = 4 * kDomThreads;  // bitmap words per domain block
+
+__global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restrict__ sides,
+                                                            const uint32_t* __restrict__ bm, uint32_t NW,
+                                                            const uint32_t* __restrict__ row_off,
+                                                            const uint64_t* __restrict__ dom_off,
+                                                            uint2* __restrict__ dom, ExpCtl* __restrict__ ctlb) {
+    __shared__ uint32_t sIt[2 * kMaxSide];
+    __shared__ uint32_t wsum[kDomThreads / 64];
+    __shared__ uint32_t b_base;
+    const uint32_t k = blockIdx.y;
+    const Side& side = sides[k];
+    const uint32_t nxy = side.nx + side.ny;
+    for (uint32_t q = threadIdx.x; q < nxy; q += blockDim.x) sIt[q] = q < side.nx ? side.X[q] : side.Y[q - side.nx];
+    __syncthreads();
+    const uint32_t w = blockIdx.x * kDomWords + 4 * threadIdx.x;  // NW is a multiple of 4
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (w < NW) {
+        v = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t k0 = 0; k0 < nxy; k0 += 8) {
+            uint4 o[8];
 #pragma unroll
-    for (int h = 0; h < kLongR; ++h) {
-        if (uint32_t(h) >= nch) break;
-        const uint32_t c = e[h].x;
-        for (uint32_t k = 0; k < nx; ++k) {
-            const uint64_t hb = __ballot(c == sX[k]);
-            if (hb) fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(e[h].y & 0xFFFFu), int(__ffsll((long long)hb) - 1))));
-        }
-        for (uint32_t k = 0; k < ny; ++k) {
-            const uint64_t hb = __ballot(c == sY[k]);
-            if (hb) lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(e[h].y >> 16), int(__ffsll((long long)hb) - 1))));
+            for (int j = 0; j < 8; ++j)
+                o[j] = k0 + j < nxy ? *reinterpret_cast<const uint4*>(bm + uint64_t(sIt[k0 + j]) * NW + w)
+                                    : make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                v.x &= o[j].x;
+                v.y &= o[j].y;
+                v.z &= o[j].z;
+                v.w &= o[j].w;
+            }
+            if (!(v.x | v.y | v.z | v.w)) break;
         }
     }
-    if (fX >= lY) return;  // X => Y does not hold in s
+    const uint32_t cnt = uint32_t(__popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w));
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(cnt);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (uint32_t q = 0; q < kDomThreads / 64; ++q) tot += wsum[q];
+        b_base = tot ? atomicAdd(&ctlb[k].nsid, tot) : 0u;
+    }
+    __syncthreads();
+    if (!cnt) return;
+    uint32_t p = b_base + incl - cnt;
+    for (uint32_t q = 0; q < wv; ++q) p += wsum[q];
+    uint2* out = dom + dom_off[k];
+    const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int h = 0; h < kLongR; ++h) {
-        if (uint32_t(h) >= nch) break;
-        if (e[h].x != kNone && e[h].x > mlo)
-            bump(e[h].x, e[h].y, fX, lY, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP, hL, hR);
+    for (int h = 0; h < 4; ++h) {
+        for (uint32_t m = ww[h]; m; m &= m - 1u) {
+            const uint32_t sid = (w + uint32_t(h)) * 32u + uint32_t(__builtin_ctz(m));
+            const uint32_t rs = row_off[sid];
+            out[p++] = make_uint2(rs, row_off[sid + 1] - rs);
+        }
     }
 }
 
-__global__ __launch_bounds__(kXBlock) void k_expand_bm(const Side* __restrict__ sides,
-                                                       const uint64_t* __restrict__ blk_off, uint32_t nslot,
-                                                       const uint32_t* __restrict__ bm, uint32_t NW,
-                                                       const uint32_t* __restrict__ row_off,
-                                                       const uint2* __restrict__ ent,
-                                                       const uint32_t* __restrict__ kid_of,
-                                                       const uint32_t* __restrict__ alive, ExpGeo geo,
-                                                       uint32_t* __restrict__ part, ExpCtl* __restrict__ ctlb,
-                                                       uint32_t* __restrict__ ndlw) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];  // hist L [KP] | hist R [KP] | alive
-    __shared__ uint32_t lrb[kExpWin], lre[kExpWin];
-    __shared__ uint32_t sXY[2 * kMaxSide];  // X then Y, as kids
-    __shared__ uint32_t sIt[2 * kMaxSide];  // X then Y, as items (bitmap rows)
+// The rows of slot b's domain (k_exp_domain's list, this block's share of it)
+// counted into LDS histograms of the kid range [kid_lo, kid_lo + KP), pass =
+// blockIdx.y.  Windows of kExpWin domain rows: their (start, length) pairs are
+// loaded coalesced and the lengths scanned; the window's rows are then walked
+// FLAT: chunks of whole rows holding at most kChunkEnt entries are spread over
+// every lane of the block (each wave a contiguous stretch of the chunk,
+// lane-interleaved: one coalesced 8-byte load per lane per step, kEpt steps
+// per lane in registers), so a 2,000-entry row is 4 steps of 8 waves instead
+// of one wave's serial chain of dependent loads, and an 8-entry row does not
+// leave 56 lanes idle.  A lane finds its row from the step's row-start mask:
+// the rows starting inside the step flag their offsets in a wave-private LDS
+// word array, one ballot turns the flags into a 64-bit mask and mbcnt counts
+// the starts up to the lane.  Each kid's role comes from one 2-bit code (dead,
+// candidate, in X, in Y; ctab).  Pass 1 (loads in flight together) marks
+// firstX / lastY of each row with LDS atomics; after one barrier pass 2 bumps
+// the candidates from the same registers.  Rows longer than a chunk are walked
+// twice (pass 1, barrier, pass 2).  Each block writes its whole histogram as
+// one dense partial row (plain coalesced stores); k_expand_reduce sums a
+// slot's rows.
+__device__ __forceinline__ uint32_t kid_code(const uint32_t* ctab, uint32_t c) {
+    return (ctab[c >> 4] >> ((c & 15u) * 2u)) & 3u;
+}
+
+__global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ sides,
+                                                      const uint64_t* __restrict__ blk_off, uint32_t nslot,
+                                                      const uint64_t* __restrict__ dom_off,
+                                                      const uint2* __restrict__ dom,
+                                                      const uint2* __restrict__ ent,
+                                                      const uint32_t* __restrict__ kid_of,
+                                                      const uint32_t* __restrict__ alive, ExpGeo geo,
+                                                      uint32_t* __restrict__ part, ExpCtl* __restrict__ ctlb,
+                                                      uint32_t* __restrict__ ndlw) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];  // hist L [KP] | hist R [KP] | ctab
+    // window rows: x = first flat entry (exclusive scan of the lengths), y = row start in
+    // `ent` minus x (u32 wrap: the ent index of flat entry q is y + q)
+    __shared__ uint2 rowv[kExpWin + 1];
+    __shared__ uint32_t sfX[kExpWin], slY[kExpWin];  // per row: firstX (max over X), lastY (min over Y)
+    __shared__ uint32_t wflag[kXBlock / 64][64];     // per wave: row-start flags of the current step (tags)
+    __shared__ uint32_t sXY[2 * kMaxSide];           // X then Y, as kids
     __shared__ uint32_t wsum[kXBlock / 64];
     const uint32_t KP = geo.KP, pass = blockIdx.y, kid_lo = pass * KP;
     uint32_t* hL = dsm;
     uint32_t* hR = dsm + KP;
-    uint32_t* al = dsm + 2 * KP;
+    uint32_t* ctab = dsm + 2 * KP;  // 2 bits per kid: 0 dead, 1 candidate, 2 in X, 3 in Y
     // slot of this block: the last b with blk_off[b] <= blockIdx.x (blocks per slot sized by its domain)
     uint32_t b = 0;
     for (uint32_t step = kMaxBatch / 2; step > 0; step >>= 1)
@@ -575,149 +625,160 @@ __global__ __launch_bounds__(kXBlock) void k_expand_bm(const Side* __restrict__ 
     if (blockIdx.x == 0 && pass == 0 && threadIdx.x == 0) *ndlw = 0u;
     const uint32_t nx = side.nx, ny = side.ny, nxy = nx + ny;
     const uint32_t doL = side.doL, doR = side.doR;
-    for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) dsm[k] = 0;
-    for (uint32_t k = threadIdx.x; k < (geo.K + 31) / 32; k += blockDim.x) al[k] = alive[k];
-    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) {
-        const uint32_t it = k < nx ? side.X[k] : side.Y[k - nx];
-        sIt[k] = it;
-        sXY[k] = kid_of[it];
-    }
-    __syncthreads();
-    const uint32_t* sX = sXY;
-    const uint32_t* sY = sXY + nx;
-    const uint32_t maxX = sX[nx - 1], maxY = sY[ny - 1];  // sides ascend by item, so by kid
     const uint32_t lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
-    uint32_t my_ent = 0, my_sid = 0;  // row entries / domain sids this wave / thread saw
-    const uint32_t w0 = uint32_t(uint64_t(bx) * NW / nbx);
-    const uint32_t w1 = uint32_t(uint64_t(bx + 1) * NW / nbx);
+    for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) dsm[k] = 0;
+    for (uint32_t k = threadIdx.x; k < (geo.K + 15) / 16; k += blockDim.x) ctab[k] = alive[k];
+    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) sXY[k] = kid_of[k < nx ? side.X[k] : side.Y[k - nx]];
+    wflag[wv][lane] = 0;
+    // this block's share of the slot's domain
+    const uint32_t nd = ctl->nsid;
+    const uint32_t d0 = uint32_t(uint64_t(nd) * bx / nbx), d1 = uint32_t(uint64_t(nd) * (bx + 1) / nbx);
+    const uint2* dl = dom + dom_off[b];
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) {  // X -> code 2, Y -> code 3
+        const uint32_t c = sXY[k], sh = (c & 15u) * 2u;
+        atomicAnd(&ctab[c >> 4], ~(3u << sh));
+        atomicOr(&ctab[c >> 4], (k < nx ? 2u : 3u) << sh);
+    }
+    const uint32_t maxX = sXY[nx - 1], maxY = sXY[nxy - 1];  // sides ascend by item, so by kid
+    uint32_t my_ent = 0;   // row entries of this block (thread 0)
+    uint32_t tag = 0;      // this wave's step tags in wflag
     // bumps of this pass start past min(max X, max Y) (both extensions need c above one of them)
     const uint32_t mlo = max(doL ? (doR ? min(maxX, maxY) : maxX) : maxY, kid_lo == 0 ? 0u : kid_lo - 1u);
-    const uint32_t mhi = kid_lo + KP;  // and stop at the pass end
-    for (uint32_t c0 = w0; c0 < w1; c0 += blockDim.x) {
-        const uint32_t w = c0 + threadIdx.x;
-        uint32_t v = 0;
-        if (w < w1) {
-            v = ~0u;
-            for (uint32_t k0 = 0; k0 < nxy && v; k0 += 8) {  // 8 operand loads in flight per round
-                uint32_t o[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    o[j] = k0 + j < nxy ? bm[uint64_t(sIt[k0 + j]) * NW + w] : ~0u;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v &= o[j];
+    for (uint32_t win = d0; win < d1; win += kExpWin) {
+        const uint32_t n = min(kExpWin, d1 - win);
+        {   // the window's rows and the exclusive scan of their lengths (rows 2t, 2t + 1 per thread)
+            const uint32_t j = 2 * threadIdx.x;
+            const uint2 r0 = j < n ? dl[win + j] : make_uint2(0u, 0u);
+            const uint2 r1 = j + 1 < n ? dl[win + j + 1] : make_uint2(0u, 0u);
+            const uint32_t pr = r0.y + r1.y, inc = wave_incl_scan(pr);
+            if (lane == 63) wsum[wv] = inc;
+            __syncthreads();  // (also: the previous window's LDS and the ctab codes are ready)
+            uint32_t bb = 0, tt = 0;
+            for (uint32_t k = 0; k < wpb; ++k) {
+                bb += k < wv ? wsum[k] : 0u;
+                tt += wsum[k];
+            }
+            const uint32_t ex = bb + inc - pr;
+            if (j < n) {
+                rowv[j] = make_uint2(ex, r0.x - ex);
+                sfX[j] = 0;
+                slY[j] = 0xFFFFFFFFu;
+            }
+            if (j + 1 < n) {
+                rowv[j + 1] = make_uint2(ex + r0.y, r1.x - (ex + r0.y));
+                sfX[j + 1] = 0;
+                slY[j + 1] = 0xFFFFFFFFu;
+            }
+            if (threadIdx.x == 0) {
+                rowv[n] = make_uint2(tt, 0u);
+                if (pass == 0) my_ent += tt;
             }
         }
-        const uint32_t cnt = uint32_t(__popc(v));
-        my_sid += cnt;
-        const uint32_t incl = wave_incl_scan(cnt);
-        if (lane == 63) wsum[wv] = incl;
         __syncthreads();
-        uint32_t base = 0, tot = 0;
-        for (uint32_t k = 0; k < wpb; ++k) {
-            base += k < wv ? wsum[k] : 0u;
-            tot += wsum[k];
-        }
-        const uint32_t pos = base + incl - cnt;
-        for (uint32_t win = 0; win < tot; win += kExpWin) {
-            // this thread's sids with block positions in the window -> row bounds in LDS
-            uint32_t vv = v, p = pos;
-            while (vv) {
-                if (p >= win && p < win + kExpWin) {
-                    const uint32_t sid = w * 32u + uint32_t(__builtin_ctz(vv));
-                    lrb[p - win] = row_off[sid];
-                    lre[p - win] = row_off[sid + 1];
+        // chunks of whole rows [j0, j1) with at most kChunkEnt entries (block-uniform loop).
+        // Every domain row holds X u Y (the bitmap AND): at least 2 entries, so the 65
+        // entries from a step's first one span at most 33 rows.
+        for (uint32_t j0 = 0; j0 < n;) {
+            const uint32_t E0 = rowv[j0].x;
+            uint32_t j1 = j0;  // the last j in [j0, n] with start(j) - E0 <= kChunkEnt
+            for (uint32_t hi = n; j1 < hi;) {
+                const uint32_t mid = (j1 + hi + 1) >> 1;
+                if (rowv[mid].x - E0 <= kChunkEnt) j1 = mid; else hi = mid - 1;
+            }
+            if (j1 == j0) {
+                // one row longer than a chunk: pass 1 over it, barrier, pass 2 reloading it
+                const uint32_t rs = rowv[j0].y + E0, len = rowv[j0 + 1].x - E0;
+                for (uint32_t q = threadIdx.x; q < len; q += blockDim.x) {
+                    const uint2 e = ent[rs + q];
+                    const uint32_t cd = kid_code(ctab, e.x);
+                    if (cd == 2u) atomicMax(&sfX[j0], e.y & 0xFFFFu);
+                    if (cd == 3u) atomicMin(&slY[j0], e.y >> 16);
                 }
-                vv &= vv - 1u;
-                ++p;
+                __syncthreads();
+                const uint32_t fX = sfX[j0], lY = slY[j0];
+                if (fX < lY) {
+                    for (uint32_t q = threadIdx.x; q < len; q += blockDim.x) {
+                        const uint2 e = ent[rs + q];
+                        if (e.x > mlo && kid_code(ctab, e.x) == 1u)
+                            bump(e.x, e.y, fX, lY, false, false, maxX, maxY, doL, doR, kid_lo, KP, hL, hR);
+                    }
+                }
+                ++j0;
+                continue;
+            }
+            const uint32_t Tc = rowv[j1].x - E0;
+            const uint32_t sw = (Tc + wpb * 64 - 1) / (wpb * 64) * 64;  // entries per wave (<= 64 kEpt)
+            const uint32_t qa = E0 + wv * sw, qz = min(E0 + Tc, qa + sw);
+            uint32_t ej[kEpt];
+            uint2 e[kEpt];
+            uint32_t codes = 0;  // 2 bits per step: the entry's kid code (0: no entry)
+            if (qa < qz) {
+                // the wave's first row: the last j in [j0, j1) with start(j) <= qa (wave-uniform)
+                uint32_t ja = j0;
+                for (uint32_t hi = j1 - 1; ja < hi;) {
+                    const uint32_t mid = (ja + hi + 1) >> 1;
+                    if (rowv[mid].x <= qa) ja = mid; else hi = mid - 1;
+                }
+                uint32_t idx[kEpt];
+                // pass 1a: the row of each entry from the step's row-start mask
+#pragma unroll
+                for (int u = 0; u < kEpt; ++u) {
+                    const uint32_t q0 = qa + 64u * uint32_t(u);  // wave-uniform
+                    idx[u] = kNone;
+                    ej[u] = 0;
+                    if (q0 < qz) {
+                        const uint32_t jl = ja + lane;
+                        const uint2 rl = jl < j1 ? rowv[jl] : make_uint2(0xFFFFFFFFu, 0u);
+                        const uint32_t pp = rl.x - q0;  // row jl starts pp entries into the step (lane 0: <= 0)
+                        ++tag;
+                        if (jl < j1 && pp - 1u < 63u) wflag[wv][pp] = tag;  // a start inside the step
+                        const uint64_t nxt = __ballot(jl < j1 && pp - 1u < 64u);  // starts in (q0, q0 + 64]
+                        __builtin_amdgcn_wave_barrier();
+                        const uint64_t m = __ballot(wflag[wv][lane] == tag);
+                        // row of lane l = ja + starts at offsets 1..l
+                        const uint32_t r = uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))) +
+                                           uint32_t((m >> lane) & 1ull);
+                        const uint32_t ab = uint32_t(__shfl(int(rl.y), int(r), 64));
+                        if (q0 + lane < qz) {
+                            idx[u] = ab + q0 + lane;
+                            ej[u] = ja + r;
+                        }
+                        ja += uint32_t(__popcll(nxt));
+                    }
+                }
+                // pass 1b: every load in flight, then firstX / lastY of the rows
+#pragma unroll
+                for (int u = 0; u < kEpt; ++u) e[u] = idx[u] != kNone ? ent[idx[u]] : make_uint2(kNone, 0u);
+#pragma unroll
+                for (int u = 0; u < kEpt; ++u) {
+                    if (idx[u] == kNone) continue;
+                    const uint32_t cd = kid_code(ctab, e[u].x);
+                    codes |= (cd | 4u) << (3 * u);  // bit 2: an entry
+                    if (cd == 2u) atomicMax(&sfX[ej[u]], e[u].y & 0xFFFFu);
+                    if (cd == 3u) atomicMin(&slY[ej[u]], e[u].y >> 16);
+                }
             }
             __syncthreads();
-            const uint32_t n = min(kExpWin, tot - win);
-            for (uint32_t q0 = wv; q0 < n; q0 += wpb * kExpSids) {
-                // kExpSids rows per wave step, the first 64 x kLongR entries of each loaded
-                // at once into registers (lane + 64 h): one load round serves both passes of
-                // every row up to 64 x kLongR entries (most domain rows)
-                uint32_t rb[kExpSids], re[kExpSids];
-                uint2 e[kExpSids][kLongR];
+            // pass 2: the bumps of the candidates in rows where X => Y holds
+            if (qa < qz) {
 #pragma unroll
-                for (int j = 0; j < kExpSids; ++j) {
-                    const uint32_t q = q0 + uint32_t(j) * wpb;
-                    rb[j] = q < n ? lrb[q] : 0u;
-                    re[j] = q < n ? lre[q] : 0u;
-#pragma unroll
-                    for (int h = 0; h < kLongR; ++h) {
-                        const uint32_t x = rb[j] + uint32_t(h) * 64u + lane;
-                        e[j][h] = x < re[j] ? ent[x] : make_uint2(kNone, 0u);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < kExpSids; ++j) {
-                    if (q0 + uint32_t(j) * wpb >= n) break;
-                    const uint32_t len = re[j] - rb[j];
-                    if (lane == 0 && pass == 0) my_ent += len;
-                    if (len <= 64u * kLongR) {
-                        expand_row(e[j], (len + 63u) >> 6, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP,
-                                   mlo, hL, hR);
-                        continue;
-                    }
-                    // longer rows: two ballot passes over 64-entry chunks, kExpGrp chunks of
-                    // loads in flight per round: pass 1 finds the X / Y items (firstX, lastY)
-                    // and the first entry past mlo; pass 2 bumps from there up to the end of
-                    // this kid pass
-                    const uint32_t rbj = rb[j], rej = re[j];
-                    uint32_t fX = 0, lY = 0xFFFFFFFFu, qs = rej;
-                    for (uint32_t g0 = rbj; g0 < rej; g0 += 64u * kExpGrp) {
-                        uint2 eg[kExpGrp];
-#pragma unroll
-                        for (int h = 0; h < kExpGrp; ++h) {
-                            const uint32_t x = g0 + uint32_t(h) * 64u + lane;
-                            eg[h] = x < rej ? ent[x] : make_uint2(kNone, 0u);
-                        }
-#pragma unroll
-                        for (int h = 0; h < kExpGrp; ++h) {
-                            const uint32_t ce = eg[h].x;
-                            const uint64_t gt = __ballot(ce != kNone && ce > mlo);
-                            if (gt && qs == rej) qs = g0 + uint32_t(h) * 64u + uint32_t(__ffsll((long long)gt)) - 1u;
-                            for (uint32_t k = 0; k < nx; ++k) {
-                                const uint64_t hb = __ballot(ce == sX[k]);
-                                if (hb) fX = max(fX, uint32_t(__builtin_amdgcn_readlane(int(eg[h].y & 0xFFFFu), int(__ffsll((long long)hb) - 1))));
-                            }
-                            for (uint32_t k = 0; k < ny; ++k) {
-                                const uint64_t hb = __ballot(ce == sY[k]);
-                                if (hb) lY = min(lY, uint32_t(__builtin_amdgcn_readlane(int(eg[h].y >> 16), int(__ffsll((long long)hb) - 1))));
-                            }
-                        }
-                    }
-                    if (fX >= lY) continue;  // X => Y does not hold in s
-                    bool past = false;
-                    for (uint32_t g0 = qs; g0 < rej && !past; g0 += 64u * kExpGrp) {
-                        uint2 eg[kExpGrp];
-#pragma unroll
-                        for (int h = 0; h < kExpGrp; ++h) {
-                            const uint32_t x = g0 + uint32_t(h) * 64u + lane;
-                            eg[h] = x < rej ? ent[x] : make_uint2(kNone, 0u);
-                        }
-#pragma unroll
-                        for (int h = 0; h < kExpGrp; ++h) {
-                            const uint32_t ce = eg[h].x;
-                            past |= __ballot(ce != kNone && ce >= mhi) != 0ull;  // wave-uniform: the pass ends here
-                            bump(ce, eg[h].y, fX, lY, sX, nx, sY, ny, maxX, maxY, doL, doR, al, kid_lo, KP, hL, hR);
-                        }
-                    }
+                for (int u = 0; u < kEpt; ++u) {
+                    if (((codes >> (3 * u)) & 7u) != 5u || e[u].x <= mlo) continue;  // an entry with code 1
+                    const uint32_t fX = sfX[ej[u]], lY = slY[ej[u]];
+                    if (fX < lY) bump(e[u].x, e[u].y, fX, lY, false, false, maxX, maxY, doL, doR, kid_lo, KP, hL, hR);
                 }
             }
-            __syncthreads();  // the window's LDS is rewritten next
+            j0 = j1;  // the next chunk's rows are disjoint: no barrier before its pass 1
         }
     }
+    __syncthreads();
     // the block's histograms -> its dense partial rows [L | R] (k_expand_reduce sums a slot's)
     uint32_t* prow = part + (uint64_t(pass) * geo.nblk + blockIdx.x) * 2 * KP;
     for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) prow[k] = dsm[k];
-    // domain and entry counters (one atomic per wave, first pass only)
-    if (pass == 0) {
-        my_sid = uint32_t(__shfl(int(wave_incl_scan(my_sid)), 63, 64));
-        if (lane == 0 && my_sid) atomicAdd(&ctl->nsid, my_sid);
-        if (lane == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
-    }
+    if (pass == 0 && threadIdx.x == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
 }
 
 // Sum each slot's partial rows per kid; keep the counts >= t (records to mapped
@@ -1049,7 +1110,7 @@ void tsr_finish(fsm_ctx* ctx, TsrDevDB* d) {
     }
     // sid bitmaps for the expansion domain (skipped when they would take more
     // than a quarter of the free HBM; FSM_TSR_BITMAP=0 forces the list path)
-    d->NW = uint32_t((d->N + 31) / 32);
+    d->NW = uint32_t((d->N + 127) / 128 * 4);  // a multiple of 4 words: k_exp_domain reads 16-byte words
     const uint64_t bm_bytes = uint64_t(d->U) * d->NW * 4;
     size_t free_b = 0, total_b = 0;
     FSM_HIP(hipMemGetInfo(&free_b, &total_b));
@@ -1254,7 +1315,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         d_kidof.alloc(size_t(std::max<uint32_t>(U, 1)) * 4);
         d_kept.alloc(size_t(K) * 4);
         d_ksup.alloc(size_t(K) * 4);
-        d_alive.alloc(size_t((K + 31) / 32) * 4);
+        d_alive.alloc(size_t((K + 15) / 16) * 4);
         FSM_HIP(hipMemcpyAsync(d_kidof.p, kid_of.data(), size_t(U) * 4, hipMemcpyHostToDevice, s));
         FSM_HIP(hipMemcpyAsync(d_kept.p, kept_items.data(), size_t(K) * 4, hipMemcpyHostToDevice, s));
         FSM_HIP(hipMemcpyAsync(d_ksup.p, ksup.data(), size_t(K) * 4, hipMemcpyHostToDevice, s));
@@ -1358,13 +1419,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     }();
     const uint64_t part_budget = std::max<uint64_t>(part_mb << 20, uint64_t(B) * row_bytes);
     const uint64_t max_blocks = use_bm ? part_budget / row_bytes : 0;
-    const size_t xlds = use_bm ? (size_t(2) * KP + (K + 31) / 32) * 4 : 0;
+    const size_t xlds = use_bm ? (size_t(2) * KP + (K + 15) / 16) * 4 : 0;
     // One set of launch buffers: the rule descriptors (pinned stage + device copy, one
     // H2D copy per launch), the per-slot control blocks, the histograms (list path:
     // per-slot HBM arrays; bitmap path: per-block partial rows) and the results (mapped
     // pinned host memory, at most ecap records per slot).
     struct ExpSet {
-        DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part;
+        DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part, dom;
         std::unique_ptr<PinnedBuf> stage, pin;
         Side* h_sides = nullptr;
         uint64_t *h_drv = nullptr, *h_wave = nullptr;
@@ -1428,9 +1489,9 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     struct Seg {
         double ms = 0;  // over the timed launches
         int64_t n = 0, timed = 0, bytes = 0;
-    } seg[3];  // expansion, reduce / collect, k_dl / k_publish
-    const char* seg_name[3] = {use_bm ? "k_expand_bm" : "k_expand", use_bm ? "k_expand_reduce" : "k_expand_collect",
-                               use_bm ? "k_dl" : "k_publish"};
+    } seg[4];  // bitmap path: domain, rows, reduce, k_dl; list path: expansion, -, collect, k_publish
+    const char* seg_name[4] = {use_bm ? "k_exp_domain" : "k_expand", use_bm ? "k_exp_rows" : "",
+                               use_bm ? "k_expand_reduce" : "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
     for (hipEvent_t& e : ctx->ev)
         if (!e) FSM_HIP(hipEventCreate(&e));
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
@@ -1457,10 +1518,15 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             std::copy(rx, rx + r->nx, sd.X);
             std::copy(ry, ry + r->ny, sd.Y);
             if (use_bm) {
-                // bitmap path: blocks sized by the expected domain (about twice the rule's
-                // support: sids holding X u Y in either order), exp_spb sids per block
+                // bitmap path: row blocks sized by the expected domain (about twice the rule's
+                // support: sids holding X u Y in either order), exp_spb sids per block; the
+                // domain list holds at most the support of the rarest item of X u Y
                 wave_off[k + 1] = wave_off[k] + std::clamp<uint64_t>((2ull * r->sup + exp_spb - 1) / exp_spb, 1,
                                                                      grid.expand);
+                uint32_t cap = kNone;
+                for (uint32_t q = 0; q < r->nx; ++q) cap = std::min(cap, sup[rx[q]]);
+                for (uint32_t q = 0; q < r->ny; ++q) cap = std::min(cap, sup[ry[q]]);
+                drv_off[k + 1] = drv_off[k] + cap;
             } else {
                 // list path: one wave per sid of the driver list: the rarest item of X
                 // (expandL needs all of sids(X)), else of X u Y
@@ -1484,6 +1550,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 wave_off[k + 1] = wave_off[k] + std::max<uint64_t>(1, n0 * (max_blocks - nb) / tot);
             }
         }
+        if (use_bm && x.dom.bytes < drv_off[nb] * sizeof(uint2))
+            x.dom.alloc(std::max<uint64_t>(drv_off[nb] * sizeof(uint2) * 5 / 4, uint64_t(1) << 20));
         std::memcpy(x.h_sides, sides.data(), nb * sizeof(Side));
         std::memcpy(x.h_drv, drv_off.data(), (nb + 1) * 8);
         std::memcpy(x.h_wave, wave_off.data(), (nb + 1) * 8);
@@ -1491,24 +1559,29 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
         const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
         if (use_bm && alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
-            hipLaunchKernelGGL(k_alive, dim3(unsigned(((K + 31) / 32 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+            hipLaunchKernelGGL(k_alive, dim3(unsigned(((K + 15) / 16 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                                d_ksup.as<uint32_t>(), K, rp.minsup, d_alive.as<uint32_t>());
             FSM_LAUNCHED("k_alive", s);
             alive_t = rp.minsup;
         }
         if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[0], s));
         if (use_bm) {
-            hipLaunchKernelGGL(k_expand_bm, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
-                               x.d_wave, nb, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), k_ent.as<uint2>(),
-                               d_kidof.as<uint32_t>(), d_alive.as<uint32_t>(), geo, x.part.as<uint32_t>(),
-                               x.ctl.as<ExpCtl>(), x.d_ndlw.as<uint32_t>());
-            FSM_LAUNCHED("k_expand_bm", s);
+            hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads), 0, s,
+                               x.d_sides, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), x.d_drv,
+                               x.dom.as<uint2>(), x.ctl.as<ExpCtl>());
+            FSM_LAUNCHED("k_exp_domain", s);
             if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
+            hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
+                               x.d_wave, nb, x.d_drv, x.dom.as<uint2>(), k_ent.as<uint2>(), d_kidof.as<uint32_t>(),
+                               d_alive.as<uint32_t>(), geo, x.part.as<uint32_t>(), x.ctl.as<ExpCtl>(),
+                               x.d_ndlw.as<uint32_t>());
+            FSM_LAUNCHED("k_exp_rows", s);
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
             hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
                                x.d_wave, geo, d_kept.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_rec, ecap,
                                x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>());
             FSM_LAUNCHED("k_expand_reduce", s);
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
             hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
                                d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), x.d_dlw.as<uint4>(),
                                x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
@@ -1525,22 +1598,23 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 FSM_LAUNCHED("k_expand", s);
             }
             if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
             hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, x.TL.as<uint32_t>(),
                                x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
                                x.ctl.as<ExpCtl>(), U, rp.minsup, x.d_rec, ecap);
             FSM_LAUNCHED("k_expand_collect", s);
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
+            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
             hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
             FSM_LAUNCHED("k_publish", s);
         }
-        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
+        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[4], s));
         const double tw0 = now_ms();
         prep_ms += tw0 - tl0;
         FSM_HIP(hipStreamSynchronize(s));
         const double tw1 = now_ms();
         wait_ms += tw1 - tw0;
         ++launches;
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < 4; ++q) {
             float ms = 0;
             if (x.timed && hipEventElapsedTime(&ms, ctx->ev[q], ctx->ev[q + 1]) == hipSuccess) {
                 seg[q].ms += ms;
@@ -1548,17 +1622,23 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             }
             seg[q].n += 1;
         }
-        if (use_bm) exp_part_bytes += int64_t(wave_off[nb] * row_bytes);
+        if (use_bm) {
+            exp_part_bytes += int64_t(wave_off[nb] * row_bytes);
+            seg[1].bytes += int64_t(wave_off[nb] * row_bytes);  // the partial rows the row kernel writes
+        }
         uint64_t nout_all = 0;
         for (uint32_t k = 0; k < nb; ++k) {
             const ExpHdr h = x.h_hdr[k];
             nout_all += h.nout;
-            if (use_bm) {  // algorithmic bytes: the |X|+|Y| bitmap operands + the domain's row entries
+            if (use_bm) {
+                // algorithmic bytes: domain = the |X|+|Y| bitmap operands + 8 B row bounds read
+                // and 8 B written per domain sid; rows = the domain list + 8 B per row entry
                 const uint64_t bmb = uint64_t(batch[k]->nx + batch[k]->ny) * d->NW * 4;
                 exp_domain += h.nsid;
                 exp_entries += h.nent;
                 exp_bitmap_bytes += int64_t(bmb);
-                seg[0].bytes += int64_t(bmb + 8ull * h.nent + 8ull * h.nsid);
+                seg[0].bytes += int64_t(bmb + 16ull * h.nsid);
+                seg[1].bytes += int64_t(8ull * h.nent + 8ull * h.nsid);
             }
             if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
             if (!use_bm && x.drv_in_x[k] && h.nx != batch[k]->nX)
@@ -1569,7 +1649,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             res.recs.assign(rec, rec + h.nout);
             std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
         }
-        seg[1].bytes += int64_t(nout_all * sizeof(ExpRec));
+        seg[2].bytes += int64_t(nout_all * sizeof(ExpRec));
         x.timed = false;
         post_ms += now_ms() - tw1;
     };
@@ -1772,7 +1852,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         o->cons_off[q + 1] = o->cons_off[q] + int64_t(r->ny);
     }
     ctx->kstats.clear();
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < 4; ++q) {
+        if (!seg_name[q][0]) continue;
         fsm_kernel_stat k{};
         std::snprintf(k.name, sizeof(k.name), "%s", seg_name[q]);
         k.launches = seg[q].n;
