@@ -360,7 +360,7 @@ static oracle_patterns* build_patterns(const nodevec* nodes) {
     return p;
 }
 
-static int spade_core(regvec* regs, int64_t n, double support, double time_limit_s, int nthreads,
+static int spade_core(regvec* regs, int64_t n, double support, double time_limit_s, int nthreads, int64_t stride,
                       oracle_patterns** out, char* err, int errlen);
 
 int oracle_spade(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
@@ -381,7 +381,7 @@ int oracle_spade(const int32_t* sids, const char* const* lines, const int64_t* l
             goto done;
         }
     }
-    rc = spade_core(&regs, n, support, 0.0, 1, out, err, errlen);
+    rc = spade_core(&regs, n, support, 0.0, 1, 1, out, err, errlen);
 done:
     VFREE(regs);
     VFREE(toks);
@@ -402,8 +402,14 @@ int oracle_spade_tokens(const int64_t* seq_off, const int64_t* tokens, int64_t n
  * schedule, one class per grab).  Each class's nodes are renumbered after the
  * root nodes in class order, so a complete run returns exactly the pattern
  * list of the sequential DFS. */
-int oracle_spade_tokens_mt(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
-                           double time_limit_s, int nthreads, oracle_patterns** out, char* err, int errlen) {
+/* Class-stride sample (bench.py's CPU baseline): only the first-level classes
+ * [x] with rank(x) % stride == 0 are mined (their root joins and their whole
+ * subtrees), so the joins/s of a bounded run is an unbiased sample of every
+ * depth of the lattice rather than its first classes only.  stride 1 = the
+ * complete mine. */
+int oracle_spade_tokens_sample(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
+                               double time_limit_s, int nthreads, int64_t stride, oracle_patterns** out, char* err,
+                               int errlen) {
     *out = NULL;
     regvec regs = {0};
     for (int64_t r = 0; r < n; r++) {
@@ -419,16 +425,22 @@ int oracle_spade_tokens_mt(const int64_t* seq_off, const int64_t* tokens, int64_
             VPUSH(regs, rg);
         }
     }
-    int rc = spade_core(&regs, n, support, time_limit_s, nthreads < 1 ? 1 : nthreads, out, err, errlen);
+    int rc = spade_core(&regs, n, support, time_limit_s, nthreads < 1 ? 1 : nthreads, stride < 1 ? 1 : stride, out,
+                        err, errlen);
     VFREE(regs);
     return rc;
+}
+
+int oracle_spade_tokens_mt(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
+                           double time_limit_s, int nthreads, oracle_patterns** out, char* err, int errlen) {
+    return oracle_spade_tokens_sample(seq_off, tokens, n, support, time_limit_s, nthreads, 1, out, err, errlen);
 }
 
 /* Top level of process_class with one OpenMP task per first-level class.
  * Task i owns a private ctx whose node table starts with copies of the root
  * nodes (so parents < nroot are root nodes), then the merge appends each
  * task's own nodes in i order, remapping parents. */
-static void process_root_mt(spade_ctx* c, member* m, int64_t n, int nthreads) {
+static void process_root_mt(spade_ctx* c, member* m, int64_t n, int nthreads, int64_t stride) {
     const int64_t nroot = c->nodes.n;
     spade_ctx* tc = calloc((size_t)(n ? n : 1), sizeof(spade_ctx));
     volatile int stop = 0;
@@ -439,6 +451,7 @@ static void process_root_mt(spade_ctx* c, member* m, int64_t n, int nthreads) {
         t->minsup = c->minsup;
         t->deadline = c->deadline;
         if (stop) { t->stopped = 1; continue; }
+        if (i % stride != 0) continue;  /* class-stride sample */
         for (int64_t k = 0; k < nroot; k++) VPUSH(t->nodes, c->nodes.a[k]);
         membervec child = {0};
         for (int64_t j = 0; j < n; j++) {  /* root members are all SEQ (P = {}) */
@@ -465,7 +478,7 @@ static void process_root_mt(spade_ctx* c, member* m, int64_t n, int nthreads) {
     free(tc);
 }
 
-static int spade_core(regvec* regsp, int64_t n, double support, double time_limit_s, int nthreads,
+static int spade_core(regvec* regsp, int64_t n, double support, double time_limit_s, int nthreads, int64_t stride,
                       oracle_patterns** out, char* err, int errlen) {
     regvec regs = *regsp;
     int rc = 0;
@@ -557,7 +570,7 @@ static int spade_core(regvec* regsp, int64_t n, double support, double time_limi
         }
         free(vert);
         const double t_f1 = mono_s() - t_start;
-        if (nthreads > 1) process_root_mt(&c, root.a, root.n, nthreads);
+        if (nthreads > 1 || stride > 1) process_root_mt(&c, root.a, root.n, nthreads, stride);
         else process_class(&c, root.a, root.n);
         for (int64_t k = 0; k < root.n; k++) ilist_free(&root.a[k].L);
         VFREE(root);

@@ -69,6 +69,10 @@ int oracle_spade_tokens(const int64_t* seq_off, const int64_t* tokens, int64_t n
 /* Same, first-level classes mined by nthreads OpenMP threads (CPU baseline mode ii). */
 int oracle_spade_tokens_mt(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
                            double time_limit_s, int nthreads, oracle_patterns** out, char* err, int errlen);
+/* only the first-level classes of rank % stride == 0 (bench.py's sampled CPU baseline) */
+int oracle_spade_tokens_sample(const int64_t* seq_off, const int64_t* tokens, int64_t n, double support,
+                               double time_limit_s, int nthreads, int64_t stride, oracle_patterns** out, char* err,
+                               int errlen);
 
 int oracle_tsr(const int32_t* sids, const char* const* lines, const int64_t* lens, int64_t n,
                int32_t k, double minconf, oracle_rules** out, char* err, int errlen);

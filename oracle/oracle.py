@@ -85,6 +85,10 @@ def lib():
                                              ctypes.c_int, ctypes.POINTER(ctypes.POINTER(_Patterns)),
                                              ctypes.c_char_p, ctypes.c_int]
         L.oracle_spade_tokens_mt.restype = ctypes.c_int
+        L.oracle_spade_tokens_sample.argtypes = [I64P, I64P, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                                 ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.POINTER(_Patterns)),
+                                                 ctypes.c_char_p, ctypes.c_int]
+        L.oracle_spade_tokens_sample.restype = ctypes.c_int
         L.oracle_pattern_support.argtypes = [I64P, I64P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                              I64P, ctypes.c_int64]
         L.oracle_pattern_support.restype = ctypes.c_int64
@@ -134,18 +138,19 @@ def _np64(a):
     return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
 
-def spade_tokens(seq_off, tokens, support, time_limit_s=0.0, want_patterns=True, threads=1):
+def spade_tokens(seq_off, tokens, support, time_limit_s=0.0, want_patterns=True, threads=1, stride=1):
     """Token-stream SPADE (sid = record index).  With time_limit_s > 0 the
-    lattice stops after that long: returns joins done and seconds (the
-    bounded CPU-baseline sample used by bench.py).  threads > 1 mines the
-    first-level classes on that many OpenMP threads (SURVEY §8d mode ii)."""
+    lattice stops after that long: returns joins done and seconds.  threads > 1
+    mines the first-level classes on that many OpenMP threads (SURVEY §8d mode
+    ii).  stride > 1 mines only the first-level classes of rank % stride == 0
+    (a class-stride sample of the whole lattice: bench.py's CPU baseline)."""
     L = lib()
     so, so_p = _np64(seq_off)
     tk, tk_p = _np64(tokens)
     out = ctypes.POINTER(_Patterns)()
     err = ctypes.create_string_buffer(512)
-    rc = L.oracle_spade_tokens_mt(so_p, tk_p, len(so) - 1, float(support), float(time_limit_s), int(threads),
-                                  ctypes.byref(out), err, 512)
+    rc = L.oracle_spade_tokens_sample(so_p, tk_p, len(so) - 1, float(support), float(time_limit_s), int(threads),
+                                      int(stride), ctypes.byref(out), err, 512)
     if rc != 0:
         raise OracleError(err.value.decode())
     p = out.contents

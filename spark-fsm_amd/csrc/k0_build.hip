@@ -13,7 +13,10 @@
 // strictly increasing, rows of more than 8192 tokens, item ranges over 2^27,
 // and every input the reference rejects, so the host reports the exact error).
 //
-//   k0_minmax     item-value range, int32 range check, TSR item presence
+//   staging       the int64 token stream narrowed to int32 on host threads into
+//                 pinned double-buffered chunks (DMA of one chunk overlaps the
+//                 narrowing of the next), with the item-value range, the int32
+//                 range check and TSR item presence computed on the way
 //   k0_rows       one wave per row of <= 64 tokens, pass 1 (count) and pass 2
 //                 (write): itemset index by ballot prefix counts, eids, the
 //                 (value, eid) pairs sorted across the wave (bitonic, shuffles),
@@ -25,12 +28,14 @@
 //   dictionary    presence bitmap -> word popcount scan -> dense ids (rank of
 //                 the value) and the ascending value table
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
 
 #include "dev_db.h"
 #include "device_util.h"
+#include "host_pool.h"
 
 namespace fsm {
 namespace {
@@ -59,36 +64,6 @@ __device__ __forceinline__ uint64_t lanemask_le() {
     return l == 63 ? ~0ull : ((2ull << l) - 1ull);
 }
 
-__global__ __launch_bounds__(256) void k0_minmax(const int64_t* __restrict__ tok, uint64_t T,
-                                                 K0Range* __restrict__ out) {
-    int32_t lo = INT32_MAX, hi = INT32_MIN;
-    uint32_t bad = 0, nonneg = 0;
-    for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < T; t += uint64_t(gridDim.x) * blockDim.x) {
-        const int64_t v = tok[t];
-        if (v == -1 || v == -2) continue;
-        if (v < INT32_MIN || v > INT32_MAX) {
-            bad = 1;
-            continue;
-        }
-        lo = min(lo, int32_t(v));
-        hi = max(hi, int32_t(v));
-        nonneg |= v > -1 ? 1u : 0u;
-    }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        lo = min(lo, __shfl_xor(lo, d, 64));
-        hi = max(hi, __shfl_xor(hi, d, 64));
-    }
-    bad = __ballot(bad != 0) ? 1u : 0u;
-    nonneg = __ballot(nonneg != 0) ? 1u : 0u;
-    if (lane_id() == 0) {
-        if (lo != INT32_MAX) atomicMin(&out->vmin, lo);
-        if (hi != INT32_MIN) atomicMax(&out->vmax, hi);
-        if (bad) atomicOr(&out->bad, 1u);
-        if (nonneg) atomicOr(&out->any_nonneg, 1u);
-    }
-}
-
 // dense id of an item value: its rank among the present values
 __device__ __forceinline__ uint32_t value_rank(int32_t v, int32_t vmin, const uint32_t* __restrict__ bm,
                                                const uint64_t* __restrict__ wpre) {
@@ -109,7 +84,7 @@ struct K0Out {  // pass 2 destinations
 
 // One wave, one row of L <= 64 tokens.
 template <int kMode, bool kWrite>
-__device__ __forceinline__ void k0_wave_row(const int64_t* __restrict__ tok, uint64_t t0, uint32_t L, uint32_t r,
+__device__ __forceinline__ void k0_wave_row(const int32_t* __restrict__ tok, uint64_t t0, uint32_t L, uint32_t r,
                                             int32_t vmin, uint32_t* __restrict__ cnt, uint32_t* lbm, uint32_t* gbm,
                                             K0Stats& st, const K0Out& o) {
     const uint32_t lane = lane_id();
@@ -202,7 +177,7 @@ __device__ __forceinline__ void k0_wave_row(const int64_t* __restrict__ tok, uin
 // are left to k0_long.  Pass 1 keeps the presence bitmap in LDS when it fits.
 template <int kMode, bool kWrite>
 __global__ __launch_bounds__(kK0Threads) void k0_rows(const uint64_t* __restrict__ so, uint32_t n,
-                                                      const int64_t* __restrict__ tok, int32_t vmin, uint32_t nw,
+                                                      const int32_t* __restrict__ tok, int32_t vmin, uint32_t nw,
                                                       uint32_t* __restrict__ cnt, uint32_t* __restrict__ gbm,
                                                       K0Stats* __restrict__ gst, K0Out o) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lbm_s[];
@@ -263,7 +238,7 @@ __device__ uint32_t block_excl_scan(uint32_t* a, uint32_t n, uint32_t* wtot) {
 // One block per row of 65..8192 tokens (rows listed by the host).
 template <int kMode, bool kWrite>
 __global__ __launch_bounds__(kK0LongThreads) void k0_long(const uint32_t* __restrict__ rows, const uint64_t* __restrict__ so,
-                                                          const int64_t* __restrict__ tok, int32_t vmin,
+                                                          const int32_t* __restrict__ tok, int32_t vmin,
                                                           uint32_t* __restrict__ cnt, uint32_t* __restrict__ gbm,
                                                           K0Stats* __restrict__ gst, K0Out o) {
     __shared__ uint64_t key[kK0Long];  // the tokens, then (in place) the pairs' sort keys
@@ -411,6 +386,72 @@ bool k0_disabled() {
     return v && !std::strcmp(v, "host");
 }
 
+// The row offsets and the token stream (int64, T tokens from seq_off[0],
+// narrowed to int32) staged on the host pool through a ring of two pinned
+// context slots of kStageBytes and DMA'd (the filling of one chunk overlaps the
+// DMA of the other; the slots stay allocated for the context's lifetime).  The
+// value range, an out-of-int32 token (bad) and TSR's "some token > -1" are
+// gathered by the narrowing (branch-free, vectorizable).  Returns after the
+// last copy.  Measured on MI355X (tools/micro/): pinned H2D 47-53 GB/s, pinned
+// allocation about 0.12 ms per MiB, and a first pageable copy of the caller's
+// arrays about 1 GB/s, so everything goes through the small pinned ring.
+constexpr uint64_t kStageBytes = uint64_t(4) << 20;
+
+K0Range k0_stage(fsm_ctx* ctx, const Source& src, int64_t n, uint64_t T, DevBuf& d_so, DevBuf& d_tok) {
+    const char* ev = std::getenv("FSM_K0_THREADS");  // tuning
+    const int64_t nthr = ev ? std::clamp<int64_t>(std::atoll(ev), 1, 64) : host_threads();
+    const double ts0 = now_ms();
+    int k = 0;  // chunks staged so far (ring position)
+    // fill(h, a, m): write elements [a, a + m) of a stream into pinned h (per host thread)
+    auto stream = [&](char* dst, uint64_t nel, uint32_t esz, auto&& fill) {
+        const uint64_t per = kStageBytes / esz;
+        for (uint64_t a = 0; a < nel; a += per, ++k) {
+            const uint64_t m = std::min<uint64_t>(per, nel - a);
+            const int slot = 2 + (k & 1);
+            char* h = static_cast<char*>(ctx->stage_host(slot, kStageBytes));
+            par_slices(m >= (uint64_t(1) << 15) ? nthr : 1, int64_t(m),
+                       [&](int64_t t, int64_t i0, int64_t i1) { fill(t, h, a, uint64_t(i0), uint64_t(i1)); });
+            ctx->stage_copy(slot, dst + a * esz, m * esz);
+        }
+    };
+    stream(static_cast<char*>(d_so.p), uint64_t(n + 1), 8, [&](int64_t, char* h, uint64_t a, uint64_t i0, uint64_t i1) {
+        std::memcpy(h + i0 * 8, src.seq_off + a + i0, (i1 - i0) * 8);
+    });
+    const int64_t* tok = src.tokens + src.seq_off[0];
+    std::vector<int64_t> lo(static_cast<size_t>(nthr), INT64_MAX), hi(static_cast<size_t>(nthr), INT64_MIN);
+    stream(static_cast<char*>(d_tok.p), T, 4, [&](int64_t t, char* h, uint64_t a, uint64_t i0, uint64_t i1) {
+        int32_t* o = reinterpret_cast<int32_t*>(h);
+        const int64_t* in = tok + a;
+        int64_t l = lo[size_t(t)], u = hi[size_t(t)];
+        for (uint64_t i = i0; i < i1; ++i) {
+            const int64_t v = in[i];
+            o[i] = int32_t(v);
+            const bool sep = uint64_t(v + 2) < 2u;  // -2 or -1
+            l = std::min(l, sep ? INT64_MAX : v);
+            u = std::max(u, sep ? INT64_MIN : v);
+        }
+        lo[size_t(t)] = l;
+        hi[size_t(t)] = u;
+    });
+    const double tf = now_ms();
+    FSM_HIP(hipStreamSynchronize(ctx->stream));
+    int64_t l = INT64_MAX, u = INT64_MIN;
+    for (int64_t t = 0; t < nthr; ++t) {
+        l = std::min(l, lo[size_t(t)]);
+        u = std::max(u, hi[size_t(t)]);
+    }
+    K0Range rng{INT32_MAX, INT32_MIN, 0, 0};
+    if (l <= u) {  // some item token
+        rng.bad = l < INT32_MIN || u > INT32_MAX;
+        rng.vmin = int32_t(std::max<int64_t>(l, INT32_MIN));
+        rng.vmax = int32_t(std::min<int64_t>(u, INT32_MAX));
+        rng.any_nonneg = u > -1;
+    }
+    if (const char* v = std::getenv("FSM_HOST_TRACE"); v && v[0] == '1')
+        std::fprintf(stderr, "[fsm k0] staging: %d chunks in %.2f ms, final sync %.2f ms\n", k, tf - ts0, now_ms() - tf);
+    return rng;
+}
+
 }  // namespace
 
 bool k0_build(fsm_ctx* ctx, int mode, const Source& src, fsm_db* db) {
@@ -419,31 +460,34 @@ bool k0_build(fsm_ctx* ctx, int mode, const Source& src, fsm_db* db) {
     if (n >= int64_t(UINT32_MAX)) return false;
     const double t0 = now_ms();
     // host checks (the reference's errors and the merged-sid case go to the host flatten)
+    // (rows checked over the host pool; the long rows collected in row order)
+    const int64_t nthr = n >= (int64_t(1) << 16) ? host_threads() : 1;
+    std::vector<std::vector<uint32_t>> lr(static_cast<size_t>(nthr));
+    std::vector<uint8_t> ok(static_cast<size_t>(nthr), 1);
+    par_slices(nthr, n, [&](int64_t t, int64_t a, int64_t z) {
+        for (int64_t r = a; r < z; ++r) {
+            const bool bad_sid = mode == FSM_MODE_SPADE ? (src.sids[r] < 0 || (r > 0 && src.sids[r] <= src.sids[r - 1]))
+                                                        : src.sids[r] != int32_t(r);
+            const int64_t L = src.seq_off[r + 1] - src.seq_off[r];
+            if (bad_sid || L < 0 || L > int64_t(kK0Long)) {
+                ok[size_t(t)] = 0;
+                return;
+            }
+            if (L > int64_t(kK0Wave)) lr[size_t(t)].push_back(uint32_t(r));
+        }
+    });
     std::vector<uint32_t> longrows;
-    for (int64_t r = 0; r < n; ++r) {
-        if (mode == FSM_MODE_SPADE ? (src.sids[r] < 0 || (r > 0 && src.sids[r] <= src.sids[r - 1]))
-                                   : src.sids[r] != int32_t(r))
-            return false;
-        const int64_t L = src.seq_off[r + 1] - src.seq_off[r];
-        if (L < 0 || L > int64_t(kK0Long)) return false;
-        if (L > int64_t(kK0Wave)) longrows.push_back(uint32_t(r));
+    for (int64_t t = 0; t < nthr; ++t) {
+        if (!ok[size_t(t)]) return false;
+        longrows.insert(longrows.end(), lr[size_t(t)].begin(), lr[size_t(t)].end());
     }
+    const double t_val = now_ms();
     hipStream_t s = ctx->stream;
     const uint64_t T = uint64_t(src.seq_off[n] - src.seq_off[0]);
-    DevBuf d_so(size_t(n + 1) * 8), d_tok(std::max<uint64_t>(T, 1) * 8), d_rng(sizeof(K0Range));
-    FSM_HIP(hipMemcpyAsync(d_so.p, src.seq_off, size_t(n + 1) * 8, hipMemcpyHostToDevice, s));
-    if (T) FSM_HIP(hipMemcpyAsync(d_tok.p, src.tokens + src.seq_off[0], T * 8, hipMemcpyHostToDevice, s));
-    FSM_HIP(hipStreamSynchronize(s));
+    DevBuf d_so(size_t(n + 1) * 8), d_tok(std::max<uint64_t>(T, 1) * 4);
+    const double t_alloc = now_ms();
+    const K0Range rng = k0_stage(ctx, src, n, T, d_so, d_tok);
     const double t_up = now_ms();
-    K0Range rng{INT32_MAX, INT32_MIN, 0, 0};
-    FSM_HIP(hipMemcpyAsync(d_rng.p, &rng, sizeof(rng), hipMemcpyHostToDevice, s));
-    if (T) {
-        const unsigned g = unsigned(std::min<uint64_t>((T + 255) / 256, 4096));
-        hipLaunchKernelGGL(k0_minmax, dim3(g), dim3(256), 0, s, d_tok.as<int64_t>(), T, d_rng.as<K0Range>());
-        FSM_LAUNCHED("k0_minmax", s);
-    }
-    FSM_HIP(hipMemcpyAsync(&rng, d_rng.p, sizeof(rng), hipMemcpyDeviceToHost, s));
-    FSM_HIP(hipStreamSynchronize(s));
     if (rng.bad) return false;                                       // host reports the bad token
     if (mode == FSM_MODE_TSR && !rng.any_nonneg) return false;      // "no items" error on the host
     const bool any_item = rng.vmin <= rng.vmax;
@@ -463,12 +507,12 @@ bool k0_build(fsm_ctx* ctx, int mode, const Source& src, fsm_db* db) {
 #define K0_PASS(MODE, WR)                                                                                         \
     do {                                                                                                          \
         hipLaunchKernelGGL((k0_rows<MODE, WR>), dim3(grid_rows), dim3(kK0Threads), WR ? 0 : lds, s,               \
-                           d_so.as<uint64_t>(), uint32_t(n), d_tok.as<int64_t>(), vmin, nw, d_cnt.as<uint32_t>(), \
+                           d_so.as<uint64_t>(), uint32_t(n), d_tok.as<int32_t>(), vmin, nw, d_cnt.as<uint32_t>(), \
                            d_bm.as<uint32_t>(), d_st.as<K0Stats>(), o);                                           \
         FSM_LAUNCHED("k0_rows", s);                                                                               \
         if (!longrows.empty()) {                                                                                  \
             hipLaunchKernelGGL((k0_long<MODE, WR>), dim3(unsigned(longrows.size())), dim3(kK0LongThreads), 0, s,  \
-                               d_long.as<uint32_t>(), d_so.as<uint64_t>(), d_tok.as<int64_t>(), vmin,            \
+                               d_long.as<uint32_t>(), d_so.as<uint64_t>(), d_tok.as<int32_t>(), vmin,            \
                                d_cnt.as<uint32_t>(), d_bm.as<uint32_t>(), d_st.as<K0Stats>(), o);                 \
             FSM_LAUNCHED("k0_long", s);                                                                           \
         }                                                                                                         \
@@ -558,6 +602,9 @@ bool k0_build(fsm_ctx* ctx, int mode, const Source& src, fsm_db* db) {
 #undef K0_PASS
     ctx->stats.ms_upload = t_up - t0;
     ctx->stats.ms_flatten = now_ms() - t_up;
+    if (const char* v = std::getenv("FSM_HOST_TRACE"); v && v[0] == '1')
+        std::fprintf(stderr, "[fsm k0] rows checked %.2f ms, device allocation %.2f ms, tokens staged + uploaded %.2f ms, "
+                     "device build %.2f ms\n", t_val - t0, t_alloc - t_val, t_up - t_alloc, ctx->stats.ms_flatten);
     ctx->stats.k0_device = 1;
     return true;
 }

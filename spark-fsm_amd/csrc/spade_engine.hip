@@ -44,6 +44,7 @@
 #include "comm.h"
 #include "dev_db.h"
 #include "device_util.h"
+#include "host_pool.h"
 
 
 namespace fsm {
@@ -993,7 +994,8 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
                                                   const uint32_t* __restrict__ kid_cid,
                                                   const uint32_t* __restrict__ child_of,
                                                   unsigned long long* __restrict__ cursor, SlabPtrs o,
-                                                  uint64_t cap, uint32_t rcap, uint32_t wd) {
+                                                  uint64_t cap, uint32_t rcap, uint32_t wd,
+                                                  const uint32_t* __restrict__ runs, const uint32_t* __restrict__ nruns) {
     constexpr uint32_t kWaves = kEmitBlock / 64;
     constexpr uint32_t kPer = 64 * kEmitRounds;  // entries of one wave per chunk
     __shared__ uint32_t r_f[kWaves][kEmitCap], r_q[kWaves][kEmitCap], r_ek[kWaves][kEmitCap];
@@ -1002,11 +1004,17 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
     __shared__ unsigned long long b_base;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
-    for (uint64_t c0 = uint64_t(blockIdx.x) * chunk; c0 < E; c0 += uint64_t(gridDim.x) * chunk) {
+    // segments: the whole batch [0, E), or (runs != nullptr) each listed run, one block per run
+    const uint32_t nseg = runs ? *nruns : 1u;
+    for (uint32_t sg = runs ? blockIdx.x : 0u; sg < nseg; sg += runs ? gridDim.x : nseg) {
+    const uint32_t sa = runs ? runs[sg] : 0u;
+    const uint32_t Ez = runs ? sa + (pos[sa] & 0xFFFFu) : E;  // segment end
+    for (uint64_t c0 = runs ? uint64_t(sa) : uint64_t(blockIdx.x) * chunk; c0 < Ez;
+         c0 += runs ? chunk : uint64_t(gridDim.x) * chunk) {
         uint32_t nrec = 0, wsum = 0;
         for (int r = 0; r < kEmitRounds; ++r) {
             const uint64_t w0 = c0 + uint64_t(r) * kEmitBlock + uint64_t(w) * 64;
-            const EmitEnt t = emit_ent(w0 + lane, E, cid, cls, mem, lohi, pos, kid_off, child_of);
+            const EmitEnt t = emit_ent(w0 + lane, Ez, cid, cls, mem, lohi, pos, kid_off, child_of);
             const uint32_t done = emit_pairs<W>(
                 t, w0, mem, lohi, mask, kid_slot, wd,
                 [&](bool ok, uint32_t ow, uint64_t, uint32_t, uint32_t q, uint32_t f, uint32_t, uint32_t k) {
@@ -1050,7 +1058,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
         } else {
             for (int r = 0; r < kEmitRounds; ++r) {
                 const uint64_t w0 = c0 + uint64_t(r) * kEmitBlock + uint64_t(w) * 64;
-                EmitEnt t = emit_ent(w0 + lane, E, cid, cls, mem, lohi, pos, kid_off, child_of);
+                EmitEnt t = emit_ent(w0 + lane, Ez, cid, cls, mem, lohi, pos, kid_off, child_of);
                 const uint32_t el = uint32_t(r) * 64u + lane;
                 const uint64_t base = wb + i_off[w][el];
                 const uint32_t n_run = i_n[w][el];
@@ -1066,6 +1074,200 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
                                                     mask, wd);
                               });
             }
+        }
+        __syncthreads();  // the LDS records are reused by the next chunk
+    }
+    }
+}
+
+// Window emission (W = 1).  k_emit1's partner lookups are dependent binary
+// searches in HBM (86 % of wave cycles waiting); here each wave
+// owns the runs STARTING in a 256-entry range of the batch and walks them in
+// windows of whole runs of at most 64 entries held in registers (one entry per
+// lane: member, lohi, mask).  An (entry, kid) pair finds its partner with a
+// fixed 6-step shuffle lower_bound over the owner's run and takes the
+// partner's lohi / mask by shuffle: no memory access between a kid's slot and
+// its join result.  Join records stay in per-wave LDS (as k_emit1), the block
+// reserves its child entries with one slab-cursor atomic per 1,024-entry chunk
+// and writes the runs; a wave whose records overflow joins again while writing.
+// Runs longer than 64 entries are appended to `longl` for k_emit1's run list.
+constexpr int kE2Block = 256;                   // 4 waves
+constexpr uint32_t kE2Waves = kE2Block / 64;
+constexpr uint32_t kE2Range = 256;              // entries per wave range (runs starting in it)
+constexpr uint32_t kE2Own = kE2Range + 64;      // owner slots per wave (a run may end 63 past the range)
+constexpr uint32_t kE2Cap = 384;                // LDS join records per wave
+
+__global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* __restrict__ cid,
+                                                    const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                    const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                                    const uint64_t* __restrict__ mask,
+                                                    const uint32_t* __restrict__ kid_off,
+                                                    const uint32_t* __restrict__ kid_slot,
+                                                    const uint32_t* __restrict__ kid_cid,
+                                                    const uint32_t* __restrict__ child_of,
+                                                    unsigned long long* __restrict__ cursor, SlabPtrs o, uint64_t cap,
+                                                    uint32_t rcap, uint32_t* __restrict__ longl,
+                                                    uint32_t* __restrict__ nlong) {
+    __shared__ uint32_t r_f[kE2Waves][kE2Cap], r_q[kE2Waves][kE2Cap], r_ek[kE2Waves][kE2Cap];
+    __shared__ uint32_t i_n[kE2Waves][kE2Own], i_off[kE2Waves][kE2Own], i_cc[kE2Waves][kE2Own], i_lt[kE2Waves][kE2Own];
+    __shared__ uint32_t w_tot[kE2Waves];
+    __shared__ unsigned long long b_base;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt();
+    constexpr uint32_t kChunkE = kE2Waves * kE2Range;
+    for (uint32_t c0 = blockIdx.x * kChunkE; c0 < E; c0 += gridDim.x * kChunkE) {
+        const uint32_t wa = c0 + w * kE2Range, wz = min(E, wa + kE2Range);
+        // the first run start in [wa, wz) (runs ending there started in an earlier range)
+        uint32_t ef = wz;
+        for (uint32_t b0 = wa; b0 < wz; b0 += 64) {
+            const uint32_t e = b0 + lane;
+            const uint64_t st = __ballot(e < wz && (pos[e] >> 16) == 0u);
+            if (st) {
+                ef = b0 + uint32_t(__ffsll((unsigned long long)st)) - 1u;
+                break;
+            }
+        }
+        for (uint32_t k = lane; k < kE2Own; k += 64) i_n[w][k] = 0;
+        uint32_t nrec = 0;
+        // the windows of whole runs [e0, e0 + cut); pass 0 records, pass 1 (overflow) writes
+        // at the bases in i_cc / i_n: on_ok(ok, f, q, owner slot, k)
+        auto walk = [&](auto&& on_ok, bool keep) {
+            for (uint32_t e0 = ef; e0 < wz;) {
+                const uint32_t e = e0 + lane;
+                const uint32_t p = e < E ? pos[e] : 0u;
+                const uint32_t len = p & 0xFFFFu;
+                const bool st = e < E && (p >> 16) == 0u;
+                // a run starting at lane s is in this window iff it starts in [e0, wz) and fits
+                const uint64_t bad = __ballot(st && (e >= wz || lane + len > 64u));
+                const uint64_t sts = __ballot(st);
+                uint32_t cut;
+                if (bad & 1ull) {  // lane 0 starts a run of more than 64 entries: k_emit1's list
+                    if (keep && lane == 0) longl[atomicAdd(nlong, 1u)] = e0;
+                    e0 += uint32_t(__shfl(int(len), 0, 64));
+                    continue;
+                }
+                if (bad) {
+                    cut = uint32_t(__ffsll((unsigned long long)bad)) - 1u;
+                } else {  // every start fits: the window ends with the last run
+                    const uint32_t ls = 63u - uint32_t(__clzll(sts));
+                    cut = ls + uint32_t(__shfl(int(len), int(ls), 64));
+                }
+                const bool in = lane < cut;
+                uint32_t mi = 0, lh = 0, cc = kNone, k0 = 0, nk = 0, lt2 = 0;
+                uint64_t mk = 0;
+                if (in) {
+                    mi = mem[e];
+                    lh = lohi[e];
+                    mk = mask[e];
+                    const DClass c = cls[cid[e]];
+                    cc = child_of[c.cbase + mi];
+                    if (cc != kNone) {
+                        k0 = kid_off[c.cbase + mi];
+                        nk = kid_off[c.cbase + mi + 1] - k0;
+                    }
+                    lt2 = (lh & 0xFFFFu) | ((mi & 1u) << 16);
+                }
+                const uint32_t rs = lane - (p >> 16), re = rs + len;  // the lane's run, as lanes
+                const uint32_t slot_own = e - ef;                     // owner slot of the wave
+                // (entry, kid) pairs flattened over the lanes: one pair per lane per step
+                const uint32_t incl = wave_incl_scan(nk), excl = incl - nk;
+                const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
+                uint32_t done = 0;
+                for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+                    const uint32_t pp = p0 + lane;
+                    uint32_t ow = 0;  // the owner lane: the largest lane whose first pair index <= pp
+#pragma unroll
+                    for (uint32_t stp = 32; stp > 0; stp >>= 1) {
+                        const uint32_t cand = ow + stp;
+                        if (uint32_t(__shfl(int(excl), int(cand), 64)) <= pp) ow = cand;
+                    }
+                    const uint32_t o_k0 = uint32_t(__shfl(int(k0), int(ow), 64));
+                    const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
+                    const uint32_t o_rs = uint32_t(__shfl(int(rs), int(ow), 64));
+                    const uint32_t o_re = uint32_t(__shfl(int(re), int(ow), 64));
+                    const uint32_t o_lt = uint32_t(__shfl(int(lt2), int(ow), 64));
+                    const uint32_t o_done = uint32_t(__shfl(int(done), int(ow), 64));
+                    const uint64_t o_mk = __shfl(mk, int(ow), 64);
+                    const bool live = pp < total;
+                    const uint32_t q = o_k0 + (pp - o_ex);
+                    const uint32_t slot = live ? kid_slot[q] : 0u;
+                    const uint32_t ct = slot & 1u;
+                    const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : (o_lt >> 16));  // partner member id
+                    // lower_bound of target in lanes [o_rs, o_re): 6 fixed steps
+                    uint32_t f = o_rs;
+#pragma unroll
+                    for (uint32_t stp = 32; stp > 0; stp >>= 1) {
+                        const uint32_t cand = f + stp;
+                        const uint32_t v = uint32_t(__shfl(int(mi), int(min(cand, 64u) - 1u), 64));
+                        if (cand <= o_re && v < target) f = cand;
+                    }
+                    const uint32_t fl = min(f, 63u);
+                    const uint32_t f_mi = uint32_t(__shfl(int(mi), int(fl), 64));
+                    const uint32_t f_lh = uint32_t(__shfl(int(lh), int(fl), 64));
+                    const uint64_t f_mk = __shfl(mk, int(fl), 64);
+                    bool ok = false;
+                    if (live && f < o_re && f_mi == target)
+                        ok = ct == kSeq ? (f_lh >> 16) > (o_lt & 0xFFFFu) : (o_mk & f_mk) != 0ull;
+                    const uint64_t succ = __ballot(ok);
+                    const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
+                    const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
+                    on_ok(ok, e0 + f, q, e0 + ow - ef, k);
+                    const uint32_t a = (excl > p0 ? excl : p0), bnd = (incl < p0 + 64 ? incl : p0 + 64);
+                    if (bnd > a) done += uint32_t(__popcll(succ & lane_range(a - p0, bnd - p0)));
+                }
+                if (keep && in) {
+                    i_n[w][slot_own] = done;
+                    i_cc[w][slot_own] = cc;
+                    i_lt[w][slot_own] = lt2;
+                }
+                e0 += cut;
+            }
+        };
+        walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k) {
+                 const uint64_t b = __ballot(ok);
+                 if (ok) {
+                     const uint32_t x = nrec + uint32_t(__popcll(b & lt));
+                     if (x < rcap) {
+                         r_f[w][x] = f;
+                         r_q[w][x] = q;
+                         r_ek[w][x] = (os << 16) | k;
+                     }
+                 }
+                 nrec += uint32_t(__popcll(b));
+             },
+             true);
+        // the wave's child run offsets (exclusive scan of i_n over its owner slots)
+        uint32_t wsum = 0;
+        for (uint32_t k0 = 0; k0 < kE2Own; k0 += 64) {
+            const uint32_t v = i_n[w][k0 + lane];
+            const uint32_t inc = wave_incl_scan(v);
+            i_off[w][k0 + lane] = wsum + inc - v;
+            wsum += uint32_t(__shfl(int(inc), 63, 64));
+        }
+        if (lane == 0) w_tot[w] = wsum;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+            for (uint32_t k = 0; k < kE2Waves; ++k) tot += w_tot[k];
+            b_base = tot ? atomicAdd(cursor, tot) : 0ull;
+        }
+        __syncthreads();
+        uint64_t wb = b_base;
+        for (uint32_t k = 0; k < w; ++k) wb += w_tot[k];
+        if (nrec <= rcap) {
+            for (uint32_t x = lane; x < nrec; x += 64) {
+                const uint32_t f = r_f[w][x], q = r_q[w][x], ek = r_ek[w][x];
+                const uint32_t os = ek >> 16, k = ek & 0xFFFFu;
+                emit_write<1>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
+                              i_lt[w][os], f, kid_slot[q], lohi, mask, 1u);
+            }
+        } else {  // the records overflowed: join again, writing at the run bases
+            walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k) {
+                     if (ok)
+                         emit_write<1>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
+                                       i_lt[w][os], f, kid_slot[q], lohi, mask, 1u);
+                 },
+                 false);
         }
         __syncthreads();  // the LDS records are reused by the next chunk
     }
@@ -1143,105 +1345,6 @@ template <class T, int kShift = 20> struct ChunkedVec {
     }
 };
 
-// A persistent pool of host threads for the per-batch bookkeeping (deep lattices
-// run dozens of parallel sections per mine: creating threads for each cost more
-// than the work).  One section at a time; a caller that finds the pool busy (a
-// concurrent mine on another context) runs its section inline.  Never destroyed:
-// the workers are detached and idle between sections.  A task that throws
-// (bad_alloc in a fill, FSM_ELIMIT) never unwinds past a running section: the
-// first exception is kept, the section drains (no worker is left inside the
-// caller's frame), then it is rethrown on the caller's thread.
-class HostPool {
-  public:
-    static HostPool& get() {
-        static HostPool* p = new HostPool();
-        return *p;
-    }
-    // fn(t) for t in [0, n): task 0 and any unclaimed ones on the caller, the rest on workers
-    bool run(int64_t n, const std::function<void(int64_t)>& fn) {
-        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
-        if (!busy.owns_lock()) return false;
-        while (int64_t(workers_) < n - 1) {
-            std::thread(&HostPool::work, this).detach();
-            ++workers_;
-        }
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            job_ = &fn;
-            n_ = n;
-            next_.store(1);
-            left_ = n;
-            ++gen_;
-        }
-        cv_.notify_all();
-        guarded(fn, 0);
-        for (int64_t t; (t = next_.fetch_add(1)) < n;) guarded(fn, t);
-        std::exception_ptr ex;
-        {
-            std::unique_lock<std::mutex> g(mu_);
-            // every worker that joined this section has left it before the next can start
-            done_cv_.wait(g, [&] { return left_ == 0 && active_ == 0; });
-            job_ = nullptr;
-            std::swap(ex, err_);
-        }
-        if (ex) std::rethrow_exception(ex);
-        return true;
-    }
-
-  private:
-    // one task: a throw is recorded (the first one wins) instead of unwinding
-    void guarded(const std::function<void(int64_t)>& fn, int64_t t) {
-        try {
-            fn(t);
-        } catch (...) {
-            std::lock_guard<std::mutex> g(mu_);
-            if (!err_) err_ = std::current_exception();
-        }
-        finish_one();
-    }
-    void finish_one() {
-        std::lock_guard<std::mutex> g(mu_);
-        if (--left_ == 0 && active_ == 0) done_cv_.notify_all();
-    }
-    void work() {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(int64_t)>* job;
-            int64_t n;
-            {
-                std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [&] { return gen_ != seen && job_ != nullptr; });
-                seen = gen_;
-                job = job_;
-                n = n_;
-                ++active_;
-            }
-            for (int64_t t; (t = next_.fetch_add(1)) < n;) guarded(*job, t);
-            std::lock_guard<std::mutex> g(mu_);
-            if (--active_ == 0 && left_ == 0) done_cv_.notify_all();
-        }
-    }
-    std::mutex run_mu_, mu_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(int64_t)>* job_ = nullptr;
-    std::exception_ptr err_;
-    int64_t n_ = 0, left_ = 0, active_ = 0;
-    uint64_t gen_ = 0;
-    std::atomic<int64_t> next_{0};
-    size_t workers_ = 0;
-};
-
-// fn(t, i0, i1) over nthr contiguous slices of [0, n) on the host pool
-template <class F> void par_slices(int64_t nthr, int64_t n, F&& fn) {
-    if (nthr <= 1) {
-        fn(int64_t(0), int64_t(0), n);
-        return;
-    }
-    const std::function<void(int64_t)> task = [&fn, nthr, n](int64_t t) { fn(t, n * t / nthr, n * (t + 1) / nthr); };
-    if (!HostPool::get().run(nthr, task))
-        for (int64_t t = 0; t < nthr; ++t) task(t);
-}
-int64_t host_threads() { return int64_t(std::clamp(std::thread::hardware_concurrency(), 1u, 16u)); }
 
 struct PNode {
     int32_t parent;
@@ -1573,6 +1676,16 @@ struct Miner {
         const char* v = std::getenv("FSM_SPLIT_FRAC");
         const double f = v ? std::atof(v) : 0.5;
         return f > 0.0 ? f : 1e300;
+    }
+    // FSM_EMIT_PATH=chunk forces k_emit1 for every batch (tests, A/B runs; default: k_emit2 at W = 1)
+    static bool emit_window() {
+        const char* v = std::getenv("FSM_EMIT_PATH");
+        return !(v && !std::strcmp(v, "chunk"));
+    }
+    // LDS join records per wave of k_emit2 (FSM_EMIT_CAP lowers it too: tests of the overflow path)
+    static uint32_t emit2_cap() {
+        const char* v = std::getenv("FSM_EMIT_CAP");
+        return v ? uint32_t(std::min<uint64_t>(std::strtoull(v, nullptr, 10), kE2Cap)) : kE2Cap;
     }
     // LDS join records per wave of k_emit1 (FSM_EMIT_CAP lowers it: tests of the overflow path)
     static uint32_t emit_cap() {
@@ -2178,25 +2291,45 @@ struct Miner {
         nb.slab.alloc(total, W);
         hp[5] += now_ms() - th2;
         nb.E = total;
-        DevBuf d_child_of;
+        DevBuf d_child_of, d_long;  // (freed into the stream-ordered pool: later launches on this stream reuse them)
         upload_staged(3, d_child_of, child_of.data(), child_of.size() * 4);
         ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
         if (b.E) {
             const SlabPtrs sp = b.slab.ptrs();
             const SlabPtrs op = nb.slab.ptrs();
-            DevBuf cursor(8);
+            DevBuf cursor(16);  // u64 slab cursor | u32 long-run count (k_emit2)
             FSM_HIP(hipMemsetAsync(cursor.p, 0, 8, s));
             const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
             const unsigned grid = unsigned(std::min<uint64_t>((b.E + chunk - 1) / chunk, emit_grid_cap()));
             const size_t tk = clk->begin("k_emit");
+            if (W == 1 && emit_window()) {
+                // windows of whole runs in registers; the runs of more than 64 entries go to
+                // k_emit1's run list (device-side count: no host round trip)
+                const uint64_t ce = uint64_t(kE2Waves) * kE2Range;
+                const unsigned g2 = unsigned(std::min<uint64_t>((b.E + ce - 1) / ce, emit_grid_cap()));
+                d_long.alloc(std::max<uint64_t>(b.E / 65 + 1, 1) * 4);
+                FSM_HIP(hipMemsetAsync(cursor.as<char>() + 8, 0, 4, s));
+                hipLaunchKernelGGL(k_emit2, dim3(g2), dim3(kE2Block), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),
+                                   sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,
+                                   d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap,
+                                   emit2_cap(), d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor.as<char>() + 8));
+                FSM_LAUNCHED("k_emit2", s);
+                hipLaunchKernelGGL(k_emit1<1>, dim3(256), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid,
+                                   b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,
+                                   b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,
+                                   nb.slab.cap, emit_cap(), 1u, d_long.as<uint32_t>(),
+                                   reinterpret_cast<const uint32_t*>(cursor.as<char>() + 8));
+                FSM_LAUNCHED("k_emit1", s);
+            } else {
 #define FSM_EMIT1(WW)                                                                                               \
     hipLaunchKernelGGL(k_emit1<WW>, dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),     \
                        sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                                         \
                        b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
-                       nb.slab.cap, emit_cap(), uint32_t(W))
-            FSM_W_DISPATCH(W, FSM_EMIT1)
+                       nb.slab.cap, emit_cap(), uint32_t(W), (const uint32_t*)nullptr, (const uint32_t*)nullptr)
+                FSM_W_DISPATCH(W, FSM_EMIT1)
 #undef FSM_EMIT1
-            FSM_LAUNCHED("k_emit", s);
+                FSM_LAUNCHED("k_emit", s);
+            }
             // reads every parent entry once, writes every child entry once
             clk->end(tk, int64_t(b.E * entry_bytes() + total * entry_bytes()));
             FSM_HIP(hipMemcpyAsync(&pend[0], cursor.p, 8, hipMemcpyDeviceToHost, s));

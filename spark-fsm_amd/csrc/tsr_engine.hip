@@ -906,6 +906,7 @@ struct Rule {
     uint32_t off = 0;  // X at pool[off], Y at pool[off + nx]
     uint16_t nx = 0, ny = 0;
     bool expandLR = false;
+    bool dropped = false;  // a speculated child its parent's commit did not register
 };
 
 struct RuleStore {
@@ -1420,10 +1421,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     const uint64_t part_budget = std::max<uint64_t>(part_mb << 20, uint64_t(B) * row_bytes);
     const uint64_t max_blocks = use_bm ? part_budget / row_bytes : 0;
     const size_t xlds = use_bm ? (size_t(2) * KP + (K + 15) / 16) * 4 : 0;
-    // One set of launch buffers: the rule descriptors (pinned stage + device copy, one
-    // H2D copy per launch), the per-slot control blocks, the histograms (list path:
-    // per-slot HBM arrays; bitmap path: per-block partial rows) and the results (mapped
-    // pinned host memory, at most ecap records per slot).
+    // Two sets of launch buffers, so the GPU runs one launch while the host commits
+    // the results of the previous one.  A set holds the rule descriptors (pinned
+    // stage + device copy, one H2D copy per launch), the per-slot control blocks,
+    // the histograms (list path: per-slot HBM arrays; bitmap path: per-block partial
+    // rows and the domain lists), the results (mapped pinned host memory, at most
+    // ecap records per slot) and its own events (completion, per-kernel timing).
     struct ExpSet {
         DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part, dom;
         std::unique_ptr<PinnedBuf> stage, pin;
@@ -1435,44 +1438,59 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         ExpRec *h_rec = nullptr, *d_rec = nullptr;
         std::vector<Rule*> batch;
         std::vector<char> drv_in_x;
-        bool timed = false;
-    } x;
-    x.ctl.alloc(B * sizeof(ExpCtl));
-    FSM_HIP(hipMemsetAsync(x.ctl.p, 0, B * sizeof(ExpCtl), s));
-    if (use_bm) {
-        x.part.alloc(max_blocks * row_bytes);
-        x.d_dlw.alloc(uint64_t(B) * ecap * sizeof(uint4));
-    } else {
-        x.TL.alloc(SU * 4);
-        x.DL.alloc(SU * 4);
-        x.TR.alloc(SU * 4);
-        x.seen.alloc(SU * 4);
-        x.list.alloc(SU * 4);
-        FSM_HIP(hipMemsetAsync(x.TL.p, 0, SU * 4, s));
-        FSM_HIP(hipMemsetAsync(x.DL.p, 0, SU * 4, s));
-        FSM_HIP(hipMemsetAsync(x.TR.p, 0, SU * 4, s));
-        FSM_HIP(hipMemsetAsync(x.seen.p, 0, SU * 4, s));
+        hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
+        bool timed = false, busy = false;
+        int depth = 0;        // speculation depth of the batch (0: heap batch)
+        int64_t seq = 0;      // launch number (the older busy set finishes first)
+        uint64_t blocks = 0;  // expansion blocks of the launch
+        ~ExpSet() {  // (unwinding: the launch may still be running on buffers about to be freed)
+            if (busy && ev[5]) (void)hipEventSynchronize(ev[5]);
+            for (hipEvent_t e : ev)
+                if (e) (void)hipEventDestroy(e);
+        }
+    } xs[2];
+    for (ExpSet& x : xs) {
+        x.ctl.alloc(B * sizeof(ExpCtl));
+        FSM_HIP(hipMemsetAsync(x.ctl.p, 0, B * sizeof(ExpCtl), s));
+        if (use_bm) {
+            x.part.alloc(max_blocks * row_bytes);
+            x.d_dlw.alloc(uint64_t(B) * ecap * sizeof(uint4));
+        } else {
+            x.TL.alloc(SU * 4);
+            x.DL.alloc(SU * 4);
+            x.TR.alloc(SU * 4);
+            x.seen.alloc(SU * 4);
+            x.list.alloc(SU * 4);
+            FSM_HIP(hipMemsetAsync(x.TL.p, 0, SU * 4, s));
+            FSM_HIP(hipMemsetAsync(x.DL.p, 0, SU * 4, s));
+            FSM_HIP(hipMemsetAsync(x.TR.p, 0, SU * 4, s));
+            FSM_HIP(hipMemsetAsync(x.seen.p, 0, SU * 4, s));
+        }
+        x.stage = std::make_unique<PinnedBuf>(kSidesB + 2 * kOffB);
+        x.d_stage.alloc(kSidesB + 2 * kOffB);
+        x.h_sides = static_cast<Side*>(x.stage->host);
+        x.h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(x.stage->host) + kSidesB);
+        x.h_wave = x.h_drv + (B + 1);
+        x.d_sides = x.d_stage.as<Side>();
+        x.d_drv = reinterpret_cast<uint64_t*>(x.d_stage.as<char>() + kSidesB);
+        x.d_wave = x.d_drv + (B + 1);
+        x.d_ndlw.alloc(16);
+        x.pin = std::make_unique<PinnedBuf>(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
+        x.h_hdr = static_cast<ExpHdr*>(x.pin->host);
+        x.h_rec = reinterpret_cast<ExpRec*>(x.h_hdr + B);
+        x.d_hdr = static_cast<ExpHdr*>(x.pin->dev);
+        x.d_rec = reinterpret_cast<ExpRec*>(x.d_hdr + B);
+        for (int q = 0; q < 5; ++q) FSM_HIP(hipEventCreate(&x.ev[q]));
+        FSM_HIP(hipEventCreateWithFlags(&x.ev[5], hipEventDisableTiming));
     }
-    x.stage = std::make_unique<PinnedBuf>(kSidesB + 2 * kOffB);
-    x.d_stage.alloc(kSidesB + 2 * kOffB);
-    x.h_sides = static_cast<Side*>(x.stage->host);
-    x.h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(x.stage->host) + kSidesB);
-    x.h_wave = x.h_drv + (B + 1);
-    x.d_sides = x.d_stage.as<Side>();
-    x.d_drv = reinterpret_cast<uint64_t*>(x.d_stage.as<char>() + kSidesB);
-    x.d_wave = x.d_drv + (B + 1);
-    x.d_ndlw.alloc(16);
-    x.pin = std::make_unique<PinnedBuf>(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
-    x.h_hdr = static_cast<ExpHdr*>(x.pin->host);
-    x.h_rec = reinterpret_cast<ExpRec*>(x.h_hdr + B);
-    x.d_hdr = static_cast<ExpHdr*>(x.pin->dev);
-    x.d_rec = reinterpret_cast<ExpRec*>(x.d_hdr + B);
     struct ExpResult {
         std::vector<ExpRec> recs;
         std::vector<Rule*> preL, preR;  // children created (and expanded) ahead of the commit, by record
     };
     std::unordered_map<Rule*, ExpResult> cache;
-    int64_t expansions = 0, launches = 0, spec_pushback = 0;
+    std::unordered_map<Rule*, int> inflight;  // rules of a busy set (results not yet taken in)
+    std::vector<std::pair<std::vector<Rule*>, int>> spec_todo;  // finished launches whose children to speculate
+    int64_t expansions = 0, launches = 0, spec_pushback = 0, gpu_rules = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     double last_log_ms = now_ms();  // verbose progress line every 20 s
     double prep_ms = 0, post_ms = 0, commit_ms = 0, pop_ms = 0;  // host time split (verbose summary)
@@ -1484,23 +1502,86 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const char* v = std::getenv("FSM_TSR_SPB");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
     }();
-    // per-kernel device time: every 16th launch records one set of events
-    // and reads them back at its sync (ctx->kstats rows)
+    // per-kernel device time: every 16th launch records one set of events and reads
+    // them back when it finishes (ctx->kstats rows)
     struct Seg {
         double ms = 0;  // over the timed launches
         int64_t n = 0, timed = 0, bytes = 0;
     } seg[4];  // bitmap path: domain, rows, reduce, k_dl; list path: expansion, -, collect, k_publish
     const char* seg_name[4] = {use_bm ? "k_exp_domain" : "k_expand", use_bm ? "k_exp_rows" : "",
                                use_bm ? "k_expand_reduce" : "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
-    for (hipEvent_t& e : ctx->ev)
-        if (!e) FSM_HIP(hipEventCreate(&e));
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
-    uint32_t alive_t = 0;  // minsup the alive bitmap was built for
-    // expand `batch`: one launch, one stream sync; results into the cache
-    auto launch = [&](const std::vector<Rule*>& batch) {
+    uint32_t alive_t = 0;  // minsup the kid codes were built for
+    int64_t seq_next = 0;
+    // Take in the results of set x (waits for its launch): records sorted into the
+    // cache, and its batch queued for child speculation.
+    auto finish = [&](ExpSet& x) {
+        const double tw0 = now_ms();
+        FSM_HIP(hipEventSynchronize(x.ev[5]));
+        const double tw1 = now_ms();
+        wait_ms += tw1 - tw0;
+        x.busy = false;
+        for (int q = 0; q < 4; ++q) {
+            float ms = 0;
+            if (x.timed && hipEventElapsedTime(&ms, x.ev[q], x.ev[q + 1]) == hipSuccess) {
+                seg[q].ms += ms;
+                seg[q].timed += 1;
+            }
+            seg[q].n += 1;
+        }
+        const uint32_t nb = uint32_t(x.batch.size());
+        if (use_bm) {
+            exp_part_bytes += int64_t(x.blocks * row_bytes);
+            seg[1].bytes += int64_t(x.blocks * row_bytes);  // the partial rows the row kernel writes
+        }
+        uint64_t nout_all = 0;
+        for (uint32_t k = 0; k < nb; ++k) {
+            Rule* r = x.batch[k];
+            const ExpHdr h = x.h_hdr[k];
+            nout_all += h.nout;
+            if (use_bm) {
+                // algorithmic bytes: domain = the |X|+|Y| bitmap operands + 8 B row bounds read
+                // and 8 B written per domain sid; rows = the domain list + 8 B per row entry
+                const uint64_t bmb = uint64_t(r->nx + r->ny) * d->NW * 4;
+                exp_domain += h.nsid;
+                exp_entries += h.nent;
+                exp_bitmap_bytes += int64_t(bmb);
+                seg[0].bytes += int64_t(bmb + 16ull * h.nsid);
+                seg[1].bytes += int64_t(8ull * h.nent + 8ull * h.nsid);
+            }
+            if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
+            if (!use_bm && x.drv_in_x[k] && h.nx != r->nX)
+                throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(h.nx) + " vs " +
+                                             std::to_string(r->nX) + ")");
+            inflight.erase(r);
+            if (r->dropped) continue;  // a speculated child its parent's commit did not register
+            ExpResult& res = cache[r];
+            const ExpRec* rec = x.h_rec + size_t(k) * ecap;
+            res.recs.assign(rec, rec + h.nout);
+            std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
+        }
+        seg[2].bytes += int64_t(nout_all * sizeof(ExpRec));
+        x.timed = false;
+        spec_todo.emplace_back(std::move(x.batch), x.depth);
+        x.batch.clear();
+        post_ms += now_ms() - tw1;
+    };
+    // expand `batch` on a free set (finishing the older busy one first when both are
+    // busy): enqueue the launch and return; finish() takes the results in
+    auto launch = [&](const std::vector<Rule*>& batch, int depth) {
+        ExpSet* xp = !xs[0].busy ? &xs[0] : (!xs[1].busy ? &xs[1] : nullptr);
+        if (!xp) {
+            xp = xs[0].seq < xs[1].seq ? &xs[0] : &xs[1];
+            finish(*xp);
+        }
+        ExpSet& x = *xp;
         const double tl0 = now_ms();
         const uint32_t nb = uint32_t(batch.size());
         x.batch = batch;
+        x.depth = depth;
+        x.seq = seq_next++;
+        gpu_rules += nb;
+        for (Rule* r : batch) inflight[r] = int(xp - xs);
         sides.assign(nb, Side{});
         drv_off.assign(nb + 1, 0);
         wave_off.assign(nb + 1, 0);
@@ -1550,6 +1631,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 wave_off[k + 1] = wave_off[k] + std::max<uint64_t>(1, n0 * (max_blocks - nb) / tot);
             }
         }
+        x.blocks = wave_off[nb];
         if (use_bm && x.dom.bytes < drv_off[nb] * sizeof(uint2))
             x.dom.alloc(std::max<uint64_t>(drv_off[nb] * sizeof(uint2) * 5 / 4, uint64_t(1) << 20));
         std::memcpy(x.h_sides, sides.data(), nb * sizeof(Side));
@@ -1564,24 +1646,24 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             FSM_LAUNCHED("k_alive", s);
             alive_t = rp.minsup;
         }
-        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[0], s));
+        if (x.timed) FSM_HIP(hipEventRecord(x.ev[0], s));
         if (use_bm) {
             hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads), 0, s,
                                x.d_sides, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), x.d_drv,
                                x.dom.as<uint2>(), x.ctl.as<ExpCtl>());
             FSM_LAUNCHED("k_exp_domain", s);
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
+            if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
             hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
                                x.d_wave, nb, x.d_drv, x.dom.as<uint2>(), k_ent.as<uint2>(), d_kidof.as<uint32_t>(),
                                d_alive.as<uint32_t>(), geo, x.part.as<uint32_t>(), x.ctl.as<ExpCtl>(),
                                x.d_ndlw.as<uint32_t>());
             FSM_LAUNCHED("k_exp_rows", s);
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
+            if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
             hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
                                x.d_wave, geo, d_kept.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_rec, ecap,
                                x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>());
             FSM_LAUNCHED("k_expand_reduce", s);
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
+            if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
             hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
                                d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), x.d_dlw.as<uint4>(),
                                x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
@@ -1597,74 +1679,36 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                    x.list.as<uint32_t>(), x.ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
                 FSM_LAUNCHED("k_expand", s);
             }
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[1], s));
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[2], s));
+            if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
+            if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
             hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, x.TL.as<uint32_t>(),
                                x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
                                x.ctl.as<ExpCtl>(), U, rp.minsup, x.d_rec, ecap);
             FSM_LAUNCHED("k_expand_collect", s);
-            if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[3], s));
+            if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
             hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
             FSM_LAUNCHED("k_publish", s);
         }
-        if (x.timed) FSM_HIP(hipEventRecord(ctx->ev[4], s));
-        const double tw0 = now_ms();
-        prep_ms += tw0 - tl0;
-        FSM_HIP(hipStreamSynchronize(s));
-        const double tw1 = now_ms();
-        wait_ms += tw1 - tw0;
+        if (x.timed) FSM_HIP(hipEventRecord(x.ev[4], s));
+        FSM_HIP(hipEventRecord(x.ev[5], s));
+        x.busy = true;
         ++launches;
-        for (int q = 0; q < 4; ++q) {
-            float ms = 0;
-            if (x.timed && hipEventElapsedTime(&ms, ctx->ev[q], ctx->ev[q + 1]) == hipSuccess) {
-                seg[q].ms += ms;
-                seg[q].timed += 1;
-            }
-            seg[q].n += 1;
-        }
-        if (use_bm) {
-            exp_part_bytes += int64_t(wave_off[nb] * row_bytes);
-            seg[1].bytes += int64_t(wave_off[nb] * row_bytes);  // the partial rows the row kernel writes
-        }
-        uint64_t nout_all = 0;
-        for (uint32_t k = 0; k < nb; ++k) {
-            const ExpHdr h = x.h_hdr[k];
-            nout_all += h.nout;
-            if (use_bm) {
-                // algorithmic bytes: domain = the |X|+|Y| bitmap operands + 8 B row bounds read
-                // and 8 B written per domain sid; rows = the domain list + 8 B per row entry
-                const uint64_t bmb = uint64_t(batch[k]->nx + batch[k]->ny) * d->NW * 4;
-                exp_domain += h.nsid;
-                exp_entries += h.nent;
-                exp_bitmap_bytes += int64_t(bmb);
-                seg[0].bytes += int64_t(bmb + 16ull * h.nsid);
-                seg[1].bytes += int64_t(8ull * h.nent + 8ull * h.nsid);
-            }
-            if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
-            if (!use_bm && x.drv_in_x[k] && h.nx != batch[k]->nX)
-                throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(h.nx) + " vs " +
-                                             std::to_string(batch[k]->nX) + ")");
-            ExpResult& res = cache[batch[k]];
-            const ExpRec* rec = x.h_rec + size_t(k) * ecap;
-            res.recs.assign(rec, rec + h.nout);
-            std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
-        }
-        seg[2].bytes += int64_t(nout_all * sizeof(ExpRec));
-        x.timed = false;
-        post_ms += now_ms() - tw1;
+        prep_ms += now_ms() - tl0;
     };
     // Speculated rules wait in `pending` (ordered like the heap, results
-    // cached) instead of going back to the heap: the next rule to commit is
-    // always the larger of the heap top and the pending front, which is
-    // exactly the one-at-a-time order; new rules only ever enter the heap.
+    // cached or in flight) instead of going back to the heap: the next rule to
+    // commit is always the larger of the heap top and the pending front, which
+    // is exactly the one-at-a-time order; new rules only ever enter the heap.
     struct PendingOrder {  // largest first (the heap's pop order)
         const RuleStore* st;
         bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(*st, a, b) > 0; }
     };
     std::set<Rule*, PendingOrder> pending(PendingOrder{&rp.st});
     // a speculated child that its parent's commit did not register: drop its
-    // cached results (and, recursively, those of its own speculated children)
+    // results (cached, or marked so that an in-flight launch's are discarded) and,
+    // recursively, those of its own speculated children
     std::function<void(Rule*)> drop_spec = [&](Rule* x) {
+        x->dropped = true;
         auto it = cache.find(x);
         if (it == cache.end()) return;
         ExpResult res = std::move(it->second);
@@ -1705,13 +1749,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
     };
 
-    // Child speculation: after a launch, the children of its rules that rank
-    // at or above the lowest pending rule (sup >= T) are the ones whose
+    // Child speculation: when a launch finishes, the children of its rules that
+    // rank at or above the lowest pending rule (sup >= T) are the ones whose
     // registration would force the next launch (a fresh rule outranking the
     // pending front).  They are created now, exactly as their parent's commit
-    // would create them, and expanded in follow-up launches of up to
-    // kExpBatch rules, a few levels deep; the commit then registers the
-    // pre-built rule (results cached) instead of deriving it again.
+    // would create them, and expanded in a follow-up launch (a few levels deep)
+    // while the host commits; the commit then registers the pre-built rule
+    // (results cached or in flight) instead of deriving it again.
     int64_t spec_made = 0, spec_launches = 0;
     int spec_depth = kSpecDepth, spec_max = kSpecMax;  // FSM_TSR_SPEC="depth,max" (tuning; "0" disables)
     double spec_frac = 1.0;  // FSM_TSR_SPEC_FRAC: speculate children with sup >= frac * T (tuning)
@@ -1726,58 +1770,69 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             spec_max = b2;
         }
     }
-    auto speculate = [&](std::vector<Rule*> level) {
-        for (int depth = 0; depth < spec_depth && !level.empty(); ++depth) {
-            uint32_t T = 0xFFFFFFFFu;
-            for (Rule* x : level) T = std::min(T, x->sup);
-            if (!pending.empty()) T = std::min(T, (*pending.rbegin())->sup);
-            T = std::max(uint32_t(double(T) * spec_frac), rp.minsup);
-            std::vector<Rule*> next;
-            for (Rule* x : level) {
-                auto it = cache.find(x);
-                if (it == cache.end()) continue;
-                ExpResult& res = it->second;
-                const size_t n = res.recs.size();
-                res.preL.assign(n, nullptr);
-                res.preR.assign(n, nullptr);
-                for (size_t i = 0; i < n && next.size() < size_t(spec_max); ++i) {
-                    const ExpRec& e = res.recs[i];
-                    if (x->expandLR && e.tl >= T) {
-                        Rule* c = rp.derive(x, e.c, kNone, e.tl, e.dl);
-                        c->expandLR = true;
-                        res.preL[i] = c;
-                        next.push_back(c);
-                    }
-                    if (e.tr >= T && next.size() < size_t(spec_max)) {
-                        Rule* c = rp.derive(x, kNone, e.c, e.tr, x->nX);
-                        c->expandLR = false;
-                        res.preR[i] = c;
-                        next.push_back(c);
-                    }
+    const bool spec_on = [] { const char* v = std::getenv("FSM_TSR_SPEC"); return !(v && v[0] == '0'); }();
+    // the next level of one finished launch's batch
+    auto speculate = [&](const std::vector<Rule*>& level, int depth) {
+        if (!spec_on || depth >= spec_depth || level.empty()) return;
+        uint32_t T = 0xFFFFFFFFu;
+        for (Rule* x : level) T = std::min(T, x->sup);
+        if (!pending.empty()) T = std::min(T, (*pending.rbegin())->sup);
+        T = std::max(uint32_t(double(T) * spec_frac), rp.minsup);
+        std::vector<Rule*> next;
+        for (Rule* x : level) {
+            auto it = cache.find(x);
+            if (it == cache.end()) continue;  // committed already, or dropped
+            ExpResult& res = it->second;
+            const size_t n = res.recs.size();
+            res.preL.assign(n, nullptr);
+            res.preR.assign(n, nullptr);
+            for (size_t i = 0; i < n && next.size() < size_t(spec_max); ++i) {
+                const ExpRec& e = res.recs[i];
+                if (x->expandLR && e.tl >= T) {
+                    Rule* c = rp.derive(x, e.c, kNone, e.tl, e.dl);
+                    c->expandLR = true;
+                    res.preL[i] = c;
+                    next.push_back(c);
+                }
+                if (e.tr >= T && next.size() < size_t(spec_max)) {
+                    Rule* c = rp.derive(x, kNone, e.c, e.tr, x->nX);
+                    c->expandLR = false;
+                    res.preR[i] = c;
+                    next.push_back(c);
                 }
             }
-            spec_made += int64_t(next.size());
-            for (size_t a = 0; a < next.size(); a += size_t(B)) {
-                const std::vector<Rule*> part(next.begin() + a,
-                                              next.begin() + std::min(next.size(), a + size_t(B)));
-                launch(part);
-                ++spec_launches;
-            }
-            level = std::move(next);
+        }
+        spec_made += int64_t(next.size());
+        for (size_t a = 0; a < next.size(); a += size_t(B)) {
+            const std::vector<Rule*> part(next.begin() + a, next.begin() + std::min(next.size(), a + size_t(B)));
+            launch(part, depth + 1);
+            ++spec_launches;
         }
     };
 
     std::vector<Rule*> batch;
     size_t sweep_at = size_t(1) << 16;
-    const bool spec_on = [] { const char* v = std::getenv("FSM_TSR_SPEC"); return !(v && v[0] == '0'); }();
     for (;;) {
+        // children of finished launches first (their launches overlap the commits below)
+        while (!spec_todo.empty()) {
+            std::vector<std::pair<std::vector<Rule*>, int>> todo;
+            todo.swap(spec_todo);
+            for (auto& [lvl, dp] : todo) speculate(lvl, dp);
+        }
         const bool have_h = !rp.cand.empty(), have_p = !pending.empty();
         if (!have_h && !have_p) break;
         const bool from_p = have_p && (!have_h || rule_cmp(rp.st, *pending.begin(), rp.cand.top().r) > 0);
         Rule* r = from_p ? *pending.begin() : rp.cand.top().r;
         if (r->sup < rp.minsup) break;
         auto ci = cache.find(r);
-        if (from_p || ci != cache.end()) {  // results at hand (speculated earlier): commit now
+        if (ci == cache.end()) {
+            auto fi = inflight.find(r);
+            if (fi != inflight.end()) {  // expanding on the GPU: take its launch in, then decide again
+                finish(xs[fi->second]);
+                continue;
+            }
+        }
+        if (ci != cache.end()) {  // results at hand: commit now
             if (from_p) pending.erase(pending.begin());
             else rp.cand.pop();
             const double tc0 = now_ms();
@@ -1792,27 +1847,30 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             }
             continue;
         }
-        // r (uncached) and the next heap rules are expanded together
+        if (from_p) throw Error(FSM_EDEVICE, "TSR: a pending rule has neither results nor a launch");
+        // r (neither cached nor in flight) and the next heap rules are expanded together
         const double tp0 = now_ms();
         batch.clear();
         while (batch.size() < size_t(B) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
             Rule* x = rp.cand.top().r;
             rp.cand.pop();
-            if (cache.count(x)) pending.insert(x);  // already expanded by speculation
+            if (cache.count(x) || inflight.count(x)) pending.insert(x);  // already expanded by speculation
             else batch.push_back(x);
         }
         pop_ms += now_ms() - tp0;
-        launch(batch);
+        launch(batch, 0);
         spec_pushback += int64_t(batch.size()) - 1;
         for (Rule* c : batch) pending.insert(c);
-        if (spec_on) speculate(batch);
     }
+    for (ExpSet& x : xs)  // speculation still in flight when the replay ended
+        if (x.busy) finish(x);
     if (ctx->opts.verbose)
         std::fprintf(stderr,
-                     "[fsm tsr] expansions %lld in %lld launches (%lld pushed back), %.0f ms waiting on the GPU; "
-                     "host: %.0f ms launch prep, %.0f ms result intake, %.0f ms commit, %.0f ms batch pops; %zu rules made\n",
-                     (long long)expansions, (long long)launches, (long long)spec_pushback, wait_ms, prep_ms, post_ms,
-                     commit_ms, pop_ms, rp.st.rules.size());
+                     "[fsm tsr] expansions %lld in %lld launches (%lld rules expanded, %lld pushed back), %.0f ms waiting on the "
+                     "GPU; host: %.0f ms launch prep, %.0f ms result intake, %.0f ms commit, %.0f ms batch pops; %zu rules "
+                     "made\n",
+                     (long long)expansions, (long long)launches, (long long)gpu_rules, (long long)spec_pushback, wait_ms,
+                     prep_ms, post_ms, commit_ms, pop_ms, rp.st.rules.size());
     if (ctx->opts.verbose)
         std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB\n",
                      (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6);

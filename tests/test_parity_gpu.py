@@ -377,22 +377,47 @@ def test_root_f2_paths_agree(eng, path, monkeypatch):
     assert pats == o["patterns"] and st["joins"] == o["joins"]
 
 
-@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some"])
-@pytest.mark.parametrize("shape", ["quest", "sign", "bible"])
+def _wide_runs_db(seed=5, n=600):
+    """W = 1 sequences (at most 60 itemsets) holding up to 240 distinct items,
+    so root and first-level runs exceed 64 entries (k_emit2's long-run list)."""
+    import numpy as np
+    from tools import gen
+    rng = np.random.default_rng(seed)
+    so, tk = [0], []
+    for _ in range(n):
+        nsets = int(rng.integers(1, 61))
+        wide = rng.random() < 0.3
+        for _ in range(nsets):
+            k = int(rng.integers(2, 9)) if wide else int(rng.integers(1, 3))
+            tk.extend(sorted(int(x) for x in rng.choice(300, size=k, replace=False)))
+            tk.append(-1)
+        tk.append(-2)
+        so.append(len(tk))
+    return gen.DataSet(np.array(so, dtype=np.int64), np.array(tk, dtype=np.int64), "wide-runs")
+
+
+@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some", "chunk"])
+@pytest.mark.parametrize("shape", ["quest", "sign", "bible", "wide"])
 def test_emit_paths_agree(eng, path, shape, monkeypatch):
-    """Child-run emission: the one-pass k_emit1 (LDS join records, slab
-    cursor) and its overflow path (records capped at 0 / 17 per wave, so waves
-    join again while writing) give the oracle's patterns and joins."""
+    """Child-run emission: the window kernel k_emit2 (W = 1: runs of <= 64
+    entries in registers, longer runs through k_emit1's run list), the chunk
+    kernel k_emit1 (FSM_EMIT_PATH=chunk; every W), and their overflow paths
+    (records capped at 0 / 17 per wave, so waves join again while writing)
+    give the oracle's patterns and joins."""
     from oracle import oracle
     from tools import gen
     if path == "overflow-all":
         monkeypatch.setenv("FSM_EMIT_CAP", "0")
     elif path == "overflow-some":
         monkeypatch.setenv("FSM_EMIT_CAP", "17")
+    elif path == "chunk":
+        monkeypatch.setenv("FSM_EMIT_PATH", "chunk")
     if shape == "quest":
         ds, sup = gen.quest(20000, seed=9), 0.003
     elif shape == "sign":
         ds, sup = gen.sign(seed=2).head(400), 0.3
+    elif shape == "wide":
+        ds, sup = _wide_runs_db(), 0.05
     else:
         ds, sup = gen.bible(seed=2).head(1500), 0.03
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
