@@ -215,13 +215,36 @@ def main():
             torch.cuda.synchronize()
 
     ds = gen.quest(args.sequences, seed=args.seed)
-    if world > 1 and args.dist_backend == "nccl" and os.environ.get("FSM_BENCH_COMM") == "rccl":
-        # libfsm's own RCCL communicator: rank 0 makes the unique id, torch broadcasts it
-        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+    eng, comm_kind = None, "none"
+    if world > 1 and args.dist_backend == "nccl" and os.environ.get("FSM_BENCH_COMM", "rccl") == "rccl":
+        # libfsm's own RCCL communicator (its collectives stay on the device): rank 0
+        # makes the unique id, torch broadcasts it; if any rank cannot create it, every
+        # rank falls back to the host-staged torch collectives below
+        uid = torch.zeros(129, dtype=torch.uint8, device="cuda")
         if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(fsm.comm_unique_id()), dtype=torch.uint8))
+            try:
+                uid[:128].copy_(torch.frombuffer(bytearray(fsm.comm_unique_id()), dtype=torch.uint8))
+                uid[128] = 1
+            except fsm.FsmError:
+                uid[128] = 0
         dist.broadcast(uid, 0)
-        eng = fsm.Engine(device=local_rank, nranks=world, rank=rank, unique_id=bytes(uid.cpu().tolist()))
+        h = uid.cpu().tolist()
+        if h[128]:
+            try:
+                eng = fsm.Engine(device=local_rank, nranks=world, rank=rank, unique_id=bytes(h[:128]))
+            except fsm.FsmError as e:
+                print("rank %d: libfsm RCCL communicator failed (%s); host-staged collectives" % (rank, e),
+                      file=sys.stderr)
+                eng = None
+        ok = torch.tensor([1 if eng is not None else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 1:
+            comm_kind = "libfsm RCCL communicator (device buffers)"
+        elif eng is not None:
+            eng.close()
+            eng = None
+    if eng is not None:
+        pass
     elif world > 1:
         # libfsm's collectives over torch's process group: RCCL (staged through a
         # device tensor) for nccl, CPU tensors for gloo (several ranks may share a GPU)
@@ -230,6 +253,7 @@ def main():
         hc = TorchHostComm(dist.group.WORLD, device=dev)
         eng = fsm.Engine(device=local_rank % max(torch.cuda.device_count(), 1), nranks=world, rank=rank,
                          host_comm=hc)
+        comm_kind = "torch.distributed %s, host-staged" % args.dist_backend
     else:
         eng = fsm.Engine(device=local_rank)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
@@ -252,12 +276,20 @@ def main():
     ms_local = (t1 - t0) * 1000.0 / max(args.steps, 1)
     ms = ms_local
     joins_all = st["joins"]
+    per_rank = None
     if world > 1:
         t = torch.tensor([ms_local], dtype=torch.float64)
         if args.dist_backend == "nccl":
             t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
+        # per-rank trace of the last step: which work each rank did (replicated vs its share)
+        mine = {"rank": rank, "ms_per_step": round(ms_local, 4),
+                "ms_f1": round(st["ms_f1"], 4), "ms_f2_root": round(st["ms_f2"], 4),
+                "ms_lattice": round(st["ms_lattice"], 4), "classes": st["classes"], "entries": st["entries"],
+                "kernels": {k["name"]: round(k["ms"], 4) for k in ks}}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
     if rank != 0:
         db.free()
@@ -293,7 +325,7 @@ def main():
         "data": "synthetic (seeded Quest-shaped generator, tools/fsmgen.c)",
         "config": {"workload": "quest-C10-T2.5-S4-I1.25-D%d-N10000-seed%d, minsup %g" % (
             args.sequences, args.seed, args.support), "parallelism": "single GPU" if world == 1 else
-            "prefix classes sharded over %d ranks (%s)" % (world, args.dist_backend)},
+            "prefix classes sharded over %d ranks (%s)" % (world, comm_kind)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_launch,
                      "kernel": dom["name"], "launches_per_step": dom["launches"],
@@ -325,6 +357,8 @@ def main():
                                       "GBps": round((k["alg_bytes"] / 1e9) / (k["ms"] / 1000.0), 1) if k["ms"] else 0}
                                      for k in ks), key=lambda k: -k["ms"])},
     }
+    if per_rank is not None:
+        line["extra"]["per_rank"] = per_rank
     if not args.no_cpu_baseline and world == 1:
         host = "%s; nproc %d, this process's CPU share %d" % (cpu_model(), os.cpu_count() or 0, cpu_share())
         cb = cpu_baseline(ds, args.support, args.cpu_seconds, 1, args.cpu_reps, args.cpu_stride)

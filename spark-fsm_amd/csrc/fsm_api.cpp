@@ -4,12 +4,14 @@
 // into java.lang.Exception so TrainActor records FAILURE, TrainActor.scala:65-67).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <new>
 
 #include "comm.h"
 #include "dev_db.h"
 #include "device_util.h"
 #include "fsm_internal.h"
+#include "host_pool.h"
 
 using fsm::Error;
 
@@ -158,6 +160,19 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
         FSM_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
         ctx->pool = std::make_shared<fsm::Pool>(ctx->opts.device);
         ctx->comm = fsm::make_comm(ctx->opts).release();
+        // the host side a DB build and a mine use from their first call: the staging
+        // ring (two 4 MiB pinned slots, each DMA'd once: the first DMA from a pinned
+        // buffer is slow) and the host thread pool's workers
+        {
+            const size_t rb = size_t(4) << 20;
+            fsm::DevBuf warm(rb);
+            for (int slot = 2; slot <= 3; ++slot) {
+                std::memset(ctx->stage_host(slot, rb), 0, rb);
+                ctx->stage_copy(slot, warm.p, rb);
+            }
+            FSM_HIP(hipStreamSynchronize(ctx->stream));
+        }
+        fsm::par_slices(fsm::host_threads(), fsm::host_threads(), [](int64_t, int64_t, int64_t) {});
     });
     if (rc != FSM_OK) {
         g_err = ctx->err;

@@ -1082,20 +1082,26 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
 
 // Window emission (W = 1).  k_emit1's partner lookups are dependent binary
 // searches in HBM (86 % of wave cycles waiting); here each wave
-// owns the runs STARTING in a 256-entry range of the batch and walks them in
+// owns the runs STARTING in a 128-entry range of the batch and walks them in
 // windows of whole runs of at most 64 entries held in registers (one entry per
 // lane: member, lohi, mask).  An (entry, kid) pair finds its partner with a
 // fixed 6-step shuffle lower_bound over the owner's run and takes the
 // partner's lohi / mask by shuffle: no memory access between a kid's slot and
 // its join result.  Join records stay in per-wave LDS (as k_emit1), the block
-// reserves its child entries with one slab-cursor atomic per 1,024-entry chunk
+// reserves its child entries with one slab-cursor atomic per 512-entry chunk
 // and writes the runs; a wave whose records overflow joins again while writing.
 // Runs longer than 64 entries are appended to `longl` for k_emit1's run list.
+#ifndef FSM_E2_RANGE
+#define FSM_E2_RANGE 128
+#endif
+#ifndef FSM_E2_CAP
+#define FSM_E2_CAP 192
+#endif
 constexpr int kE2Block = 256;                   // 4 waves
 constexpr uint32_t kE2Waves = kE2Block / 64;
-constexpr uint32_t kE2Range = 256;              // entries per wave range (runs starting in it)
+constexpr uint32_t kE2Range = FSM_E2_RANGE;     // entries per wave range (runs starting in it)
 constexpr uint32_t kE2Own = kE2Range + 64;      // owner slots per wave (a run may end 63 past the range)
-constexpr uint32_t kE2Cap = 384;                // LDS join records per wave
+constexpr uint32_t kE2Cap = FSM_E2_CAP;         // LDS join records per wave
 
 __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* __restrict__ cid,
                                                     const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
@@ -1271,6 +1277,132 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
         }
         __syncthreads();  // the LDS records are reused by the next chunk
     }
+}
+
+// Window count (W = 1).  k_count's atomics execute at the memory side, one
+// request per distinct 64-byte line of a wave-instruction (MI355X_MICROARCH
+// §Global float atomics: a coalesced 256-B instruction is four requests); with
+// one thread per entry the 64 lanes of an instruction add into 64 different
+// counter rows.  Here each wave walks windows of whole runs (<= 64 entries, in
+// registers, as k_emit2) and flattens the window's (entry, partner) pairs over
+// the lanes in entry order, so the lanes of one instruction add into the rows
+// of the few entries of that step, and the partner's member / lohi / mask come
+// by shuffle.  Runs longer than 64 entries are counted thread-per-entry.
+constexpr uint32_t kC2Range = 128;  // entries per wave range (runs starting in it)
+
+__global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* __restrict__ cid,
+                                                   const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                   const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
+                                                   const uint64_t* __restrict__ mask, uint32_t mlo, uint32_t mhi,
+                                                   uint32_t* __restrict__ cnt, unsigned long long* __restrict__ tests) {
+    __shared__ uint32_t blk_tests;
+    if (threadIdx.x == 0) blk_tests = 0;
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+    uint32_t my_tests = 0;
+    for (uint32_t wa = wave * kC2Range; wa < E; wa += nwaves * kC2Range) {
+        const uint32_t wz = min(E, wa + kC2Range);
+        uint32_t e0 = wz;  // the first run start in [wa, wz)
+        for (uint32_t b0 = wa; b0 < wz; b0 += 64) {
+            const uint32_t e = b0 + lane;
+            const uint64_t st = __ballot(e < wz && (pos[e] >> 16) == 0u);
+            if (st) {
+                e0 = b0 + uint32_t(__ffsll((unsigned long long)st)) - 1u;
+                break;
+            }
+        }
+        while (e0 < wz) {
+            const uint32_t e = e0 + lane;
+            const uint32_t p = e < E ? pos[e] : 0u;
+            const uint32_t len = p & 0xFFFFu;
+            const bool st = e < E && (p >> 16) == 0u;
+            const uint64_t bad = __ballot(st && (e >= wz || lane + len > 64u));
+            const uint64_t sts = __ballot(st);
+            if (bad & 1ull) {  // lane 0 starts a run of more than 64 entries: thread per entry
+                const uint32_t rl = uint32_t(__shfl(int(len), 0, 64));
+                for (uint32_t i0 = e0; i0 < e0 + rl; i0 += 64) {
+                    const uint32_t ei = i0 + lane;
+                    if (ei >= e0 + rl) continue;
+                    const uint32_t mi = mem[ei];
+                    if (!(mi - mlo < mhi - mlo)) continue;
+                    my_tests += rl;
+                    const DClass c = cls[cid[ei]];
+                    const uint32_t lo_i = lohi[ei] & 0xFFFFu, ti = mi & 1u, ri = mi >> 1;
+                    const uint64_t mk = mask[ei];
+                    uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
+                    for (uint32_t f = e0; f < e0 + rl; ++f) {
+                        const uint32_t mj = mem[f], tj = mj & 1u, rj = mj >> 1;
+                        if (tj == kSeq) {
+                            if ((lohi[f] >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
+                            if (ti == kSeq && rj > ri && (mk & mask[f])) atomicAdd(rowc + (rj << 1 | 1u), 1u);
+                        } else if (ti == kItm && rj > ri && (mk & mask[f])) {
+                            atomicAdd(rowc + (rj << 1 | 1u), 1u);
+                        }
+                    }
+                }
+                e0 += rl;
+                continue;
+            }
+            uint32_t cut;
+            if (bad) {
+                cut = uint32_t(__ffsll((unsigned long long)bad)) - 1u;
+            } else {
+                const uint32_t ls = 63u - uint32_t(__clzll(sts));
+                cut = ls + uint32_t(__shfl(int(len), int(ls), 64));
+            }
+            const bool in = lane < cut;
+            uint32_t mi = 0, lh = 0, np = 0;
+            uint64_t mk = 0, rowa = 0;
+            if (in) {
+                mi = mem[e];
+                lh = lohi[e];
+                mk = mask[e];
+                if (mi - mlo < mhi - mlo) {  // (sharded root: this rank's member rows only)
+                    const DClass c = cls[cid[e]];
+                    rowa = c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
+                    np = len;  // partners: every entry of its run
+                    my_tests += len;
+                }
+            }
+            const uint32_t rs = lane - (p >> 16);  // first lane of the lane's run
+            const uint32_t incl = wave_incl_scan(np), excl = incl - np;
+            const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
+            for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+                const uint32_t pp = p0 + lane;
+                uint32_t ow = 0;  // the owner lane: the largest lane whose first pair index <= pp
+#pragma unroll
+                for (uint32_t stp = 32; stp > 0; stp >>= 1) {
+                    const uint32_t cand = ow + stp;
+                    if (uint32_t(__shfl(int(excl), int(cand), 64)) <= pp) ow = cand;
+                }
+                const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
+                const uint32_t o_rs = uint32_t(__shfl(int(rs), int(ow), 64));
+                const uint32_t o_mi = uint32_t(__shfl(int(mi), int(ow), 64));
+                const uint32_t o_lo = uint32_t(__shfl(int(lh), int(ow), 64)) & 0xFFFFu;
+                const uint64_t o_mk = __shfl(mk, int(ow), 64);
+                const uint64_t o_row = __shfl(rowa, int(ow), 64);
+                const uint32_t f = min(o_rs + (pp - o_ex), 63u);  // the partner lane
+                const uint32_t mj = uint32_t(__shfl(int(mi), int(f), 64));
+                const uint32_t hj = uint32_t(__shfl(int(lh), int(f), 64)) >> 16;
+                const uint64_t mkj = __shfl(mk, int(f), 64);
+                if (pp < total) {
+                    const uint32_t ti = o_mi & 1u, ri = o_mi >> 1, tj = mj & 1u, rj = mj >> 1;
+                    uint32_t* rowc = cnt + o_row;
+                    if (tj == kSeq) {
+                        if (hj > o_lo) atomicAdd(rowc + (rj << 1), 1u);
+                        if (ti == kSeq && rj > ri && (o_mk & mkj)) atomicAdd(rowc + (rj << 1 | 1u), 1u);
+                    } else if (ti == kItm && rj > ri && (o_mk & mkj)) {
+                        atomicAdd(rowc + (rj << 1 | 1u), 1u);
+                    }
+                }
+            }
+            e0 += cut;
+        }
+    }
+    atomicAdd(&blk_tests, my_tests);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
 }
 
 // ------------------------------------------------------------- host side
@@ -1677,6 +1809,11 @@ struct Miner {
         const double f = v ? std::atof(v) : 0.5;
         return f > 0.0 ? f : 1e300;
     }
+    // FSM_COUNT_KERNEL=thread forces the thread-per-entry k_count (tests, A/B runs; default: k_count2 at W = 1)
+    static bool count_window() {
+        const char* v = std::getenv("FSM_COUNT_KERNEL");
+        return !(v && !std::strcmp(v, "thread"));
+    }
     // FSM_EMIT_PATH=chunk forces k_emit1 for every batch (tests, A/B runs; default: k_emit2 at W = 1)
     static bool emit_window() {
         const char* v = std::getenv("FSM_EMIT_PATH");
@@ -1974,7 +2111,14 @@ struct Miner {
                        member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>(), d_tests.as<unsigned long long>(),    \
                        uint32_t(W))
                 const size_t tk = clk->begin("k_count");
-                FSM_W_DISPATCH(W, FSM_COUNT)
+                if (W == 1 && count_window()) {
+                    const unsigned g = unsigned(std::min<uint64_t>((b.E + 4 * kC2Range - 1) / (4 * kC2Range), 1u << 16));
+                    hipLaunchKernelGGL(k_count2, dim3(g), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid,
+                                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, member_lo(b),
+                                       member_hi(b), cnt.as<uint32_t>(), d_tests.as<unsigned long long>());
+                } else {
+                    FSM_W_DISPATCH(W, FSM_COUNT)
+                }
 #undef FSM_COUNT
                 FSM_LAUNCHED("k_count", s);
                 clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));

@@ -154,3 +154,6 @@ def test_bench_two_ranks_dry_run(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0
     assert d["extra"]["patterns"] == FULL["c3"]["digest"]["n"] and d["extra"]["joins"] == FULL["c3"]["joins"]
+    pr = d["extra"]["per_rank"]  # the per-rank trace: each rank mined its share of the classes
+    assert [r["rank"] for r in pr] == [0, 1] and all(r["classes"] > 0 for r in pr)
+    assert sum(r["classes"] for r in pr) > max(r["classes"] for r in pr)

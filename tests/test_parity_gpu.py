@@ -434,16 +434,21 @@ def test_timestamp_limit(eng, fsm):
     assert ei.value.code == fsm.FSM_ELIMIT and "65536" in str(ei.value)
 
 
-@pytest.mark.parametrize("path", ["keys", "atomic", "default"])
-@pytest.mark.parametrize("shape", ["quest", "sign", "bible", "sign-low"])
+@pytest.mark.parametrize("path", ["keys", "atomic", "atomic-thread", "default"])
+@pytest.mark.parametrize("shape", ["quest", "sign", "bible", "sign-low", "wide"])
 def test_count_paths_agree(eng, path, shape, monkeypatch):
     """Class counting: the keyed count (group-aligned counter layout, u16 keys
     in (group, block) regions, LDS counting, counters written out) forced on
-    every batch, the global-atomic k_count, and the default size switch give
-    the oracle's patterns and joins, and the same executed pair tests."""
+    every batch, the global-atomic count (k_count2's run windows at W = 1, runs
+    over 64 entries thread-per-entry; or k_count thread-per-entry throughout,
+    FSM_COUNT_KERNEL=thread), and the default size switch give the oracle's
+    patterns and joins, and the same executed pair tests."""
     from oracle import oracle
     from tools import gen
-    if path != "default":
+    if path == "atomic-thread":
+        monkeypatch.setenv("FSM_COUNT_PATH", "atomic")
+        monkeypatch.setenv("FSM_COUNT_KERNEL", "thread")
+    elif path != "default":
         monkeypatch.setenv("FSM_COUNT_PATH", path)
     if shape == "quest":
         ds, sup = gen.quest(20000, seed=9), 0.003
@@ -451,6 +456,8 @@ def test_count_paths_agree(eng, path, shape, monkeypatch):
         ds, sup = gen.sign(seed=2).head(400), 0.3
     elif shape == "bible":
         ds, sup = gen.bible(seed=2).head(1500), 0.03
+    elif shape == "wide":  # runs of more than 64 entries at W = 1
+        ds, sup = _wide_runs_db(), 0.05
     else:  # low support: first-level classes whose counter matrix spans several groups
         ds, sup = gen.sign(seed=3).head(60), 0.08
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
