@@ -2,13 +2,17 @@
 same host (the BASELINE.md table).  bench.py is the driver's one-line contract
 (config 3); this is the per-config sweep, run on the GPU box:
 
-    python tools/bench_configs.py [--only c2,c4] [--cpu-seconds 20] > gpurun_out/configs.jsonl
+    python tools/bench_configs.py [--only c2,c4] [--cpu-reps 3] > gpurun_out/configs.jsonl
 
 One JSON line per config.  GPU: median of 3 timed fsm_*_mine calls after one
-warmup, DB resident in HBM.  CPU: oracle/fsm_oracle.c, 1 thread, same DB and
-parameters, bounded to --cpu-seconds (SPADE: joins/s over the completed part;
-TSR: a full run on the largest sequence prefix that completes in the bound,
-with the GPU timed on that same prefix as well).
+warmup, DB resident in HBM.  CPU: oracle/fsm_oracle.c on the same DB and
+parameters, 1 thread and every CPU of this process's share:
+  SPADE c1, c2, c5: complete mines (median of --cpu-reps), lattice seconds
+                    (F1 vertical build excluded, as the GPU's flatten + upload)
+  SPADE c3:         a class-stride sample (every 128th first-level class mined
+                    completely, 1 thread; every 8th on all CPUs): joins/s
+  TSR c4:           a full run on the largest sequence prefix that completes
+                    in --cpu-seconds, the GPU timed on that same prefix too.
 """
 import argparse
 import json
@@ -58,26 +62,58 @@ def time_gpu(fn, reps=3, warmup=True):
     return statistics.median(ts), out
 
 
-def run_spade(eng, fsm, name, ds, sup, cpu_s):
+def cpu_share():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_spade(ds, sup, reps, threads, stride):
     from oracle import oracle
+    runs = [oracle.spade_tokens(ds.seq_off, ds.tokens, sup, want_patterns=False, threads=threads, stride=stride)
+            for _ in range(reps)]
+    lat = [r["seconds"] - r["seconds_f1"] for r in runs]
+    return {"threads": threads, "class_stride": stride, "reps": reps, "complete": all(r["complete"] for r in runs),
+            "joins": runs[0]["joins"], "seconds_total": [round(r["seconds"], 3) for r in runs],
+            "seconds_lattice": [round(v, 3) for v in lat], "seconds_lattice_median": statistics.median(lat),
+            "joins_per_s": statistics.median(r["joins"] / max(v, 1e-9) for r, v in zip(runs, lat))}
+
+
+def run_spade(eng, fsm, name, ds, sup, cpu_reps):
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
     prep = eng.stats()
     ms, (csr, meta) = time_gpu(lambda: eng.spade_csr(db, sup))
     st = eng.stats()
     ks = sorted(eng.kernel_stats(), key=lambda k: -k["ms"])[:4]
     db.free()
-    log("%s: GPU %.2f ms; CPU restatement (bound %.0f s)" % (name, ms, cpu_s))
-    r = oracle.spade_tokens(ds.seq_off, ds.tokens, sup, time_limit_s=cpu_s, want_patterns=False)
-    return {"config": name, "algo": "SPADE", "dataset": ds.name, "sequences": len(ds), "minsup": sup,
-            "minsup_abs": meta["minsup"], "gpu_mine_ms": ms, "patterns": meta["n"], "joins": st["joins"],
-            "gpu_joins_per_s": st["joins"] / (ms / 1000.0), "mask_words": st["mask_words"],
-            "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
-            "top_kernels": [{"name": k["name"], "ms": round(k["ms"], 3),
-                             "GBps": round(k["alg_bytes"] / 1e9 / (k["ms"] / 1e3), 1) if k["ms"] else 0}
-                            for k in ks],
-            "cpu_1thr_joins_per_s": r["joins"] / r["seconds"], "cpu_complete": r["complete"],
-            "cpu_seconds": r["seconds"], "cpu_joins": r["joins"],
-            "speedup_joins_per_s": (st["joins"] / (ms / 1000.0)) / (r["joins"] / r["seconds"])}
+    nt = cpu_share()
+    sampled = name == "c3"  # the complete single-thread mine takes most of an hour
+    log("%s: GPU %.2f ms; CPU restatement (%s)" % (name, ms, "class-stride sample" if sampled else "complete"))
+    c1 = cpu_spade(ds, sup, 1 if sampled else cpu_reps, 1, 128 if sampled else 1)
+    ca = cpu_spade(ds, sup, 1 if sampled else cpu_reps, nt, 8 if sampled else 1) if nt > 1 else None
+    out = {"config": name, "algo": "SPADE", "dataset": ds.name, "sequences": len(ds), "minsup": sup,
+           "minsup_abs": meta["minsup"], "gpu_mine_ms": ms, "patterns": meta["n"], "joins": st["joins"],
+           "gpu_joins_per_s": st["joins"] / (ms / 1000.0), "mask_words": st["mask_words"],
+           "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
+           "top_kernels": [{"name": k["name"], "ms": round(k["ms"], 3),
+                            "GBps": round(k["alg_bytes"] / 1e9 / (k["ms"] / 1e3), 1) if k["ms"] else 0}
+                           for k in ks],
+           "cpu_1thr": c1, "cpu_all_cores": ca, "cpu_share": nt}
+    out["speedup_vs_cpu_1thr_joins_per_s"] = out["gpu_joins_per_s"] / c1["joins_per_s"]
+    if not sampled:
+        out["speedup_vs_cpu_1thr_time"] = c1["seconds_lattice_median"] * 1000.0 / ms
+        if ca:
+            out["speedup_vs_cpu_all_cores_time"] = ca["seconds_lattice_median"] * 1000.0 / ms
+    return out
 
 
 def run_tsr(eng, fsm, name, ds, params, cpu_s):
@@ -119,7 +155,8 @@ def run_tsr(eng, fsm, name, ds, params, cpu_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="bound of the TSR prefix runs")
+    ap.add_argument("--cpu-reps", type=int, default=1, help="complete SPADE CPU mines per config (median)")
     ap.add_argument("--verbose", action="store_true", help="engine progress on stderr (long TSR runs)")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime per process, see _lib.py)
@@ -130,7 +167,10 @@ def main():
             algo, shape, kw, par = CONFIGS[name]
             log("%s: generating %s" % (name, shape))
             ds = dataset(shape, kw)
-            res = (run_spade if algo == "spade" else run_tsr)(eng, fsm, name, ds, par, args.cpu_seconds)
+            if algo == "spade":
+                res = run_spade(eng, fsm, name, ds, par, args.cpu_reps)
+            else:
+                res = run_tsr(eng, fsm, name, ds, par, args.cpu_seconds)
             print(json.dumps(res), flush=True)
 
 

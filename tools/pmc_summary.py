@@ -24,8 +24,10 @@ def kernel_name(demangled):
     base, targs = m.group(1), m.group(3) or ""
     if base == "k_emit":
         return "k_emit<write>" if "true" in targs else "k_emit<count>"
-    if base == "k_emit1":  # the one-pass emit: fsm_get_kernel_stats calls it "k_emit"
+    if base in ("k_emit1", "k_emit2"):  # the emit kernels: fsm_get_kernel_stats times them as "k_emit"
         return "k_emit"
+    if base == "k_count2":  # the window count: timed as "k_count"
+        return "k_count"
     return base
 
 
