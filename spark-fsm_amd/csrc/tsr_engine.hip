@@ -781,35 +781,59 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
     if (pass == 0 && threadIdx.x == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
 }
 
-// Sum each slot's partial rows per kid; keep the counts >= t (records to mapped
-// pinned host memory, any order: the host sorts them by item) and queue the
-// left extensions for k_dl.  grid = (blocks per slot, slots, kid passes).
+// Sum each slot's partial rows per kid and keep the counts >= t: block x of
+// (slot, pass) owns the kid range [x q, (x + 1) q) of the pass (q = ceil(KP /
+// gridDim.x)) and writes its kept records IN KID ORDER from that range's start
+// (block-ordered ballot compaction), with the count in rcnt, so the host takes
+// every slot's records in item order without sorting.  Left extensions are
+// queued for k_dl.  grid = (blocks per slot, slots, kid passes).
 __global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __restrict__ part,
                                                           const uint64_t* __restrict__ blk_off, ExpGeo geo,
                                                           const uint32_t* __restrict__ kept,
                                                           ExpCtl* __restrict__ ctlb, ExpRec* __restrict__ outb,
                                                           uint32_t cap, uint4* __restrict__ dlw,
-                                                          uint32_t* __restrict__ ndlw) {
+                                                          uint32_t* __restrict__ ndlw, uint32_t* __restrict__ rcnt) {
+    __shared__ uint32_t wsum[kBlock / 64];
     const uint32_t b = blockIdx.y, pass = blockIdx.z, KP = geo.KP, kid_lo = pass * KP;
     const uint64_t r0 = blk_off[b], r1 = blk_off[b + 1];
-    ExpCtl* ctl = ctlb + b;
-    ExpRec* out = outb + uint64_t(b) * cap;
+    const uint32_t q = (KP + gridDim.x - 1) / gridDim.x;
+    const uint32_t c0 = blockIdx.x * q, c1 = min(KP, c0 + q);
+    ExpRec* out = outb + uint64_t(b) * cap + kid_lo + c0;  // this range's records, from its start
     const uint32_t* rows = part + uint64_t(pass) * geo.nblk * 2 * KP;
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < KP && kid_lo + c < geo.K; c += gridDim.x * blockDim.x) {
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    uint32_t n = 0;  // records written by this block (block-uniform)
+    for (uint32_t cb = c0; cb < c1; cb += blockDim.x) {
+        const uint32_t c = cb + threadIdx.x;
         uint32_t tl = 0, tr = 0;
-        for (uint64_t r = r0; r < r1; ++r) {
-            tl += rows[r * 2 * KP + c];
-            tr += rows[r * 2 * KP + KP + c];
-        }
-        if (tl >= geo.t || tr >= geo.t) {
-            const uint32_t it = kept[kid_lo + c];
-            const uint32_t idx = atomicAdd(&ctl->nout, 1u);
-            if (idx < cap) {
-                out[idx] = ExpRec{it, tl, 0u, tr};
-                // |sids(X u {c})| of a left extension comes from k_dl
-                if (tl >= geo.t) dlw[atomicAdd(ndlw, 1u)] = make_uint4(b, it, idx, 0u);
+        bool keep = false;
+        if (c < c1 && kid_lo + c < geo.K) {
+            for (uint64_t r = r0; r < r1; ++r) {
+                tl += rows[r * 2 * KP + c];
+                tr += rows[r * 2 * KP + KP + c];
             }
+            keep = tl >= geo.t || tr >= geo.t;
         }
+        const uint64_t bal = __ballot(keep);
+        if (lane == 0) wsum[wv] = uint32_t(__popcll(bal));
+        __syncthreads();
+        uint32_t at = n, tot = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+            at += k < wv ? wsum[k] : 0u;
+            tot += wsum[k];
+        }
+        if (keep) {
+            const uint32_t idx = at + uint32_t(__popcll(bal & lanemask_lt()));
+            const uint32_t it = kept[kid_lo + c];
+            out[idx] = ExpRec{it, tl, 0u, tr};
+            // |sids(X u {c})| of a left extension comes from k_dl
+            if (tl >= geo.t) dlw[atomicAdd(ndlw, 1u)] = make_uint4(b, it, kid_lo + c0 + idx, 0u);
+        }
+        n += tot;
+        __syncthreads();  // wsum is rewritten next round
+    }
+    if (threadIdx.x == 0) {
+        rcnt[(uint64_t(b) * gridDim.z + pass) * gridDim.x + blockIdx.x] = n;
+        if (n) atomicAdd(&ctlb[b].nout, n);
     }
 }
 
@@ -1427,6 +1451,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // the histograms (list path: per-slot HBM arrays; bitmap path: per-block partial
     // rows and the domain lists), the results (mapped pinned host memory, at most
     // ecap records per slot) and its own events (completion, per-kernel timing).
+    const TsrGrid grid;
     struct ExpSet {
         DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part, dom;
         std::unique_ptr<PinnedBuf> stage, pin;
@@ -1436,6 +1461,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         uint64_t *d_drv = nullptr, *d_wave = nullptr;
         ExpHdr *h_hdr = nullptr, *d_hdr = nullptr;
         ExpRec *h_rec = nullptr, *d_rec = nullptr;
+        uint32_t *h_rcnt = nullptr, *d_rcnt = nullptr;  // bitmap path: records per reduce block
         std::vector<Rule*> batch;
         std::vector<char> drv_in_x;
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
@@ -1475,11 +1501,15 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.d_drv = reinterpret_cast<uint64_t*>(x.d_stage.as<char>() + kSidesB);
         x.d_wave = x.d_drv + (B + 1);
         x.d_ndlw.alloc(16);
-        x.pin = std::make_unique<PinnedBuf>(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec));
+        // [headers | records, ecap per slot | bitmap path: reduce region counts, B x P x collect]
+        const size_t nrc = use_bm ? size_t(B) * P * grid.collect : 0;
+        x.pin = std::make_unique<PinnedBuf>(B * sizeof(ExpHdr) + B * size_t(ecap) * sizeof(ExpRec) + nrc * 4);
         x.h_hdr = static_cast<ExpHdr*>(x.pin->host);
         x.h_rec = reinterpret_cast<ExpRec*>(x.h_hdr + B);
+        x.h_rcnt = reinterpret_cast<uint32_t*>(x.h_rec + size_t(B) * ecap);
         x.d_hdr = static_cast<ExpHdr*>(x.pin->dev);
         x.d_rec = reinterpret_cast<ExpRec*>(x.d_hdr + B);
+        x.d_rcnt = reinterpret_cast<uint32_t*>(x.d_rec + size_t(B) * ecap);
         for (int q = 0; q < 5; ++q) FSM_HIP(hipEventCreate(&x.ev[q]));
         FSM_HIP(hipEventCreateWithFlags(&x.ev[5], hipEventDisableTiming));
     }
@@ -1494,10 +1524,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     double last_log_ms = now_ms();  // verbose progress line every 20 s
     double prep_ms = 0, post_ms = 0, commit_ms = 0, pop_ms = 0;  // host time split (verbose summary)
-    std::vector<Side> sides;
-    std::vector<uint64_t> drv_off, wave_off;
 
-    const TsrGrid grid;
     const uint64_t exp_spb = [] {  // bitmap path: target domain sids per expansion block (FSM_TSR_SPB, tuning)
         const char* v = std::getenv("FSM_TSR_SPB");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
@@ -1557,8 +1584,20 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (r->dropped) continue;  // a speculated child its parent's commit did not register
             ExpResult& res = cache[r];
             const ExpRec* rec = x.h_rec + size_t(k) * ecap;
-            res.recs.assign(rec, rec + h.nout);
-            std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
+            if (use_bm) {  // the reduce blocks' kid ranges, in kid (= item) order
+                res.recs.clear();
+                res.recs.reserve(h.nout);
+                const uint32_t* rc = x.h_rcnt + size_t(k) * P * grid.collect;
+                const uint32_t q = (KP + grid.collect - 1) / grid.collect;
+                for (uint32_t p = 0; p < P; ++p)
+                    for (uint32_t g = 0; g < grid.collect; ++g) {
+                        const ExpRec* r0 = rec + size_t(p) * KP + size_t(g) * q;
+                        res.recs.insert(res.recs.end(), r0, r0 + rc[p * grid.collect + g]);
+                    }
+            } else {
+                res.recs.assign(rec, rec + h.nout);
+                std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
+            }
         }
         seg[2].bytes += int64_t(nout_all * sizeof(ExpRec));
         x.timed = false;
@@ -1582,14 +1621,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.seq = seq_next++;
         gpu_rules += nb;
         for (Rule* r : batch) inflight[r] = int(xp - xs);
-        sides.assign(nb, Side{});
-        drv_off.assign(nb + 1, 0);
-        wave_off.assign(nb + 1, 0);
+        // descriptors written in place into the set's pinned stage (only the used items:
+        // the kernels read X[0, nx) and Y[0, ny))
+        uint64_t* drv_off = x.h_drv;
+        uint64_t* wave_off = x.h_wave;
+        drv_off[0] = wave_off[0] = 0;
         x.drv_in_x.assign(nb, 1);
         for (uint32_t k = 0; k < nb; ++k) {
             const Rule* r = batch[k];
             const uint32_t *rx = rp.st.X(r), *ry = rp.st.Y(r);
-            Side& sd = sides[k];
+            Side& sd = x.h_sides[k];
             sd.nx = r->nx;
             sd.ny = r->ny;
             sd.doL = r->expandLR;
@@ -1634,9 +1675,6 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.blocks = wave_off[nb];
         if (use_bm && x.dom.bytes < drv_off[nb] * sizeof(uint2))
             x.dom.alloc(std::max<uint64_t>(drv_off[nb] * sizeof(uint2) * 5 / 4, uint64_t(1) << 20));
-        std::memcpy(x.h_sides, sides.data(), nb * sizeof(Side));
-        std::memcpy(x.h_drv, drv_off.data(), (nb + 1) * 8);
-        std::memcpy(x.h_wave, wave_off.data(), (nb + 1) * 8);
         FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
         x.timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
         const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
@@ -1661,7 +1699,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
             hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
                                x.d_wave, geo, d_kept.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_rec, ecap,
-                               x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>());
+                               x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>(), x.d_rcnt);
             FSM_LAUNCHED("k_expand_reduce", s);
             if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
             hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
