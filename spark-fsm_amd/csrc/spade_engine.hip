@@ -704,6 +704,33 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
     }
 }
 
+// Child class of every member slot x of a batch, from its kids CSR (unsharded
+// runs): the children are created in slot order, one per slot with kids except
+// a slot whose only kid is an itemset-extension (count_and_freq), so the child
+// index of slot x is the number of such slots before it.  k_child_flag marks
+// them, a scan numbers them, k_child_of writes the index relative to the
+// emitted group [ga, gb) or kNone (no host table, no upload per emit).
+__device__ __forceinline__ uint32_t child_flag(const uint32_t* __restrict__ koff, const uint32_t* __restrict__ kslot,
+                                               uint32_t x) {
+    const uint32_t a = koff[x], n = koff[x + 1] - a;
+    return n > 1 || (n == 1 && (kslot[a] & 1u) == kSeq) ? 1u : 0u;
+}
+__global__ __launch_bounds__(kBlock) void k_child_flag(const uint32_t* __restrict__ koff,
+                                                       const uint32_t* __restrict__ kslot, uint32_t n,
+                                                       uint32_t* __restrict__ flag) {
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x)
+        flag[x] = child_flag(koff, kslot, x);
+}
+__global__ __launch_bounds__(kBlock) void k_child_of(const uint32_t* __restrict__ koff,
+                                                     const uint32_t* __restrict__ kslot,
+                                                     const uint64_t* __restrict__ pre, uint32_t n, uint32_t ga,
+                                                     uint32_t gb, uint32_t* __restrict__ child_of) {
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+        const uint32_t c = uint32_t(pre[x]);
+        child_of[x] = child_flag(koff, kslot, x) && c >= ga && c < gb ? c - ga : kNone;
+    }
+}
+
 // Ordered frequent extraction (large batches): k_freq_count -> scan -> k_freq_write
 // gives the records in (row, slot) order with their child ids, no host ordering.
 __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ rows, uint32_t nrows,
@@ -1522,6 +1549,7 @@ struct Batch {
     const uint32_t* kid_off = nullptr;
     const uint32_t* kid_slot = nullptr;
     const uint32_t* kid_cid = nullptr;
+    DevBuf child_pre;  // unsharded: u64 exclusive scan of "member slot has a child class" (emit's child_of)
     uint64_t E = 0;                     // entries in the slab (runs of all classes, any order)
     uint64_t n_cnt = 0, cbase_total = 0;
     std::vector<uint32_t> rank_item;  // member tables of cls (see ClassMeta)
@@ -1548,6 +1576,7 @@ struct Batch {
         h_cls.clear();
         d_cls.release();
         kid_tab.release();
+        child_pre.release();
         kid_off = kid_slot = kid_cid = nullptr;
         E = n_cnt = cbase_total = 0;
         rank_item.clear();
@@ -1591,7 +1620,14 @@ struct Miner {
 
     double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
     // FSM_HOST_TRACE=1: host time of the bookkeeping phases, printed at the end of the mine
-    double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f2 sort, kids, children, groups, emit tables, slab alloc, count prep, count
+    double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // finer host split (FSM_HOST_TRACE): lap(i, t) adds the time since t to hq[i] and restarts t
+    double hq[16] = {};
+    void lap(int i, double& t) {
+        const double n = now_ms();
+        hq[i] += n - t;
+        t = n;
+    }  // f2 sort, kids, children, groups, emit tables, slab alloc, count prep, count
 
     // Sharded mining: the work between two collectives runs through
     // run_or_defer; agree() before the next collective (comm.h Agreement)
@@ -1819,6 +1855,15 @@ struct Miner {
         const char* v = std::getenv("FSM_EMIT_PATH");
         return !(v && !std::strcmp(v, "chunk"));
     }
+    // emit's child_of table: built on the device for unsharded batches of at least 2^17
+    // member slots (below that the launches cost more than the host fill + copy);
+    // FSM_CHILD_OF=host / device forces either (tests, A/B)
+    static bool child_of_device(uint64_t slots) {
+        const char* v = std::getenv("FSM_CHILD_OF");
+        if (v && !std::strcmp(v, "host")) return false;
+        if (v && !std::strcmp(v, "device")) return true;
+        return slots >= (uint64_t(1) << 17);
+    }
     // LDS join records per wave of k_emit2 (FSM_EMIT_CAP lowers it too: tests of the overflow path)
     static uint32_t emit2_cap() {
         const char* v = std::getenv("FSM_EMIT_CAP");
@@ -1952,12 +1997,14 @@ struct Miner {
     // batches; same tables, same node ids: node of record q = first + q).  Rows of
     // records -> per-row sizes (parallel) -> table offsets (prefix) -> fill (parallel).
     void children_parallel(Batch& b, const FreqRec* R, uint64_t nfreq, const std::vector<DRow>& rows) {
+        double tl = now_ms();
         std::vector<uint64_t> gs;  // first record of each row group
         gs.reserve(nfreq / 2 + 2);
         for (uint64_t q = 0; q < nfreq; ++q)
             if (q == 0 || R[q].row != R[q - 1].row) gs.push_back(q);
         const int64_t ng = int64_t(gs.size());
         gs.push_back(nfreq);
+        lap(0, tl);
         const int64_t nthr = host_threads();
         std::vector<uint32_t> r2(size_t(ng) + 1, 0);
         std::vector<uint8_t> keep(size_t(ng), 0);
@@ -1976,11 +2023,14 @@ struct Miner {
             ri[size_t(i) + 1] = ri[size_t(i)] + r2[size_t(i)];
             kidx[size_t(i) + 1] = kidx[size_t(i)] + keep[size_t(i)];
         }
+        lap(1, tl);
         b.child_rank_item.assign(ri[size_t(ng)], 0u);
         b.child_node_of.assign(2 * ri[size_t(ng)], -1);
+        lap(2, tl);
         b.children.resize(kidx[size_t(ng)]);
         const size_t node0 = nodes.size();
         nodes.grow(nfreq);
+        lap(3, tl);
         std::vector<int64_t> jb(size_t(nthr), 0);
         std::vector<int> bad(size_t(nthr), 0);
         par_slices(nthr, ng, [&](int64_t t, int64_t i0, int64_t i1) {
@@ -2015,6 +2065,7 @@ struct Miner {
             }
             jb[size_t(t)] = acc;
         });
+        lap(4, tl);
         for (int64_t t = 0; t < nthr; ++t) {
             if (bad[size_t(t)] & 1) throw Error(FSM_ELIMIT, "SPADE: a pattern exceeds 65534 items");
             if (bad[size_t(t)] & 2) throw Error(FSM_ELIMIT, "SPADE: a prefix class has more than 65535 frequent children");
@@ -2025,9 +2076,12 @@ struct Miner {
     // count kernel + frequent-candidate extraction; fills b.children / b.groups / kids
     void count_and_freq(Batch& b) {
         const double tc0 = now_ms();
+        double tl = tc0;
         dump(b);
         const int cmode = count_mode(b);
+        lap(5, tl);
         const bool keyed_layout = prepare(b, cmode != 0);
+        lap(6, tl);
         const bool shard = comm && b.root;  // root rows split over ranks, frequent pairs all-gathered
         const int64_t ncls = int64_t(b.cls.size());
         const int64_t nthr = ncls >= (int64_t(1) << 15) ? host_threads() : 1;
@@ -2055,6 +2109,7 @@ struct Miner {
             }
             ctx->stats.classes += ncls;
         }
+        lap(7, tl);
         fsm_stats& st = ctx->stats;
         st.batches += 1;
         const uint64_t tot_ent = b.E;
@@ -2090,6 +2145,7 @@ struct Miner {
         const FreqRec* ext = nullptr;  // ordered extraction: the records in pinned host memory
         uint64_t ext_n = 0;
         DevBuf cnt;
+        lap(8, tl);
         hp[6] += now_ms() - tc0;  // prepare + stats + rows
         const double tc1 = now_ms();
         auto compute = [&] {
@@ -2212,6 +2268,8 @@ struct Miner {
         uint32_t* koff = ktab.data();
         uint32_t* kslot = koff + nko;
         uint32_t* kcid = kslot + nfreq;
+        double tl2 = th;
+        lap(9, tl2);
         // records are in (row, slot) order, and a row's member slot cbase + mi ascends
         // with the row: koff[x] = records of slots < x, by a merge (threads split x)
         auto slot_of = [&](uint64_t q) { return uint64_t(b.cls[rows[R[q].row].cls].cbase) + rows[R[q].row].mi; };
@@ -2234,7 +2292,9 @@ struct Miner {
                 kcid[q] = R[q].cid;
             }
         });
+        lap(10, tl2);
         upload_staged(2, b.kid_tab, ktab.data(), ktab.size() * 4);
+        lap(11, tl2);
         b.kid_off = b.kid_tab.as<uint32_t>();
         b.kid_slot = b.kid_off + nko;
         b.kid_cid = b.kid_slot + nfreq;
@@ -2385,8 +2445,12 @@ struct Miner {
     void emit(Batch& b, size_t g, Batch& nb) {
         const double th = now_ms();
         const auto [ga, gb] = b.groups[g];
+        // unsharded, large batches: the child class of each member slot comes from the kids
+        // CSR on the device (k_child_of); sharded runs keep only their share of the
+        // children, so the host builds the table
+        const bool dev_child_of = comm == nullptr && child_of_device(b.cbase_total);
         std::vector<uint32_t>& child_of = child_of_s;
-        child_of.assign(b.cbase_total, kNone);
+        if (!dev_child_of) child_of.assign(b.cbase_total, kNone);
         uint64_t total = 0;
         // the only group: the children and their member tables move over whole (swapped:
         // the parent, released after this emit and recycled, keeps nb's old capacity)
@@ -2407,7 +2471,7 @@ struct Miner {
             par_slices(nthr, n, [&](int64_t t, int64_t k0, int64_t k1) {
                 uint64_t acc = 0;
                 for (int64_t k = k0; k < k1; ++k) {
-                    co[pc[cc[k].pcls].cbase + cc[k].pmi] = uint32_t(k);
+                    if (!dev_child_of) co[pc[cc[k].pcls].cbase + cc[k].pmi] = uint32_t(k);
                     acc += cc[k].cap;
                 }
                 tt[size_t(t)] = acc;
@@ -2425,7 +2489,7 @@ struct Miner {
                                     b.child_rank_item.begin() + int64_t(ch.ri_off + ch.D / 2));
                 nb.node_of.insert(nb.node_of.end(), b.child_node_of.begin() + int64_t(ch.no_off),
                                   b.child_node_of.begin() + int64_t(ch.no_off + ch.D));
-                child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
+                if (!dev_child_of) child_of[b.cls[ch.pcls].cbase + ch.pmi] = uint32_t(k - ga);
                 total += ch.cap;
             }
         }
@@ -2436,7 +2500,27 @@ struct Miner {
         hp[5] += now_ms() - th2;
         nb.E = total;
         DevBuf d_child_of, d_long;  // (freed into the stream-ordered pool: later launches on this stream reuse them)
-        upload_staged(3, d_child_of, child_of.data(), child_of.size() * 4);
+        if (dev_child_of) {
+            const uint32_t n = uint32_t(b.cbase_total);
+            d_child_of.alloc(std::max<size_t>(n, 1) * 4);
+            if (n) {
+                if (b.child_pre.p == nullptr) {  // the slot numbering, once per batch (every group reuses it)
+                    DevBuf flag(size_t(n) * 4);
+                    b.child_pre.alloc((size_t(n) + 1) * 8);
+                    const unsigned gr = unsigned(std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192));
+                    hipLaunchKernelGGL(k_child_flag, dim3(gr), dim3(kBlock), 0, s, b.kid_off, b.kid_slot, n,
+                                       flag.as<uint32_t>());
+                    FSM_LAUNCHED("k_child_flag", s);
+                    scan_exclusive(flag.as<uint32_t>(), b.child_pre.as<uint64_t>(), n, s);
+                }
+                const unsigned gr = unsigned(std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192));
+                hipLaunchKernelGGL(k_child_of, dim3(gr), dim3(kBlock), 0, s, b.kid_off, b.kid_slot,
+                                   b.child_pre.as<uint64_t>(), n, uint32_t(ga), uint32_t(gb), d_child_of.as<uint32_t>());
+                FSM_LAUNCHED("k_child_of", s);
+            }
+        } else {
+            upload_staged(3, d_child_of, child_of.data(), child_of.size() * 4);
+        }
         ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
         if (b.E) {
             const SlabPtrs sp = b.slab.ptrs();
@@ -2833,6 +2917,11 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         std::fprintf(stderr, "[fsm host] f2 sort %.3f, kids %.3f, children %.3f, groups %.3f, emit tables %.3f, "
                      "slab alloc %.3f, count prep %.3f, count+extract %.3f, gpu wait %.3f ms\n", mn.hp[0], mn.hp[1],
                      mn.hp[2], mn.hp[3], mn.hp[4], mn.hp[5], mn.hp[6], mn.hp[7], mn.wait_ms);
+    if (const char* v = std::getenv("FSM_HOST_TRACE"); v && v[0] == '1') {
+        std::fprintf(stderr, "[fsm host laps]");
+        for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %d:%.2f", i, mn.hq[i]);
+        std::fprintf(stderr, "\n");
+    }
     clock.finish(ctx->kstats);
     for (const fsm_kernel_stat& k : ctx->kstats) {
         const std::string nm = k.name;

@@ -1,10 +1,28 @@
 """Engine: one fsm_ctx (HIP stream + device buffers) and its flattened DBs."""
 import ctypes
+import weakref
 
 import numpy as np
 
 from . import _lib
 from ._lib import MODE_SPADE, MODE_TSR, check
+
+
+class _ResultOwner:
+    """Keeps a libfsm result struct alive while numpy views of its arrays exist:
+    every view's buffer holds a reference to this object, whose finalizer calls
+    the library's free function once the last view is gone."""
+
+    def __init__(self, free_fn, ptr):
+        weakref.finalize(self, free_fn, ptr)
+
+    def view(self, ptr, n, dtype):
+        dt = np.dtype(dtype)
+        if n <= 0 or not ptr:
+            return np.zeros(0, dtype=dt)
+        buf = (np.ctypeslib.as_ctypes_type(dt) * int(n)).from_address(ctypes.addressof(ptr.contents))
+        buf._owner = self
+        return np.frombuffer(buf, dtype=dt)
 
 
 class Engine:
@@ -97,20 +115,22 @@ class Engine:
 
     # ------------------------------------------------------------ mining
     def spade_csr(self, db, support, dfs=True):
-        """fsm_spade_mine -> CSR numpy arrays (support, pat_off, set_off, items), meta."""
+        """fsm_spade_mine -> CSR numpy arrays (support, pat_off, set_off, items), meta.
+
+        The arrays are views of the library's result buffers (no copy of the
+        hundreds of MB a dense mine returns); fsm_patterns_free runs when the
+        last of them is garbage-collected."""
         out = ctypes.POINTER(_lib.Patterns)()
         check(self._L.fsm_spade_mine(self._ctx, db.handle, float(support), 1 if dfs else 0,
                                      ctypes.byref(out)), self._ctx)
-        try:
-            p = out.contents
-            n = p.n
-            sup = np.ctypeslib.as_array(p.support, shape=(max(n, 1),))[:n].copy() if n else np.zeros(0, np.int32)
-            po = np.ctypeslib.as_array(p.pat_off, shape=(n + 1,)).copy()
-            so = np.ctypeslib.as_array(p.set_off, shape=(p.n_sets + 1,)).copy()
-            it = np.ctypeslib.as_array(p.items, shape=(max(p.n_items, 1),))[:p.n_items].copy()
-            meta = {"total": p.total, "minsup": p.minsup, "n": n}
-        finally:
-            self._L.fsm_patterns_free(out)
+        owner = _ResultOwner(self._L.fsm_patterns_free, out)
+        p = out.contents
+        n = p.n
+        sup = owner.view(p.support, n, np.int32)
+        po = owner.view(p.pat_off, n + 1, np.int64)
+        so = owner.view(p.set_off, p.n_sets + 1, np.int64)
+        it = owner.view(p.items, p.n_items, np.int32)
+        meta = {"total": p.total, "minsup": p.minsup, "n": n}
         return (sup, po, so, it), meta
 
     def spade(self, db, support, dfs=True):

@@ -396,14 +396,15 @@ def _wide_runs_db(seed=5, n=600):
     return gen.DataSet(np.array(so, dtype=np.int64), np.array(tk, dtype=np.int64), "wide-runs")
 
 
-@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some", "chunk"])
+@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some", "chunk", "host-child-of", "device-child-of"])
 @pytest.mark.parametrize("shape", ["quest", "sign", "bible", "wide"])
 def test_emit_paths_agree(eng, path, shape, monkeypatch):
     """Child-run emission: the window kernel k_emit2 (W = 1: runs of <= 64
     entries in registers, longer runs through k_emit1's run list), the chunk
     kernel k_emit1 (FSM_EMIT_PATH=chunk; every W), and their overflow paths
     (records capped at 0 / 17 per wave, so waves join again while writing)
-    give the oracle's patterns and joins."""
+    give the oracle's patterns and joins; so do both builds of the child class
+    table (FSM_CHILD_OF=host, or device: k_child_flag / scan / k_child_of)."""
     from oracle import oracle
     from tools import gen
     if path == "overflow-all":
@@ -412,6 +413,10 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
         monkeypatch.setenv("FSM_EMIT_CAP", "17")
     elif path == "chunk":
         monkeypatch.setenv("FSM_EMIT_PATH", "chunk")
+    elif path == "host-child-of":
+        monkeypatch.setenv("FSM_CHILD_OF", "host")
+    elif path == "device-child-of":
+        monkeypatch.setenv("FSM_CHILD_OF", "device")
     if shape == "quest":
         ds, sup = gen.quest(20000, seed=9), 0.003
     elif shape == "sign":
