@@ -1463,6 +1463,18 @@ struct Slab {
     }
 };
 
+// Allocator whose resize(n) leaves the new elements unwritten (the per-batch tables of
+// millions of classes and nodes are filled by index afterwards, by host threads: a
+// value-initialising resize would write every byte once more, serially)
+template <class T> struct NoInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U> void construct(U*) noexcept {}
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+template <class T> using RawVec = std::vector<T, NoInitAlloc<T>>;
+
 // Per-class member tables live in flat per-batch arrays (no per-class heap
 // vectors: deep lattices have millions of small classes).
 // One record per prefix class.  A batch's children (the classes its frequent
@@ -1542,8 +1554,8 @@ void order_recs(std::vector<FreqRec>& recs, uint32_t nrows) {
 
 struct Batch {
     Slab slab;
-    std::vector<ClassMeta> cls;
-    std::vector<DClass> h_cls;
+    RawVec<ClassMeta> cls;
+    RawVec<DClass> h_cls;
     DevBuf d_cls;
     DevBuf kid_tab;  // frequent children of every member (CSR over cbase + mi): offsets | slots | child ids
     const uint32_t* kid_off = nullptr;
@@ -1552,11 +1564,11 @@ struct Batch {
     DevBuf child_pre;  // unsharded: u64 exclusive scan of "member slot has a child class" (emit's child_of)
     uint64_t E = 0;                     // entries in the slab (runs of all classes, any order)
     uint64_t n_cnt = 0, cbase_total = 0;
-    std::vector<uint32_t> rank_item;  // member tables of cls (see ClassMeta)
-    std::vector<int32_t> node_of;
-    std::vector<ChildInfo> children;
-    std::vector<uint32_t> child_rank_item;  // member tables of children
-    std::vector<int32_t> child_node_of;
+    RawVec<uint32_t> rank_item;  // member tables of cls (see ClassMeta)
+    RawVec<int32_t> node_of;
+    RawVec<ChildInfo> children;
+    RawVec<uint32_t> child_rank_item;  // member tables of children
+    RawVec<int32_t> child_node_of;
     std::vector<std::pair<size_t, size_t>> groups;
     size_t next_group = 0;
     int64_t depth = 1;  // items per member pattern of this batch's classes
@@ -1614,20 +1626,22 @@ struct Miner {
     std::vector<uint8_t> node_dup;  // sharded: nodes of split classes, output by rank 0 only
 
     // host scratch reused by every batch (capacity kept: no fresh pages per batch)
-    std::vector<DRow> rows_s;
+    RawVec<DRow> rows_s;
     std::vector<FreqRec> recs_s;
-    std::vector<uint32_t> ktab_s, child_of_s;
+    RawVec<uint32_t> ktab_s, child_of_s;
+    RawVec<uint64_t> gs_s;
+    RawVec<uint32_t> r2_s;
 
     double wait_ms = 0;  // host time blocked on the stream (the rest of the lattice time is host work)
     // FSM_HOST_TRACE=1: host time of the bookkeeping phases, printed at the end of the mine
-    double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double hp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f2 sort, kids, children, groups, emit tables, slab alloc, count prep, count
     // finer host split (FSM_HOST_TRACE): lap(i, t) adds the time since t to hq[i] and restarts t
     double hq[16] = {};
     void lap(int i, double& t) {
         const double n = now_ms();
         hq[i] += n - t;
         t = n;
-    }  // f2 sort, kids, children, groups, emit tables, slab alloc, count prep, count
+    }
 
     // Sharded mining: the work between two collectives runs through
     // run_or_defer; agree() before the next collective (comm.h Agreement)
@@ -1674,36 +1688,67 @@ struct Miner {
     // boundary with a power-of-two row stride, so no counter row straddles a
     // group).  Returns false (plain layout) when a row exceeds a group.
     bool prepare(Batch& b, bool keyed) {
-        b.h_cls.resize(b.cls.size());
+        const int64_t ncls = int64_t(b.cls.size());
+        // many classes: host-thread slices laid out from 0, then moved to their base (a
+        // keyed slice starts on a group boundary, so the rules above hold across slices)
+        const int64_t nthr = ncls >= (int64_t(1) << 15) ? host_threads() : 1;
+        b.h_cls.resize(size_t(ncls));
+        std::vector<uint64_t> toff(size_t(nthr) + 1, 0), tcb(size_t(nthr) + 1, 0);
+        std::vector<uint8_t> tok(size_t(nthr), 1);
         for (int pass = keyed ? 0 : 1; pass < 2; ++pass) {
             const bool kl = pass == 0;
-            uint64_t off = 0, cb = 0;
-            bool ok = true;
-            for (size_t c = 0; c < b.cls.size() && ok; ++c) {
-                ClassMeta& m = b.cls[c];
-                const uint64_t rows = m.D >> m.mshift;
-                uint32_t stride = m.D;
-                if (kl) {
-                    if (rows * m.D <= kGroupCounters) {
-                        if ((off & (kGroupCounters - 1)) + rows * m.D > kGroupCounters)
+            par_slices(nthr, ncls, [&](int64_t t, int64_t c0, int64_t c1) {
+                uint64_t off = 0, cb = 0;
+                bool ok = true;
+                for (int64_t c = c0; c < c1 && ok; ++c) {
+                    ClassMeta& m = b.cls[size_t(c)];
+                    const uint64_t rows = m.D >> m.mshift;
+                    uint32_t stride = m.D;
+                    if (kl) {
+                        if (rows * m.D <= kGroupCounters) {
+                            if ((off & (kGroupCounters - 1)) + rows * m.D > kGroupCounters)
+                                off = (off + kGroupCounters - 1) & ~uint64_t(kGroupCounters - 1);
+                        } else if (m.D <= kGroupCounters) {
+                            stride = m.D <= 1 ? 1u : 1u << (32 - __builtin_clz(m.D - 1));
                             off = (off + kGroupCounters - 1) & ~uint64_t(kGroupCounters - 1);
-                    } else if (m.D <= kGroupCounters) {
-                        stride = m.D <= 1 ? 1u : 1u << (32 - __builtin_clz(m.D - 1));
-                        off = (off + kGroupCounters - 1) & ~uint64_t(kGroupCounters - 1);
-                    } else {
-                        ok = false;
+                        } else {
+                            ok = false;
+                        }
                     }
+                    m.cnt_off = off;
+                    m.cbase = uint32_t(cb);
+                    off += rows * stride;
+                    cb += m.D;
+                    b.h_cls[size_t(c)] = DClass{m.cnt_off, m.D, m.cbase, m.mshift, stride, {0, 0}};
                 }
-                m.cnt_off = off;
-                m.cbase = uint32_t(cb);
-                off += rows * stride;
-                cb += m.D;
-                b.h_cls[c] = DClass{m.cnt_off, m.D, m.cbase, m.mshift, stride, {0, 0}};
+                toff[size_t(t) + 1] = off;
+                tcb[size_t(t) + 1] = cb;
+                tok[size_t(t)] = ok;
+            });
+            bool ok = true;
+            for (int64_t t = 0; t < nthr; ++t) {
+                ok = ok && tok[size_t(t)];
+                uint64_t next = toff[size_t(t)] + toff[size_t(t) + 1];
+                if (kl && t + 1 < nthr) next = (next + kGroupCounters - 1) & ~uint64_t(kGroupCounters - 1);
+                toff[size_t(t) + 1] = next;
+                tcb[size_t(t) + 1] += tcb[size_t(t)];
             }
             if (!ok) continue;
-            if (cb >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
-            b.n_cnt = off;
-            b.cbase_total = cb;
+            if (tcb[size_t(nthr)] >= kNone) throw Error(FSM_ELIMIT, "SPADE: class batch member space exceeds 2^32");
+            if (nthr > 1)
+                par_slices(nthr, ncls, [&](int64_t t, int64_t c0, int64_t c1) {
+                    const uint64_t bo = toff[size_t(t)];
+                    const uint32_t bc = uint32_t(tcb[size_t(t)]);
+                    for (int64_t c = c0; c < c1; ++c) {
+                        ClassMeta& m = b.cls[size_t(c)];
+                        m.cnt_off += bo;
+                        m.cbase += bc;
+                        b.h_cls[size_t(c)].cnt_off = m.cnt_off;
+                        b.h_cls[size_t(c)].cbase = m.cbase;
+                    }
+                });
+            b.n_cnt = toff[size_t(nthr)];
+            b.cbase_total = tcb[size_t(nthr)];
             upload_staged(0, b.d_cls, b.h_cls.data(), b.h_cls.size() * sizeof(DClass));
             return kl;
         }
@@ -1731,10 +1776,23 @@ struct Miner {
             return v ? uint64_t(std::strtoull(v, nullptr, 10)) : uint64_t(kKeyedMinEntries);
         }();
         if (b.E < min_e) return 0;
+        const int64_t ncls = int64_t(b.cls.size());
+        const int64_t nthr = ncls >= (int64_t(1) << 15) ? host_threads() : 1;
+        std::vector<double> te(size_t(nthr), 0), tn(size_t(nthr), 0);
+        par_slices(nthr, ncls, [&](int64_t t, int64_t c0, int64_t c1) {
+            double e = 0, n = 0;
+            for (int64_t c = c0; c < c1; ++c) {
+                const ClassMeta& m = b.cls[size_t(c)];
+                e += double(m.cap) * double(m.cap) / double(std::max<uint32_t>(m.psup, 1));
+                n += double(m.D >> m.mshift) * double(m.D);
+            }
+            te[size_t(t)] = e;
+            tn[size_t(t)] = n;
+        });
         double est = 0, ncnt = 0;
-        for (const ClassMeta& m : b.cls) {
-            est += double(m.cap) * double(m.cap) / double(std::max<uint32_t>(m.psup, 1));
-            ncnt += double(m.D >> m.mshift) * double(m.D);
+        for (int64_t t = 0; t < nthr; ++t) {
+            est += te[size_t(t)];
+            ncnt += tn[size_t(t)];
         }
         if (ctx->opts.verbose)
             std::fprintf(stderr, "[fsm] batch entries %llu: estimated joins %.3g, counters %.3g\n",
@@ -1994,40 +2052,58 @@ struct Miner {
         return true;
     }
     // The children loop of count_and_freq split over host threads (unsharded, large
-    // batches; same tables, same node ids: node of record q = first + q).  Rows of
-    // records -> per-row sizes (parallel) -> table offsets (prefix) -> fill (parallel).
-    void children_parallel(Batch& b, const FreqRec* R, uint64_t nfreq, const std::vector<DRow>& rows) {
+    // batches; same tables, same node ids: node of record q = first + q).  Every step
+    // runs over the same host-thread slices: row groups of the records (counts, then
+    // positions) -> per-group sizes and per-slice sums -> slice bases -> fill, each
+    // slice initialising its own ranges of the member tables.
+    void children_parallel(Batch& b, const FreqRec* R, uint64_t nfreq, const RawVec<DRow>& rows) {
         double tl = now_ms();
-        std::vector<uint64_t> gs;  // first record of each row group
-        gs.reserve(nfreq / 2 + 2);
-        for (uint64_t q = 0; q < nfreq; ++q)
-            if (q == 0 || R[q].row != R[q - 1].row) gs.push_back(q);
-        const int64_t ng = int64_t(gs.size());
-        gs.push_back(nfreq);
-        lap(0, tl);
         const int64_t nthr = host_threads();
-        std::vector<uint32_t> r2(size_t(ng) + 1, 0);
-        std::vector<uint8_t> keep(size_t(ng), 0);
-        par_slices(nthr, ng, [&](int64_t, int64_t i0, int64_t i1) {
+        std::vector<int64_t> tg(size_t(nthr) + 1, 0);
+        par_slices(nthr, int64_t(nfreq), [&](int64_t t, int64_t q0, int64_t q1) {
+            int64_t c = 0;
+            for (int64_t q = q0; q < q1; ++q) c += q == 0 || R[q].row != R[q - 1].row;
+            tg[size_t(t) + 1] = c;
+        });
+        for (int64_t t = 0; t < nthr; ++t) tg[size_t(t) + 1] += tg[size_t(t)];
+        const int64_t ng = tg[size_t(nthr)];
+        RawVec<uint64_t>& gs = gs_s;  // first record of each row group
+        gs.resize(size_t(ng) + 1);
+        par_slices(nthr, int64_t(nfreq), [&](int64_t t, int64_t q0, int64_t q1) {
+            int64_t at = tg[size_t(t)];
+            for (int64_t q = q0; q < q1; ++q)
+                if (q == 0 || R[q].row != R[q - 1].row) gs[size_t(at++)] = uint64_t(q);
+        });
+        gs[size_t(ng)] = nfreq;
+        lap(0, tl);
+        // r2: member ranks of each group's child (bit 31: the child is kept; a lone
+        // itemset-extension opens no class)
+        RawVec<uint32_t>& r2 = r2_s;
+        r2.resize(size_t(ng));
+        std::vector<uint64_t> tri(size_t(nthr) + 1, 0), tk(size_t(nthr) + 1, 0);
+        par_slices(nthr, ng, [&](int64_t t, int64_t i0, int64_t i1) {
+            uint64_t sri = 0, sk = 0;
             for (int64_t i = i0; i < i1; ++i) {
                 uint32_t maxcid = 0;
                 for (uint64_t q = gs[size_t(i)]; q < gs[size_t(i) + 1]; ++q) maxcid = std::max(maxcid, R[q].cid);
-                r2[size_t(i)] = (maxcid >> 1) + 1;
+                const uint32_t r = (maxcid >> 1) + 1;
                 const uint64_t nch = gs[size_t(i) + 1] - gs[size_t(i)];
-                keep[size_t(i)] = !(nch == 1 && (R[gs[size_t(i)]].slot & 1u) == kItm);
+                const bool keep = !(nch == 1 && (R[gs[size_t(i)]].slot & 1u) == kItm);
+                r2[size_t(i)] = r | (keep ? 0x80000000u : 0u);
+                sri += r;
+                sk += keep;
             }
+            tri[size_t(t) + 1] = sri;
+            tk[size_t(t) + 1] = sk;
         });
-        std::vector<uint64_t> ri(size_t(ng) + 1, 0);
-        std::vector<uint32_t> kidx(size_t(ng) + 1, 0);
-        for (int64_t i = 0; i < ng; ++i) {
-            ri[size_t(i) + 1] = ri[size_t(i)] + r2[size_t(i)];
-            kidx[size_t(i) + 1] = kidx[size_t(i)] + keep[size_t(i)];
+        for (int64_t t = 0; t < nthr; ++t) {
+            tri[size_t(t) + 1] += tri[size_t(t)];
+            tk[size_t(t) + 1] += tk[size_t(t)];
         }
         lap(1, tl);
-        b.child_rank_item.assign(ri[size_t(ng)], 0u);
-        b.child_node_of.assign(2 * ri[size_t(ng)], -1);
-        lap(2, tl);
-        b.children.resize(kidx[size_t(ng)]);
+        b.child_rank_item.resize(tri[size_t(nthr)]);
+        b.child_node_of.resize(2 * tri[size_t(nthr)]);
+        b.children.resize(tk[size_t(nthr)]);
         const size_t node0 = nodes.size();
         nodes.grow(nfreq);
         lap(3, tl);
@@ -2035,8 +2111,10 @@ struct Miner {
         std::vector<int> bad(size_t(nthr), 0);
         par_slices(nthr, ng, [&](int64_t t, int64_t i0, int64_t i1) {
             int64_t acc = 0;
+            uint64_t ri = tri[size_t(t)], kidx = tk[size_t(t)];
             for (int64_t i = i0; i < i1; ++i) {
                 const uint64_t q0 = gs[size_t(i)], q1 = gs[size_t(i) + 1];
+                const uint32_t r = r2[size_t(i)] & 0x7FFFFFFFu;
                 const DRow pr = rows[R[q0].row];
                 const ClassMeta& pm = b.cls[pr.cls];
                 const int32_t parent = b.node_of[pm.no_off + pr.mi];
@@ -2046,10 +2124,12 @@ struct Miner {
                 ChildInfo ch;
                 ch.pcls = pr.cls;
                 ch.pmi = pr.mi;
-                ch.D = 2 * r2[size_t(i)];
-                ch.ri_off = ri[size_t(i)];
-                ch.no_off = 2 * ri[size_t(i)];
+                ch.D = 2 * r;
+                ch.ri_off = ri;
+                ch.no_off = 2 * ri;
                 ch.psup = nodes[size_t(parent)].support;
+                std::fill_n(b.child_rank_item.data() + ri, r, 0u);
+                std::fill_n(b.child_node_of.data() + 2 * ri, 2 * r, -1);
                 for (uint64_t q = q0; q < q1; ++q) {
                     const FreqRec& fr = R[q];
                     const uint32_t item = b.rank_item[pm.ri_off + (fr.slot >> 1)];
@@ -2061,7 +2141,8 @@ struct Miner {
                     if ((fr.slot & 1u) == kSeq) { ++ch.nS; ch.sS += fr.sup; } else { ++ch.nI; ch.sI += fr.sup; }
                     acc += int64_t(12ull * fr.sup);
                 }
-                if (keep[size_t(i)]) b.children[kidx[size_t(i)]] = ch;
+                ri += r;
+                if (r2[size_t(i)] >> 31) b.children[kidx++] = ch;
             }
             jb[size_t(t)] = acc;
         });
@@ -2117,20 +2198,25 @@ struct Miner {
         st.bytes_streamed += int64_t(tot_ent * entry_bytes());
         st.bytes_count_alg += int64_t(tot_ent * entry_bytes());
         // member rows of the counter matrix
-        std::vector<DRow>& rows = rows_s;
+        RawVec<DRow>& rows = rows_s;
         rows.clear();
         if (nthr == 1) {
             for (size_t c = 0; c < b.cls.size(); ++c)
                 for (uint32_t mi = 0; mi < b.cls[c].D; ++mi)
                     if (b.node_of[b.cls[c].no_off + mi] >= 0) rows.push_back(DRow{uint32_t(c), mi});
-        } else {  // a class's rows are its members (nS + nI of them): offsets, then a parallel fill
-            std::vector<uint64_t> ro(size_t(ncls) + 1, 0);
-            for (int64_t c = 0; c < ncls; ++c) ro[size_t(c) + 1] = ro[size_t(c)] + b.cls[size_t(c)].nS + b.cls[size_t(c)].nI;
-            rows.resize(ro[size_t(ncls)]);
-            par_slices(nthr, ncls, [&](int64_t, int64_t c0, int64_t c1) {
+        } else {  // a class's rows are its members (nS + nI of them): slice sums, then a parallel fill
+            std::vector<uint64_t> ro(size_t(nthr) + 1, 0);
+            par_slices(nthr, ncls, [&](int64_t t, int64_t c0, int64_t c1) {
+                uint64_t n = 0;
+                for (int64_t c = c0; c < c1; ++c) n += b.cls[size_t(c)].nS + b.cls[size_t(c)].nI;
+                ro[size_t(t) + 1] = n;
+            });
+            for (int64_t t = 0; t < nthr; ++t) ro[size_t(t) + 1] += ro[size_t(t)];
+            rows.resize(ro[size_t(nthr)]);
+            par_slices(nthr, ncls, [&](int64_t t, int64_t c0, int64_t c1) {
+                uint64_t at = ro[size_t(t)];
                 for (int64_t c = c0; c < c1; ++c) {
                     const ClassMeta& m = b.cls[size_t(c)];
-                    uint64_t at = ro[size_t(c)];
                     for (uint32_t mi = 0; mi < m.D; ++mi)
                         if (b.node_of[m.no_off + mi] >= 0) rows[at++] = DRow{uint32_t(c), mi};
                 }
@@ -2263,7 +2349,8 @@ struct Miner {
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
         // one table, one H2D copy: [koff: cbase_total + 1 | kslot: nfreq | kcid: nfreq]
         const size_t nko = size_t(b.cbase_total) + 1;
-        std::vector<uint32_t>& ktab = ktab_s;
+        RawVec<uint32_t>& ktab = ktab_s;
+        ktab.clear();  // (a growing resize then copies nothing over)
         ktab.resize(nko + 2 * size_t(nfreq));
         uint32_t* koff = ktab.data();
         uint32_t* kslot = koff + nko;
@@ -2378,7 +2465,7 @@ struct Miner {
             shard_plan(vol.data(), int64_t(vol.size()), comm->nranks(), owner.data());
             std::vector<uint8_t> keep(nc, 0);
             for (size_t q = 0; q < idx.size(); ++q) keep[idx[q]] = owner[q] == comm->rank();
-            std::vector<ChildInfo> kept;
+            RawVec<ChildInfo> kept;
             size_t nheavy = 0;
             for (size_t k = 0; k < nc; ++k) {
                 b.children[k].split = heavy[k] != 0;
@@ -2392,7 +2479,7 @@ struct Miner {
         } else if (comm) {
             // sub-classes of a split class: LPT over that class's sub-classes alone
             // (the same on every rank whatever the batching), this rank keeps its share
-            std::vector<ChildInfo> kept;
+            RawVec<ChildInfo> kept;
             for (size_t k = 0; k < b.children.size();) {
                 size_t k2 = k;
                 const uint32_t pc = b.children[k].pcls;
@@ -2421,7 +2508,30 @@ struct Miner {
         uint64_t acc = 0;
         const uint64_t max_ent = uint64_t(1) << 31;
         uint64_t acc_ent = 0;
-        for (size_t k = 0; k < b.children.size(); ++k) {
+        const int64_t nch = int64_t(b.children.size());
+        bool one = false;  // many children: the common case (all fit one group) from threaded sums
+        if (nch >= (int64_t(1) << 16)) {
+            const int64_t nthr = host_threads();
+            std::vector<uint64_t> tn(size_t(nthr), 0), te(size_t(nthr), 0);
+            par_slices(nthr, nch, [&](int64_t t, int64_t k0, int64_t k1) {
+                uint64_t n = 0, e = 0;
+                for (int64_t k = k0; k < k1; ++k) {
+                    const ChildInfo& c = b.children[size_t(k)];
+                    n += c.cap * entry_bytes() + uint64_t(c.D) * c.D * 4;
+                    e += c.cap;
+                }
+                tn[size_t(t)] = n;
+                te[size_t(t)] = e;
+            });
+            uint64_t n = 0, e = 0;
+            for (int64_t t = 0; t < nthr; ++t) {
+                n += tn[size_t(t)];
+                e += te[size_t(t)];
+            }
+            one = n <= budget && e <= max_ent;
+        }
+        if (one) gs = b.children.size();
+        for (size_t k = one ? b.children.size() : 0; k < b.children.size(); ++k) {
             const uint64_t need = b.children[k].cap * entry_bytes() + uint64_t(b.children[k].D) * b.children[k].D * 4;
             if (k > gs && (acc + need > budget || acc_ent + b.children[k].cap > max_ent)) {
                 b.groups.push_back({gs, k});
@@ -2432,7 +2542,8 @@ struct Miner {
             acc += need;
             acc_ent += b.children[k].cap;
         }
-        if (gs < b.children.size()) b.groups.push_back({gs, b.children.size()});
+        if (one) b.groups.push_back({0, b.children.size()});
+        else if (gs < b.children.size()) b.groups.push_back({gs, b.children.size()});
         hp[3] += now_ms() - th;
         if (ctx->opts.verbose)
             std::fprintf(stderr, "[fsm] batch: classes=%zu entries=%llu freq=%llu children=%zu groups=%zu\n",
@@ -2449,7 +2560,7 @@ struct Miner {
         // CSR on the device (k_child_of); sharded runs keep only their share of the
         // children, so the host builds the table
         const bool dev_child_of = comm == nullptr && child_of_device(b.cbase_total);
-        std::vector<uint32_t>& child_of = child_of_s;
+        RawVec<uint32_t>& child_of = child_of_s;
         if (!dev_child_of) child_of.assign(b.cbase_total, kNone);
         uint64_t total = 0;
         // the only group: the children and their member tables move over whole (swapped:
@@ -2648,7 +2759,7 @@ struct Miner {
         m.mshift = 1;  // root members are all sequence-extensions: counter rows by rank
         m.ri_off = 0;
         m.no_off = 0;
-        root.rank_item = freq_items;
+        root.rank_item.assign(freq_items.begin(), freq_items.end());
         root.node_of.assign(m.D, -1);
         for (uint32_t r = 0; r < F; ++r) {
             root.node_of[2 * r] = int32_t(nodes.size());
