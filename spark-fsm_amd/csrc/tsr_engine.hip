@@ -931,6 +931,8 @@ struct Rule {
     uint16_t nx = 0, ny = 0;
     bool expandLR = false;
     bool dropped = false;  // a speculated child its parent's commit did not register
+    int8_t inset = -1;     // replay: the launch set expanding it (results not yet taken in), or -1
+    int32_t res = -1;      // replay: its expansion results (slot of the result pool), or -1
 };
 
 struct RuleStore {
@@ -1513,12 +1515,40 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         for (int q = 0; q < 5; ++q) FSM_HIP(hipEventCreate(&x.ev[q]));
         FSM_HIP(hipEventCreateWithFlags(&x.ev[5], hipEventDisableTiming));
     }
+    // Expansion results of rules not yet committed: slots of a pool (Rule::res; a deque,
+    // so slots never move; released slots keep their vectors' capacity for the next
+    // rule).  Rules in flight carry their launch set in Rule::inset.
     struct ExpResult {
         std::vector<ExpRec> recs;
         std::vector<Rule*> preL, preR;  // children created (and expanded) ahead of the commit, by record
+        Rule* owner = nullptr;
     };
-    std::unordered_map<Rule*, ExpResult> cache;
-    std::unordered_map<Rule*, int> inflight;  // rules of a busy set (results not yet taken in)
+    std::deque<ExpResult> res_pool;
+    std::vector<int32_t> res_free;
+    size_t res_live = 0;
+    auto res_get = [&](Rule* r) -> ExpResult& {
+        if (r->res < 0) {
+            if (res_free.empty()) {
+                res_free.push_back(int32_t(res_pool.size()));
+                res_pool.emplace_back();
+            }
+            r->res = res_free.back();
+            res_free.pop_back();
+            res_pool[size_t(r->res)].owner = r;
+            ++res_live;
+        }
+        return res_pool[size_t(r->res)];
+    };
+    auto res_release = [&](Rule* r) {
+        ExpResult& e = res_pool[size_t(r->res)];
+        e.recs.clear();
+        e.preL.clear();
+        e.preR.clear();
+        e.owner = nullptr;
+        res_free.push_back(r->res);
+        r->res = -1;
+        --res_live;
+    };
     std::vector<std::pair<std::vector<Rule*>, int>> spec_todo;  // finished launches whose children to speculate
     int64_t expansions = 0, launches = 0, spec_pushback = 0, gpu_rules = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
@@ -1580,9 +1610,9 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (!use_bm && x.drv_in_x[k] && h.nx != r->nX)
                 throw Error(FSM_EDEVICE, "TSR: |sids(X)| mismatch in expansion (" + std::to_string(h.nx) + " vs " +
                                              std::to_string(r->nX) + ")");
-            inflight.erase(r);
+            r->inset = -1;
             if (r->dropped) continue;  // a speculated child its parent's commit did not register
-            ExpResult& res = cache[r];
+            ExpResult& res = res_get(r);
             const ExpRec* rec = x.h_rec + size_t(k) * ecap;
             if (use_bm) {  // the reduce blocks' kid ranges, in kid (= item) order
                 res.recs.clear();
@@ -1620,7 +1650,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.depth = depth;
         x.seq = seq_next++;
         gpu_rules += nb;
-        for (Rule* r : batch) inflight[r] = int(xp - xs);
+        for (Rule* r : batch) r->inset = int8_t(xp - xs);
         // descriptors written in place into the set's pinned stage (only the used items:
         // the kernels read X[0, nx) and Y[0, ny))
         uint64_t* drv_off = x.h_drv;
@@ -1737,22 +1767,75 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // cached or in flight) instead of going back to the heap: the next rule to
     // commit is always the larger of the heap top and the pending front, which
     // is exactly the one-at-a-time order; new rules only ever enter the heap.
-    struct PendingOrder {  // largest first (the heap's pop order)
+    // The rules of one batch pop leave the heap in its order, so `pending` is a
+    // merge of sorted runs (one per pop loop): a small heap of runs keyed by their
+    // fronts, no per-rule tree node.
+    struct PendingRuns {
         const RuleStore* st;
-        bool operator()(const Rule* a, const Rule* b) const { return rule_cmp(*st, a, b) > 0; }
+        struct Run {
+            std::vector<Rule*> v;  // largest first
+            size_t h = 0;          // front
+        };
+        std::vector<Run> runs;
+        std::vector<int> free_ids, heap;  // heap: live runs, the largest front on top
+        bool front_less(int a, int b) const {
+            return rule_cmp(*st, runs[size_t(a)].v[runs[size_t(a)].h], runs[size_t(b)].v[runs[size_t(b)].h]) < 0;
+        }
+        bool empty() const { return heap.empty(); }
+        Rule* front() const { return runs[size_t(heap[0])].v[runs[size_t(heap[0])].h]; }
+        void pop() {
+            auto cmp = [this](int a, int b) { return front_less(a, b); };
+            const int id = heap[0];
+            std::pop_heap(heap.begin(), heap.end(), cmp);
+            heap.pop_back();
+            Run& r = runs[size_t(id)];
+            if (++r.h < r.v.size()) {
+                heap.push_back(id);
+                std::push_heap(heap.begin(), heap.end(), cmp);
+            } else {
+                r.v.clear();
+                r.h = 0;
+                free_ids.push_back(id);
+            }
+        }
+        void add(std::vector<Rule*>& v) {  // v: in heap pop order; taken over (left empty)
+            if (v.empty()) return;
+            int id;
+            if (free_ids.empty()) {
+                id = int(runs.size());
+                runs.emplace_back();
+            } else {
+                id = free_ids.back();
+                free_ids.pop_back();
+            }
+            runs[size_t(id)].v.swap(v);
+            runs[size_t(id)].h = 0;
+            v.clear();
+            heap.push_back(id);
+            std::push_heap(heap.begin(), heap.end(), [this](int a, int b) { return front_less(a, b); });
+        }
+        uint32_t min_sup() const {  // support of the smallest pending rule (the runs' backs)
+            uint32_t m = 0xFFFFFFFFu;
+            for (int id : heap) m = std::min(m, runs[size_t(id)].v.back()->sup);
+            return m;
+        }
     };
-    std::set<Rule*, PendingOrder> pending(PendingOrder{&rp.st});
+    PendingRuns pending{&rp.st, {}, {}, {}};
+    std::vector<Rule*> popped;  // one pop loop's rules (a run of `pending`)
     // a speculated child that its parent's commit did not register: drop its
     // results (cached, or marked so that an in-flight launch's are discarded) and,
     // recursively, those of its own speculated children
     std::function<void(Rule*)> drop_spec = [&](Rule* x) {
         x->dropped = true;
-        auto it = cache.find(x);
-        if (it == cache.end()) return;
-        ExpResult res = std::move(it->second);
-        cache.erase(it);
-        for (Rule* c : res.preL) if (c) drop_spec(c);
-        for (Rule* c : res.preR) if (c) drop_spec(c);
+        if (x->res < 0) return;
+        std::vector<Rule*> kids;
+        {
+            const ExpResult& e = res_pool[size_t(x->res)];
+            for (Rule* c : e.preL) if (c) kids.push_back(c);
+            for (Rule* c : e.preR) if (c) kids.push_back(c);
+        }
+        res_release(x);
+        for (Rule* c : kids) drop_spec(c);
     };
     auto commit = [&](Rule* r, ExpResult& res) {
         const std::vector<ExpRec>& er = res.recs;
@@ -1814,13 +1897,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         if (!spec_on || depth >= spec_depth || level.empty()) return;
         uint32_t T = 0xFFFFFFFFu;
         for (Rule* x : level) T = std::min(T, x->sup);
-        if (!pending.empty()) T = std::min(T, (*pending.rbegin())->sup);
+        if (!pending.empty()) T = std::min(T, pending.min_sup());
         T = std::max(uint32_t(double(T) * spec_frac), rp.minsup);
         std::vector<Rule*> next;
         for (Rule* x : level) {
-            auto it = cache.find(x);
-            if (it == cache.end()) continue;  // committed already, or dropped
-            ExpResult& res = it->second;
+            if (x->res < 0) continue;  // committed already, or dropped
+            ExpResult& res = res_pool[size_t(x->res)];
             const size_t n = res.recs.size();
             res.preL.assign(n, nullptr);
             res.preR.assign(n, nullptr);
@@ -1859,29 +1941,24 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
         const bool have_h = !rp.cand.empty(), have_p = !pending.empty();
         if (!have_h && !have_p) break;
-        const bool from_p = have_p && (!have_h || rule_cmp(rp.st, *pending.begin(), rp.cand.top().r) > 0);
-        Rule* r = from_p ? *pending.begin() : rp.cand.top().r;
+        const bool from_p = have_p && (!have_h || rule_cmp(rp.st, pending.front(), rp.cand.top().r) > 0);
+        Rule* r = from_p ? pending.front() : rp.cand.top().r;
         if (r->sup < rp.minsup) break;
-        auto ci = cache.find(r);
-        if (ci == cache.end()) {
-            auto fi = inflight.find(r);
-            if (fi != inflight.end()) {  // expanding on the GPU: take its launch in, then decide again
-                finish(xs[fi->second]);
-                continue;
-            }
+        if (r->res < 0 && r->inset >= 0) {  // expanding on the GPU: take its launch in, then decide again
+            finish(xs[r->inset]);
+            continue;
         }
-        if (ci != cache.end()) {  // results at hand: commit now
-            if (from_p) pending.erase(pending.begin());
+        if (r->res >= 0) {  // results at hand: commit now
+            if (from_p) pending.pop();
             else rp.cand.pop();
             const double tc0 = now_ms();
-            ExpResult res = std::move(ci->second);
-            cache.erase(ci);
-            commit(r, res);
+            commit(r, res_pool[size_t(r->res)]);
+            if (r->res >= 0) res_release(r);
             commit_ms += now_ms() - tc0;
-            if (cache.size() > sweep_at) {  // results of rules now below minsup can never be committed
-                for (auto it = cache.begin(); it != cache.end();)
-                    it = it->first->sup < rp.minsup ? cache.erase(it) : std::next(it);
-                sweep_at = std::max<size_t>(2 * cache.size(), 1u << 16);
+            if (res_live > sweep_at) {  // results of rules now below minsup can never be committed
+                for (ExpResult& e : res_pool)
+                    if (e.owner && e.owner->sup < rp.minsup) res_release(e.owner);
+                sweep_at = std::max<size_t>(2 * res_live, 1u << 16);
             }
             continue;
         }
@@ -1889,16 +1966,17 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         // r (neither cached nor in flight) and the next heap rules are expanded together
         const double tp0 = now_ms();
         batch.clear();
+        popped.clear();
         while (batch.size() < size_t(B) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
             Rule* x = rp.cand.top().r;
             rp.cand.pop();
-            if (cache.count(x) || inflight.count(x)) pending.insert(x);  // already expanded by speculation
-            else batch.push_back(x);
+            popped.push_back(x);
+            if (x->res < 0 && x->inset < 0) batch.push_back(x);  // else already expanded by speculation
         }
+        pending.add(popped);
         pop_ms += now_ms() - tp0;
         launch(batch, 0);
         spec_pushback += int64_t(batch.size()) - 1;
-        for (Rule* c : batch) pending.insert(c);
     }
     for (ExpSet& x : xs)  // speculation still in flight when the replay ended
         if (x.busy) finish(x);
