@@ -1330,7 +1330,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // bitmap path: sid bitmaps built, K <= kMaxKids, itemset indexes < 2^16 (packed rows)
     bool use_bm = d->bm.p != nullptr && K > 0 && K <= kMaxKids;
     DevBuf k_off, k_item, k_first, k_last, k_sup;  // list path rows (SoA)
-    DevBuf k_ent, d_kidof, d_kept, d_ksup, d_alive;  // bitmap path rows (packed) and kid tables
+    DevBuf k_ent, d_kidof, d_kept, d_ksup;  // bitmap path rows (packed) and kid tables
     uint64_t E2 = 0;
     const unsigned rows_grid = unsigned(std::min<uint64_t>((N * 64 + kBlock - 1) / kBlock, 65536));
     if (use_bm) {
@@ -1342,7 +1342,6 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         d_kidof.alloc(size_t(std::max<uint32_t>(U, 1)) * 4);
         d_kept.alloc(size_t(K) * 4);
         d_ksup.alloc(size_t(K) * 4);
-        d_alive.alloc(size_t((K + 15) / 16) * 4);
         FSM_HIP(hipMemcpyAsync(d_kidof.p, kid_of.data(), size_t(U) * 4, hipMemcpyHostToDevice, s));
         FSM_HIP(hipMemcpyAsync(d_kept.p, kept_items.data(), size_t(K) * 4, hipMemcpyHostToDevice, s));
         FSM_HIP(hipMemcpyAsync(d_ksup.p, ksup.data(), size_t(K) * 4, hipMemcpyHostToDevice, s));
@@ -1467,6 +1466,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         std::vector<Rule*> batch;
         std::vector<char> drv_in_x;
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
+        // the set's own stream: the two sets' launches are independent, so the GPU runs
+        // one set's kernels while the other's are in flight (FSM_TSR_STREAMS=1: ctx stream)
+        hipStream_t st = nullptr;
+        bool own_stream = false;
+        DevBuf alive;          // kid codes for alive_t (each set its own: k_alive never races a launch)
+        uint32_t alive_t = 0;  // minsup the set's kid codes were built for
         bool timed = false, busy = false;
         int depth = 0;        // speculation depth of the batch (0: heap batch)
         int64_t seq = 0;      // launch number (the older busy set finishes first)
@@ -1475,9 +1480,21 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (busy && ev[5]) (void)hipEventSynchronize(ev[5]);
             for (hipEvent_t e : ev)
                 if (e) (void)hipEventDestroy(e);
+            if (own_stream && st) {
+                (void)hipStreamSynchronize(st);
+                (void)hipStreamDestroy(st);
+            }
         }
     } xs[2];
+    const bool set_streams = [] { const char* v = std::getenv("FSM_TSR_STREAMS"); return !(v && v[0] == '1'); }();
     for (ExpSet& x : xs) {
+        if (set_streams) {
+            FSM_HIP(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
+            x.own_stream = true;
+        } else {
+            x.st = s;
+        }
+        if (use_bm) x.alive.alloc(size_t((K + 15) / 16) * 4);
         x.ctl.alloc(B * sizeof(ExpCtl));
         FSM_HIP(hipMemsetAsync(x.ctl.p, 0, B * sizeof(ExpCtl), s));
         if (use_bm) {
@@ -1515,6 +1532,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         for (int q = 0; q < 5; ++q) FSM_HIP(hipEventCreate(&x.ev[q]));
         FSM_HIP(hipEventCreateWithFlags(&x.ev[5], hipEventDisableTiming));
     }
+    FSM_HIP(hipStreamSynchronize(s));  // the DB, kid tables and set buffers are ready for the set streams
     // Expansion results of rules not yet committed: slots of a pool (Rule::res; a deque,
     // so slots never move; released slots keep their vectors' capacity for the next
     // rule).  Rules in flight carry their launch set in Rule::inset.
@@ -1568,7 +1586,6 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     const char* seg_name[4] = {use_bm ? "k_exp_domain" : "k_expand", use_bm ? "k_exp_rows" : "",
                                use_bm ? "k_expand_reduce" : "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
-    uint32_t alive_t = 0;  // minsup the kid codes were built for
     int64_t seq_next = 0;
     // Take in the results of set x (waits for its launch): records sorted into the
     // cache, and its batch queued for child speculation.
@@ -1705,14 +1722,15 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.blocks = wave_off[nb];
         if (use_bm && x.dom.bytes < drv_off[nb] * sizeof(uint2))
             x.dom.alloc(std::max<uint64_t>(drv_off[nb] * sizeof(uint2) * 5 / 4, uint64_t(1) << 20));
+        hipStream_t s = x.st;  // (shadows the context stream for this launch)
         FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
         x.timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
         const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
-        if (use_bm && alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
+        if (use_bm && x.alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
             hipLaunchKernelGGL(k_alive, dim3(unsigned(((K + 15) / 16 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               d_ksup.as<uint32_t>(), K, rp.minsup, d_alive.as<uint32_t>());
+                               d_ksup.as<uint32_t>(), K, rp.minsup, x.alive.as<uint32_t>());
             FSM_LAUNCHED("k_alive", s);
-            alive_t = rp.minsup;
+            x.alive_t = rp.minsup;
         }
         if (x.timed) FSM_HIP(hipEventRecord(x.ev[0], s));
         if (use_bm) {
@@ -1723,7 +1741,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
             hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
                                x.d_wave, nb, x.d_drv, x.dom.as<uint2>(), k_ent.as<uint2>(), d_kidof.as<uint32_t>(),
-                               d_alive.as<uint32_t>(), geo, x.part.as<uint32_t>(), x.ctl.as<ExpCtl>(),
+                               x.alive.as<uint32_t>(), geo, x.part.as<uint32_t>(), x.ctl.as<ExpCtl>(),
                                x.d_ndlw.as<uint32_t>());
             FSM_LAUNCHED("k_exp_rows", s);
             if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
