@@ -94,9 +94,16 @@ template <int W> __device__ __forceinline__ void mask_clear_upto(uint64_t (&m)[W
 template <int W> __device__ __forceinline__ uint32_t mask_words(uint32_t wd) { return W ? uint32_t(W) : wd; }
 
 // a mask operand: in registers (W > 0) or by address (W == 0)
+// load(p, wd, lh) / and_any(b, wd, lh_b): W >= 2 skips the partner's mask when the
+// two entries' eid ranges (lohi: first | last set eid << 16) do not overlap
 template <int W> struct MaskV {
     uint64_t w[W];
+    uint32_t lh = 0;
     __device__ __forceinline__ void load(const uint64_t* __restrict__ p, uint32_t) { load_mask<W>(p, w); }
+    __device__ __forceinline__ void load(const uint64_t* __restrict__ p, uint32_t, uint32_t l) {
+        lh = l;
+        load_mask<W>(p, w);
+    }
     __device__ __forceinline__ bool and_any(const uint64_t* __restrict__ b, uint32_t) const {
         uint64_t bm[W];
         load_mask<W>(b, bm);
@@ -105,14 +112,23 @@ template <int W> struct MaskV {
         for (int k = 0; k < W; ++k) acc |= w[k] & bm[k];
         return acc != 0;
     }
+    __device__ __forceinline__ bool and_any(const uint64_t* __restrict__ b, uint32_t wd, uint32_t lb) const {
+        if constexpr (W >= 2)
+            if (max(lh & 0xFFFFu, lb & 0xFFFFu) > min(lh >> 16, lb >> 16)) return false;
+        return and_any(b, wd);
+    }
 };
 template <> struct MaskV<0> {
     const uint64_t* p;
     __device__ __forceinline__ void load(const uint64_t* __restrict__ q, uint32_t) { p = q; }
+    __device__ __forceinline__ void load(const uint64_t* __restrict__ q, uint32_t, uint32_t) { p = q; }
     __device__ __forceinline__ bool and_any(const uint64_t* __restrict__ b, uint32_t wd) const {
         for (uint32_t k = 0; k < wd; ++k)
             if (p[k] & b[k]) return true;
         return false;
+    }
+    __device__ __forceinline__ bool and_any(const uint64_t* __restrict__ b, uint32_t wd, uint32_t) const {
+        return and_any(b, wd);
     }
 };
 

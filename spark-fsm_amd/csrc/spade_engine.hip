@@ -29,6 +29,7 @@
 // The root class is the flattened DB restricted to frequent items (F1 = k_f1,
 // row filter = k_root_count / k_root_write).
 #include <algorithm>
+#include <sys/mman.h>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -182,23 +183,24 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
         if (mi - mlo >= mhi - mlo) continue;  // member rows of another rank (sharded root)
         my_tests += p & 0xFFFFu;
         const DClass c = cls[cid[e]];
-        const uint32_t lo_i = lohi[e] & 0xFFFFu;
+        const uint32_t lh_i = lohi[e], lo_i = lh_i & 0xFFFFu;
         const uint32_t ti = mi & 1u, ri = mi >> 1;
         const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
         MaskV<W> mk;
-        mk.load(mask + size_t(e) * mw, wd);
+        mk.load(mask + size_t(e) * mw, wd, lh_i);
         uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
         for (uint32_t q = 0; q < rl; ++q) {
             const uint32_t f = rb + q;
             const uint32_t mj = mem[f];
             const uint32_t tj = mj & 1u, rj = mj >> 1;
+            const uint32_t lh_f = lohi[f];
             if (tj == kSeq) {
                 // P x -> y  /  P->x -> y : bits of L(j) strictly after first bit of L(i)
-                if ((lohi[f] >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
+                if ((lh_f >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
                 // P->(x y), y > x : L(i) & L(j)
-                if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * mw, wd))
+                if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * mw, wd, lh_f))
                     atomicAdd(rowc + (rj << 1 | 1u), 1u);
-            } else if (ti == kItm && rj > ri && mk.and_any(mask + size_t(f) * mw, wd)) {
+            } else if (ti == kItm && rj > ri && mk.and_any(mask + size_t(f) * mw, wd, lh_f)) {
                 // P(x y), y > x
                 atomicAdd(rowc + (rj << 1 | 1u), 1u);
             }
@@ -253,10 +255,11 @@ __device__ __forceinline__ void class_joins(uint32_t ti, uint32_t ri, uint32_t l
     const uint32_t mw = mask_words<W>(wd);
     const uint32_t mj = mem[f];
     const uint32_t tj = mj & 1u, rj = mj >> 1;
+    const uint32_t lh_f = lohi[f];
     if (tj == kSeq) {
-        if ((lohi[f] >> 16) > lo_i) key(rj << 1);
-        if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * mw, wd)) key(rj << 1 | 1u);
-    } else if (ti == kItm && rj > ri && mk.and_any(mask + size_t(f) * mw, wd)) {
+        if ((lh_f >> 16) > lo_i) key(rj << 1);
+        if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * mw, wd, lh_f)) key(rj << 1 | 1u);
+    } else if (ti == kItm && rj > ri && mk.and_any(mask + size_t(f) * mw, wd, lh_f)) {
         key(rj << 1 | 1u);
     }
 }
@@ -292,10 +295,11 @@ __global__ __launch_bounds__(1024) void k_cnt_keys(uint32_t E, uint32_t epb, con
             const uint64_t rbase = row_base(cls[cid[e]], mi);
             g = uint32_t(rbase >> kGroupShift);
             kb = uint32_t(rbase) & (kGroupCounters - 1u);
-            lo_i = lohi[e] & 0xFFFFu;
+            const uint32_t lh_i = lohi[e];
+            lo_i = lh_i & 0xFFFFu;
             ti = mi & 1u;
             ri = mi >> 1;
-            mk.load(mask + size_t(e) * mask_words<W>(wd), wd);
+            mk.load(mask + size_t(e) * mask_words<W>(wd), wd, lh_i);
             for (uint32_t q = 0; q < rl; ++q)
                 class_joins<W>(ti, ri, lo_i, mk, rb + q, mem, lohi, mask, wd, [&](uint32_t) { ++n; });
         }
@@ -914,8 +918,8 @@ __device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, co
                     ok = (lohi[f] >> 16) > (o_lt & 0xFFFFu);
                 } else {
                     MaskV<W> mk;
-                    mk.load(mask + size_t(o_e) * mask_words<W>(wd), wd);
-                    ok = mk.and_any(mask + size_t(f) * mask_words<W>(wd), wd);
+                    mk.load(mask + size_t(o_e) * mask_words<W>(wd), wd, lohi[o_e]);
+                    ok = mk.and_any(mask + size_t(f) * mask_words<W>(wd), wd, lohi[f]);
                 }
             }
         }
@@ -1498,20 +1502,33 @@ using ChildInfo = ClassMeta;
 
 // append-only array in fixed chunks: growth never copies (or faults in again) what
 // is already there (pattern nodes: millions in deep lattices)
+// (chunks of trivially copyable T, 2 MiB aligned and marked for transparent huge
+// pages: the host threads that fill a fresh chunk fault it in 2 MiB at a time)
 template <class T, int kShift = 20> struct ChunkedVec {
-    std::vector<std::unique_ptr<T[]>> ch;
+    struct Free {
+        void operator()(T* p) const { std::free(p); }
+    };
+    std::vector<std::unique_ptr<T[], Free>> ch;
     size_t n = 0;
     static constexpr size_t kMask = (size_t(1) << kShift) - 1;
     size_t size() const { return n; }
     T& operator[](size_t i) { return ch[i >> kShift][i & kMask]; }
     const T& operator[](size_t i) const { return ch[i >> kShift][i & kMask]; }
+    void add_chunk() {
+        constexpr size_t kHuge = size_t(2) << 20;
+        const size_t bytes = ((sizeof(T) << kShift) + kHuge - 1) & ~(kHuge - 1);
+        T* p = static_cast<T*>(std::aligned_alloc(kHuge, bytes));
+        if (!p) throw Error(FSM_ENOMEM, "pattern node chunk allocation failed");
+        (void)madvise(p, bytes, MADV_HUGEPAGE);
+        ch.emplace_back(p);
+    }
     void push_back(const T& v) {
-        if ((n >> kShift) == ch.size()) ch.emplace_back(new T[size_t(1) << kShift]);
+        if ((n >> kShift) == ch.size()) add_chunk();
         ch[n >> kShift][n & kMask] = v;
         ++n;
     }
     void grow(size_t m) {  // size n + m; the new elements are written by index afterwards
-        while (((n + m + kMask) >> kShift) > ch.size()) ch.emplace_back(new T[size_t(1) << kShift]);
+        while (((n + m + kMask) >> kShift) > ch.size()) add_chunk();
         n += m;
     }
 };
@@ -2790,7 +2807,18 @@ template <class T> struct MallocArr {
     T* p = nullptr;
     size_t n = 0;
     explicit MallocArr(size_t n_) : n(n_) {
-        p = static_cast<T*>(std::malloc(std::max<size_t>(n, 1) * sizeof(T)));
+        // large result arrays: 2 MiB aligned and marked for transparent huge pages, so
+        // the threads that fill them fault in 2 MiB at a time instead of 4 KiB (a dense
+        // mine's CSR is hundreds of MB of fresh pages); free()-compatible either way
+        static const bool thp = [] { const char* v = std::getenv("FSM_OUTPUT_THP"); return !(v && v[0] == '0'); }();
+        const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        constexpr size_t kHuge = size_t(2) << 20;
+        if (thp && bytes >= 4 * kHuge) {
+            p = static_cast<T*>(std::aligned_alloc(kHuge, (bytes + kHuge - 1) & ~(kHuge - 1)));
+            if (p) (void)madvise(p, (bytes + kHuge - 1) & ~(kHuge - 1), MADV_HUGEPAGE);
+        } else {
+            p = static_cast<T*>(std::malloc(bytes));
+        }
         if (!p) throw Error(FSM_ENOMEM, "malloc failed");
     }
     MallocArr(const MallocArr&) = delete;
@@ -3087,6 +3115,73 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     pat_off[size_t(n)] = tsets[size_t(nthr)];
     set_off[set_off.n - 1] = titems[size_t(nthr)];
     const int32_t* ival = db->spade.item_val.data();
+    static const bool walk = [] { const char* v = std::getenv("FSM_OUTPUT_WALK"); return v && v[0] == '1'; }();
+    if (first == 0 && !any_dup && nthr > 1 && !walk) {
+        // Every node is output at its own index and its parent precedes it, so a pattern
+        // is its parent's pattern plus one item: offsets first, then one parallel pass per
+        // pattern length copying the parent's items and itemset starts (written by the
+        // previous pass) instead of walking the whole parent chain per pattern.
+        std::vector<uint32_t> tmax(size_t(nthr), 0);
+        par([&](int64_t t, int64_t k0, int64_t k1) {
+            int64_t ps = tsets[size_t(t)], pi = titems[size_t(t)];
+            uint32_t mx = 0;
+            for (int64_t k = k0; k < k1; ++k) {
+                const uint32_t ls = nodes[size_t(k)].len_sets;
+                pat_off[size_t(k)] = ps;
+                set_off[size_t(ps)] = pi;  // the first itemset starts at the pattern's first item
+                ps += ls & 0xFFFFu;
+                pi += ls >> 16;
+                mx = std::max(mx, ls >> 16);
+            }
+            tmax[size_t(t)] = mx;
+        });
+        const uint32_t maxL = *std::max_element(tmax.begin(), tmax.end());
+        // node indices bucketed by pattern length (threads' counts, then their slots)
+        std::vector<int64_t> cnt(size_t(nthr) * (maxL + 2), 0);
+        par([&](int64_t t, int64_t k0, int64_t k1) {
+            int64_t* c = cnt.data() + size_t(t) * (maxL + 2);
+            for (int64_t k = k0; k < k1; ++k) ++c[nodes[size_t(k)].len_sets >> 16];
+        });
+        std::vector<int64_t> lstart(maxL + 2, 0);
+        int64_t acc = 0;
+        for (uint32_t L = 0; L <= maxL; ++L) {
+            lstart[L] = acc;
+            for (int64_t t = 0; t < nthr; ++t) {
+                int64_t& c = cnt[size_t(t) * (maxL + 2) + L];
+                const int64_t v = c;
+                c = acc;
+                acc += v;
+            }
+        }
+        lstart[maxL + 1] = acc;
+        RawVec<uint32_t> order(static_cast<size_t>(n));
+        par([&](int64_t t, int64_t k0, int64_t k1) {
+            int64_t* c = cnt.data() + size_t(t) * (maxL + 2);
+            for (int64_t k = k0; k < k1; ++k) order[size_t(c[nodes[size_t(k)].len_sets >> 16]++)] = uint32_t(k);
+        });
+        for (uint32_t L = 1; L <= maxL; ++L) {
+            const int64_t a = lstart[L], z = lstart[L + 1];
+            if (z <= a) continue;
+            par_slices(z - a >= (int64_t(1) << 12) ? nthr : 1, z - a, [&](int64_t, int64_t i0, int64_t i1) {
+                for (int64_t i = a + i0; i < a + i1; ++i) {
+                    const int64_t k = order[size_t(i)];
+                    const PNode& nd = nodes[size_t(k)];
+                    const int64_t ps = pat_off[size_t(k)], pi = set_off[size_t(ps)];
+                    sup[size_t(k)] = int32_t(nd.support);
+                    if (nd.parent < 0) {
+                        items[size_t(pi)] = ival[nd.item];
+                        continue;
+                    }
+                    const int64_t pp = nd.parent, pps = pat_off[size_t(pp)], pns = pat_off[size_t(pp) + 1] - pps;
+                    const int64_t ppi = set_off[size_t(pps)];
+                    std::memcpy(&items[size_t(pi)], &items[size_t(ppi)], size_t(L - 1) * sizeof(int32_t));
+                    items[size_t(pi + L - 1)] = ival[nd.item];
+                    for (int64_t q = 1; q < pns; ++q) set_off[size_t(ps + q)] = set_off[size_t(pps + q)] - ppi + pi;
+                    if (nd.type == kSeq) set_off[size_t(ps + pns)] = pi + L - 1;
+                }
+            });
+        }
+    } else
     par([&](int64_t t, int64_t k0, int64_t k1) {
         int64_t ps = tsets[size_t(t)], pi = titems[size_t(t)];
         for (int64_t k = k0; k < k1; ++k) {

@@ -13,4 +13,4 @@ for l in open('gpurun_out/t19.log'):
 "; grep "fsm host" gpurun_out/t19.log | tail -2; }
 SHAPE=sign SUP=0.015 r FSM_HOST_TRACE=1
 SHAPE=bible SUP=0.004 r FSM_HOST_TRACE=1
-SHAPE="quest --D 1000000" SUP=0.001 r FSM_HOST_TRACE=1
+SHAPE=sign SUP=0.015 r FSM_X=1
