@@ -1122,6 +1122,9 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
 // reserves its child entries with one slab-cursor atomic per 512-entry chunk
 // and writes the runs; a wave whose records overflow joins again while writing.
 // Runs longer than 64 entries are appended to `longl` for k_emit1's run list.
+// W > 1 (up to 8 words): the same windows; an equality join reads the owner's and
+// the partner's masks at their known slab slots (no search), after the eid-range
+// overlap test on the lohi words it already holds.
 #ifndef FSM_E2_RANGE
 #define FSM_E2_RANGE 128
 #endif
@@ -1134,6 +1137,7 @@ constexpr uint32_t kE2Range = FSM_E2_RANGE;     // entries per wave range (runs 
 constexpr uint32_t kE2Own = kE2Range + 64;      // owner slots per wave (a run may end 63 past the range)
 constexpr uint32_t kE2Cap = FSM_E2_CAP;         // LDS join records per wave
 
+template <int W>
 __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* __restrict__ cid,
                                                     const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
                                                     const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
@@ -1195,7 +1199,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
                 if (in) {
                     mi = mem[e];
                     lh = lohi[e];
-                    mk = mask[e];
+                    if constexpr (W == 1) mk = mask[e];
                     const DClass c = cls[cid[e]];
                     cc = child_of[c.cbase + mi];
                     if (cc != kNone) {
@@ -1224,7 +1228,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
                     const uint32_t o_re = uint32_t(__shfl(int(re), int(ow), 64));
                     const uint32_t o_lt = uint32_t(__shfl(int(lt2), int(ow), 64));
                     const uint32_t o_done = uint32_t(__shfl(int(done), int(ow), 64));
-                    const uint64_t o_mk = __shfl(mk, int(ow), 64);
+                    const uint64_t o_mk = W == 1 ? __shfl(mk, int(ow), 64) : 0ull;
                     const bool live = pp < total;
                     const uint32_t q = o_k0 + (pp - o_ex);
                     const uint32_t slot = live ? kid_slot[q] : 0u;
@@ -1241,10 +1245,23 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
                     const uint32_t fl = min(f, 63u);
                     const uint32_t f_mi = uint32_t(__shfl(int(mi), int(fl), 64));
                     const uint32_t f_lh = uint32_t(__shfl(int(lh), int(fl), 64));
-                    const uint64_t f_mk = __shfl(mk, int(fl), 64);
+                    const uint64_t f_mk = W == 1 ? __shfl(mk, int(fl), 64) : 0ull;
                     bool ok = false;
-                    if (live && f < o_re && f_mi == target)
-                        ok = ct == kSeq ? (f_lh >> 16) > (o_lt & 0xFFFFu) : (o_mk & f_mk) != 0ull;
+                    if constexpr (W == 1) {
+                        if (live && f < o_re && f_mi == target)
+                            ok = ct == kSeq ? (f_lh >> 16) > (o_lt & 0xFFFFu) : (o_mk & f_mk) != 0ull;
+                    } else {
+                        const uint32_t o_lh = uint32_t(__shfl(int(lh), int(ow), 64));
+                        if (live && f < o_re && f_mi == target) {
+                            if (ct == kSeq) {
+                                ok = (f_lh >> 16) > (o_lt & 0xFFFFu);
+                            } else {
+                                MaskV<W> om;
+                                om.load(mask + size_t(e0 + ow) * W, uint32_t(W), o_lh);
+                                ok = om.and_any(mask + size_t(e0 + f) * W, uint32_t(W), f_lh);
+                            }
+                        }
+                    }
                     const uint64_t succ = __ballot(ok);
                     const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
                     const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
@@ -1295,14 +1312,14 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
             for (uint32_t x = lane; x < nrec; x += 64) {
                 const uint32_t f = r_f[w][x], q = r_q[w][x], ek = r_ek[w][x];
                 const uint32_t os = ek >> 16, k = ek & 0xFFFFu;
-                emit_write<1>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
-                              i_lt[w][os], f, kid_slot[q], lohi, mask, 1u);
+                emit_write<W>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
+                              i_lt[w][os], f, kid_slot[q], lohi, mask, uint32_t(W));
             }
         } else {  // the records overflowed: join again, writing at the run bases
             walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k) {
                      if (ok)
-                         emit_write<1>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
-                                       i_lt[w][os], f, kid_slot[q], lohi, mask, 1u);
+                         emit_write<W>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
+                                       i_lt[w][os], f, kid_slot[q], lohi, mask, uint32_t(W));
                  },
                  false);
         }
@@ -1470,10 +1487,26 @@ struct Slab {
 // Allocator whose resize(n) leaves the new elements unwritten (the per-batch tables of
 // millions of classes and nodes are filled by index afterwards, by host threads: a
 // value-initialising resize would write every byte once more, serially)
+// Arrays of 4 MiB and more come 2 MiB aligned and marked for transparent huge pages
+// (a mine's Miner and batches are fresh: their tables fault in 2 MiB at a time).
 template <class T> struct NoInitAlloc : std::allocator<T> {
     template <class U> struct rebind { using other = NoInitAlloc<U>; };
     NoInitAlloc() = default;
     template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    static constexpr size_t kHuge = size_t(2) << 20;
+    T* allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < 2 * kHuge) return std::allocator<T>::allocate(n);
+        const size_t rb = (bytes + kHuge - 1) & ~(kHuge - 1);
+        void* p = std::aligned_alloc(kHuge, rb);
+        if (!p) throw std::bad_alloc();
+        (void)madvise(p, rb, MADV_HUGEPAGE);
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t n) {
+        if (n * sizeof(T) < 2 * kHuge) std::allocator<T>::deallocate(p, n);
+        else std::free(p);
+    }
     template <class U> void construct(U*) noexcept {}
     template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
 };
@@ -2658,24 +2691,31 @@ struct Miner {
             const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
             const unsigned grid = unsigned(std::min<uint64_t>((b.E + chunk - 1) / chunk, emit_grid_cap()));
             const size_t tk = clk->begin("k_emit");
-            if (W == 1 && emit_window()) {
+            if ((W == 1 || W == 2 || W == 4 || W == 8) && emit_window()) {
                 // windows of whole runs in registers; the runs of more than 64 entries go to
                 // k_emit1's run list (device-side count: no host round trip)
                 const uint64_t ce = uint64_t(kE2Waves) * kE2Range;
                 const unsigned g2 = unsigned(std::min<uint64_t>((b.E + ce - 1) / ce, emit_grid_cap()));
                 d_long.alloc(std::max<uint64_t>(b.E / 65 + 1, 1) * 4);
                 FSM_HIP(hipMemsetAsync(cursor.as<char>() + 8, 0, 4, s));
-                hipLaunchKernelGGL(k_emit2, dim3(g2), dim3(kE2Block), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),
-                                   sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,
-                                   d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap,
-                                   emit2_cap(), d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor.as<char>() + 8));
-                FSM_LAUNCHED("k_emit2", s);
-                hipLaunchKernelGGL(k_emit1<1>, dim3(256), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid,
-                                   b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,
-                                   b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,
-                                   nb.slab.cap, emit_cap(), 1u, d_long.as<uint32_t>(),
-                                   reinterpret_cast<const uint32_t*>(cursor.as<char>() + 8));
-                FSM_LAUNCHED("k_emit1", s);
+#define FSM_EMIT2(WW)                                                                                       \
+    hipLaunchKernelGGL(k_emit2<WW>, dim3(g2), dim3(kE2Block), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),  \
+                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,                         \
+                       d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap, emit2_cap(),   \
+                       d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor.as<char>() + 8));               \
+    FSM_LAUNCHED("k_emit2", s);                                                                                    \
+    hipLaunchKernelGGL(k_emit1<WW>, dim3(256), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid,                     \
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
+                       d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap, emit_cap(),    \
+                       uint32_t(WW), d_long.as<uint32_t>(), reinterpret_cast<const uint32_t*>(cursor.as<char>() + 8)); \
+    FSM_LAUNCHED("k_emit1", s);
+                switch (W) {
+                    case 1: FSM_EMIT2(1) break;
+                    case 2: FSM_EMIT2(2) break;
+                    case 4: FSM_EMIT2(4) break;
+                    default: FSM_EMIT2(8) break;
+                }
+#undef FSM_EMIT2
             } else {
 #define FSM_EMIT1(WW)                                                                                               \
     hipLaunchKernelGGL(k_emit1<WW>, dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),     \

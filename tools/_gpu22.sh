@@ -3,7 +3,7 @@ cat /sys/kernel/mm/transparent_hugepage/enabled /sys/kernel/mm/transparent_hugep
 timeout -k 10 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread -m gpu tests/test_fullsize_gpu.py -k "spade_fullsize" > gpurun_out/t22_full.log 2>&1
 rc=$?; echo "fullsize rc=$rc"; tail -2 gpurun_out/t22_full.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 400 python -u -m pytest -x -q --timeout 250 --timeout-method thread -m gpu tests/test_parity_gpu.py -k "emit or count or wide or long or golden" > gpurun_out/t22_par.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 250 --timeout-method thread -m gpu tests/test_parity_gpu.py -k "emit or count or wide or long or golden or timestamp" > gpurun_out/t22_par.log 2>&1
 rc=$?; echo "parity rc=$rc"; tail -2 gpurun_out/t22_par.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 r() { echo "== $*"; env "$@" timeout -k 10 120 python -u tools/run_one.py spade $SHAPE --support $SUP --reps 4 > gpurun_out/t22.log 2>&1; echo "rc=$?"; python3 -c "
@@ -14,7 +14,7 @@ for l in open('gpurun_out/t22.log'):
 "; }
 SHAPE=sign SUP=0.015 r FSM_X=1
 SHAPE=sign SUP=0.015 r FSM_LIB_PATH=spark-fsm_amd/build/var/prev/libfsm.so
-SHAPE=sign SUP=0.015 r FSM_OUTPUT_THP=0
-SHAPE=sign SUP=0.015 r FSM_OUTPUT_WALK=1
+SHAPE=sign SUP=0.015 r FSM_EMIT_PATH=chunk
+SHAPE=bible SUP=0.004 r FSM_EMIT_PATH=chunk
 SHAPE=bible SUP=0.004 r FSM_X=1
 SHAPE=bible SUP=0.004 r FSM_LIB_PATH=spark-fsm_amd/build/var/prev/libfsm.so
