@@ -1336,8 +1336,11 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
 // the lanes in entry order, so the lanes of one instruction add into the rows
 // of the few entries of that step, and the partner's member / lohi / mask come
 // by shuffle.  Runs longer than 64 entries are counted thread-per-entry.
+// W > 1 (up to 8 words): equality tests read both masks at their slab slots after
+// the eid-range overlap test (as k_emit2).
 constexpr uint32_t kC2Range = 128;  // entries per wave range (runs starting in it)
 
+template <int W>
 __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* __restrict__ cid,
                                                    const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
                                                    const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
@@ -1376,15 +1379,17 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
                     if (!(mi - mlo < mhi - mlo)) continue;
                     my_tests += rl;
                     const DClass c = cls[cid[ei]];
-                    const uint32_t lo_i = lohi[ei] & 0xFFFFu, ti = mi & 1u, ri = mi >> 1;
-                    const uint64_t mk = mask[ei];
+                    const uint32_t lh_i = lohi[ei], lo_i = lh_i & 0xFFFFu, ti = mi & 1u, ri = mi >> 1;
+                    MaskV<W> mk;
+                    mk.load(mask + size_t(ei) * W, uint32_t(W), lh_i);
                     uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
                     for (uint32_t f = e0; f < e0 + rl; ++f) {
-                        const uint32_t mj = mem[f], tj = mj & 1u, rj = mj >> 1;
+                        const uint32_t mj = mem[f], tj = mj & 1u, rj = mj >> 1, lh_f = lohi[f];
                         if (tj == kSeq) {
-                            if ((lohi[f] >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
-                            if (ti == kSeq && rj > ri && (mk & mask[f])) atomicAdd(rowc + (rj << 1 | 1u), 1u);
-                        } else if (ti == kItm && rj > ri && (mk & mask[f])) {
+                            if ((lh_f >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
+                            if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * W, uint32_t(W), lh_f))
+                                atomicAdd(rowc + (rj << 1 | 1u), 1u);
+                        } else if (ti == kItm && rj > ri && mk.and_any(mask + size_t(f) * W, uint32_t(W), lh_f)) {
                             atomicAdd(rowc + (rj << 1 | 1u), 1u);
                         }
                     }
@@ -1405,7 +1410,7 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
             if (in) {
                 mi = mem[e];
                 lh = lohi[e];
-                mk = mask[e];
+                if constexpr (W == 1) mk = mask[e];
                 if (mi - mlo < mhi - mlo) {  // (sharded root: this rank's member rows only)
                     const DClass c = cls[cid[e]];
                     rowa = c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
@@ -1427,20 +1432,30 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
                 const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
                 const uint32_t o_rs = uint32_t(__shfl(int(rs), int(ow), 64));
                 const uint32_t o_mi = uint32_t(__shfl(int(mi), int(ow), 64));
-                const uint32_t o_lo = uint32_t(__shfl(int(lh), int(ow), 64)) & 0xFFFFu;
-                const uint64_t o_mk = __shfl(mk, int(ow), 64);
+                const uint32_t o_lh = uint32_t(__shfl(int(lh), int(ow), 64)), o_lo = o_lh & 0xFFFFu;
+                const uint64_t o_mk = W == 1 ? __shfl(mk, int(ow), 64) : 0ull;
                 const uint64_t o_row = __shfl(rowa, int(ow), 64);
                 const uint32_t f = min(o_rs + (pp - o_ex), 63u);  // the partner lane
                 const uint32_t mj = uint32_t(__shfl(int(mi), int(f), 64));
-                const uint32_t hj = uint32_t(__shfl(int(lh), int(f), 64)) >> 16;
-                const uint64_t mkj = __shfl(mk, int(f), 64);
+                const uint32_t lj = uint32_t(__shfl(int(lh), int(f), 64)), hj = lj >> 16;
+                const uint64_t mkj = W == 1 ? __shfl(mk, int(f), 64) : 0ull;
                 if (pp < total) {
                     const uint32_t ti = o_mi & 1u, ri = o_mi >> 1, tj = mj & 1u, rj = mj >> 1;
                     uint32_t* rowc = cnt + o_row;
+                    // the equality join L(i) & L(j) (W > 1: the masks at slab slots e0 + ow, e0 + f)
+                    auto eq = [&]() -> bool {
+                        if constexpr (W == 1) {
+                            return (o_mk & mkj) != 0ull;
+                        } else {
+                            MaskV<W> om;
+                            om.load(mask + size_t(e0 + ow) * W, uint32_t(W), o_lh);
+                            return om.and_any(mask + size_t(e0 + f) * W, uint32_t(W), lj);
+                        }
+                    };
                     if (tj == kSeq) {
                         if (hj > o_lo) atomicAdd(rowc + (rj << 1), 1u);
-                        if (ti == kSeq && rj > ri && (o_mk & mkj)) atomicAdd(rowc + (rj << 1 | 1u), 1u);
-                    } else if (ti == kItm && rj > ri && (o_mk & mkj)) {
+                        if (ti == kSeq && rj > ri && eq()) atomicAdd(rowc + (rj << 1 | 1u), 1u);
+                    } else if (ti == kItm && rj > ri && eq()) {
                         atomicAdd(rowc + (rj << 1 | 1u), 1u);
                     }
                 }
@@ -2303,11 +2318,19 @@ struct Miner {
                        member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>(), d_tests.as<unsigned long long>(),    \
                        uint32_t(W))
                 const size_t tk = clk->begin("k_count");
-                if (W == 1 && count_window()) {
+                if ((W == 1 || W == 2 || W == 4 || W == 8) && count_window()) {
                     const unsigned g = unsigned(std::min<uint64_t>((b.E + 4 * kC2Range - 1) / (4 * kC2Range), 1u << 16));
-                    hipLaunchKernelGGL(k_count2, dim3(g), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid,
-                                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, member_lo(b),
-                                       member_hi(b), cnt.as<uint32_t>(), d_tests.as<unsigned long long>());
+#define FSM_COUNT2(WW)                                                                                  \
+    hipLaunchKernelGGL(k_count2<WW>, dim3(g), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
+                       sp.mem, sp.lohi, sp.pos, sp.mask, member_lo(b), member_hi(b), cnt.as<uint32_t>(),      \
+                       d_tests.as<unsigned long long>())
+                    switch (W) {
+                        case 1: FSM_COUNT2(1); break;
+                        case 2: FSM_COUNT2(2); break;
+                        case 4: FSM_COUNT2(4); break;
+                        default: FSM_COUNT2(8); break;
+                    }
+#undef FSM_COUNT2
                 } else {
                     FSM_W_DISPATCH(W, FSM_COUNT)
                 }
