@@ -927,7 +927,7 @@ struct Rule {
     double conf = 0;
     uint32_t sup = 0;
     uint32_t nX = 0;   // |sids(X)|
-    uint32_t off = 0;  // X at pool[off], Y at pool[off + nx]
+    uint32_t* it = nullptr;  // X at it[0, nx), Y at it[nx, nx + ny) (RuleStore's item chunks)
     uint16_t nx = 0, ny = 0;
     bool expandLR = false;
     bool dropped = false;  // a speculated child its parent's commit did not register
@@ -935,11 +935,32 @@ struct Rule {
     int32_t res = -1;      // replay: its expansion results (slot of the result pool), or -1
 };
 
+// Rules and their items in large chunks that never move (a c4 replay makes millions
+// of rules: no per-rule allocation, no copy of a growing pool)
 struct RuleStore {
-    std::deque<Rule> rules;
-    std::vector<uint32_t> pool;
-    const uint32_t* X(const Rule* r) const { return pool.data() + r->off; }
-    const uint32_t* Y(const Rule* r) const { return pool.data() + r->off + r->nx; }
+    static constexpr size_t kRuleChunk = size_t(1) << 16, kItemChunk = size_t(1) << 22;
+    std::vector<std::unique_ptr<Rule[]>> rule_chunks;
+    std::vector<std::unique_ptr<uint32_t[]>> item_chunks;
+    size_t n_rules = 0, item_used = kItemChunk;
+    size_t size() const { return n_rules; }
+    Rule& new_rule() {
+        if (n_rules % kRuleChunk == 0) rule_chunks.emplace_back(new Rule[kRuleChunk]);
+        Rule& r = rule_chunks.back()[n_rules % kRuleChunk];
+        r = Rule{};
+        ++n_rules;
+        return r;
+    }
+    uint32_t* new_items(size_t n) {  // n <= 2 * kMaxSide
+        if (item_used + n > kItemChunk) {
+            item_chunks.emplace_back(new uint32_t[kItemChunk]);
+            item_used = 0;
+        }
+        uint32_t* p = item_chunks.back().get() + item_used;
+        item_used += n;
+        return p;
+    }
+    const uint32_t* X(const Rule* r) const { return r->it; }
+    const uint32_t* Y(const Rule* r) const { return r->it + r->nx; }
 };
 
 // RuleG.compareTo [EXT, recalled; SURVEY A.3]
@@ -1049,14 +1070,14 @@ struct Replay {
         const uint32_t mx = nx0 + (ax != kNone), my = ny0 + (ay != kNone);
         if (mx >= uint32_t(kMaxSide) || my >= uint32_t(kMaxSide))
             throw Error(FSM_ELIMIT, "TSR: rule side exceeds " + std::to_string(kMaxSide - 1) + " items");
-        if (st.pool.size() + mx + my >= kNone) throw Error(FSM_ELIMIT, "TSR: rule item pool exceeds 2^32");
-        const uint32_t so = src ? src->off : 0u;
-        Rule& r = st.rules.emplace_back();
-        r.off = uint32_t(st.pool.size());
-        for (uint32_t q = 0; q < nx0; ++q) st.pool.push_back(st.pool[so + q]);
-        if (ax != kNone) st.pool.push_back(ax);
-        for (uint32_t q = 0; q < ny0; ++q) st.pool.push_back(st.pool[so + nx0 + q]);
-        if (ay != kNone) st.pool.push_back(ay);
+        Rule& r = st.new_rule();
+        uint32_t* d = st.new_items(mx + my);
+        r.it = d;
+        const uint32_t* si = src ? src->it : nullptr;
+        for (uint32_t q = 0; q < nx0; ++q) *d++ = si[q];
+        if (ax != kNone) *d++ = ax;
+        for (uint32_t q = 0; q < ny0; ++q) *d++ = si[nx0 + q];
+        if (ay != kNone) *d++ = ay;
         r.nx = uint16_t(mx);
         r.ny = uint16_t(my);
         r.sup = sup;
@@ -1513,12 +1534,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
         x.stage = std::make_unique<PinnedBuf>(kSidesB + 2 * kOffB);
         x.d_stage.alloc(kSidesB + 2 * kOffB);
-        x.h_sides = static_cast<Side*>(x.stage->host);
-        x.h_drv = reinterpret_cast<uint64_t*>(static_cast<char*>(x.stage->host) + kSidesB);
+        // [drv offsets | wave offsets | sides]: a launch copies the offsets and its nb sides
+        x.h_drv = static_cast<uint64_t*>(x.stage->host);
         x.h_wave = x.h_drv + (B + 1);
-        x.d_sides = x.d_stage.as<Side>();
-        x.d_drv = reinterpret_cast<uint64_t*>(x.d_stage.as<char>() + kSidesB);
+        x.h_sides = reinterpret_cast<Side*>(static_cast<char*>(x.stage->host) + 2 * kOffB);
+        x.d_drv = x.d_stage.as<uint64_t>();
         x.d_wave = x.d_drv + (B + 1);
+        x.d_sides = reinterpret_cast<Side*>(x.d_stage.as<char>() + 2 * kOffB);
         x.d_ndlw.alloc(16);
         // [headers | records, ecap per slot | bitmap path: reduce region counts, B x P x collect]
         const size_t nrc = use_bm ? size_t(B) * P * grid.collect : 0;
@@ -1723,7 +1745,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         if (use_bm && x.dom.bytes < drv_off[nb] * sizeof(uint2))
             x.dom.alloc(std::max<uint64_t>(drv_off[nb] * sizeof(uint2) * 5 / 4, uint64_t(1) << 20));
         hipStream_t s = x.st;  // (shadows the context stream for this launch)
-        FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, kSidesB + 2 * kOffB, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, 2 * kOffB + size_t(nb) * sizeof(Side), hipMemcpyHostToDevice,
+                               s));
         x.timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
         const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
         if (use_bm && x.alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
@@ -2004,7 +2027,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      "GPU; host: %.0f ms launch prep, %.0f ms result intake, %.0f ms commit, %.0f ms batch pops; %zu rules "
                      "made\n",
                      (long long)expansions, (long long)launches, (long long)gpu_rules, (long long)spec_pushback, wait_ms,
-                     prep_ms, post_ms, commit_ms, pop_ms, rp.st.rules.size());
+                     prep_ms, post_ms, commit_ms, pop_ms, rp.st.size());
     if (ctx->opts.verbose)
         std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB\n",
                      (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6);
