@@ -1009,7 +1009,9 @@ struct Replay {
     };
     // candidates: one max-heap per support value (the comparator's first key),
     // so a pop sifts through the rules of one support only, and the buckets
-    // below minsup (never expandable: minsup only rises) are freed as it rises
+    // below minsup (never expandable: minsup only rises) are freed as it rises.
+    // The heaps are 4-ary (half the levels of a binary heap, a node's children
+    // side by side): the same pop order, the comparator being a total order.
     struct CandQueue {
         std::vector<std::vector<HeapEnt>> bucket;
         std::vector<uint64_t> occ;  // bit s: bucket[s] non-empty (the next lower bucket is a word scan away)
@@ -1027,8 +1029,15 @@ struct Replay {
                 occ.resize(size_t(sp) / 64 + 1, 0);
             }
             std::vector<HeapEnt>& b = bucket[sp];
+            size_t i = b.size();
             b.push_back(e);
-            std::push_heap(b.begin(), b.end(), cmp);
+            while (i > 0) {
+                const size_t up = (i - 1) >> 2;
+                if (!cmp(b[up], e)) break;
+                b[i] = b[up];
+                i = up;
+            }
+            b[i] = e;
             occ[sp >> 6] |= 1ull << (sp & 63u);
             if (n == 0 || sp > top_sup) top_sup = sp;
             ++n;
@@ -1045,8 +1054,24 @@ struct Replay {
         const HeapEnt& top() { return settle().front(); }
         void pop() {
             std::vector<HeapEnt>& b = settle();
-            std::pop_heap(b.begin(), b.end(), cmp);
+            const HeapEnt last = b.back();
             b.pop_back();
+            const size_t m = b.size();
+            if (m) {
+                size_t i = 0;
+                for (;;) {
+                    const size_t c = 4 * i + 1;
+                    if (c >= m) break;
+                    size_t best = c;
+                    const size_t ce = std::min(c + 4, m);
+                    for (size_t j = c + 1; j < ce; ++j)
+                        if (cmp(b[best], b[j])) best = j;
+                    if (!cmp(last, b[best])) break;
+                    b[i] = b[best];
+                    i = best;
+                }
+                b[i] = last;
+            }
             if (b.empty()) occ[top_sup >> 6] &= ~(1ull << (top_sup & 63u));
             --n;
         }
