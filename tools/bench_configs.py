@@ -88,26 +88,28 @@ def cpu_spade(ds, sup, reps, threads, stride):
             "joins_per_s": statistics.median(r["joins"] / max(v, 1e-9) for r, v in zip(runs, lat))}
 
 
-def run_spade(eng, fsm, name, ds, sup, cpu_reps):
+def run_spade(eng, fsm, name, ds, sup, cpu_reps, gpu_only=False):
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
     prep = eng.stats()
     ms, (csr, meta) = time_gpu(lambda: eng.spade_csr(db, sup))
     st = eng.stats()
     ks = sorted(eng.kernel_stats(), key=lambda k: -k["ms"])[:4]
     db.free()
-    nt = cpu_share()
-    sampled = name == "c3"  # the complete single-thread mine takes most of an hour
-    log("%s: GPU %.2f ms; CPU restatement (%s)" % (name, ms, "class-stride sample" if sampled else "complete"))
-    c1 = cpu_spade(ds, sup, 1 if sampled else cpu_reps, 1, 128 if sampled else 1)
-    ca = cpu_spade(ds, sup, 1 if sampled else cpu_reps, nt, 8 if sampled else 1) if nt > 1 else None
     out = {"config": name, "algo": "SPADE", "dataset": ds.name, "sequences": len(ds), "minsup": sup,
            "minsup_abs": meta["minsup"], "gpu_mine_ms": ms, "patterns": meta["n"], "joins": st["joins"],
            "gpu_joins_per_s": st["joins"] / (ms / 1000.0), "mask_words": st["mask_words"],
            "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
            "top_kernels": [{"name": k["name"], "ms": round(k["ms"], 3),
                             "GBps": round(k["alg_bytes"] / 1e9 / (k["ms"] / 1e3), 1) if k["ms"] else 0}
-                           for k in ks],
-           "cpu_1thr": c1, "cpu_all_cores": ca, "cpu_share": nt}
+                           for k in ks]}
+    if gpu_only:
+        return out
+    nt = cpu_share()
+    sampled = name == "c3"  # the complete single-thread mine takes most of an hour
+    log("%s: GPU %.2f ms; CPU restatement (%s)" % (name, ms, "class-stride sample" if sampled else "complete"))
+    c1 = cpu_spade(ds, sup, 1 if sampled else cpu_reps, 1, 128 if sampled else 1)
+    ca = cpu_spade(ds, sup, 1 if sampled else cpu_reps, nt, 8 if sampled else 1) if nt > 1 else None
+    out.update({"cpu_1thr": c1, "cpu_all_cores": ca, "cpu_share": nt})
     out["speedup_vs_cpu_1thr_joins_per_s"] = out["gpu_joins_per_s"] / c1["joins_per_s"]
     if not sampled:
         out["speedup_vs_cpu_1thr_time"] = c1["seconds_lattice_median"] * 1000.0 / ms
@@ -116,17 +118,18 @@ def run_spade(eng, fsm, name, ds, sup, cpu_reps):
     return out
 
 
-def run_tsr(eng, fsm, name, ds, params, cpu_s):
+def run_tsr(eng, fsm, name, ds, params, cpu_s, gpu_only=False):
     from oracle import oracle
     k, mc = params
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
     prep = eng.stats()
-    ms, (rules, meta) = time_gpu(lambda: eng.tsr(db, k, mc), reps=1, warmup=False)  # a full run is tens of s
+    # (a full run is seconds: median of 3 after a warmup when the CPU legs are skipped)
+    ms, (rules, meta) = time_gpu(lambda: eng.tsr(db, k, mc), reps=3 if gpu_only else 1, warmup=gpu_only)
     st = eng.stats()
     ks = sorted(eng.kernel_stats(), key=lambda q: -q["ms"])[:4]
     db.free()
     # CPU: the largest prefix (halving from TSR_CPU_PREFIX) whose full run fits the bound
-    n = min(len(ds), TSR_CPU_PREFIX)
+    n = 0 if gpu_only else min(len(ds), TSR_CPU_PREFIX)
     cpu = None
     log("%s: GPU %.2f ms; CPU restatement on prefixes (bound %.0f s each)" % (name, ms, cpu_s))
     while n >= 1000:
@@ -148,7 +151,8 @@ def run_tsr(eng, fsm, name, ds, params, cpu_s):
            "expansions": st["expansions"], "ms_pair_phase": st["ms_f2"], "ms_expansions": st["ms_lattice"],
            "ms_flatten": prep["ms_flatten"], "ms_upload": prep["ms_upload"],
            "top_kernels": [{"name": q["name"], "ms": round(q["ms"], 3)} for q in ks]}
-    out.update(cpu or {"cpu": "no prefix >= 1000 sequences completed within the bound"})
+    if not gpu_only:
+        out.update(cpu or {"cpu": "no prefix >= 1000 sequences completed within the bound"})
     return out
 
 
@@ -158,6 +162,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="bound of the TSR prefix runs")
     ap.add_argument("--cpu-reps", type=int, default=1, help="complete SPADE CPU mines per config (median)")
     ap.add_argument("--verbose", action="store_true", help="engine progress on stderr (long TSR runs)")
+    ap.add_argument("--gpu-only", action="store_true", help="GPU legs only (the CPU columns from an earlier sweep)")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime per process, see _lib.py)
     import spark_fsm_amd as fsm
@@ -168,9 +173,9 @@ def main():
             log("%s: generating %s" % (name, shape))
             ds = dataset(shape, kw)
             if algo == "spade":
-                res = run_spade(eng, fsm, name, ds, par, args.cpu_reps)
+                res = run_spade(eng, fsm, name, ds, par, args.cpu_reps, args.gpu_only)
             else:
-                res = run_tsr(eng, fsm, name, ds, par, args.cpu_seconds)
+                res = run_tsr(eng, fsm, name, ds, par, args.cpu_seconds, args.gpu_only)
             print(json.dumps(res), flush=True)
 
 
