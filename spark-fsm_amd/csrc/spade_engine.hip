@@ -757,7 +757,8 @@ __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ 
 __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ rows, uint32_t nrows,
                                                        const DClass* __restrict__ cls, const uint32_t* __restrict__ cnt,
                                                        uint32_t minsup, const uint64_t* __restrict__ rowoff,
-                                                       uint32_t row_base, FreqRec* __restrict__ out) {
+                                                       uint32_t row_base, FreqRec* __restrict__ out,
+                                                       uint32_t* __restrict__ kslot, uint32_t* __restrict__ kcid) {
     const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (g >= nrows) return;
     const DRow r = rows[g];
@@ -775,9 +776,39 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
         const uint64_t lead = __ballot((fr || partner) && !(lane & 1u));
         const uint32_t crank = nrank + uint32_t(__popcll(lead & lead_lt));
         const uint64_t fb = __ballot(fr);
-        if (fr) out[o + __popcll(fb & lanemask_lt())] = FreqRec{row_base + g, slot, v, crank << 1 | (slot & 1u)};
+        if (fr) {
+            const uint64_t q = o + __popcll(fb & lanemask_lt());
+            out[q] = FreqRec{row_base + g, slot, v, crank << 1 | (slot & 1u)};
+            if (kslot) {  // the batch's kid table, straight into HBM (unsharded)
+                kslot[q] = slot;
+                kcid[q] = crank << 1 | (slot & 1u);
+            }
+        }
         o += uint64_t(__popcll(fb));
         nrank += uint32_t(__popcll(lead));
+    }
+}
+
+// Kid offsets of every member slot x (CSR over cbase + mi): row g (slots ascend with
+// the rows) writes rowoff[g] over the slots after the previous row's up to its own;
+// the last row also closes the table (slots past it: nfreq).
+__global__ __launch_bounds__(kBlock) void k_kid_off(const DRow* __restrict__ rows, uint32_t nrows,
+                                                    const DClass* __restrict__ cls, const uint64_t* __restrict__ rowoff,
+                                                    uint32_t nko, uint32_t* __restrict__ koff) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nrows) return;
+    const DRow r = rows[g];
+    const uint32_t x = cls[r.cls].cbase + r.mi;
+    uint32_t a = 0;
+    if (g > 0) {
+        const DRow p = rows[g - 1];
+        a = cls[p.cls].cbase + p.mi + 1;
+    }
+    const uint32_t v = uint32_t(rowoff[g]);
+    for (uint32_t y = a; y <= x; ++y) koff[y] = v;
+    if (g + 1 == nrows) {
+        const uint32_t n = uint32_t(rowoff[nrows]);
+        for (uint32_t y = x + 1; y < nko; ++y) koff[y] = n;
     }
 }
 
@@ -1973,6 +2004,12 @@ struct Miner {
         const char* v = std::getenv("FSM_COUNT_KERNEL");
         return !(v && !std::strcmp(v, "thread"));
     }
+    // FSM_KIDS=host builds the kid table on the host for every batch (tests, A/B; default:
+    // large unsharded batches get it from k_freq_write + k_kid_off on the device)
+    static bool kids_host() {
+        const char* v = std::getenv("FSM_KIDS");
+        return v && !std::strcmp(v, "host");
+    }
     // FSM_EMIT_PATH=chunk forces k_emit1 for every batch (tests, A/B runs; default: k_emit2 at W = 1)
     static bool emit_window() {
         const char* v = std::getenv("FSM_EMIT_PATH");
@@ -2295,6 +2332,7 @@ struct Miner {
         recs.clear();
         const FreqRec* ext = nullptr;  // ordered extraction: the records in pinned host memory
         uint64_t ext_n = 0;
+        bool kids_dev = false;  // the kid table was built on the device (k_freq_write + k_kid_off)
         DevBuf cnt;
         lap(8, tl);
         hp[6] += now_ms() - tc0;  // prepare + stats + rows
@@ -2358,11 +2396,27 @@ struct Miner {
                 const uint64_t nf = pend[1];
                 if (nf) {  // records straight into mapped pinned host memory, read there after the sync
                     PinnedBuf* pb = ctx->pinned_big(nf * sizeof(FreqRec));
+                    // unsharded: the kid table [koff | kslot | kcid] is built here, in HBM
+                    const bool dk = !comm && !kids_host() && rlo == 0 && nrows == rows.size();
+                    const size_t nko = size_t(b.cbase_total) + 1;
+                    uint32_t *kslot = nullptr, *kcid = nullptr;
+                    if (dk) {
+                        b.kid_tab.alloc((nko + 2 * size_t(nf)) * 4);
+                        kslot = b.kid_tab.as<uint32_t>() + nko;
+                        kcid = kslot + nf;
+                    }
                     const size_t tk = clk->begin("k_freq_write");
                     hipLaunchKernelGGL(k_freq_write, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
                                        b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rowoff.as<uint64_t>(), rlo,
-                                       static_cast<FreqRec*>(pb->dev));
+                                       static_cast<FreqRec*>(pb->dev), kslot, kcid);
                     FSM_LAUNCHED("k_freq_write", s);
+                    if (dk) {
+                        hipLaunchKernelGGL(k_kid_off, dim3(unsigned((nrows + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                                           d_rows.as<DRow>(), nrows, b.d_cls.as<DClass>(), rowoff.as<uint64_t>(),
+                                           uint32_t(nko), b.kid_tab.as<uint32_t>());
+                        FSM_LAUNCHED("k_kid_off", s);
+                        kids_dev = true;
+                    }
                     clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4 +
                                          nf * sizeof(FreqRec)));
                     sync();
@@ -2422,6 +2476,11 @@ struct Miner {
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
         // one table, one H2D copy: [koff: cbase_total + 1 | kslot: nfreq | kcid: nfreq]
         const size_t nko = size_t(b.cbase_total) + 1;
+        if (kids_dev) {
+            b.kid_off = b.kid_tab.as<uint32_t>();
+            b.kid_slot = b.kid_off + nko;
+            b.kid_cid = b.kid_slot + nfreq;
+        } else {
         RawVec<uint32_t>& ktab = ktab_s;
         ktab.clear();  // (a growing resize then copies nothing over)
         ktab.resize(nko + 2 * size_t(nfreq));
@@ -2458,6 +2517,7 @@ struct Miner {
         b.kid_off = b.kid_tab.as<uint32_t>();
         b.kid_slot = b.kid_off + nko;
         b.kid_cid = b.kid_slot + nfreq;
+        }
         hp[1] += now_ms() - th;
         th = now_ms();
         // children (new pattern nodes) in deterministic (row, slot) order

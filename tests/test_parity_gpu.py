@@ -396,7 +396,7 @@ def _wide_runs_db(seed=5, n=600):
     return gen.DataSet(np.array(so, dtype=np.int64), np.array(tk, dtype=np.int64), "wide-runs")
 
 
-@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some", "chunk", "host-child-of", "device-child-of"])
+@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some", "chunk", "host-child-of", "device-child-of", "host-kids"])
 @pytest.mark.parametrize("shape", ["quest", "sign", "bible", "wide"])
 def test_emit_paths_agree(eng, path, shape, monkeypatch):
     """Child-run emission: the window kernel k_emit2 (W = 1: runs of <= 64
@@ -417,6 +417,8 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
         monkeypatch.setenv("FSM_CHILD_OF", "host")
     elif path == "device-child-of":
         monkeypatch.setenv("FSM_CHILD_OF", "device")
+    elif path == "host-kids":  # the kid table from the host records (default: k_freq_write + k_kid_off)
+        monkeypatch.setenv("FSM_KIDS", "host")
     if shape == "quest":
         ds, sup = gen.quest(20000, seed=9), 0.003
     elif shape == "sign":

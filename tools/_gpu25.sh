@@ -5,8 +5,8 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 400 python -u -m pytest -x -q --timeout 250 --timeout-method thread -m gpu tests/test_parity_gpu.py -k "emit or golden or random or sharded" > gpurun_out/t25_par.log 2>&1
 rc=$?; echo "parity rc=$rc"; tail -2 gpurun_out/t25_par.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 400 python -u tools/bench_configs.py --gpu-only > gpurun_out/configs_gpu.jsonl 2> gpurun_out/configs_gpu.log
-echo "configs rc=$?"
+
+
 r() { echo "== $*"; env "$@" timeout -k 10 120 python -u tools/run_one.py spade $SHAPE --support $SUP --reps 4 > gpurun_out/t25.log 2>&1; echo "rc=$?"; python3 -c "
 import json
 for l in open('gpurun_out/t25.log'):
