@@ -1651,7 +1651,6 @@ void order_recs(std::vector<FreqRec>& recs, uint32_t nrows) {
 struct Batch {
     Slab slab;
     RawVec<ClassMeta> cls;
-    RawVec<DClass> h_cls;
     DevBuf d_cls;
     DevBuf kid_tab;  // frequent children of every member (CSR over cbase + mi): offsets | slots | child ids
     const uint32_t* kid_off = nullptr;
@@ -1681,7 +1680,6 @@ struct Batch {
     void recycle() {
         slab = Slab{};
         cls.clear();
-        h_cls.clear();
         d_cls.release();
         kid_tab.release();
         child_pre.release();
@@ -1788,7 +1786,8 @@ struct Miner {
         // many classes: host-thread slices laid out from 0, then moved to their base (a
         // keyed slice starts on a group boundary, so the rules above hold across slices)
         const int64_t nthr = ncls >= (int64_t(1) << 15) ? host_threads() : 1;
-        b.h_cls.resize(size_t(ncls));
+        // the descriptors are written straight into the pinned staging slot (no host copy)
+        DClass* hc = static_cast<DClass*>(ctx->stage_host(0, std::max<size_t>(size_t(ncls), 1) * sizeof(DClass)));
         std::vector<uint64_t> toff(size_t(nthr) + 1, 0), tcb(size_t(nthr) + 1, 0);
         std::vector<uint8_t> tok(size_t(nthr), 1);
         for (int pass = keyed ? 0 : 1; pass < 2; ++pass) {
@@ -1815,7 +1814,7 @@ struct Miner {
                     m.cbase = uint32_t(cb);
                     off += rows * stride;
                     cb += m.D;
-                    b.h_cls[size_t(c)] = DClass{m.cnt_off, m.D, m.cbase, m.mshift, stride, {0, 0}};
+                    hc[size_t(c)] = DClass{m.cnt_off, m.D, m.cbase, m.mshift, stride, {0, 0}};
                 }
                 toff[size_t(t) + 1] = off;
                 tcb[size_t(t) + 1] = cb;
@@ -1839,13 +1838,14 @@ struct Miner {
                         ClassMeta& m = b.cls[size_t(c)];
                         m.cnt_off += bo;
                         m.cbase += bc;
-                        b.h_cls[size_t(c)].cnt_off = m.cnt_off;
-                        b.h_cls[size_t(c)].cbase = m.cbase;
+                        hc[size_t(c)].cnt_off = m.cnt_off;
+                        hc[size_t(c)].cbase = m.cbase;
                     }
                 });
             b.n_cnt = toff[size_t(nthr)];
             b.cbase_total = tcb[size_t(nthr)];
-            upload_staged(0, b.d_cls, b.h_cls.data(), b.h_cls.size() * sizeof(DClass));
+            b.d_cls.alloc(std::max<size_t>(size_t(ncls) * sizeof(DClass), 4));
+            ctx->stage_copy(0, b.d_cls.p, size_t(ncls) * sizeof(DClass));
             return kl;
         }
         return false;
