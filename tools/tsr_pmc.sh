@@ -11,7 +11,7 @@ cd /tmp
 timeout -s KILL 60 rocprofv3 -L > "$OUT/avail.txt" 2>&1 || true
 pass() {
     local name=$1; shift
-    timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "/tmp/tp_$name" -o run -- \
+    timeout -s KILL ${PMC_LIMIT:-120} rocprofv3 --pmc "$@" --output-format csv -d "/tmp/tp_$name" -o run -- \
         python3 "$R/tools/run_one.py" $ARGS > "$OUT/$name.log" 2>&1
     python3 - "/tmp/tp_$name" "$OUT/$name.json" <<'PY'
 import csv, glob, json, sys, collections
