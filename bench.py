@@ -117,6 +117,43 @@ def cpu_baseline(ds, support, seconds, threads, reps, stride):
             "complete": all(r["complete"] for r in runs), "joins_per_sample": [r["joins"] for r in runs]}
 
 
+def c2_leg(fsm, gen, cpu_reps, steps=20):
+    """BASELINE config 2 (Quest C10 T2.5 S4 I1.25 D100K, minsup 0.5 %): the GPU mine
+    (median of `steps` after warmup) beside the COMPLETE single-thread CPU restatement of
+    the same mine (every class; SURVEY §8d: wall time from the flattened DB to the
+    results, the CPU's F1 vertical build included, median of `cpu_reps`)."""
+    from oracle import oracle
+    support = 0.005
+    ds = gen.quest(100000, seed=1)
+    with fsm.Engine(0) as eng:
+        db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+        for _ in range(3):
+            eng.spade_csr(db, support)
+        t = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            _, meta = eng.spade_csr(db, support)
+            t.append((time.perf_counter() - t0) * 1000.0)
+        st = eng.stats()
+        db.free()
+    runs = [oracle.spade_tokens(ds.seq_off, ds.tokens, support, want_patterns=False, threads=1)
+            for _ in range(max(1, cpu_reps))]
+    if any(r["joins"] != st["joins"] for r in runs):
+        raise SystemExit("c2 leg: CPU restatement and GPU disagree on the join count")
+    cpu_s = statistics.median(r["seconds"] for r in runs)
+    gpu_ms = statistics.median(t)
+    return {"workload": "quest-C10-T2.5-S4-I1.25-D100000-N10000-seed1, minsup 0.005",
+            "gpu_mine_ms": gpu_ms, "gpu_joins_per_s": st["joins"] / (gpu_ms / 1000.0),
+            "patterns": meta["n"], "joins": st["joins"],
+            "cpu_baseline": {"value": st["joins"] / cpu_s, "unit": "joins/s", "cores": 1, "kind": "port",
+                             "seconds": [round(r["seconds"], 2) for r in runs], "median_s": cpu_s,
+                             "complete": all(r["complete"] for r in runs),
+                             "sample": "the complete mine (every class, F1 vertical build included) by the "
+                                       "single-thread CPU restatement (oracle/fsm_oracle.c), median of %d"
+                                       % max(1, cpu_reps)},
+            "gpu_vs_cpu_1thread": (cpu_s * 1000.0) / gpu_ms}
+
+
 def tsr_leg(fsm, gen, cpu_seconds, cpu_reps, cpu):
     """BASELINE config 4 (TSR, 990,002 Kosarak-shaped sequences, k = 1000,
     minconf 0.5): one mine after a warmup mine, expansions/s, the roofline of
@@ -134,7 +171,8 @@ def tsr_leg(fsm, gen, cpu_seconds, cpu_reps, cpu):
         st, ks = eng.stats(), eng.kernel_stats()
         db.free()
     dom = max(ks, key=lambda q: q["ms"])
-    ach = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] else 0.0
+    ach = (dom["survey_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] else 0.0
+    ach_own = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] else 0.0
     leg = {"metric": "TSR expansions/s, Kosarak-shaped 990,002 sequences, k = 1000, minconf 0.5",
            "value": st["expansions"] / (ms / 1000.0), "unit": "expansions/s", "mine_ms": ms,
            "rules": len(rules), "final_minsup": meta["final_minsup"], "expansions": st["expansions"],
@@ -142,10 +180,14 @@ def tsr_leg(fsm, gen, cpu_seconds, cpu_reps, cpu):
            "ms_gpu_wait": st["ms_count_kernel"],
            "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": ach, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": dom["ms"],
-                        "alg_bytes": dom["alg_bytes"], "launches": dom["launches"],
-                        "bytes_basis": "SURVEY §8(d) TSR unit: 12 B per scanned row entry (item, first, last) + "
-                                       "8 B per domain sid + the |X|+|Y| sid-bitmap operands (N/8 B each); "
-                                       "kernel time sampled every 16th launch with HIP events"},
+                        "alg_bytes": dom["survey_bytes"], "launches": dom["launches"],
+                        "bytes_basis": "SURVEY §8(d) TSR unit for the row kernel: 4 B token + 4 B first/last per "
+                                       "scanned row position (8 B per packed (kid, first|last) entry); the sid-bitmap "
+                                       "operands (N/8 B each) are k_exp_domain's; kernel time sampled every 16th "
+                                       "launch with HIP events",
+                        "own_bytes": dom["alg_bytes"], "own_frac": ach_own / HBM_PEAK_GBS,
+                        "own_bytes_basis": "tsr_engine.hip: 8 B per scanned row entry + 8 B per domain sid + "
+                                           "the partial histogram rows written"},
            "kernels": [{"name": q["name"], "launches": q["launches"], "ms": round(q["ms"], 1)} for q in ks]}
     if cpu:
         # the restatement needs hours at 990K sequences, so both sides run the same
@@ -183,13 +225,14 @@ def main():
     ap.add_argument("--support", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="bound of one CPU sample")
-    ap.add_argument("--cpu-reps", type=int, default=1)
+    ap.add_argument("--cpu-reps", type=int, default=3, help="CPU samples per leg (median; SURVEY §8d: 3)")
     ap.add_argument("--cpu-stride", type=int, default=128, help="class stride of the 1-thread CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     # all-cores CPU mode (SURVEY §8d ii); 0 = every CPU of this process's share (0 skips: -1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: CPU dry run)")
     ap.add_argument("--no-tsr", action="store_true", help="skip the config-4 TSR leg (N = 1 only)")
+    ap.add_argument("--no-c2", action="store_true", help="skip the config-2 complete-CPU leg (N = 1 only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -219,7 +262,9 @@ def main():
     if world > 1 and args.dist_backend == "nccl" and os.environ.get("FSM_BENCH_COMM", "rccl") == "rccl":
         # libfsm's own RCCL communicator (its collectives stay on the device): rank 0
         # makes the unique id, torch broadcasts it; if any rank cannot create it, every
-        # rank falls back to the host-staged torch collectives below
+        # rank falls back to the host-staged torch collectives below.  The communicator
+        # init is non-blocking and bounded (FSM_COMM_INIT_TIMEOUT_S, comm.cpp), so a peer
+        # that fails before its own init makes the others fail over, not hang.
         uid = torch.zeros(129, dtype=torch.uint8, device="cuda")
         if rank == 0:
             try:
@@ -299,10 +344,13 @@ def main():
         return
 
     value = joins_all / (ms / 1000.0)  # joins of all ranks (libfsm sums them) / slowest rank
-    # roofline of the dominant kernel: its algorithmic bytes / its device
-    # time (HIP events on libfsm's stream, summed over the launches of the last step)
+    # roofline of the dominant kernel: its work priced in SURVEY §8(d) units (12-B (sid, mask)
+    # id-list entries read + written) / its device time (HIP events on libfsm's stream, summed
+    # over the launches of the last step); the same time over the kernel's own slab bytes
+    # (24-B entries: cid, mem, lohi, pos + mask) is `roofline_slab`
     dom = max(ks, key=lambda k: k["ms"])
-    achieved = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
+    achieved = (dom["survey_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
+    achieved_slab = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
     traffic = pmc_traffic(dom["name"])  # per step
     traffic_launch = traffic / dom["launches"] if traffic is not None and dom["launches"] else None
     # SURVEY §8(d) unit for the F2: 8 B per (item, sid) first/last pair read per pass,
@@ -329,13 +377,19 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_launch,
                      "kernel": dom["name"], "launches_per_step": dom["launches"],
-                     "kernel_ms_per_step": dom["ms"], "alg_bytes_per_step": dom["alg_bytes"],
-                     "alg_bytes_per_launch": dom["alg_bytes"] / max(dom["launches"], 1),
+                     "kernel_ms_per_step": dom["ms"], "alg_bytes_per_step": dom["survey_bytes"],
+                     "alg_bytes_per_launch": dom["survey_bytes"] / max(dom["launches"], 1),
                      "traffic_per_step": traffic,
                      "traffic_basis": "HBM bytes per launch (average over the step's launches) = "
                                       "(2 x FETCH_SIZE + WRITE_SIZE) / launches from the committed PMC passes",
-                     "bytes_basis": "the kernel's compulsory reads + writes per launch (DESIGN.md §4)",
+                     "bytes_basis": "SURVEY §8(d): one 12-B (sid u32, eid mask u64) id-list entry per parent entry "
+                                    "read and per child entry written (4 + 8W B for W mask words)",
                      "traffic_source": PMC_FILE if traffic is not None else None},
+        "roofline_slab": {"bound": "hbm", "achieved": achieved_slab, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": achieved_slab / HBM_PEAK_GBS, "kernel": dom["name"],
+                          "alg_bytes_per_step": dom["alg_bytes"],
+                          "bytes_basis": "the kernel's own slab layout: 16 + 8W B per entry (cid, mem, lohi, pos, "
+                                         "mask) read and written (DESIGN.md §4)"},
         "roofline_survey_f2": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                                "bytes_basis": "SURVEY §8(d): 8 B per root (item, sid) entry per F2 pass",
                                "alg_bytes": f2_bytes, "kernels_ms": f2_ms,
@@ -378,6 +432,8 @@ def main():
     eng.close()
     if not args.no_tsr and world == 1:
         line["tsr_c4"] = tsr_leg(fsm, gen, args.cpu_seconds, args.cpu_reps, not args.no_cpu_baseline)
+    if not args.no_c2 and not args.no_cpu_baseline and world == 1:
+        line["c2_complete"] = c2_leg(fsm, gen, args.cpu_reps)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

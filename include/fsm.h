@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FSM_ABI_VERSION 4
+#define FSM_ABI_VERSION 5
 
 /* status codes */
 #define FSM_OK 0
@@ -53,14 +53,20 @@ typedef struct fsm_db fsm_db;
 typedef enum { FSM_MODE_SPADE = 0, FSM_MODE_TSR = 1 } fsm_mode;
 
 /* Host-side collectives, an alternative to RCCL for nranks > 1 (several ranks
- * on one GPU, or any host transport).  Both are called collectively by every
- * rank with the same sizes and return 0 on success.  Buffers are host memory.
+ * on one GPU, or any host transport).  The first two are called collectively by
+ * every rank with the same sizes and return 0 on success.  Buffers are host memory.
  *   allreduce_u32: buf[0..n) <- element-wise sum over ranks (in place)
- *   allgather:     recv[r*bytes .. (r+1)*bytes) <- rank r's send[0..bytes)   */
+ *   allgather:     recv[r*bytes .. (r+1)*bytes) <- rank r's send[0..bytes)
+ *   fetch_add:     (optional, NULL = none) NOT collective: atomically adds inc to
+ *                  the shared counter `key` (0 before its first add) and returns
+ *                  its previous value, or -1 on failure.  The work-stealing claim of
+ *                  the sharded SPADE lattice; without it the ranks
+ *                  split the classes by a static plan.  Keys are never reused.  */
 typedef struct {
     void* user;
     int (*allreduce_u32)(void* user, uint32_t* buf, int64_t n);
     int (*allgather)(void* user, const void* send, void* recv, int64_t bytes);
+    int64_t (*fetch_add)(void* user, int64_t key, int64_t inc);
 } fsm_host_comm;
 
 typedef struct {
@@ -136,6 +142,11 @@ typedef struct {
     int64_t exp_domain;         /* TSR: sids expanded over (sum over expansions of |sids(X u Y)|) */
     int64_t exp_entries;        /* TSR: row entries read by the expansions */
     int64_t exp_bitmap_bytes;   /* TSR: sid-bitmap operand bytes ANDed by the expansions */
+    /* this rank's own share of a sharded mine (not summed over ranks) */
+    int64_t rank_claims;        /* SPADE: work units (first-level classes / sub-classes) this rank claimed */
+    int64_t rank_root_owned;    /* SPADE: root entries this rank joined as the owner (F2 keys + root emit) */
+    int64_t rank_root_slab;     /* SPADE: root entries this rank wrote to a root slab (0: DB-direct root) */
+    int64_t rank_units;         /* TSR: expansion rule slots this rank counted */
 } fsm_stats;
 
 /* Per-kernel device time of the last fsm_*_mine call (HIP events on the
@@ -144,8 +155,10 @@ typedef struct {
 typedef struct {
     char name[40];
     int64_t launches;
-    int64_t alg_bytes;          /* algorithmic HBM bytes over all launches */
+    int64_t alg_bytes;          /* algorithmic HBM bytes over all launches (the kernel's own layout) */
     double ms;                  /* summed device time over all launches */
+    int64_t survey_bytes;       /* the same work priced in SURVEY §8(d) units (12-B (sid, mask) id-list
+                                   entries for SPADE, 8 B per scanned position for TSR); 0 = not priced */
 } fsm_kernel_stat;
 
 int fsm_abi_version(void);

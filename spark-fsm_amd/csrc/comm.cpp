@@ -10,6 +10,9 @@
 //             run several ranks on one GPU (tests) or over any host transport.
 //             Device buffers are staged through host memory around the callback.
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -17,6 +20,7 @@
 #include <cstring>
 
 #include <mutex>
+#include <thread>
 
 #include <rccl/rccl.h>
 
@@ -27,7 +31,9 @@ namespace {
 
 struct RcclApi {
     ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
-    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
+    ncclResult_t (*comm_get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                hipStream_t) = nullptr;
@@ -47,13 +53,17 @@ const RcclApi& rccl() {
             return;
         }
         api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
-        api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        api.comm_init_rank_config =
+            reinterpret_cast<decltype(api.comm_init_rank_config)>(dlsym(h, "ncclCommInitRankConfig"));
+        api.comm_get_async_error =
+            reinterpret_cast<decltype(api.comm_get_async_error)>(dlsym(h, "ncclCommGetAsyncError"));
+        api.comm_abort = reinterpret_cast<decltype(api.comm_abort)>(dlsym(h, "ncclCommAbort"));
         api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
         api.all_reduce = reinterpret_cast<decltype(api.all_reduce)>(dlsym(h, "ncclAllReduce"));
         api.all_gather = reinterpret_cast<decltype(api.all_gather)>(dlsym(h, "ncclAllGather"));
         api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(h, "ncclGetErrorString"));
-        if (!api.get_unique_id || !api.comm_init_rank || !api.comm_destroy || !api.all_reduce || !api.all_gather ||
-            !api.error_string) {
+        if (!api.get_unique_id || !api.comm_init_rank_config || !api.comm_get_async_error || !api.comm_abort ||
+            !api.comm_destroy || !api.all_reduce || !api.all_gather || !api.error_string) {
             err = "librccl.so.1 lacks an expected symbol";
             api = RcclApi{};
         }
@@ -66,24 +76,102 @@ void nccl_check(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw Error(FSM_ECOMM, std::string(what) + ": " + rccl().error_string(r));
 }
 
+// The communicator is created non-blocking, so that a peer that never joins (it
+// failed before its own init) cannot block this rank forever: the init is polled
+// up to FSM_COMM_INIT_TIMEOUT_S seconds (default 300), then aborted with FSM_ECOMM.
+// Non-blocking communicators may return ncclInProgress from a collective's enqueue
+// as well; wait() polls the communicator's state until the enqueue has completed.
 class RcclComm final : public Comm {
   public:
     RcclComm(int nranks, int rank, const uint8_t id[128]) : Comm(nranks, rank) {
         ncclUniqueId uid;
         std::memcpy(uid.internal, id, sizeof(uid.internal));
-        nccl_check(rccl().comm_init_rank(&comm_, nranks, uid, rank), "ncclCommInitRank");
+        // the work-stealing counters: one shared-memory segment of the node, named after the
+        // unique id, opened by every rank BEFORE the communicator init (which returns only
+        // once every rank has joined), unlinked by rank 0 after it (the mappings stay)
+        char name[64];
+        uint64_t h = 1469598103934665603ull;  // FNV-1a of the unique id
+        for (int k = 0; k < 128; ++k) h = (h ^ id[k]) * 1099511628211ull;
+        std::snprintf(name, sizeof(name), "/fsm-claims-%016llx", (unsigned long long)h);
+        const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+        if (fd >= 0) {
+            if (ftruncate(fd, off_t(kSlots * sizeof(int64_t))) == 0) {
+                void* p = mmap(nullptr, kSlots * sizeof(int64_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+                if (p != MAP_FAILED) ctr_ = static_cast<int64_t*>(p);
+            }
+            close(fd);
+        }
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t r = rccl().comm_init_rank_config(&comm_, nranks, uid, rank, &cfg);
+        if (r != ncclSuccess && r != ncclInProgress) {
+            if (comm_) (void)rccl().comm_abort(comm_);
+            comm_ = nullptr;
+            nccl_check(r, "ncclCommInitRankConfig");
+        }
+        const char* tv = std::getenv("FSM_COMM_INIT_TIMEOUT_S");
+        const double limit_ms = 1000.0 * (tv ? std::max(1.0, std::atof(tv)) : 300.0);
+        try {
+            wait("ncclCommInitRankConfig", limit_ms);
+        } catch (...) {
+            if (rank == 0) shm_unlink(name);
+            unmap();
+            throw;
+        }
+        if (rank == 0) shm_unlink(name);
     }
     ~RcclComm() override {
         if (comm_) (void)rccl().comm_destroy(comm_);
+        unmap();
+    }
+    bool has_fetch_add() const override { return ctr_ != nullptr; }
+    int64_t fetch_add(int64_t key, int64_t inc) override {
+        if (!ctr_) return -1;
+        return __atomic_fetch_add(&ctr_[size_t(key) % kSlots], inc, __ATOMIC_SEQ_CST);
+    }
+    void reset_counter(int64_t key) override {
+        // slot key % kSlots was last used kSlots mines ago, long past that mine's final gather
+        if (ctr_ && rank() == 0) __atomic_store_n(&ctr_[size_t(key) % kSlots], int64_t(0), __ATOMIC_SEQ_CST);
     }
     void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
-        if (n) nccl_check(rccl().all_reduce(dev, dev, n, ncclUint32, ncclSum, comm_, s), "ncclAllReduce");
+        if (n) enqueued(rccl().all_reduce(dev, dev, n, ncclUint32, ncclSum, comm_, s), "ncclAllReduce");
     }
     void allgather(const void* dev_send, void* dev_recv, size_t bytes, hipStream_t s) override {
-        if (bytes) nccl_check(rccl().all_gather(dev_send, dev_recv, bytes, ncclUint8, comm_, s), "ncclAllGather");
+        if (bytes) enqueued(rccl().all_gather(dev_send, dev_recv, bytes, ncclUint8, comm_, s), "ncclAllGather");
     }
 
   private:
+    void enqueued(ncclResult_t r, const char* what) {
+        if (r == ncclInProgress) wait(what, 1e300);
+        else nccl_check(r, what);
+    }
+    // poll until the communicator leaves ncclInProgress (abort past limit_ms)
+    void wait(const char* what, double limit_ms) {
+        const double t0 = now_ms();
+        for (;;) {
+            ncclResult_t st = ncclSuccess;
+            nccl_check(rccl().comm_get_async_error(comm_, &st), "ncclCommGetAsyncError");
+            if (st == ncclSuccess) return;
+            if (st != ncclInProgress) {
+                (void)rccl().comm_abort(comm_);
+                comm_ = nullptr;
+                nccl_check(st, what);
+            }
+            if (now_ms() - t0 > limit_ms) {
+                (void)rccl().comm_abort(comm_);
+                comm_ = nullptr;
+                throw Error(FSM_ECOMM, std::string(what) + ": timed out waiting for the peer ranks "
+                                                           "(FSM_COMM_INIT_TIMEOUT_S)");
+            }
+            std::this_thread::yield();
+        }
+    }
+    void unmap() {
+        if (ctr_) munmap(ctr_, kSlots * sizeof(int64_t));
+        ctr_ = nullptr;
+    }
+    static constexpr size_t kSlots = 512;
+    int64_t* ctr_ = nullptr;
     ncclComm_t comm_ = nullptr;
 };
 
@@ -117,6 +205,10 @@ class HostComm final : public Comm {
         if (cb_.allgather(cb_.user, send, recv, int64_t(bytes)) != 0)
             throw Error(FSM_ECOMM, "host all-gather callback failed");
     }
+    bool has_fetch_add() const override { return cb_.fetch_add != nullptr; }
+    int64_t fetch_add(int64_t key, int64_t inc) override {
+        return cb_.fetch_add ? cb_.fetch_add(cb_.user, key, inc) : -1;  // (keys are never reused: no reset)
+    }
 
   private:
     fsm_host_comm cb_;
@@ -140,12 +232,18 @@ void Comm::host_allgather(const void* send, void* recv, size_t bytes, hipStream_
     FSM_HIP(hipStreamSynchronize(s));
 }
 
-std::vector<uint8_t> Comm::gather_blobs(const std::vector<uint8_t>& mine, std::vector<size_t>& sizes, hipStream_t s) {
+std::vector<uint8_t> Comm::gather_blobs(const std::vector<uint8_t>& mine, std::vector<size_t>& sizes, hipStream_t s,
+                                        Agreement* agr, uint32_t* extra, size_t n_extra) {
     const int N = nranks();
-    std::vector<uint32_t> sz(size_t(N) * 2, 0);  // (lo, hi) u32 halves of each rank's size
+    // (lo, hi) u32 halves of each rank's size | 8 failure flags | the caller's extra values
+    std::vector<uint32_t> sz(size_t(N) * 2 + 8 + n_extra, 0);
     sz[size_t(rank()) * 2] = uint32_t(mine.size() & 0xFFFFFFFFu);
     sz[size_t(rank()) * 2 + 1] = uint32_t(uint64_t(mine.size()) >> 32);
+    if (agr) agr->flags(sz.data() + size_t(N) * 2);
+    for (size_t k = 0; k < n_extra; ++k) sz[size_t(N) * 2 + 8 + k] = extra[k];
     host_allreduce_u32(sz.data(), sz.size(), s);
+    if (agr) agr->check(sz.data() + size_t(N) * 2);
+    for (size_t k = 0; k < n_extra; ++k) extra[k] = sz[size_t(N) * 2 + 8 + k];
     sizes.assign(size_t(N), 0);
     size_t mx = 0;
     for (int r = 0; r < N; ++r) {
@@ -200,11 +298,15 @@ namespace fsm {
 void Agreement::agree(hipStream_t s) {
     if (!comm) return;
     std::vector<uint32_t> v(8, 0u);
-    if (code) v[size_t(std::clamp(code, 1, 7))] = 1u;
+    flags(v.data());
     comm->host_allreduce_u32(v.data(), v.size(), s);
+    check(v.data());
+}
+
+void Agreement::check(const uint32_t* v) const {
     if (code) throw Error(code, msg);
     for (int c = 1; c < 8; ++c)
-        if (v[size_t(c)])
+        if (v[c])
             throw Error(c, std::string(what) + ": a peer rank failed (FSM error " + std::to_string(c) +
                                "); the sharded mine is aborted on every rank");
 }

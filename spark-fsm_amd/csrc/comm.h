@@ -1,6 +1,7 @@
 // comm.h — collectives of the sharded SPADE path (see comm.cpp).
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <string>
 
@@ -8,12 +9,25 @@
 
 namespace fsm {
 
+struct Agreement;
+
 class Comm {
   public:
     Comm(int nranks, int rank) : nranks_(nranks), rank_(rank) {}
     virtual ~Comm() = default;
     int nranks() const { return nranks_; }
     int rank() const { return rank_; }
+    // Work-stealing counters shared by the ranks (not collective): fetch_add returns the
+    // counter's previous value (-1: failed).  The RCCL communicator keeps them in a POSIX
+    // shared-memory segment of the node, the host communicator calls fsm_host_comm.fetch_add.
+    // reset_counter(key) runs on every rank before the collective that precedes the first
+    // claim on `key` (the shared-memory slots are reused).  next_key() advances identically
+    // on every rank (one key per sharded mine).
+    virtual bool has_fetch_add() const { return false; }
+    virtual int64_t fetch_add(int64_t /*key*/, int64_t /*inc*/) { return -1; }
+    virtual void reset_counter(int64_t /*key*/) {}
+    int64_t next_key() { return key_++; }
+    int claim_mode = -1;  // agreed over the ranks at the first sharded mine: 1 claims, 0 static plan
     // in-place sum over ranks of a device u32 array (stream-ordered)
     virtual void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) = 0;
     // recv[r * bytes .. (r+1) * bytes) = rank r's send block (device buffers)
@@ -21,11 +35,16 @@ class Comm {
     // host-memory forms (synchronous)
     virtual void host_allreduce_u32(uint32_t* h, size_t n, hipStream_t s);
     virtual void host_allgather(const void* send, void* recv, size_t bytes, hipStream_t s);
-    // every rank's byte blob, concatenated in rank order; sizes[r] = rank r's length
-    std::vector<uint8_t> gather_blobs(const std::vector<uint8_t>& mine, std::vector<size_t>& sizes, hipStream_t s);
+    // every rank's byte blob, concatenated in rank order; sizes[r] = rank r's length.
+    // agr: the failure agreement rides on the size all-reduce (no round trip of its own):
+    // if any rank failed, every rank throws its FSM_E* before the blobs move.  extra[0..n):
+    // u32 values summed over the ranks in the same all-reduce.
+    std::vector<uint8_t> gather_blobs(const std::vector<uint8_t>& mine, std::vector<size_t>& sizes, hipStream_t s,
+                                      Agreement* agr = nullptr, uint32_t* extra = nullptr, size_t n_extra = 0);
 
   private:
     int nranks_, rank_;
+    int64_t key_ = 0;
 };
 
 // Failure agreement of a sharded phase: a failure on one rank must not leave
@@ -58,6 +77,12 @@ struct Agreement {
         }
     }
     void agree(hipStream_t s);
+    // flags[c] (c = 1..7) summed over the ranks: throw this rank's failure or a peer's
+    void check(const uint32_t* flags) const;
+    void flags(uint32_t* f) const {  // this rank's 8 flag slots
+        for (int c = 0; c < 8; ++c) f[c] = 0;
+        if (code) f[std::clamp(code, 1, 7)] = 1u;
+    }
     // FSM_INJECT_FAIL="<rank>,<phase>": throw FSM_ELIMIT on that rank at that phase
     // (test hook for the agreement)
     void maybe_inject(const char* phase) const;

@@ -14,6 +14,11 @@ struct SpadeDevDB {
     fsm::DevBuf mask;     // u64 [E*W]
     int64_t R = 0, E = 0, U = 0;
     int W = 1;
+    // the DB-direct root (spade_engine.hip): offset in row << 16 | row length of every
+    // entry, made by the first mine that needs it; pos_state 0 = not made, 1 = made,
+    // -1 = a row exceeds 65535 entries (that DB keeps the root slab)
+    fsm::DevBuf pos;      // u32 [E]
+    int pos_state = 0;
 };
 
 // TSR: horizontal rows (sid = row) of (item, first, last itemset index),

@@ -249,7 +249,7 @@ size_t KernelClock::begin(const char* name) {
     size_t idx = recs.size();
     for (size_t k = 0; k < recs.size(); ++k)
         if (recs[k].name == name) idx = k;
-    if (idx == recs.size()) recs.push_back(Rec{name, {}, 0});
+    if (idx == recs.size()) recs.push_back(Rec{name, {}, 0, 0});
     hipEvent_t a, b;
     FSM_HIP(hipEventCreate(&a));
     if (hipEventCreate(&b) != hipSuccess) {
@@ -261,9 +261,10 @@ size_t KernelClock::begin(const char* name) {
     return idx;
 }
 
-void KernelClock::end(size_t idx, int64_t alg_bytes) {
+void KernelClock::end(size_t idx, int64_t alg_bytes, int64_t survey_bytes) {
     FSM_HIP(hipEventRecord(recs[idx].ev.back().second, s));
     recs[idx].bytes += alg_bytes;
+    recs[idx].survey += survey_bytes;
 }
 
 void KernelClock::finish(std::vector<fsm_kernel_stat>& out) {
@@ -274,6 +275,7 @@ void KernelClock::finish(std::vector<fsm_kernel_stat>& out) {
         std::snprintf(k.name, sizeof(k.name), "%s", r.name.c_str());
         k.launches = int64_t(r.ev.size());
         k.alg_bytes = r.bytes;
+        k.survey_bytes = r.survey;
         for (auto& e : r.ev) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) k.ms += ms;

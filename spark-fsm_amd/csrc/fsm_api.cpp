@@ -127,7 +127,12 @@ int fsm_comm_selftest(const fsm_opts* opts) {
         std::vector<uint8_t> mine(size_t(r) * 3 + 1);
         for (size_t j = 0; j < mine.size(); ++j) mine[j] = uint8_t(r * 7 + j);
         std::vector<size_t> sizes;
-        const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, nullptr);
+        // (the work-stealing counter of the claim test below is reset before this gather, which
+        // also agrees on whether every rank has the shared counters)
+        const int64_t key = comm->next_key();
+        comm->reset_counter(key);
+        uint32_t ex = comm->has_fetch_add() ? 1u : 0u;
+        const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, nullptr, nullptr, &ex, 1);
         size_t at = 0;
         for (uint32_t q = 0; q < N; ++q) {
             if (sizes[q] != size_t(q) * 3 + 1) throw Error(FSM_ECOMM, "selftest: gather size mismatch");
@@ -136,6 +141,33 @@ int fsm_comm_selftest(const fsm_opts* opts) {
             at += sizes[q];
         }
         if (at != all.size()) throw Error(FSM_ECOMM, "selftest: gather length mismatch");
+        if (ex == N) {
+            // claims: the ranks take ranges of r + 1 units of [0, 997) from the shared counter
+            // until it runs out; every unit must be claimed exactly once
+            constexpr int64_t kUnits = 997;
+            std::vector<uint8_t> got;
+            for (;;) {
+                const int64_t old = comm->fetch_add(key, int64_t(r) + 1);
+                if (old < 0) throw Error(FSM_ECOMM, "selftest: fetch_add failed");
+                if (old >= kUnits) break;
+                for (int64_t u = old; u < std::min<int64_t>(old + r + 1, kUnits); ++u) {
+                    const uint16_t v16 = uint16_t(u);
+                    got.push_back(uint8_t(v16 & 0xFF));
+                    got.push_back(uint8_t(v16 >> 8));
+                }
+            }
+            std::vector<size_t> csz;
+            const std::vector<uint8_t> claimed = comm->gather_blobs(got, csz, nullptr);
+            std::vector<int> seen(kUnits, 0);
+            for (size_t j = 0; j + 1 < claimed.size(); j += 2) {
+                const size_t u = size_t(claimed[j]) | (size_t(claimed[j + 1]) << 8);
+                if (u >= size_t(kUnits)) throw Error(FSM_ECOMM, "selftest: claimed unit out of range");
+                ++seen[u];
+            }
+            for (int64_t u = 0; u < kUnits; ++u)
+                if (seen[size_t(u)] != 1) throw Error(FSM_ECOMM, "selftest: a unit was claimed " +
+                                                                     std::to_string(seen[size_t(u)]) + " times");
+        }
     });
 }
 
@@ -164,6 +196,8 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
         // ring (two 4 MiB pinned slots, each DMA'd once: the first DMA from a pinned
         // buffer is slow) and the host thread pool's workers
         {
+            // (from the context's own pool: guarded() captured the pool before it existed)
+            fsm::PoolScope ps(ctx->pool);
             const size_t rb = size_t(4) << 20;
             fsm::DevBuf warm(rb);
             for (int slot = 2; slot <= 3; ++slot) {

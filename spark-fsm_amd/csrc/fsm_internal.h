@@ -54,6 +54,7 @@ struct KernelClock {
         std::string name;
         std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
         int64_t bytes = 0;
+        int64_t survey = 0;  // SURVEY §8(d) bytes (fsm_kernel_stat.survey_bytes)
     };
     hipStream_t s = nullptr;
     std::vector<Rec> recs;
@@ -62,8 +63,11 @@ struct KernelClock {
     KernelClock& operator=(const KernelClock&) = delete;
     ~KernelClock() { release(); }
     size_t begin(const char* name);
-    void end(size_t idx, int64_t alg_bytes);
-    void add_bytes(size_t idx, int64_t alg_bytes) { recs[idx].bytes += alg_bytes; }  // known after a later sync
+    void end(size_t idx, int64_t alg_bytes, int64_t survey_bytes = 0);
+    void add_bytes(size_t idx, int64_t alg_bytes, int64_t survey_bytes = 0) {  // known after a later sync
+        recs[idx].bytes += alg_bytes;
+        recs[idx].survey += survey_bytes;
+    }
     void finish(std::vector<fsm_kernel_stat>& out);
     void release();
 };

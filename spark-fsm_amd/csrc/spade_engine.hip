@@ -80,6 +80,7 @@ struct SlabPtrs {
     uint32_t* lohi;
     uint32_t* pos;
     uint64_t* mask;
+    uint32_t* lim = nullptr;  // emit target: set when a child run exceeds 65535 entries (pos fields)
 };
 
 // ------------------------------------------------------------------ kernels
@@ -449,8 +450,112 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
         cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + 7u) & ~7u;
 }
 
-template <int W>
-__global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restrict__ roff, uint32_t R, uint32_t rpb,
+// ---- DB-direct root.  The root class is the DB restricted to the frequent items, so
+// its kernels (F2 plan, F2 keys, root emit) read the DB rows themselves instead of a
+// root slab written per mine (k_root_count + k_root_write: 0.5 ms and 24 B per entry
+// at D1M, replicated on every rank of a sharded mine).  A DB entry's member id is
+// rk2[item]: 2 x rank for a frequent item (a root member is a sequence-extension), and
+// an ODD value for an infrequent one, 2 x (frequent items below it) - 1, so that in
+// wrapped order (v + 1) the row stays sorted and an infrequent entry never equals a
+// partner target (even).  Its lohi comes from the mask; its pos (offset in row << 16 |
+// row length) from the DB's own pos array (k_db_pos, once per DB).
+struct RootRef {
+    const uint32_t* item;  // DB entry -> dense item (nullptr: not the DB-direct root)
+    const uint32_t* rk2;   // dense item -> member id (above)
+};
+template <int W> __device__ __forceinline__ uint32_t lohi_of(const uint64_t* __restrict__ mask, size_t e) {
+    uint64_t m[W];
+    load_mask<W>(mask + e * W, m);
+    return mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+}
+// entry accessors of a batch slab (kRoot = false) or of the DB-direct root (kRoot = true)
+template <int W, bool kRoot> struct Ent {
+    static constexpr bool kRootEnt = kRoot;
+    const uint32_t* __restrict__ cid;
+    const uint32_t* __restrict__ mem;
+    const uint32_t* __restrict__ lohi;
+    const uint64_t* __restrict__ mask;
+    RootRef rr;
+    __device__ __forceinline__ uint32_t c(size_t e) const {
+        if constexpr (kRoot) return 0u; else return cid[e];
+    }
+    __device__ __forceinline__ uint32_t m(size_t e) const {
+        if constexpr (kRoot) return rr.rk2[rr.item[e]]; else return mem[e];
+    }
+    __device__ __forceinline__ uint32_t lh(size_t e) const {
+        if constexpr (kRoot) return lohi_of<W>(mask, e); else return lohi[e];
+    }
+};
+// member ids in the wrapped order of the DB-direct root (identity order for batch slabs,
+// whose member ids stay below 2^31)
+__device__ __forceinline__ bool mem_less(uint32_t a, uint32_t b) { return a + 1u < b + 1u; }
+
+// pos of every DB entry: offset in its row << 16 | row length (rows <= 65535 entries;
+// longer ones raise *flag and the mine keeps the root slab)
+__global__ __launch_bounds__(kBlock) void k_db_pos(const uint32_t* __restrict__ row_off, uint32_t R,
+                                                   uint32_t* __restrict__ pos, uint32_t* __restrict__ flag) {
+    const uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= R) return;
+    const uint32_t rb = row_off[r], re = row_off[r + 1], len = re - rb;
+    if (len > 0xFFFFu) {
+        if (lane_id() == 0) atomicOr(flag, 1u);
+        return;
+    }
+    for (uint32_t e = rb + lane_id(); e < re; e += 64) pos[e] = ((e - rb) << 16) | len;
+}
+
+// F2 plan of the DB-direct root: block b histograms, by rank group, the key capacity of
+// the frequent entries of its rpb rows that lie in the member range [mlo, mhi)
+// (temporal <= row's frequent entries, equality <= frequent partners after it) and
+// counts the rows' frequent entries (the root entries, *nroot).
+__global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __restrict__ row_off,
+                                                          const uint32_t* __restrict__ item,
+                                                          const uint32_t* __restrict__ rk2, uint32_t R, uint32_t rpb,
+                                                          uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
+                                                          uint32_t mhi, uint32_t* __restrict__ cap,
+                                                          unsigned long long* __restrict__ nroot) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
+    __shared__ uint32_t blk_root;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
+    if (threadIdx.x == 0) blk_root = 0;
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+    uint32_t my_root = 0;
+    for (uint32_t r = r0 + wave; r < r1; r += kF2Waves) {
+        const uint32_t rb = row_off[r], e1 = row_off[r + 1];
+        // the row's frequent entries (first chunk kept in registers: rows are short)
+        uint32_t v0 = kNone, len = 0;
+        for (uint32_t b0 = rb; b0 < e1; b0 += 64) {
+            const uint32_t e = b0 + lane;
+            const uint32_t v = e < e1 ? rk2[item[e]] : kNone;
+            if (b0 == rb) v0 = v;
+            len += uint32_t(__popcll(__ballot(e < e1 && !(v & 1u))));
+        }
+        my_root += len;
+        uint32_t k = 0;
+        for (uint32_t b0 = rb; b0 < e1; b0 += 64) {
+            const uint32_t e = b0 + lane;
+            const uint32_t v = b0 == rb ? v0 : (e < e1 ? rk2[item[e]] : kNone);
+            const bool fr = e < e1 && !(v & 1u);
+            const uint64_t bal = __ballot(fr);
+            const uint32_t p = k + uint32_t(__popcll(bal & lt));
+            if (fr && v - mlo < mhi - mlo) atomicAdd(&h[group_of(v >> 1, pm)], 2 * len - 1 - p);
+            k += uint32_t(__popcll(bal));
+        }
+    }
+    if (lane == 0) atomicAdd(&blk_root, my_root);
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + 7u) & ~7u;
+    if (threadIdx.x == 0 && blk_root) atomicAdd(nroot, (unsigned long long)blk_root);
+}
+
+// kRoot: the rows are the DB's (row_off32), entries read through rr (DB-direct root)
+template <int W, bool kRoot>
+__global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restrict__ roff,
+                                                        const uint32_t* __restrict__ row_off32, RootRef rr,
+                                                        uint32_t R, uint32_t rpb,
                                                         const uint32_t* __restrict__ mem,
                                                         const uint32_t* __restrict__ lohi,
                                                         const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
@@ -467,8 +572,9 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[f2_region(g, b, nblk)]);
-    for (uint32_t r = r0 + threadIdx.x; r <= r1; r += blockDim.x) srow[r - r0] = uint32_t(roff[r]);
+    for (uint32_t r = r0 + threadIdx.x; r <= r1; r += blockDim.x) srow[r - r0] = kRoot ? row_off32[r] : uint32_t(roff[r]);
     if (threadIdx.x == 0) blk_keys = 0;
+    const Ent<W == 0 ? 1 : W, kRoot> en_{nullptr, mem, lohi, mask, rr};
     __syncthreads();
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     F2Ent* stage = stage_all + wave * 64;
@@ -483,9 +589,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
         nrb = srow[rr - r0];
         nrl = srow[rr - r0 + 1] - nrb;
         if (W == 1 && nrl <= 64 && lane < nrl) {
-            nme = mem[nrb + lane];
-            nlh = lohi[nrb + lane];
+            nme = en_.m(nrb + lane);
             nmk = mask[nrb + lane];
+            if constexpr (kRoot) nlh = uint32_t(__builtin_ctzll(nmk)) | ((63u - uint32_t(__builtin_clzll(nmk))) << 16);
+            else nlh = lohi[nrb + lane];
         }
     };
     fetch(r0 + wave);
@@ -498,13 +605,14 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
             // ---- lane-per-pair: segments of S lanes, lane s0 + j tests partner j
             // entries i are this rank's members only (sharded root: the other
             // ranks count the rest); every entry of the row is a partner j
-            const bool act = lane < rl && me - mlo < mhi - mlo;
+            // (an odd member id: an infrequent DB entry of the DB-direct root, neither i nor j)
+            const bool act = lane < rl && !(me & 1u) && me - mlo < mhi - mlo;
             const uint64_t actb = __ballot(act);
             const uint32_t nact = uint32_t(__popcll(actb));
             if (lane < rl) {
                 const uint32_t ri = me >> 1, g = group_of(ri, pm);
                 F2Ent en;
-                en.x = ri | ((lh & 0xFFFFu) << 16);
+                en.x = ((me & 1u) ? 0xFFFFu : ri) | ((lh & 0xFFFFu) << 16);
                 en.y = (act ? g : 0xFFFFu) | ((ri - g * per) * D << 16);
                 en.mask = mk;
                 stage[lane] = en;
@@ -516,9 +624,9 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
             const uint32_t j = lane & (S - 1), s0 = lane & ~(S - 1);
             const uint64_t segm = S == 64 ? ~0ull : (((1ull << S) - 1ull) << s0);
             const uint64_t seg_lt = lt & segm;
-            const bool vj = j < rl;
-            // this lane's partner j (fixed for the row)
-            const F2Ent ej = stage[vj ? j : 0];
+            // this lane's partner j (fixed for the row; not an infrequent DB entry)
+            const F2Ent ej = stage[j < rl ? j : 0];
+            const bool vj = j < rl && (ej.x & 0xFFFFu) != 0xFFFFu;
             const uint32_t hi_j = uint32_t(__shfl(int(lh), int(j), 64)) >> 16;
             const uint32_t rj = ej.x & 0xFFFFu;
             for (uint32_t i0 = 0; i0 < nact; i0 += k) {
@@ -546,10 +654,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
         } else {
             // ---- generic: entry i wave-uniform, partners in chunks of 64 lanes (any W, any length)
             for (uint32_t i = 0; i < rl; ++i) {
-                const uint32_t me = rfl(mem[rb + i]);
-                if (!(me - mlo < mhi - mlo)) continue;
+                const uint32_t me = rfl(kRoot ? en_.m(rb + i) : mem[rb + i]);
+                if ((me & 1u) || !(me - mlo < mhi - mlo)) continue;
                 const uint32_t ri = me >> 1, g = group_of(ri, pm);
-                const uint32_t li = rfl(lohi[rb + i]) & 0xFFFFu;
+                const uint32_t li = rfl(kRoot ? en_.lh(rb + i) : lohi[rb + i]) & 0xFFFFu;
                 const uint32_t kb = (ri - g * per) * D;
                 MaskV<W> mi;  // entry i's mask, wave-uniform (by address when W == 0)
                 if constexpr (W == 0) {
@@ -567,9 +675,12 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                     bool t_ok = false, e_ok = false;
                     uint32_t rq = 0;
                     if (v) {
-                        rq = mem[rb + q] >> 1;
-                        t_ok = (lohi[rb + q] >> 16) > li;
-                        if (q > i) e_ok = mi.and_any(mask + size_t(rb + q) * mask_words<W>(wd), wd);
+                        const uint32_t mq = kRoot ? en_.m(rb + q) : mem[rb + q];
+                        rq = mq >> 1;
+                        if (!(mq & 1u)) {
+                            t_ok = ((kRoot ? en_.lh(rb + q) : lohi[rb + q]) >> 16) > li;
+                            if (q > i) e_ok = mi.and_any(mask + size_t(rb + q) * mask_words<W>(wd), wd);
+                        }
                     }
                     const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
                     const uint32_t nt = uint32_t(__popcll(tb)), n = nt + uint32_t(__popcll(eb));
@@ -587,7 +698,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     }
     atomicAdd(&blk_keys, my_keys);
     __syncthreads();
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+    // the fills of the groups of the member range [mlo, mhi) only (a pass over other groups
+    // leaves theirs as an earlier pass wrote them)
+    const uint32_t glo = (mlo >> 1) / per, ghi = mhi == kNone ? G : min(G, ((mhi >> 1) + per - 1) / per);
+    for (uint32_t g = glo + threadIdx.x; g < ghi; g += blockDim.x)
         fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[f2_region(g, b, nblk)]);
     if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
@@ -878,24 +992,23 @@ struct EmitEnt {
     uint32_t k0, nk, cc, rb, re, lt;  // kids [k0, k0 + nk), child class, run [rb, re), lo | type << 16
 };
 
-__device__ __forceinline__ EmitEnt emit_ent(uint64_t e64, uint32_t E, const uint32_t* __restrict__ cid,
-                                            const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
-                                            const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
-                                            const uint32_t* __restrict__ kid_off,
+template <class EntT>
+__device__ __forceinline__ EmitEnt emit_ent(uint64_t e64, uint32_t E, const EntT& en, const DClass* __restrict__ cls,
+                                            const uint32_t* __restrict__ pos, const uint32_t* __restrict__ kid_off,
                                             const uint32_t* __restrict__ child_of) {
     EmitEnt t{0, 0, kNone, 0, 0, 0};
     if (e64 < E) {
         const uint32_t e = uint32_t(e64);
-        const DClass c = cls[cid[e]];
-        const uint32_t mi = mem[e];
-        t.cc = child_of[c.cbase + mi];
+        const DClass c = cls[en.c(e)];
+        const uint32_t mi = en.m(e);
+        t.cc = EntT::kRootEnt && (mi & 1u) ? kNone : child_of[c.cbase + mi];  // (infrequent DB entry: no class)
         if (t.cc != kNone) {
             t.k0 = kid_off[c.cbase + mi];
             t.nk = kid_off[c.cbase + mi + 1] - t.k0;
             const uint32_t p = pos[e];
             t.rb = e - (p >> 16);
             t.re = t.rb + (p & 0xFFFFu);
-            t.lt = (lohi[e] & 0xFFFFu) | ((mi & 1u) << 16);
+            t.lt = (en.lh(e) & 0xFFFFu) | ((mi & 1u) << 16);
         }
     }
     return t;
@@ -907,9 +1020,9 @@ __device__ __forceinline__ EmitEnt emit_ent(uint64_t e64, uint32_t E, const uint
 // partner f, kid slot, k) runs on EVERY lane each step (it may shuffle); k is
 // the rank of a non-empty join within the owner's child run.  Returns the
 // lane's own non-empty join count (its child run length).
-template <int W, class OnOk>
-__device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, const uint32_t* __restrict__ mem,
-                                               const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask,
+template <int W, class EntT, class OnOk>
+__device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, const EntT& en,
+                                               const uint64_t* __restrict__ mask,
                                                const uint32_t* __restrict__ kid_slot, uint32_t wd, OnOk&& on_ok) {
     const uint32_t lane = lane_id();
     const uint32_t incl = wave_incl_scan(t.nk), excl = incl - t.nk;
@@ -941,16 +1054,17 @@ __device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, co
             uint32_t lo = o_rb, hi = o_re;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (mem[mid] < target) lo = mid + 1; else hi = mid;
+                if (mem_less(en.m(mid), target)) lo = mid + 1; else hi = mid;
             }
             f = lo;
-            if (f < o_re && mem[f] == target) {
+            if (f < o_re && en.m(f) == target) {
+                const uint32_t f_lh = en.lh(f);
                 if (ct == kSeq) {
-                    ok = (lohi[f] >> 16) > (o_lt & 0xFFFFu);
+                    ok = (f_lh >> 16) > (o_lt & 0xFFFFu);
                 } else {
                     MaskV<W> mk;
-                    mk.load(mask + size_t(o_e) * mask_words<W>(wd), wd, lohi[o_e]);
-                    ok = mk.and_any(mask + size_t(f) * mask_words<W>(wd), wd, lohi[f]);
+                    mk.load(mask + size_t(o_e) * mask_words<W>(wd), wd, en.lh(o_e));
+                    ok = mk.and_any(mask + size_t(f) * mask_words<W>(wd), wd, f_lh);
                 }
             }
         }
@@ -972,6 +1086,10 @@ __device__ __forceinline__ void emit_write(const SlabPtrs& o, uint64_t cap, uint
                                            const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask,
                                            uint32_t wd) {
     if (d >= cap) return;  // a count mismatch: the host reports it, nothing lands past the slab
+    if (n > 0xFFFFu) {  // a child run longer than the 16-bit pos fields: the host raises FSM_ELIMIT
+        atomicOr(o.lim, 1u);
+        return;
+    }
     if constexpr (W == 0) {  // runtime width: word by word through HBM
         const uint64_t* src = mask + size_t(f) * wd;
         uint64_t* dst = o.mask + d * wd;
@@ -1006,7 +1124,7 @@ __device__ __forceinline__ void emit_write(const SlabPtrs& o, uint64_t cap, uint
     load_mask<W>(mask + size_t(f) * W, m);
     uint32_t lo2, hi2;
     if ((slot & 1u) == kSeq) {
-        hi2 = lohi[f] >> 16;
+        hi2 = mask_hi<W>(m);  // the partner's last eid (its lohi; the DB-direct root has none stored)
         mask_clear_upto<W>(m, o_lt & 0xFFFFu);
         lo2 = mask_lo<W>(m);
     } else {
@@ -1046,8 +1164,8 @@ constexpr int kEmitBlock = FSM_EMIT_BLOCK;  // threads of a k_emit1 block (one s
 constexpr int kEmitRounds = FSM_EMIT_ROUNDS;      // 64-entry rounds per wave per chunk
 constexpr uint32_t kEmitCap = FSM_EMIT_RECORDS;  // LDS join records per wave
 
-template <int W>
-__global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t* __restrict__ cid,
+template <int W, bool kRoot>
+__global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, RootRef rr, const uint32_t* __restrict__ cid,
                                                   const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
                                                   const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
                                                   const uint64_t* __restrict__ mask,
@@ -1066,6 +1184,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
     __shared__ unsigned long long b_base;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
+    const Ent<W == 0 ? 1 : W, kRoot> en{cid, mem, lohi, mask, rr};
     // segments: the whole batch [0, E), or (runs != nullptr) each listed run, one block per run
     const uint32_t nseg = runs ? *nruns : 1u;
     for (uint32_t sg = runs ? blockIdx.x : 0u; sg < nseg; sg += runs ? gridDim.x : nseg) {
@@ -1076,9 +1195,9 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
         uint32_t nrec = 0, wsum = 0;
         for (int r = 0; r < kEmitRounds; ++r) {
             const uint64_t w0 = c0 + uint64_t(r) * kEmitBlock + uint64_t(w) * 64;
-            const EmitEnt t = emit_ent(w0 + lane, Ez, cid, cls, mem, lohi, pos, kid_off, child_of);
+            const EmitEnt t = emit_ent(w0 + lane, Ez, en, cls, pos, kid_off, child_of);
             const uint32_t done = emit_pairs<W>(
-                t, w0, mem, lohi, mask, kid_slot, wd,
+                t, w0, en, mask, kid_slot, wd,
                 [&](bool ok, uint32_t ow, uint64_t, uint32_t, uint32_t q, uint32_t f, uint32_t, uint32_t k) {
                     const uint64_t b = __ballot(ok);
                     if (ok) {
@@ -1120,12 +1239,12 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, const uint32_t
         } else {
             for (int r = 0; r < kEmitRounds; ++r) {
                 const uint64_t w0 = c0 + uint64_t(r) * kEmitBlock + uint64_t(w) * 64;
-                EmitEnt t = emit_ent(w0 + lane, Ez, cid, cls, mem, lohi, pos, kid_off, child_of);
+                EmitEnt t = emit_ent(w0 + lane, Ez, en, cls, pos, kid_off, child_of);
                 const uint32_t el = uint32_t(r) * 64u + lane;
                 const uint64_t base = wb + i_off[w][el];
                 const uint32_t n_run = i_n[w][el];
                 if (n_run == 0) t.nk = 0;
-                emit_pairs<W>(t, w0, mem, lohi, mask, kid_slot, wd,
+                emit_pairs<W>(t, w0, en, mask, kid_slot, wd,
                               [&](bool ok, uint32_t ow, uint64_t o_e, uint32_t o_lt, uint32_t q, uint32_t f,
                                   uint32_t slot, uint32_t k) {
                                   const uint32_t o_n = uint32_t(__shfl(int(n_run), int(ow), 64));
@@ -1168,8 +1287,8 @@ constexpr uint32_t kE2Range = FSM_E2_RANGE;     // entries per wave range (runs 
 constexpr uint32_t kE2Own = kE2Range + 64;      // owner slots per wave (a run may end 63 past the range)
 constexpr uint32_t kE2Cap = FSM_E2_CAP;         // LDS join records per wave
 
-template <int W>
-__global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* __restrict__ cid,
+template <int W, bool kRoot>
+__global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, const uint32_t* __restrict__ cid,
                                                     const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
                                                     const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
                                                     const uint64_t* __restrict__ mask,
@@ -1187,6 +1306,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt();
     constexpr uint32_t kChunkE = kE2Waves * kE2Range;
+    const Ent<W, kRoot> en{cid, mem, lohi, mask, rr};
     for (uint32_t c0 = blockIdx.x * kChunkE; c0 < E; c0 += gridDim.x * kChunkE) {
         const uint32_t wa = c0 + w * kE2Range, wz = min(E, wa + kE2Range);
         // the first run start in [wa, wz) (runs ending there started in an earlier range)
@@ -1228,11 +1348,16 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
                 uint32_t mi = 0, lh = 0, cc = kNone, k0 = 0, nk = 0, lt2 = 0;
                 uint64_t mk = 0;
                 if (in) {
-                    mi = mem[e];
-                    lh = lohi[e];
-                    if constexpr (W == 1) mk = mask[e];
-                    const DClass c = cls[cid[e]];
-                    cc = child_of[c.cbase + mi];
+                    mi = en.m(e);
+                    if constexpr (W == 1) {
+                        mk = mask[e];
+                        if constexpr (kRoot) lh = uint32_t(__builtin_ctzll(mk)) | ((63u - uint32_t(__builtin_clzll(mk))) << 16);
+                        else lh = lohi[e];
+                    } else {
+                        lh = en.lh(e);
+                    }
+                    const DClass c = cls[en.c(e)];
+                    cc = kRoot && (mi & 1u) ? kNone : child_of[c.cbase + mi];  // (infrequent DB entry: no class)
                     if (cc != kNone) {
                         k0 = kid_off[c.cbase + mi];
                         nk = kid_off[c.cbase + mi + 1] - k0;
@@ -1271,7 +1396,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, const uint32_t* 
                     for (uint32_t stp = 32; stp > 0; stp >>= 1) {
                         const uint32_t cand = f + stp;
                         const uint32_t v = uint32_t(__shfl(int(mi), int(min(cand, 64u) - 1u), 64));
-                        if (cand <= o_re && v < target) f = cand;
+                        if (cand <= o_re && mem_less(v, target)) f = cand;
                     }
                     const uint32_t fl = min(f, 63u);
                     const uint32_t f_mi = uint32_t(__shfl(int(mi), int(fl), 64));
@@ -1526,7 +1651,7 @@ struct Slab {
     }
     SlabPtrs ptrs() const {
         return SlabPtrs{cid.as<uint32_t>(), mem.as<uint32_t>(), lohi.as<uint32_t>(), pos.as<uint32_t>(),
-                        mask.as<uint64_t>()};
+                        mask.as<uint64_t>(), nullptr};
     }
 };
 
@@ -1674,6 +1799,18 @@ struct Batch {
     bool f2_planned = false;
     DevBuf f2_base;
     uint64_t f2_nslots = 0;
+    // DB-direct root (no root slab): its kernels read the DB rows through rk2 (dense item ->
+    // member id, odd for an infrequent item)
+    bool db_direct = false;
+    DevBuf rk2;
+    // sharded root with work stealing: children [0, nshared_children) are the
+    // heavy classes every rank mines; the rest, largest first, are claimed in ranges from the
+    // shared counter claim_key (-1: no claims; groups fixed)
+    int64_t claim_key = -1;
+    size_t nshared_children = 0;
+    bool claims_done = false;
+    int claims_made = 0;
+    std::vector<uint64_t> claim_pre;  // prefix volumes of the claimable children
 
     // back to an empty batch: device buffers released, host vectors cleared with their
     // capacity kept (the DFS reuses popped batches: no fresh pages per batch)
@@ -1699,6 +1836,13 @@ struct Batch {
         f2_planned = false;
         f2_base.release();
         f2_nslots = 0;
+        db_direct = false;
+        rk2.release();
+        claim_key = -1;
+        nshared_children = 0;
+        claims_done = false;
+        claims_made = 0;
+        claim_pre.clear();
     }
 };
 
@@ -1754,6 +1898,8 @@ struct Miner {
     bool pend_check = false;
 
     uint64_t entry_bytes() const { return 16ull + 8ull * uint64_t(W); }  // cid, mem, lohi, pos, mask
+    // one (sid u32, eid mask) id-list entry, 4 + 8 ceil(E/64) bytes (12 B at W = 1)
+    uint64_t survey_entry_bytes() const { return 4ull + 8ull * uint64_t(W); }
 
     // large per-batch tables: copied into a pinned staging slot (over the host pool
     // when large) and DMA'd asynchronously (pageable copies run at a fraction of that)
@@ -1931,7 +2077,7 @@ struct Miner {
         FSM_W_DISPATCH(W, FSM_CK)
 #undef FSM_CK
         FSM_LAUNCHED("k_cnt_keys", s);
-        clk->end(tk, int64_t(b.E * entry_bytes() + nd * 12));
+        clk->end(tk, int64_t(b.E * entry_bytes() + nd * 12), int64_t(b.E * survey_entry_bytes()));
         cnt.alloc(std::max<uint64_t>(G64 << kGroupShift, 1) * 4);
         // few groups: several blocks per group (each over a range of the regions) keep the CUs busy
         const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>({64u, 512u / G, nblk}));
@@ -1960,7 +2106,7 @@ struct Miner {
     void dump(Batch& b) {
         static const bool on = [] { const char* v = std::getenv("FSM_DEBUG_DUMP"); return v && v[0] == '1'; }();
         const uint64_t n = b.E;
-        if (!on || n > 4096) return;
+        if (!on || n > 4096 || b.db_direct) return;
         std::vector<uint32_t> cid(n), mem(n), lohi(n), pos(n);
         std::vector<uint64_t> mk(n * uint64_t(W));
         FSM_HIP(hipMemcpyAsync(cid.data(), b.slab.cid.p, n * 4, hipMemcpyDeviceToHost, s));
@@ -2039,6 +2185,11 @@ struct Miner {
         const char* v = std::getenv("FSM_COUNT_CHUNK");
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kChunk;
     }
+    // passes of the root F2 over ranges of rank groups (FSM_F2_PASSES overrides, for tuning)
+    static uint32_t f2_passes() {
+        const char* v = std::getenv("FSM_F2_PASSES");
+        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 64)) : 1u;
+    }
     // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
     static uint32_t f2_blocks() {
         const char* v = std::getenv("FSM_F2_BLOCKS");
@@ -2081,7 +2232,7 @@ struct Miner {
 
     bool root_f2(Batch& b, std::vector<FreqRec>& recs) {
         const ClassMeta& m = b.cls[0];
-        if (b.root_rows.p == nullptr) return false;
+        if (b.root_rows.p == nullptr && !b.db_direct) return false;
         const F2Geo geo = f2_geometry(b, m.D, m.cap, b.R);
         if (!geo.ok) return false;
         const uint32_t D = geo.D, F = geo.F, per = geo.per, G = geo.G, pm = geo.pm, mlo = geo.mlo, mhi = geo.mhi;
@@ -2093,41 +2244,71 @@ struct Miner {
         if (!b.f2_planned) return false;  // the plan is made while the root rows are written
         DevBuf base = std::move(b.f2_base), fill(nd * 4);
         const uint64_t nslots = b.f2_nslots;
-        size_t tk = 0;
+
         if (nslots >= (uint64_t(1) << 32) - 4096) return false;  // region cursors are u32
         // the one enumeration (keys padded: k_f2_count reads whole 16-byte words past a region's end)
         DevBuf keys((nslots + 1024) * 2), nk(8);
         FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
-        tk = clk->begin("k_f2_keys");
         const size_t kshm = size_t(kF2Waves) * 64 * (sizeof(F2Ent) + 4) + (size_t(kF2MaxRows) + 1) * 4 + size_t(G) * 4;
-#define FSM_F2K(WW)                                                                                                   \
-    hipLaunchKernelGGL(k_f2_keys<WW>, dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(), R, rpb,      \
-                       sp.mem, sp.lohi, sp.mask, D, per, pm, G, nblk, mlo, mhi, base.as<uint64_t>(),                   \
-                       fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>(), uint32_t(W))
-        FSM_W_DISPATCH(W, FSM_F2K)
-#undef FSM_F2K
-        FSM_LAUNCHED("k_f2_keys", s);
-        // reads the slab (mem, lohi, mask) and the region bases, writes the fills;
-        // + 2 B per key actually written, added once the count is back
-        clk->end(tk, E0 * int64_t(8 + 8 * W) + int64_t(nd) * 12);
-        const size_t tk_keys = tk;
         // count + frequent pairs of this rank's slice
         const uint32_t g0 = rlo / per, g1 = rhi == 0 ? 0u : (rhi - 1) / per + 1;
         uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * D, uint64_t(1) << 20));
         DevBuf d_nrec(4);
         DevBuf d_recs;
         unsigned long long nkeys = 0;
-        size_t tk_cnt = 0;
+        size_t tk_cnt = 0, tk_keys = 0;
+        // passes over ranges of whole rank groups: each pass enumerates only the entries of its
+        // groups, so the keys it writes (and k_f2_count reads right after) stay on-die
+        const uint32_t npass = std::max<uint32_t>(1, std::min<uint32_t>(f2_passes(), g1 > g0 ? g1 - g0 : 1));
         for (int attempt = 0;; ++attempt) {
             d_recs.alloc(std::max<uint32_t>(cap_recs, 1) * sizeof(FreqRec));
             FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
-            tk_cnt = clk->begin("k_f2_count");
-            if (g1 > g0)
-                hipLaunchKernelGGL(k_f2_count<false>, dim3(g1 - g0), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
-                                   fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), D, per, g0, rlo, rhi, minsup,
-                                   d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u);
-            FSM_LAUNCHED("k_f2_count", s);
-            clk->end(tk_cnt, int64_t(g1 - g0) * nblk * 12);
+            if (attempt == 0) FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
+            for (uint32_t ps = 0; ps < npass; ++ps) {
+                const uint32_t pg0 = g0 + uint32_t(uint64_t(g1 - g0) * ps / npass);
+                const uint32_t pg1 = g0 + uint32_t(uint64_t(g1 - g0) * (ps + 1) / npass);
+                const uint32_t prlo = std::max(rlo, pg0 * per), prhi = std::min(rhi, pg1 * per);
+                if (attempt == 0) {  // a retry (record overflow) counts from the keys already written
+                    const uint32_t pmlo = npass == 1 ? mlo : 2 * prlo, pmhi = npass == 1 ? mhi : 2 * prhi;
+                    tk_keys = clk->begin("k_f2_keys");
+#define FSM_F2K(WW)                                                                                                   \
+    hipLaunchKernelGGL((k_f2_keys<WW, false>), dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(),      \
+                       (const uint32_t*)nullptr, RootRef{nullptr, nullptr}, R, rpb, sp.mem, sp.lohi, sp.mask, D, per,  \
+                       pm, G, nblk, pmlo, pmhi, base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(),        \
+                       nk.as<unsigned long long>(), uint32_t(W))
+#define FSM_F2KD(WW)                                                                                                  \
+    hipLaunchKernelGGL((k_f2_keys<WW, true>), dim3(nblk), dim3(kF2Threads), kshm, s, (const uint64_t*)nullptr,         \
+                       db->row_off.as<uint32_t>(), RootRef{db->item.as<uint32_t>(), b.rk2.as<uint32_t>()}, R, rpb,     \
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr, db->mask.as<uint64_t>(), D, per, pm, G,     \
+                       nblk, pmlo, pmhi, base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(),               \
+                       nk.as<unsigned long long>(), uint32_t(WW))
+                    if (b.db_direct) {
+                        switch (W) {
+                            case 1: FSM_F2KD(1); break;
+                            case 2: FSM_F2KD(2); break;
+                            case 4: FSM_F2KD(4); break;
+                            default: FSM_F2KD(8); break;
+                        }
+                    } else {
+                        FSM_W_DISPATCH(W, FSM_F2K)
+                    }
+#undef FSM_F2K
+#undef FSM_F2KD
+                    FSM_LAUNCHED("k_f2_keys", s);
+                    // reads the slab (mem, lohi, mask) and the region bases, writes the fills;
+                    // + 2 B per key actually written, added once the count is back
+                    // DB-direct: the DB rows (item + mask per entry) instead of the slab's (mem, lohi, mask)
+                    const int64_t rowb = b.db_direct ? db->E * int64_t(4 + 8 * W) : E0 * int64_t(8 + 8 * W);
+                    clk->end(tk_keys, rowb + int64_t(nd) * 12, ps == 0 ? E0 * 8 : 0);
+                }
+                tk_cnt = clk->begin("k_f2_count");
+                if (pg1 > pg0)
+                    hipLaunchKernelGGL(k_f2_count<false>, dim3(pg1 - pg0), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
+                                       fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), D, per, pg0, prlo, prhi, minsup,
+                                       d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u);
+                FSM_LAUNCHED("k_f2_count", s);
+                clk->end(tk_cnt, int64_t(pg1 - pg0) * nblk * 12);
+            }
             uint32_t nrec = 0;
             FSM_HIP(hipMemcpyAsync(&nrec, d_nrec.p, 4, hipMemcpyDeviceToHost, s));
             FSM_HIP(hipMemcpyAsync(&nkeys, nk.p, 8, hipMemcpyDeviceToHost, s));
@@ -2222,7 +2403,6 @@ struct Miner {
                 const int32_t parent = b.node_of[pm.no_off + pr.mi];
                 const uint32_t pls = nodes[size_t(parent)].len_sets;
                 if ((pls >> 16) >= 0xFFFFu) bad[size_t(t)] |= 1;
-                if (q1 - q0 > 0xFFFFu) bad[size_t(t)] |= 2;
                 ChildInfo ch;
                 ch.pcls = pr.cls;
                 ch.pmi = pr.mi;
@@ -2251,7 +2431,6 @@ struct Miner {
         lap(4, tl);
         for (int64_t t = 0; t < nthr; ++t) {
             if (bad[size_t(t)] & 1) throw Error(FSM_ELIMIT, "SPADE: a pattern exceeds 65534 items");
-            if (bad[size_t(t)] & 2) throw Error(FSM_ELIMIT, "SPADE: a prefix class has more than 65535 frequent children");
             ctx->stats.bytes_join_equiv += jb[size_t(t)];
         }
     }
@@ -2340,6 +2519,8 @@ struct Miner {
         auto compute = [&] {
         // the root: pairs counted per rank group, only the frequent ones leave the device
         const bool root_done = b.E && b.root && !root_atomic() && root_f2(b, recs);
+        if (b.db_direct && b.E && !root_done)
+            throw Error(FSM_EDEVICE, "SPADE internal error: the DB-direct root F2 did not apply");
         if (b.E) st.count_launches += 1;
         const bool keyed_done = !root_done && keyed_layout && keyed_count(b, cnt);
         if (!root_done && !keyed_done) {
@@ -2374,7 +2555,7 @@ struct Miner {
                 }
 #undef FSM_COUNT
                 FSM_LAUNCHED("k_count", s);
-                clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4));
+                clk->end(tk, int64_t(b.E * entry_bytes() + b.n_cnt * 4), int64_t(b.E * survey_entry_bytes()));
             }
             DevBuf d_rows;
             upload_staged(1, d_rows, rows.data() + rlo, size_t(nrows) * sizeof(DRow));
@@ -2452,9 +2633,8 @@ struct Miner {
             order_recs(recs, rhi);
         }
         };
-        if (shard) {  // a failure here or in run_root reaches every rank before the gather below
+        if (shard) {  // a failure here or in run_root reaches every rank in the gather below
             run_or_defer(compute);
-            agree();
         } else {
             compute();
         }
@@ -2463,10 +2643,19 @@ struct Miner {
         cnt.release();
         hp[7] += now_ms() - tc1;  // device count + extraction + ordering (incl. waits)
         if (shard) {  // every rank gets every frequent pair, in row order (slices ascend with the rank)
+            if (agr.code) nfreq = 0;
             std::vector<uint8_t> mine(nfreq * sizeof(FreqRec));
             if (nfreq) std::memcpy(mine.data(), R, mine.size());
             std::vector<size_t> sizes;
-            const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s);
+            // the claim counter of this mine's first-level classes is reset before this gather
+            // (the collective every rank passes before its first claim); the same all-reduce
+            // carries the failure agreement and, at the first sharded mine, whether every rank
+            // has the shared counters
+            b.claim_key = comm->next_key();
+            comm->reset_counter(b.claim_key);
+            uint32_t ex = comm->has_fetch_add() && claims_env() ? 1u : 0u;
+            const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s, &agr, &ex, 1);
+            if (comm->claim_mode < 0) comm->claim_mode = ex == uint32_t(comm->nranks()) ? 1 : 0;
             nfreq = all.size() / sizeof(FreqRec);
             recs.resize(nfreq);
             if (nfreq) std::memcpy(recs.data(), all.data(), all.size());
@@ -2569,8 +2758,6 @@ struct Miner {
                 last_type = fr.slot & 1u;
             }
             const size_t nch = q2 - q;
-            if (nch > 0xFFFFu)
-                throw Error(FSM_ELIMIT, "SPADE: a prefix class has more than 65535 frequent children");
             if (!(nch == 1 && last_type == kItm)) b.children.push_back(std::move(ch));
             q = q2;
         }
@@ -2594,21 +2781,38 @@ struct Miner {
                     idx.push_back(k);
                 }
             }
-            std::vector<int32_t> owner(vol.size());
-            shard_plan(vol.data(), int64_t(vol.size()), comm->nranks(), owner.data());
-            std::vector<uint8_t> keep(nc, 0);
-            for (size_t q = 0; q < idx.size(); ++q) keep[idx[q]] = owner[q] == comm->rank();
-            RawVec<ChildInfo> kept;
             size_t nheavy = 0;
             for (size_t k = 0; k < nc; ++k) {
                 b.children[k].split = heavy[k] != 0;
                 nheavy += heavy[k];
-                if (heavy[k] || keep[k]) kept.push_back(std::move(b.children[k]));
             }
-            b.children = std::move(kept);
+            if (comm->claim_mode == 1) {
+                // work stealing: heavy classes first (every rank), then the rest largest first;
+                // the groups after the shared ones are claimed from the shared counter
+                std::vector<size_t> ord(idx);
+                std::stable_sort(ord.begin(), ord.end(),
+                                 [&](size_t x, size_t y) { return b.children[x].cap > b.children[y].cap; });
+                RawVec<ChildInfo> all;
+                for (size_t k = 0; k < nc; ++k)
+                    if (heavy[k]) all.push_back(std::move(b.children[k]));
+                const size_t h = all.size();
+                for (size_t k : ord) all.push_back(std::move(b.children[k]));
+                b.children = std::move(all);
+                b.nshared_children = h;
+            } else {
+                std::vector<int32_t> owner(vol.size());
+                shard_plan(vol.data(), int64_t(vol.size()), comm->nranks(), owner.data());
+                std::vector<uint8_t> keep(nc, 0);
+                for (size_t q = 0; q < idx.size(); ++q) keep[idx[q]] = owner[q] == comm->rank();
+                RawVec<ChildInfo> kept;
+                for (size_t k = 0; k < nc; ++k)
+                    if (heavy[k] || keep[k]) kept.push_back(std::move(b.children[k]));
+                b.children = std::move(kept);
+                b.claim_key = -1;
+            }
             if (ctx->opts.verbose)
-                std::fprintf(stderr, "[fsm] rank %d: %zu first-level classes, %zu kept, %zu heavy (split)\n",
-                             comm->rank(), nc, b.children.size(), nheavy);
+                std::fprintf(stderr, "[fsm] rank %d: %zu first-level classes, %zu %s, %zu heavy (split)\n",
+                             comm->rank(), nc, b.children.size(), comm->claim_mode == 1 ? "claimable" : "kept", nheavy);
         } else if (comm) {
             // sub-classes of a split class: LPT over that class's sub-classes alone
             // (the same on every rank whatever the batching), this rank keeps its share
@@ -2634,6 +2838,17 @@ struct Miner {
         }
         hp[2] += now_ms() - th;
         th = now_ms();
+        if (b.claim_key >= 0) {
+            // work stealing: the shared (heavy) groups now, the claimed ones as they come
+            b.groups.clear();
+            b.next_group = 0;
+            append_groups(b, 0, b.nshared_children);
+            const size_t h = b.nshared_children, n = b.children.size() - h;
+            b.claim_pre.assign(n + 1, 0);
+            for (size_t k = 0; k < n; ++k) b.claim_pre[k + 1] = b.claim_pre[k] + b.children[h + k].cap;
+            hp[3] += now_ms() - th;
+            return;
+        }
         // groups of children that fit the frontier budget
         b.groups.clear();
         b.next_group = 0;
@@ -2684,6 +2899,70 @@ struct Miner {
                          b.children.size(), b.groups.size());
     }
 
+    // groups of children [a, z) that fit the frontier budget, appended to b.groups
+    void append_groups(Batch& b, size_t a, size_t z) {
+        const uint64_t max_ent = uint64_t(1) << 31;
+        size_t gs = a;
+        uint64_t acc = 0, acc_ent = 0;
+        for (size_t k = a; k < z; ++k) {
+            const ChildInfo& c = b.children[k];
+            const uint64_t need = c.cap * entry_bytes() + uint64_t(c.D) * c.D * 4;
+            if (k > gs && (acc + need > budget || acc_ent + c.cap > max_ent)) {
+                b.groups.push_back({gs, k});
+                gs = k;
+                acc = acc_ent = 0;
+            }
+            acc += need;
+            acc_ent += c.cap;
+        }
+        if (gs < z) b.groups.push_back({gs, z});
+    }
+    // FSM_SPADE_CLAIMS=0: the sharded lattice splits the first-level classes by the static
+    // plan even when the shared counters exist (tests, A/B)
+    static bool claims_env() {
+        const char* v = std::getenv("FSM_SPADE_CLAIMS");
+        return !(v && v[0] == '0');
+    }
+    // a rank's first claim takes this fraction of its fair share of the claimable volume
+    // (FSM_CLAIM_FIRST); later claims half of the remaining volume's fair share, at least
+    // 1/8 of the fair share (guided self-scheduling: few claims, each an emit pass over the DB)
+    static double claim_first() {
+        const char* v = std::getenv("FSM_CLAIM_FIRST");
+        return v ? std::clamp(std::atof(v), 0.01, 1.0) : 0.7;
+    }
+    // Claim the next range of first-level classes from the shared counter and append its
+    // groups; false when every class is claimed.  Two atomics: a read of the counter to
+    // size the claim by the remaining volume, then the add that takes it.
+    bool claim_more(Batch& b) {
+        if (b.claim_key < 0 || b.claims_done) return false;
+        const size_t h = b.nshared_children, n = b.children.size() - h;
+        const int64_t pos0 = comm->fetch_add(b.claim_key, 0);
+        if (pos0 < 0) throw Error(FSM_ECOMM, "SPADE: work-stealing counter failed");
+        if (uint64_t(pos0) >= n) {
+            b.claims_done = true;
+            return false;
+        }
+        const uint64_t N = uint64_t(comm->nranks()), tot = b.claim_pre[n], rem = tot - b.claim_pre[size_t(pos0)];
+        uint64_t target = b.claims_made == 0 ? uint64_t(claim_first() * double(tot) / double(N))
+                                              : std::max(rem / (2 * N), tot / (8 * N));
+        target = std::max<uint64_t>(target, 1);
+        // the fewest classes from pos0 whose volume reaches the target
+        const uint64_t want = b.claim_pre[size_t(pos0)] + target;
+        size_t m = size_t(std::lower_bound(b.claim_pre.begin() + pos0 + 1, b.claim_pre.end(), want) -
+                          b.claim_pre.begin()) - size_t(pos0);
+        m = std::clamp<size_t>(m, 1, n - size_t(pos0));
+        const int64_t old = comm->fetch_add(b.claim_key, int64_t(m));
+        if (old < 0) throw Error(FSM_ECOMM, "SPADE: work-stealing counter failed");
+        if (uint64_t(old) >= n) {
+            b.claims_done = true;
+            return false;
+        }
+        append_groups(b, h + size_t(old), h + std::min<size_t>(size_t(old) + m, n));
+        ++b.claims_made;
+        ctx->stats.rank_claims += 1;
+        return true;
+    }
+
     // emit child rows of group g of batch b into a new batch (k_emit1: one
     // pass, LDS join records, slab cursor)
     void emit(Batch& b, size_t g, Batch& nb) {
@@ -2696,6 +2975,8 @@ struct Miner {
         RawVec<uint32_t>& child_of = child_of_s;
         if (!dev_child_of) child_of.assign(b.cbase_total, kNone);
         uint64_t total = 0;
+        if (b.root)  // the root entries this rank joins as the owner: its first-level classes' prefix supports
+            for (size_t k = ga; k < gb; ++k) ctx->stats.rank_root_owned += int64_t(b.children[k].psup);
         // the only group: the children and their member tables move over whole (swapped:
         // the parent, released after this emit and recycled, keeps nb's old capacity)
         const bool whole = ga == 0 && gb == b.children.size() && b.groups.size() == 1;
@@ -2767,53 +3048,86 @@ struct Miner {
         }
         ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
         if (b.E) {
-            const SlabPtrs sp = b.slab.ptrs();
-            const SlabPtrs op = nb.slab.ptrs();
-            DevBuf cursor(16);  // u64 slab cursor | u32 long-run count (k_emit2)
-            FSM_HIP(hipMemsetAsync(cursor.p, 0, 8, s));
+            // the DB-direct root is read from the DB rows themselves (pos: the DB's row
+            // positions, members through rk2, lohi from the masks)
+            const bool rootdb = b.db_direct;
+            const uint64_t Eg = rootdb ? uint64_t(db->E) : b.E;  // entries the kernels walk
+            SlabPtrs sp = b.slab.ptrs();
+            RootRef rr{nullptr, nullptr};
+            if (rootdb) {
+                sp = SlabPtrs{nullptr, nullptr, nullptr, db->pos.as<uint32_t>(), db->mask.as<uint64_t>(), nullptr};
+                rr = RootRef{db->item.as<uint32_t>(), b.rk2.as<uint32_t>()};
+            }
+            SlabPtrs op = nb.slab.ptrs();
+            DevBuf cursor(16);  // u64 slab cursor | u32 long-run count (k_emit2) | u32 run-length flag
+            op.lim = reinterpret_cast<uint32_t*>(cursor.as<char>() + 12);
+            FSM_HIP(hipMemsetAsync(cursor.p, 0, 16, s));
             const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
-            const unsigned grid = unsigned(std::min<uint64_t>((b.E + chunk - 1) / chunk, emit_grid_cap()));
+            const unsigned grid = unsigned(std::min<uint64_t>((Eg + chunk - 1) / chunk, emit_grid_cap()));
             const size_t tk = clk->begin("k_emit");
             if ((W == 1 || W == 2 || W == 4 || W == 8) && emit_window()) {
                 // windows of whole runs in registers; the runs of more than 64 entries go to
                 // k_emit1's run list (device-side count: no host round trip)
                 const uint64_t ce = uint64_t(kE2Waves) * kE2Range;
-                const unsigned g2 = unsigned(std::min<uint64_t>((b.E + ce - 1) / ce, emit_grid_cap()));
-                d_long.alloc(std::max<uint64_t>(b.E / 65 + 1, 1) * 4);
+                const unsigned g2 = unsigned(std::min<uint64_t>((Eg + ce - 1) / ce, emit_grid_cap()));
+                d_long.alloc(std::max<uint64_t>(Eg / 65 + 1, 1) * 4);
                 FSM_HIP(hipMemsetAsync(cursor.as<char>() + 8, 0, 4, s));
-#define FSM_EMIT2(WW)                                                                                       \
-    hipLaunchKernelGGL(k_emit2<WW>, dim3(g2), dim3(kE2Block), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),  \
-                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,                         \
+#define FSM_EMIT2(WW, RT)                                                                                       \
+    hipLaunchKernelGGL((k_emit2<WW, RT>), dim3(g2), dim3(kE2Block), 0, s, uint32_t(Eg), rr, sp.cid,                  \
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
                        d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap, emit2_cap(),   \
                        d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor.as<char>() + 8));               \
     FSM_LAUNCHED("k_emit2", s);                                                                                    \
-    hipLaunchKernelGGL(k_emit1<WW>, dim3(256), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid,                     \
+    hipLaunchKernelGGL((k_emit1<WW, RT>), dim3(256), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,              \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
                        d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap, emit_cap(),    \
                        uint32_t(WW), d_long.as<uint32_t>(), reinterpret_cast<const uint32_t*>(cursor.as<char>() + 8)); \
     FSM_LAUNCHED("k_emit1", s);
-                switch (W) {
-                    case 1: FSM_EMIT2(1) break;
-                    case 2: FSM_EMIT2(2) break;
-                    case 4: FSM_EMIT2(4) break;
-                    default: FSM_EMIT2(8) break;
+                switch (W * 2 + (rootdb ? 1 : 0)) {
+                    case 2: FSM_EMIT2(1, false) break;
+                    case 3: FSM_EMIT2(1, true) break;
+                    case 4: FSM_EMIT2(2, false) break;
+                    case 5: FSM_EMIT2(2, true) break;
+                    case 8: FSM_EMIT2(4, false) break;
+                    case 9: FSM_EMIT2(4, true) break;
+                    case 16: FSM_EMIT2(8, false) break;
+                    default: FSM_EMIT2(8, true) break;
                 }
 #undef FSM_EMIT2
             } else {
 #define FSM_EMIT1(WW)                                                                                               \
-    hipLaunchKernelGGL(k_emit1<WW>, dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(),     \
-                       sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                                         \
+    hipLaunchKernelGGL((k_emit1<WW, false>), dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,                \
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                   \
                        b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
                        nb.slab.cap, emit_cap(), uint32_t(W), (const uint32_t*)nullptr, (const uint32_t*)nullptr)
-                FSM_W_DISPATCH(W, FSM_EMIT1)
+#define FSM_EMIT1R(WW)                                                                                              \
+    hipLaunchKernelGGL((k_emit1<WW, true>), dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,                 \
+                       b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                   \
+                       b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
+                       nb.slab.cap, emit_cap(), uint32_t(W), (const uint32_t*)nullptr, (const uint32_t*)nullptr)
+                if (rootdb) {
+                    switch (W) {
+                        case 1: FSM_EMIT1R(1); break;
+                        case 2: FSM_EMIT1R(2); break;
+                        case 4: FSM_EMIT1R(4); break;
+                        default: FSM_EMIT1R(8); break;
+                    }
+                } else {
+                    FSM_W_DISPATCH(W, FSM_EMIT1)
+                }
 #undef FSM_EMIT1
+#undef FSM_EMIT1R
                 FSM_LAUNCHED("k_emit", s);
             }
-            // reads every parent entry once, writes every child entry once
-            clk->end(tk, int64_t(b.E * entry_bytes() + total * entry_bytes()));
+            // reads every parent entry once (DB-direct root: the DB entry's item, pos and mask),
+            // writes every child entry once
+            const uint64_t rd = rootdb ? Eg * (8 + 8 * uint64_t(W)) : b.E * entry_bytes();
+            clk->end(tk, int64_t(rd + total * entry_bytes()), int64_t((b.E + total) * survey_entry_bytes()));
             FSM_HIP(hipMemcpyAsync(&pend[0], cursor.p, 8, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&pend[7], cursor.as<char>() + 12, 4, hipMemcpyDeviceToHost, s));
         } else {
             pend[0] = 0;
+            pend[7] = 0;
         }
         // no sync: the host prepares the next count while the emit runs; the runs must add
         // up exactly to the capacities (sum of child supports), checked at the next sync
@@ -2825,9 +3139,117 @@ struct Miner {
         if (!pend_check) return;
         pend_check = false;
         const uint64_t written = pend[0];
+        if (pend[7] & 0xFFFFFFFFu)
+            throw Error(FSM_ELIMIT, "SPADE: a class holds more than 65535 entries of one sequence");
         if (written != pend_total)
             throw Error(FSM_EDEVICE, "SPADE emit: wrote " + std::to_string(written) + " child entries, expected " +
                                          std::to_string(pend_total));
+    }
+
+    // FSM_ROOT_DB=0 keeps the root slab (k_root_count + k_root_write) for every mine (tests, A/B)
+    static bool root_db_env() {
+        const char* v = std::getenv("FSM_ROOT_DB");
+        return !(v && v[0] == '0');
+    }
+    // the DB's row positions for the DB-direct root (once per DB); false = a row is too long
+    bool ensure_db_pos() {
+        if (db->pos_state == 0) {
+            const uint32_t R = uint32_t(db->R);
+            db->pos.alloc(std::max<int64_t>(db->E, 1) * 4);
+            DevBuf flag(4);
+            FSM_HIP(hipMemsetAsync(flag.p, 0, 4, s));
+            if (R)
+                hipLaunchKernelGGL(k_db_pos, dim3(unsigned((uint64_t(R) * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                                   db->row_off.as<uint32_t>(), R, db->pos.as<uint32_t>(), flag.as<uint32_t>());
+            FSM_LAUNCHED("k_db_pos", s);
+            pend[6] = 0;
+            FSM_HIP(hipMemcpyAsync(&pend[6], flag.p, 4, hipMemcpyDeviceToHost, s));
+            sync();
+            db->pos_state = (pend[6] & 0xFFFFFFFFu) ? -1 : 1;
+            if (db->pos_state < 0) db->pos.release();
+        }
+        return db->pos_state > 0;
+    }
+
+    // The DB-direct root: no root slab.  The F2 plan (key capacities per rank group and row
+    // block, and the root entry count) is made from the DB rows; the F2 keys and the root
+    // emit read the same rows.  Returns false (nothing launched that matters) when the
+    // geometry does not apply: the caller then builds the root slab.
+    bool run_root_db(Batch& root, const std::vector<uint32_t>& freq_items, const std::vector<uint32_t>& f1,
+                     const std::vector<uint32_t>& rank) {
+        if (!(W == 1 || W == 2 || W == 4 || W == 8) || !root_db_env() || root_atomic() || db->R == 0) return false;
+        const uint32_t F = uint32_t(freq_items.size());
+        root.root = true;
+        const F2Geo geo = f2_geometry(root, 2 * F, uint64_t(db->E), uint64_t(db->R));
+        if (!geo.ok || !ensure_db_pos()) {
+            root.root = false;
+            return false;
+        }
+        // rk2: 2 rank for a frequent item; 2 (frequent items below it) - 1 for an infrequent one
+        std::vector<uint32_t> rk2(size_t(db->U));
+        uint32_t below = 0;
+        for (size_t u = 0; u < rk2.size(); ++u) {
+            if (rank[u] != kNone) {
+                rk2[u] = 2 * rank[u];
+                ++below;
+            } else {
+                rk2[u] = 2 * below - 1u;  // wraps to 0xFFFFFFFF below the first frequent item
+            }
+        }
+        upload(root.rk2, rk2);
+        DevBuf cap(geo.nd * 4), nroot(8);
+        root.f2_base.alloc((geo.nd + 1) * 8);
+        FSM_HIP(hipMemsetAsync(nroot.p, 0, 8, s));
+        const size_t tk = clk->begin("k_f2_plan");
+        hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,
+                           db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), root.rk2.as<uint32_t>(), geo.R,
+                           geo.rpb, geo.pm, geo.G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(),
+                           nroot.as<unsigned long long>());
+        FSM_LAUNCHED("k_f2_plan", s);
+        clk->end(tk, int64_t(db->R) * 4 + db->E * 4 + int64_t(geo.nd) * 4);
+        scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), geo.nd, s);
+        pend[2] = pend[4] = 0;
+        FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + geo.nd, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(&pend[4], nroot.p, 8, hipMemcpyDeviceToHost, s));
+        root_meta(root, freq_items, f1);
+        sync();
+        const uint64_t E0 = pend[4];
+        if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
+        if (pend[2] >= (uint64_t(1) << 32) - 4096) {  // region cursors are u32: the slab path counts it
+            root.recycle();
+            nodes.n = 0;
+            return false;
+        }
+        root.E = E0;
+        root.R = uint64_t(db->R);
+        root.cls[0].cap = E0;
+        ctx->stats.root_entries = int64_t(E0);
+        root.f2_planned = true;
+        root.f2_nslots = pend[2];
+        root.db_direct = true;
+        return true;
+    }
+
+    // the root class record (one class: every frequent item a sequence-extension member)
+    // and the 1-pattern nodes
+    void root_meta(Batch& root, const std::vector<uint32_t>& freq_items, const std::vector<uint32_t>& f1) {
+        const uint32_t F = uint32_t(freq_items.size());
+        ClassMeta m;
+        m.D = 2 * F;
+        m.mshift = 1;  // root members are all sequence-extensions: counter rows by rank
+        m.ri_off = 0;
+        m.no_off = 0;
+        root.rank_item.assign(freq_items.begin(), freq_items.end());
+        root.node_of.assign(m.D, -1);
+        for (uint32_t r = 0; r < F; ++r) {
+            root.node_of[2 * r] = int32_t(nodes.size());
+            nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]], (1u << 16) | 1u});
+        }
+        m.cap = 0;  // set from the read-back count
+        m.nS = F;
+        for (uint32_t r = 0; r < F; ++r) m.sS += f1[freq_items[r]];
+        root.cls.push_back(std::move(m));
+        root.root = true;
     }
 
     void run_root(Batch& root, const std::vector<uint32_t>& freq_items, const std::vector<uint32_t>& f1) {
@@ -2836,6 +3258,8 @@ struct Miner {
         // rank map (dense item -> frequent rank)
         std::vector<uint32_t> rank(size_t(db->U), kNone);
         for (size_t r = 0; r < freq_items.size(); ++r) rank[freq_items[r]] = uint32_t(r);
+        if (run_root_db(root, freq_items, f1, rank)) return;
+        ctx->stats.rank_root_slab = R ? db->E : 0;  // (an upper bound: the root entries are read back below)
         DevBuf d_rank, rcnt((r1 - r0 + 1) * 4), roff((r1 - r0 + 1) * 8), flag(4);
         upload(d_rank, rank);
         FSM_HIP(hipMemsetAsync(flag.p, 0, 4, s));
@@ -2894,22 +3318,7 @@ struct Miner {
             clk->end(tk, int64_t(uint64_t(db->E) * (8 + 8 * uint64_t(W))));
             tk_rw = tk;
         }
-        ClassMeta m;
-        m.D = 2 * F;
-        m.mshift = 1;  // root members are all sequence-extensions: counter rows by rank
-        m.ri_off = 0;
-        m.no_off = 0;
-        root.rank_item.assign(freq_items.begin(), freq_items.end());
-        root.node_of.assign(m.D, -1);
-        for (uint32_t r = 0; r < F; ++r) {
-            root.node_of[2 * r] = int32_t(nodes.size());
-            nodes.push_back(PNode{-1, freq_items[r], kSeq, f1[freq_items[r]], (1u << 16) | 1u});
-        }
-        m.cap = 0;  // set from the read-back count below
-        m.nS = F;
-        for (uint32_t r = 0; r < F; ++r) m.sS += f1[freq_items[r]];
-        root.cls.push_back(std::move(m));
-        root.root = true;
+        root_meta(root, freq_items, f1);
         root.root_rows = std::move(roff);
         root.R = r1 - r0;
         sync();
@@ -2919,6 +3328,7 @@ struct Miner {
         root.E = E0;
         root.cls[0].cap = E0;
         ctx->stats.root_entries = int64_t(E0);
+        ctx->stats.rank_root_slab = int64_t(E0);
         if (tk_rw != size_t(-1)) clk->add_bytes(tk_rw, int64_t(E0 * (16 + 8 * uint64_t(W))));
         if (root.f2_planned) root.f2_nslots = pend[2];
     }
@@ -2929,7 +3339,12 @@ struct Miner {
 template <class T> struct MallocArr {
     T* p = nullptr;
     size_t n = 0;
-    explicit MallocArr(size_t n_) : n(n_) {
+    MallocArr() = default;
+    explicit MallocArr(size_t n_) { alloc(n_); }
+    void alloc(size_t n_) {
+        std::free(p);
+        p = nullptr;
+        n = n_;
         // large result arrays: 2 MiB aligned and marked for transparent huge pages, so
         // the threads that fill them fault in 2 MiB at a time instead of 4 KiB (a dense
         // mine's CSR is hundreds of MB of fresh pages); free()-compatible either way
@@ -2961,15 +3376,35 @@ template <class T> void copy_out(T*& dst, const std::vector<T>& src) {
     if (!src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(T));
 }
 
-// every rank's pattern CSR, concatenated in rank order, on every rank
+// the work counters of a sharded mine that are summed over the ranks (joins etc. are
+// counted where the work ran)
+constexpr size_t kSumStats = 11;
+void sum_stats_fields(fsm_stats& st, int64_t* f[kSumStats]) {
+    int64_t* g[kSumStats] = {&st.joins, &st.classes, &st.batches, &st.entries, &st.bytes_join_equiv,
+                             &st.bytes_streamed, &st.bytes_count_alg, &st.count_launches, &st.joins_root,
+                             &st.root_keys, &st.pair_tests};
+    for (size_t k = 0; k < kSumStats; ++k) f[k] = g[k];
+}
+
+// every rank's pattern CSR, concatenated in rank order, on every rank, with the summed work
+// counters; one gather, which also carries the failure agreement of the mine (agr)
 void gather_patterns(Comm* comm, hipStream_t s, std::vector<int32_t>& sup, std::vector<int64_t>& pat_off,
-                     std::vector<int64_t>& set_off, std::vector<int32_t>& items) {
-    // blob (int32): n, n_sets, n_items, sup[n], sets-per-pattern[n], set sizes[n_sets], items[n_items]
+                     std::vector<int64_t>& set_off, std::vector<int32_t>& items, fsm_stats& st, Agreement* agr) {
+    // blob (int32): stats (2 x kSumStats), n, n_sets, n_items, sup[n], sets-per-pattern[n],
+    // set sizes[n_sets], items[n_items]
     const size_t n = sup.size(), ns = set_off.size() - 1, ni = items.size();
     if (n > size_t(INT32_MAX) || ns > size_t(INT32_MAX) || ni > size_t(INT32_MAX))
         throw Error(FSM_ELIMIT, "SPADE: pattern output of one rank exceeds 2^31 entries");
+    int64_t* f[kSumStats];
+    sum_stats_fields(st, f);
     std::vector<int32_t> b;
-    b.reserve(3 + 2 * n + ns + ni);
+    b.reserve(2 * kSumStats + 3 + 2 * n + ns + ni);
+    for (size_t k = 0; k < kSumStats; ++k) {
+        int32_t w[2];
+        std::memcpy(w, f[k], 8);
+        b.push_back(w[0]);
+        b.push_back(w[1]);
+    }
     b.push_back(int32_t(n));
     b.push_back(int32_t(ns));
     b.push_back(int32_t(ni));
@@ -2980,18 +3415,25 @@ void gather_patterns(Comm* comm, hipStream_t s, std::vector<int32_t>& sup, std::
     std::vector<uint8_t> mine(b.size() * 4);
     std::memcpy(mine.data(), b.data(), mine.size());
     std::vector<size_t> sizes;
-    const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s);
+    const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s, agr);
     sup.clear();
     items.clear();
     pat_off.assign(1, 0);
     set_off.assign(1, 0);
+    for (size_t k = 0; k < kSumStats; ++k) *f[k] = 0;
     size_t at = 0;
     for (size_t r = 0; r < sizes.size(); ++r) {
         std::vector<int32_t> v(sizes[r] / 4);
         if (!v.empty()) std::memcpy(v.data(), all.data() + at, sizes[r]);
         at += sizes[r];
-        const size_t rn = size_t(v[0]), rs = size_t(v[1]), ri = size_t(v[2]);
-        const int32_t* p = v.data() + 3;
+        for (size_t k = 0; k < kSumStats; ++k) {
+            int64_t x;
+            std::memcpy(&x, v.data() + 2 * k, 8);
+            *f[k] += x;
+        }
+        const int32_t* q = v.data() + 2 * kSumStats;
+        const size_t rn = size_t(q[0]), rs = size_t(q[1]), ri = size_t(q[2]);
+        const int32_t* p = q + 3;
         sup.insert(sup.end(), p, p + rn);
         for (size_t k = 0; k < rn; ++k) pat_off.push_back(pat_off.back() + p[rn + k]);
         for (size_t k = 0; k < rs; ++k) set_off.push_back(set_off.back() + p[2 * rn + k]);
@@ -2999,24 +3441,6 @@ void gather_patterns(Comm* comm, hipStream_t s, std::vector<int32_t>& sup, std::
     }
 }
 
-// sum the work counters of all ranks (joins etc. are counted where the work ran)
-void gather_stats(Comm* comm, hipStream_t s, fsm_stats& st) {
-    int64_t* f[] = {&st.joins, &st.classes, &st.batches, &st.entries, &st.bytes_join_equiv,
-                    &st.bytes_streamed, &st.bytes_count_alg, &st.count_launches, &st.joins_root,
-                    &st.root_keys, &st.pair_tests};
-    constexpr size_t K = sizeof(f) / sizeof(f[0]);
-    std::vector<uint8_t> mine(K * 8);
-    for (size_t k = 0; k < K; ++k) std::memcpy(mine.data() + 8 * k, f[k], 8);
-    std::vector<size_t> sizes;
-    const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s);
-    for (size_t k = 0; k < K; ++k) *f[k] = 0;
-    for (size_t r = 0; r < sizes.size(); ++r)
-        for (size_t k = 0; k < K; ++k) {
-            int64_t v;
-            std::memcpy(&v, all.data() + r * K * 8 + 8 * k, 8);
-            *f[k] += v;
-        }
-}
 
 }  // namespace
 
@@ -3088,7 +3512,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             hipLaunchKernelGGL(k_f1, dim3(grid), dim3(kBlock), use_lds ? size_t(d->U) * 4 : 0, ctx->stream,
                                d->item.as<uint32_t>(), e0, e1, d_f1.as<uint32_t>(), uint32_t(d->U), use_lds);
             FSM_LAUNCHED("k_f1", ctx->stream);
-            clock.end(tk, int64_t((e1 - e0) * 4 + uint64_t(d->U) * 4));
+            clock.end(tk, int64_t((e1 - e0) * 4 + uint64_t(d->U) * 4), int64_t((e1 - e0) * 4));
         }
         if (comm) comm->allreduce_u32(d_f1.as<uint32_t>(), size_t(d->U), ctx->stream);
         if (d->U) FSM_HIP(hipMemcpyAsync(f1.data(), d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -3140,7 +3564,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     };
     while (!stack.empty()) {
         Batch& top = *stack.back();
-        if (top.next_group >= top.groups.size()) {
+        if (top.next_group >= top.groups.size() && !mn.claim_more(top)) {
             pop();
             continue;
         }
@@ -3158,8 +3582,9 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             throw Error(FSM_EDEVICE, "SPADE internal error: lattice depth " + std::to_string(nb->depth) +
                                          " exceeds the longest sequence (" + std::to_string(db->spade.max_occ) + ")");
         mn.emit(top, g, *nb);
-        if (top.next_group >= top.groups.size()) {
-            // parent fully emitted: release it before descending
+        if (top.next_group >= top.groups.size() && top.claim_key < 0) {
+            // parent fully emitted: release it before descending (a claiming root stays until
+            // its claims run out)
             pop();
         }
         mn.count_and_freq(*nb);
@@ -3167,13 +3592,13 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     }
     mn.sync();  // the last deferred emit check, before the agreement
     });
-    mn.agree();
-    {
+    // sharded: a failure from here on is agreed on in the pattern gather (no round trip of its own)
+    mn.run_or_defer([&] {
         unsigned long long tests = 0;
         FSM_HIP(hipMemcpyAsync(&tests, mn.d_tests.p, 8, hipMemcpyDeviceToHost, ctx->stream));
         mn.sync();
         ctx->stats.pair_tests = int64_t(tests);
-    }
+    });
     ctx->stats.ms_lattice = now_ms() - t2;
     if (const char* v = std::getenv("FSM_HOST_TRACE"); v && v[0] == '1')
         std::fprintf(stderr, "[fsm host] f2 sort %.3f, kids %.3f, children %.3f, groups %.3f, emit tables %.3f, "
@@ -3184,7 +3609,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %d:%.2f", i, mn.hq[i]);
         std::fprintf(stderr, "\n");
     }
-    clock.finish(ctx->kstats);
+    mn.run_or_defer([&] { clock.finish(ctx->kstats); });
     for (const fsm_kernel_stat& k : ctx->kstats) {
         const std::string nm = k.name;
         if (nm == "k_count" || nm.rfind("k_root_keys", 0) == 0 || nm == "k_group_count") ctx->stats.ms_count_kernel += k.ms;
@@ -3199,6 +3624,10 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     // fresh output pages are first touched by the threads that fill them).
     const double to0 = now_ms();
     ctx->stats.ms_gpu_wait = mn.wait_ms;
+    MallocArr<int32_t> sup, items;
+    MallocArr<int64_t> pat_off, set_off;
+    int64_t n = 0;
+    mn.run_or_defer([&] {
     const auto& nodes = mn.nodes;
     const int64_t NN = int64_t(nodes.size());
     const int64_t first = (comm && comm->rank() != 0) ? int64_t(mn.n_shared) : 0;
@@ -3211,7 +3640,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             if (size_t(k) >= mn.node_dup.size() || !mn.node_dup[size_t(k)]) outn.push_back(int32_t(k));
     }
     auto node_at = [&](int64_t k) -> int64_t { return any_dup ? int64_t(outn[size_t(k)]) : first + k; };
-    int64_t n = any_dup ? int64_t(outn.size()) : NN - first;
+    n = any_dup ? int64_t(outn.size()) : NN - first;
     const int64_t nthr = n >= (int64_t(1) << 16) ? host_threads() : 1;
     auto par = [&](auto&& fn) { par_slices(nthr, n, fn); };  // fn(t, k0, k1) over nthr slices of [0, n)
     std::vector<int64_t> tsets(size_t(nthr) + 1, 0), titems(size_t(nthr) + 1, 0);
@@ -3231,10 +3660,10 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     }
     // the output arrays are filled in place (malloc'd, handed to the caller:
     // no zero-fill and no second copy of multi-hundred-MB pattern sets)
-    MallocArr<int32_t> sup{static_cast<size_t>(n)};
-    MallocArr<int64_t> pat_off{static_cast<size_t>(n) + 1};
-    MallocArr<int64_t> set_off{static_cast<size_t>(tsets[size_t(nthr)]) + 1};
-    MallocArr<int32_t> items{static_cast<size_t>(titems[size_t(nthr)])};
+    sup.alloc(static_cast<size_t>(n));
+    pat_off.alloc(static_cast<size_t>(n) + 1);
+    set_off.alloc(static_cast<size_t>(tsets[size_t(nthr)]) + 1);
+    items.alloc(static_cast<size_t>(titems[size_t(nthr)]));
     pat_off[size_t(n)] = tsets[size_t(nthr)];
     set_off[set_off.n - 1] = titems[size_t(nthr)];
     const int32_t* ival = db->spade.item_val.data();
@@ -3322,17 +3751,24 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             sup[size_t(k)] = int32_t(nodes[size_t(nk)].support);
         }
     });
+    });
     ctx->stats.ms_output = now_ms() - to0;
     auto* p = static_cast<fsm_patterns*>(std::calloc(1, sizeof(fsm_patterns)));
     if (!p) throw Error(FSM_ENOMEM, "calloc failed");
     p->total = total;
     p->minsup = int32_t(std::min<uint32_t>(mn.minsup, 0x7FFFFFFFu));
-    if (comm) {  // every rank's CSR, concatenated in rank order
-        std::vector<int32_t> vs(sup.p, sup.p + sup.n), vi(items.p, items.p + items.n);
-        std::vector<int64_t> vp(pat_off.p, pat_off.p + pat_off.n), vo(set_off.p, set_off.p + set_off.n);
-        gather_patterns(comm, ctx->stream, vs, vp, vo, vi);
+    if (comm) {  // every rank's CSR, concatenated in rank order (after the failure agreement)
+        if (mn.agr.code) n = 0;
+        std::vector<int32_t> vs, vi;
+        std::vector<int64_t> vp{0}, vo{0};
+        if (!mn.agr.code) {
+            vs.assign(sup.p, sup.p + sup.n);
+            vi.assign(items.p, items.p + items.n);
+            vp.assign(pat_off.p, pat_off.p + pat_off.n);
+            vo.assign(set_off.p, set_off.p + set_off.n);
+        }
+        gather_patterns(comm, ctx->stream, vs, vp, vo, vi, ctx->stats, &mn.agr);
         n = int64_t(vs.size());
-        gather_stats(comm, ctx->stream, ctx->stats);
         p->n_sets = int64_t(vo.size()) - 1;
         p->n_items = int64_t(vi.size());
         copy_out(p->support, vs);

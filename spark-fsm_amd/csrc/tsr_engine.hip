@@ -606,7 +606,8 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
     // window rows: x = first flat entry (exclusive scan of the lengths), y = row start in
     // `ent` minus x (u32 wrap: the ent index of flat entry q is y + q)
     __shared__ uint2 rowv[kExpWin + 1];
-    __shared__ uint32_t sfX[kExpWin], slY[kExpWin];  // per row: firstX (max over X), lastY (min over Y)
+    __shared__ uint2 sfl[kExpWin];                   // per row: firstX (x: max over X), lastY (y: min over Y)
+    __shared__ unsigned long long s_bloom;
     __shared__ uint32_t wflag[kXBlock / 64][64];     // per wave: row-start flags of the current step (tags)
     __shared__ uint32_t sXY[2 * kMaxSide];           // X then Y, as kids
     __shared__ uint32_t wsum[kXBlock / 64];
@@ -641,6 +642,11 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
         atomicAnd(&ctab[c >> 4], ~(3u << sh));
         atomicOr(&ctab[c >> 4], (k < nx ? 2u : 3u) << sh);
     }
+    if (threadIdx.x == 0) {  // bit (c & 63) of every kid c of X u Y: most entries skip the ctab read
+        unsigned long long bl = 0;
+        for (uint32_t k = 0; k < nxy; ++k) bl |= 1ull << (sXY[k] & 63u);
+        s_bloom = bl;
+    }
     const uint32_t maxX = sXY[nx - 1], maxY = sXY[nxy - 1];  // sides ascend by item, so by kid
     uint32_t my_ent = 0;   // row entries of this block (thread 0)
     uint32_t tag = 0;      // this wave's step tags in wflag
@@ -663,13 +669,11 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
             const uint32_t ex = bb + inc - pr;
             if (j < n) {
                 rowv[j] = make_uint2(ex, r0.x - ex);
-                sfX[j] = 0;
-                slY[j] = 0xFFFFFFFFu;
+                sfl[j] = make_uint2(0u, 0xFFFFFFFFu);
             }
             if (j + 1 < n) {
                 rowv[j + 1] = make_uint2(ex + r0.y, r1.x - (ex + r0.y));
-                sfX[j + 1] = 0;
-                slY[j + 1] = 0xFFFFFFFFu;
+                sfl[j + 1] = make_uint2(0u, 0xFFFFFFFFu);
             }
             if (threadIdx.x == 0) {
                 rowv[n] = make_uint2(tt, 0u);
@@ -677,6 +681,12 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
             }
         }
         __syncthreads();
+        // an entry's kid code: 1 (a candidate) when its bloom bit is clear (not in X u Y;
+        // whether the kid is still alive does not matter: a dead kid's count stays below
+        // t, so k_expand_reduce drops it), else the exact code from ctab
+        const uint64_t bloom = s_bloom;
+        auto code_of = [&](uint32_t c) -> uint32_t { return ((bloom >> (c & 63u)) & 1ull) ? kid_code(ctab, c) : 1u; };
+        uint32_t* sflw = reinterpret_cast<uint32_t*>(sfl);  // [2 j] = firstX, [2 j + 1] = lastY
         // chunks of whole rows [j0, j1) with at most kChunkEnt entries (block-uniform loop).
         // Every domain row holds X u Y (the bitmap AND): at least 2 entries, so the 65
         // entries from a step's first one span at most 33 rows.
@@ -692,16 +702,17 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                 const uint32_t rs = rowv[j0].y + E0, len = rowv[j0 + 1].x - E0;
                 for (uint32_t q = threadIdx.x; q < len; q += blockDim.x) {
                     const uint2 e = ent[rs + q];
-                    const uint32_t cd = kid_code(ctab, e.x);
-                    if (cd == 2u) atomicMax(&sfX[j0], e.y & 0xFFFFu);
-                    if (cd == 3u) atomicMin(&slY[j0], e.y >> 16);
+                    const uint32_t cd = code_of(e.x);
+                    if (cd == 2u) atomicMax(&sflw[2 * j0], e.y & 0xFFFFu);
+                    if (cd == 3u) atomicMin(&sflw[2 * j0 + 1], e.y >> 16);
                 }
                 __syncthreads();
-                const uint32_t fX = sfX[j0], lY = slY[j0];
+                const uint2 fl = sfl[j0];
+                const uint32_t fX = fl.x, lY = fl.y;
                 if (fX < lY) {
                     for (uint32_t q = threadIdx.x; q < len; q += blockDim.x) {
                         const uint2 e = ent[rs + q];
-                        if (e.x > mlo && kid_code(ctab, e.x) == 1u)
+                        if (e.x > mlo && code_of(e.x) == 1u)
                             bump(e.x, e.y, fX, lY, false, false, maxX, maxY, doL, doR, kid_lo, KP, hL, hR);
                     }
                 }
@@ -755,10 +766,10 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
 #pragma unroll
                 for (int u = 0; u < kEpt; ++u) {
                     if (idx[u] == kNone) continue;
-                    const uint32_t cd = kid_code(ctab, e[u].x);
+                    const uint32_t cd = code_of(e[u].x);
                     codes |= (cd | 4u) << (3 * u);  // bit 2: an entry
-                    if (cd == 2u) atomicMax(&sfX[ej[u]], e[u].y & 0xFFFFu);
-                    if (cd == 3u) atomicMin(&slY[ej[u]], e[u].y >> 16);
+                    if (cd == 2u) atomicMax(&sflw[2 * ej[u]], e[u].y & 0xFFFFu);
+                    if (cd == 3u) atomicMin(&sflw[2 * ej[u] + 1], e[u].y >> 16);
                 }
             }
             __syncthreads();
@@ -767,7 +778,8 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
 #pragma unroll
                 for (int u = 0; u < kEpt; ++u) {
                     if (((codes >> (3 * u)) & 7u) != 5u || e[u].x <= mlo) continue;  // an entry with code 1
-                    const uint32_t fX = sfX[ej[u]], lY = slY[ej[u]];
+                    const uint2 fl = sfl[ej[u]];
+                    const uint32_t fX = fl.x, lY = fl.y;
                     if (fX < lY) bump(e[u].x, e[u].y, fX, lY, false, false, maxX, maxY, doL, doR, kid_lo, KP, hL, hR);
                 }
             }
@@ -1628,7 +1640,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // them back when it finishes (ctx->kstats rows)
     struct Seg {
         double ms = 0;  // over the timed launches
-        int64_t n = 0, timed = 0, bytes = 0;
+        int64_t n = 0, timed = 0, bytes = 0, survey = 0;  // survey: SURVEY §8(d) TSR units
     } seg[4];  // bitmap path: domain, rows, reduce, k_dl; list path: expansion, -, collect, k_publish
     const char* seg_name[4] = {use_bm ? "k_exp_domain" : "k_expand", use_bm ? "k_exp_rows" : "",
                                use_bm ? "k_expand_reduce" : "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
@@ -1669,6 +1681,9 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 exp_bitmap_bytes += int64_t(bmb);
                 seg[0].bytes += int64_t(bmb + 16ull * h.nsid);
                 seg[1].bytes += int64_t(8ull * h.nent + 8ull * h.nsid);
+                // SURVEY: N/8 B per sid-bitmap operand; 4 B token + 4 B first/last per scanned position
+                seg[0].survey += int64_t(bmb);
+                seg[1].survey += int64_t(8ull * h.nent);
             }
             if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
             if (!use_bm && x.drv_in_x[k] && h.nx != r->nX)
@@ -2099,6 +2114,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         k.launches = seg[q].n;
         k.ms = seg[q].timed ? seg[q].ms * double(seg[q].n) / double(seg[q].timed) : 0.0;  // sampled, scaled
         k.alg_bytes = seg[q].bytes;
+        k.survey_bytes = seg[q].survey;
         ctx->kstats.push_back(k);
     }
     ctx->stats.exp_domain = exp_domain;

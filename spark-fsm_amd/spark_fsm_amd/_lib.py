@@ -30,6 +30,7 @@ class FsmParseError(FsmError):
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int64)
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+FETCH_ADD_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64)
 
 
 class HostComm(ctypes.Structure):
@@ -37,6 +38,7 @@ class HostComm(ctypes.Structure):
         ("user", ctypes.c_void_p),
         ("allreduce_u32", ALLREDUCE_FN),
         ("allgather", ALLGATHER_FN),
+        ("fetch_add", FETCH_ADD_FN),
     ]
 
 
@@ -112,7 +114,7 @@ FMT_SPMF, FMT_INDEXED, FMT_BMS, FMT_CSV, FMT_KOSARAK, FMT_SNAKE = range(6)
 
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 40), ("launches", ctypes.c_int64), ("alg_bytes", ctypes.c_int64),
-                ("ms", ctypes.c_double)]
+                ("ms", ctypes.c_double), ("survey_bytes", ctypes.c_int64)]
 
 
 class Stats(ctypes.Structure):
@@ -124,7 +126,7 @@ class Stats(ctypes.Structure):
         "count_launches", "mask_words", "bytes_count_alg")] + [(n, ctypes.c_double) for n in (
         "ms_gpu_wait", "ms_output")] + [(n, ctypes.c_int64) for n in (
         "joins_root", "root_keys", "pair_tests", "root_entries", "k0_device", "exp_domain", "exp_entries",
-        "exp_bitmap_bytes")]
+        "exp_bitmap_bytes", "rank_claims", "rank_root_owned", "rank_root_slab", "rank_units")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -8,6 +8,7 @@ gloo).  The host form runs several ranks on one GPU, which is how the sharded
 path is tested on a one-GPU box, and drives the CPU tests of the plumbing.
 """
 import ctypes
+import uuid
 
 import numpy as np
 
@@ -42,16 +43,41 @@ class TorchHostComm:
     failure flags, pattern CSRs) run over the same RCCL communicator torch
     already set up for the job."""
 
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, store=None, claims=True):
+        """claims: give libfsm the work-stealing counter (fsm_host_comm.fetch_add) over
+        `store` (default: the process group's default store, e.g. the TCPStore of an
+        env:// rendezvous).  Construct collectively (every rank of `group`), and one
+        per Engine: the counter keys are per communicator."""
         import torch.distributed as dist
         self._dist = dist
         self._group = group
         self._device = device
         self._ar = _lib.ALLREDUCE_FN(self._allreduce)
         self._ag = _lib.ALLGATHER_FN(self._allgather)
-        self.struct = _lib.HostComm(None, self._ar, self._ag)
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self._store = None
+        # a key prefix common to the ranks (rank 0's), so that counters never collide with
+        # another communicator's on the same store (collective: every rank, claims or not)
+        obj = [uuid.uuid4().hex if self.rank == 0 else None]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(obj, src=src, group=group)
+        self._prefix = "fsm-claims/%s/" % obj[0]
+        if claims:
+            if store is None:
+                try:
+                    store = dist.distributed_c10d._get_default_store()
+                except Exception:  # noqa: BLE001 - no default store: static plan
+                    store = None
+            self._store = store
+        self._fa = _lib.FETCH_ADD_FN(self._fetch_add) if self._store is not None else _lib.FETCH_ADD_FN()
+        self.struct = _lib.HostComm(None, self._ar, self._ag, self._fa)
+
+    def _fetch_add(self, user, key, inc):
+        try:
+            return int(self._store.add(self._prefix + str(int(key)), int(inc))) - int(inc)
+        except Exception:  # noqa: BLE001 - must not unwind through C
+            return -1
 
     def _allreduce(self, user, buf, n):
         try:

@@ -22,7 +22,9 @@ class _ResultOwner:
             return np.zeros(0, dtype=dt)
         buf = (np.ctypeslib.as_ctypes_type(dt) * int(n)).from_address(ctypes.addressof(ptr.contents))
         buf._owner = self
-        return np.frombuffer(buf, dtype=dt)
+        arr = np.frombuffer(buf, dtype=dt)
+        arr.flags.writeable = False  # library memory: read-only views
+        return arr
 
 
 class Engine:
@@ -114,12 +116,15 @@ class Engine:
         return img
 
     # ------------------------------------------------------------ mining
-    def spade_csr(self, db, support, dfs=True):
+    def spade_csr(self, db, support, dfs=True, copy=False):
         """fsm_spade_mine -> CSR numpy arrays (support, pat_off, set_off, items), meta.
 
-        The arrays are views of the library's result buffers (no copy of the
-        hundreds of MB a dense mine returns); fsm_patterns_free runs when the
-        last of them is garbage-collected."""
+        By default the arrays are read-only views of the library's result
+        buffers (no copy of the hundreds of MB a dense mine returns).  The four
+        views share ONE lifetime: fsm_patterns_free runs when the last of them
+        is garbage-collected, so keeping any one of them (say only `support`)
+        keeps every result buffer of the mine alive.  copy=True returns
+        independent, writable copies and frees the library's buffers at once."""
         out = ctypes.POINTER(_lib.Patterns)()
         check(self._L.fsm_spade_mine(self._ctx, db.handle, float(support), 1 if dfs else 0,
                                      ctypes.byref(out)), self._ctx)
@@ -131,6 +136,8 @@ class Engine:
         so = owner.view(p.set_off, p.n_sets + 1, np.int64)
         it = owner.view(p.items, p.n_items, np.int32)
         meta = {"total": p.total, "minsup": p.minsup, "n": n}
+        if copy:
+            sup, po, so, it = sup.copy(), po.copy(), so.copy(), it.copy()
         return (sup, po, so, it), meta
 
     def spade(self, db, support, dfs=True):
@@ -161,6 +168,13 @@ class Engine:
             self._L.fsm_rules_free(out)
         return rules, meta
 
+    def tsr_mined(self, db, k, minconf):
+        """fsm_tsr_mine -> MinedRules: the library's rule set kept as mined (no copy), for
+        the rule queries and documents that run on it through the C ABI."""
+        out = ctypes.POINTER(_lib.Rules)()
+        check(self._L.fsm_tsr_mine(self._ctx, db.handle, int(k), float(minconf), ctypes.byref(out)), self._ctx)
+        return MinedRules(self._L, out)
+
     def kernel_stats(self):
         """[{name, launches, alg_bytes, ms}] of the last mine call (device time, HIP events)."""
         n = ctypes.c_int32()
@@ -174,6 +188,46 @@ class Engine:
         st = _lib.Stats()
         check(self._L.fsm_get_stats(self._ctx, ctypes.byref(st)), self._ctx)
         return st.as_dict()
+
+
+class MinedRules:
+    """A mined fsm_rules (library-owned, freed with the object): its rules, and the
+    rule queries (fsm_rules_query, FSMQuestor.scala:46-98) and json4s document
+    (fsm_rules_json) computed on it by the library."""
+
+    def __init__(self, L, ptr):
+        self._L, self._p = L, ptr
+        weakref.finalize(self, L.fsm_rules_free, ptr)
+        r = ptr.contents
+        self.total, self.final_minsup, self.n = r.total, r.final_minsup, r.n
+
+    def rules(self):
+        """[(antecedent, consequent, support, confidence)] in the library's order."""
+        r = self._p.contents
+        out = []
+        for i in range(r.n):
+            x = tuple(r.ante[q] for q in range(r.ante_off[i], r.ante_off[i + 1]))
+            y = tuple(r.cons[q] for q in range(r.cons_off[i], r.cons_off[i + 1]))
+            out.append((x, y, r.support[i], r.confidence[i]))
+        return out
+
+    def query(self, side, items):
+        """Indexes (ascending) of the rules whose antecedent (side 0) / consequent (side 1)
+        items all occur in `items`."""
+        q = np.ascontiguousarray(list(items), np.int32)
+        idx = np.zeros(max(self.n, 1), np.int64)
+        n = ctypes.c_int64()
+        check(self._L.fsm_rules_query(self._p, int(side), q.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(q),
+                                      idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(n)))
+        return idx[:n.value].tolist()
+
+    def to_json(self):
+        out, n = ctypes.c_void_p(), ctypes.c_int64()
+        check(self._L.fsm_rules_json(self._p, ctypes.byref(out), ctypes.byref(n)))
+        try:
+            return ctypes.string_at(out, n.value).decode("utf-8")
+        finally:
+            self._L.fsm_buffer_free(out)
 
 
 class DB:

@@ -27,8 +27,11 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     import spark_fsm_amd as fsm
     from spark_fsm_amd import dist as fdist
-    hc = fdist.TorchHostComm()
-    res = {"rank": rank, "world": world}
+    # FSM_TEST_CLAIMS=0: no work-stealing counter (the static class plan); "rank0": only rank 0
+    # offers one (the ranks must agree on the static plan)
+    cl = os.environ.get("FSM_TEST_CLAIMS", "1")
+    hc = fdist.TorchHostComm(claims=cl == "1" or (cl == "rank0" and rank == 0))
+    res = {"rank": rank, "world": world, "claims": hc._store is not None}
     if mode == "selftest":
         fdist.selftest(world, rank, host_comm=hc)
         res["ok"] = True

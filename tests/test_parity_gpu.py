@@ -360,17 +360,19 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic"])
+@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic", "passes-3", "passes-64"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
     """The root F2 implementations (key runs counted per rank group, at the
-    default and at a small block chunk; global atomics) give the oracle's
-    patterns and joins."""
+    default and at a small block chunk, in several passes over group ranges;
+    global atomics) give the oracle's patterns and joins."""
     from oracle import oracle
     from tools import gen
     if path == "atomic":
         monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
     if path == "group-few-blocks":
         monkeypatch.setenv("FSM_F2_BLOCKS", "3")
+    if path.startswith("passes"):
+        monkeypatch.setenv("FSM_F2_PASSES", path.split("-")[1])
     ds = gen.quest(20000, seed=4)
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
     pats, meta, st = gpu_spade(eng, None, 0.003, tokens=ds)
@@ -667,3 +669,38 @@ def test_ingested_files_mine_like_their_lines(eng):
     ot = oracle.tsr(recs, 60, 0.3)
     assert rules == ot["rules"]
     assert RuleSet(rules, rmeta["total"]).to_json() == ref.rules_json(ot["rules"], ot["total"])
+
+
+def test_rule_queries_on_gpu_mined_rules(eng):
+    """§8f row 4 (FSMQuestor.scala:46-98, get:antecedent / get:consequent) on rules the
+    GPU mined: a Kosarak-shaped prefix mined by fsm_tsr_mine (rules identical to the
+    oracle's), then fsm_rules_query on the library's own fsm_rules (no copy) for random
+    item sets of both sides, against the restatement (oracle/spmf_builder.rules_query)
+    over the same rules in the same order; the json4s document as well."""
+    import random
+    from oracle import oracle, spmf_builder as ref
+    from spark_fsm_amd import MODE_TSR
+    from tools import gen
+    ds = gen.kosarak(D=5000, seed=1)
+    recs = ds.records()
+    db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)
+    try:
+        mr = eng.tsr_mined(db, 300, 0.5)
+    finally:
+        db.free()
+    rules = mr.rules()
+    o = oracle.tsr(recs, 300, 0.5)
+    assert sorted(rules, key=lambda t: (-t[2], t[0], t[1])) == o["rules"]
+    assert mr.final_minsup == o["final_minsup"] and mr.total == 5000 and len(rules) >= 300
+    rng = random.Random(8)
+    items = sorted({i for x, y, _, _ in rules for i in x + y})
+    hits = 0
+    for _ in range(80):
+        q = rng.sample(items, rng.randint(0, min(len(items), 25))) + [rng.randint(1, 41270) for _ in range(3)]
+        for side in (0, 1):
+            got = mr.query(side, q)
+            assert got == ref.rules_query(rules, side, q)
+            hits += len(got)
+    assert hits > 0  # the queries do select rules
+    assert mr.query(0, []) == [] and mr.query(1, items) == list(range(len(rules)))
+    assert mr.to_json() == ref.rules_json(rules, mr.total)
