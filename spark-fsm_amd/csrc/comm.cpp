@@ -81,26 +81,58 @@ void nccl_check(ncclResult_t r, const char* what) {
 // up to FSM_COMM_INIT_TIMEOUT_S seconds (default 300), then aborted with FSM_ECOMM.
 // Non-blocking communicators may return ncclInProgress from a collective's enqueue
 // as well; wait() polls the communicator's state until the enqueue has completed.
-class RcclComm final : public Comm {
+// The work-stealing counters of the ranks of one node: a POSIX shared-memory segment
+// named after the communicator's unique id.  Every rank opens it BEFORE the collective
+// that completes the communicator's setup (so every rank has it open once that returns);
+// rank 0 then unlinks the name (the mappings stay until each rank unmaps).  Slots are
+// reused every kSlots keys: reset(key) zeroes key's slot on rank 0 before the
+// collective that precedes its first claim.
+class ShmCounters {
   public:
-    RcclComm(int nranks, int rank, const uint8_t id[128]) : Comm(nranks, rank) {
-        ncclUniqueId uid;
-        std::memcpy(uid.internal, id, sizeof(uid.internal));
-        // the work-stealing counters: one shared-memory segment of the node, named after the
-        // unique id, opened by every rank BEFORE the communicator init (which returns only
-        // once every rank has joined), unlinked by rank 0 after it (the mappings stay)
-        char name[64];
+    static constexpr size_t kSlots = 512;
+    explicit ShmCounters(const uint8_t id[128]) {
         uint64_t h = 1469598103934665603ull;  // FNV-1a of the unique id
         for (int k = 0; k < 128; ++k) h = (h ^ id[k]) * 1099511628211ull;
-        std::snprintf(name, sizeof(name), "/fsm-claims-%016llx", (unsigned long long)h);
-        const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
-        if (fd >= 0) {
-            if (ftruncate(fd, off_t(kSlots * sizeof(int64_t))) == 0) {
-                void* p = mmap(nullptr, kSlots * sizeof(int64_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-                if (p != MAP_FAILED) ctr_ = static_cast<int64_t*>(p);
-            }
-            close(fd);
+        std::snprintf(name_, sizeof(name_), "/fsm-claims-%016llx", (unsigned long long)h);
+        const int fd = shm_open(name_, O_CREAT | O_RDWR, 0600);
+        if (fd < 0) return;
+        if (ftruncate(fd, off_t(kSlots * sizeof(int64_t))) == 0) {
+            void* p = mmap(nullptr, kSlots * sizeof(int64_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            if (p != MAP_FAILED) ctr_ = static_cast<int64_t*>(p);
         }
+        close(fd);
+    }
+    ~ShmCounters() {
+        if (ctr_) munmap(ctr_, kSlots * sizeof(int64_t));
+    }
+    ShmCounters(const ShmCounters&) = delete;
+    ShmCounters& operator=(const ShmCounters&) = delete;
+    void unlink_name() { shm_unlink(name_); }  // rank 0, once every rank has opened it
+    bool ok() const { return ctr_ != nullptr; }
+    int64_t fetch_add(int64_t key, int64_t inc) {
+        return ctr_ ? __atomic_fetch_add(&ctr_[size_t(key) % kSlots], inc, __ATOMIC_SEQ_CST) : -1;
+    }
+    void reset(int64_t key) {
+        // slot key % kSlots was last used kSlots keys ago, long past that mine's final gather
+        if (ctr_) __atomic_store_n(&ctr_[size_t(key) % kSlots], int64_t(0), __ATOMIC_SEQ_CST);
+    }
+
+  private:
+    char name_[64] = {0};
+    int64_t* ctr_ = nullptr;
+};
+
+bool id_set(const uint8_t id[128]) {
+    for (int k = 0; k < 128; ++k)
+        if (id[k]) return true;
+    return false;
+}
+
+class RcclComm final : public Comm {
+  public:
+    RcclComm(int nranks, int rank, const uint8_t id[128]) : Comm(nranks, rank), shm_(id) {
+        ncclUniqueId uid;
+        std::memcpy(uid.internal, id, sizeof(uid.internal));
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.blocking = 0;
         ncclResult_t r = rccl().comm_init_rank_config(&comm_, nranks, uid, rank, &cfg);
@@ -114,24 +146,18 @@ class RcclComm final : public Comm {
         try {
             wait("ncclCommInitRankConfig", limit_ms);
         } catch (...) {
-            if (rank == 0) shm_unlink(name);
-            unmap();
+            if (rank == 0) shm_.unlink_name();
             throw;
         }
-        if (rank == 0) shm_unlink(name);
+        if (rank == 0) shm_.unlink_name();
     }
     ~RcclComm() override {
         if (comm_) (void)rccl().comm_destroy(comm_);
-        unmap();
     }
-    bool has_fetch_add() const override { return ctr_ != nullptr; }
-    int64_t fetch_add(int64_t key, int64_t inc) override {
-        if (!ctr_) return -1;
-        return __atomic_fetch_add(&ctr_[size_t(key) % kSlots], inc, __ATOMIC_SEQ_CST);
-    }
+    bool has_fetch_add() const override { return shm_.ok(); }
+    int64_t fetch_add(int64_t key, int64_t inc) override { return shm_.fetch_add(key, inc); }
     void reset_counter(int64_t key) override {
-        // slot key % kSlots was last used kSlots mines ago, long past that mine's final gather
-        if (ctr_ && rank() == 0) __atomic_store_n(&ctr_[size_t(key) % kSlots], int64_t(0), __ATOMIC_SEQ_CST);
+        if (rank() == 0) shm_.reset(key);
     }
     void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
         if (n) enqueued(rccl().all_reduce(dev, dev, n, ncclUint32, ncclSum, comm_, s), "ncclAllReduce");
@@ -166,19 +192,23 @@ class RcclComm final : public Comm {
             std::this_thread::yield();
         }
     }
-    void unmap() {
-        if (ctr_) munmap(ctr_, kSlots * sizeof(int64_t));
-        ctr_ = nullptr;
-    }
-    static constexpr size_t kSlots = 512;
-    int64_t* ctr_ = nullptr;
+    ShmCounters shm_;
     ncclComm_t comm_ = nullptr;
 };
 
+// Host callbacks.  Without a fetch_add callback but with a unique id in fsm_opts, the
+// ranks (one node) share the RCCL communicator's shared-memory counters instead: the
+// segment is opened before a first all-reduce and unlinked by rank 0 after it.
 class HostComm final : public Comm {
   public:
-    HostComm(int nranks, int rank, const fsm_host_comm& cb) : Comm(nranks, rank), cb_(cb) {
+    HostComm(int nranks, int rank, const fsm_host_comm& cb, const uint8_t id[128]) : Comm(nranks, rank), cb_(cb) {
         if (!cb_.allreduce_u32 || !cb_.allgather) throw Error(FSM_EINVAL, "fsm_host_comm: missing callback");
+        if (!cb_.fetch_add && id_set(id)) {
+            shm_ = std::make_unique<ShmCounters>(id);
+            uint32_t one = 1;
+            host_allreduce_u32(&one, 1, nullptr);  // every rank has the segment open
+            if (rank == 0) shm_->unlink_name();
+        }
     }
     void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
         std::vector<uint32_t> h(n);
@@ -205,13 +235,18 @@ class HostComm final : public Comm {
         if (cb_.allgather(cb_.user, send, recv, int64_t(bytes)) != 0)
             throw Error(FSM_ECOMM, "host all-gather callback failed");
     }
-    bool has_fetch_add() const override { return cb_.fetch_add != nullptr; }
+    bool has_fetch_add() const override { return cb_.fetch_add != nullptr || (shm_ && shm_->ok()); }
     int64_t fetch_add(int64_t key, int64_t inc) override {
-        return cb_.fetch_add ? cb_.fetch_add(cb_.user, key, inc) : -1;  // (keys are never reused: no reset)
+        if (cb_.fetch_add) return cb_.fetch_add(cb_.user, key, inc);  // (keys are never reused: no reset)
+        return shm_ ? shm_->fetch_add(key, inc) : -1;
+    }
+    void reset_counter(int64_t key) override {
+        if (!cb_.fetch_add && shm_ && rank() == 0) shm_->reset(key);
     }
 
   private:
     fsm_host_comm cb_;
+    std::unique_ptr<ShmCounters> shm_;
 };
 
 }  // namespace
@@ -269,7 +304,7 @@ void rccl_unique_id(uint8_t out[128]) {
 std::unique_ptr<Comm> make_comm(const fsm_opts& o) {
     if (o.nranks <= 1) return nullptr;
     if (o.rank < 0 || o.rank >= o.nranks) throw Error(FSM_EINVAL, "rank out of range");
-    if (o.host_comm) return std::make_unique<HostComm>(o.nranks, o.rank, *o.host_comm);
+    if (o.host_comm) return std::make_unique<HostComm>(o.nranks, o.rank, *o.host_comm, o.unique_id);
     return std::make_unique<RcclComm>(o.nranks, o.rank, o.unique_id);
 }
 

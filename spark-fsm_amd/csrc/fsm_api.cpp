@@ -141,6 +141,8 @@ int fsm_comm_selftest(const fsm_opts* opts) {
             at += sizes[q];
         }
         if (at != all.size()) throw Error(FSM_ECOMM, "selftest: gather length mismatch");
+        if (ex != N && std::getenv("FSM_SELFTEST_REQUIRE_CLAIMS"))
+            throw Error(FSM_ECOMM, "selftest: the ranks have no common work-stealing counter");
         if (ex == N) {
             // claims: the ranks take ranges of r + 1 units of [0, 997) from the shared counter
             // until it runs out; every unit must be claimed exactly once

@@ -49,6 +49,9 @@
 
 
 namespace fsm {
+// sparse_count.hip
+void sparse_sort_rle(const uint64_t* keys, uint64_t* sorted, uint64_t n, unsigned end_bit, uint64_t* uniq,
+                     uint32_t* counts, uint32_t* nruns, hipStream_t s);
 namespace {
 
 constexpr uint32_t kSeq = 0, kItm = 1;
@@ -336,6 +339,102 @@ __global__ __launch_bounds__(1024) void k_cnt_keys(uint32_t E, uint32_t epb, con
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
         fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[uint64_t(g) * nblk + b]);
     if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
+}
+
+// ---- Sparse class count (batches whose dense D x D counter matrices would be far
+// larger than their joins: a class with tens of thousands of frequent children,
+// mostly absent from one another's sequences).  k_sparse_cap sums every entry's key
+// capacity (temporal: any partner; equality: partners after it); k_sparse_keys
+// writes every successful join as the u64 key (member slot cbase + mi) << 32 |
+// column; sparse_sort_rle (sparse_count.hip: rocPRIM radix sort + run-length
+// encode) leaves the non-zero counters in (slot, column) order; k_sparse_flag +
+// scan + k_sparse_recs keep the frequent ones as FreqRec in (row, slot) order.
+__global__ __launch_bounds__(kBlock) void k_sparse_cap(uint32_t E, const uint32_t* __restrict__ mem,
+                                                       const uint32_t* __restrict__ pos, uint32_t mlo, uint32_t mhi,
+                                                       unsigned long long* __restrict__ cap) {
+    __shared__ unsigned long long bs;
+    if (threadIdx.x == 0) bs = 0;
+    __syncthreads();
+    unsigned long long c = 0;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+        const uint32_t mi = mem[e], p = pos[e];
+        if (mi - mlo < mhi - mlo) c += 2ull * (p & 0xFFFFu) - 1ull - (p >> 16);
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+    if (lane_id() == 0) atomicAdd(&bs, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && bs) atomicAdd(cap, bs);
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_sparse_keys(uint32_t E, const uint32_t* __restrict__ cid,
+                                                        const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
+                                                        const uint32_t* __restrict__ lohi,
+                                                        const uint32_t* __restrict__ pos,
+                                                        const uint64_t* __restrict__ mask, uint32_t mlo, uint32_t mhi,
+                                                        uint32_t wd, unsigned long long* __restrict__ keys,
+                                                        unsigned long long* __restrict__ cursor,
+                                                        unsigned long long* __restrict__ tests) {
+    const uint32_t lane = lane_id();
+    uint32_t my_tests = 0;
+    // wave-uniform trip count (the key reservation is a wave scan)
+    for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < E; b0 += gridDim.x * blockDim.x) {
+        const uint32_t e = b0 + threadIdx.x;
+        const uint32_t mi = e < E ? mem[e] : 0u;
+        const bool live = e < E && mi - mlo < mhi - mlo;
+        uint32_t n = 0, rl = 0, rb = 0, lo_i = 0, ti = 0, ri = 0, slot = 0;
+        MaskV<W> mk;
+        if (live) {
+            const uint32_t p = pos[e];
+            rl = p & 0xFFFFu;
+            rb = e - (p >> 16);
+            my_tests += rl;
+            slot = cls[cid[e]].cbase + mi;
+            const uint32_t lh_i = lohi[e];
+            lo_i = lh_i & 0xFFFFu;
+            ti = mi & 1u;
+            ri = mi >> 1;
+            mk.load(mask + size_t(e) * mask_words<W>(wd), wd, lh_i);
+            for (uint32_t q = 0; q < rl; ++q)
+                class_joins<W>(ti, ri, lo_i, mk, rb + q, mem, lohi, mask, wd, [&](uint32_t) { ++n; });
+        }
+        const uint32_t incl = wave_incl_scan(n), tot = uint32_t(__shfl(int(incl), 63, 64));
+        unsigned long long base = 0;
+        if (lane == 63 && tot) base = atomicAdd(cursor, (unsigned long long)tot);
+        base = __shfl(base, 63, 64);
+        if (n) {
+            unsigned long long at = base + incl - n;
+            const unsigned long long hi = (unsigned long long)slot << 32;
+            for (uint32_t q = 0; q < rl; ++q)
+                class_joins<W>(ti, ri, lo_i, mk, rb + q, mem, lohi, mask, wd, [&](uint32_t col) { keys[at++] = hi | col; });
+        }
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) my_tests += uint32_t(__shfl_xor(int(my_tests), d, 64));
+    if (lane == 0 && my_tests) atomicAdd(tests, (unsigned long long)my_tests);
+}
+
+__global__ __launch_bounds__(kBlock) void k_sparse_flag(const uint32_t* __restrict__ counts,
+                                                        const uint32_t* __restrict__ nruns, uint32_t n, uint32_t minsup,
+                                                        uint32_t* __restrict__ flag) {
+    const uint32_t nr = *nruns;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        flag[i] = i < nr && counts[i] >= minsup ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sparse_recs(const uint64_t* __restrict__ uniq,
+                                                        const uint32_t* __restrict__ counts,
+                                                        const uint32_t* __restrict__ nruns,
+                                                        const uint64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ slot2row, uint32_t minsup,
+                                                        FreqRec* __restrict__ out) {
+    const uint32_t nr = *nruns;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += gridDim.x * blockDim.x)
+        if (counts[i] >= minsup) {
+            const uint64_t k = uniq[i];
+            out[off[i]] = FreqRec{slot2row[uint32_t(k >> 32)], uint32_t(k & 0xFFFFFFFFu), counts[i], 0u};
+        }
 }
 
 __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bits [a, b), 0 <= a <= b <= 64
@@ -2091,6 +2190,78 @@ struct Miner {
         return true;
     }
 
+    // the sparse count for batches whose dense counter matrices exceed 4 GiB (FSM_COUNT_PATH=
+    // sparse forces it: tests); sparse_count itself falls back (false) when the keys would
+    // not be smaller than the matrices
+    bool sparse_wanted(const Batch& b) const {
+        const char* v = std::getenv("FSM_COUNT_PATH");
+        if (v && !std::strcmp(v, "sparse")) return true;
+        return b.n_cnt * 4 >= (uint64_t(1) << 32);
+    }
+    bool sparse_count(Batch& b, std::vector<FreqRec>& recs, const RawVec<DRow>& rows) {
+        const SlabPtrs sp = b.slab.ptrs();
+        const uint32_t E = uint32_t(b.E), mlo = member_lo(b), mhi = member_hi(b);
+        const unsigned grid = unsigned(std::min<uint64_t>((b.E + kBlock - 1) / kBlock, 8192));
+        DevBuf capd(8), cur(8), nruns(4);
+        FSM_HIP(hipMemsetAsync(capd.p, 0, 8, s));
+        hipLaunchKernelGGL(k_sparse_cap, dim3(grid), dim3(kBlock), 0, s, E, sp.mem, sp.pos, mlo, mhi,
+                           capd.as<unsigned long long>());
+        FSM_LAUNCHED("k_sparse_cap", s);
+        FSM_HIP(hipMemcpyAsync(&pend[3], capd.p, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        const uint64_t capk = pend[3];
+        const bool forced = [] { const char* v = std::getenv("FSM_COUNT_PATH"); return v && !std::strcmp(v, "sparse"); }();
+        // keys, their sorted copy, the unique keys and counts: about 28 B per key
+        if (!forced && (capk * 28 >= b.n_cnt * 4 || capk * 28 > budget)) return false;
+        recs.clear();
+        if (capk == 0) return true;
+        DevBuf keys(capk * 8), sorted(capk * 8);
+        FSM_HIP(hipMemsetAsync(cur.p, 0, 8, s));
+        const size_t tk = clk->begin("k_count");
+#define FSM_SK(WW)                                                                                                  \
+    hipLaunchKernelGGL(k_sparse_keys<WW>, dim3(grid), dim3(kBlock), 0, s, E, sp.cid, b.d_cls.as<DClass>(), sp.mem,   \
+                       sp.lohi, sp.pos, sp.mask, mlo, mhi, uint32_t(W), keys.as<unsigned long long>(),              \
+                       cur.as<unsigned long long>(), d_tests.as<unsigned long long>())
+        FSM_W_DISPATCH(W, FSM_SK)
+#undef FSM_SK
+        FSM_LAUNCHED("k_sparse_keys", s);
+        clk->end(tk, int64_t(b.E * entry_bytes()), int64_t(b.E * survey_entry_bytes()));
+        FSM_HIP(hipMemcpyAsync(&pend[3], cur.p, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        const uint64_t n = pend[3];
+        if (n > capk) throw Error(FSM_EDEVICE, "SPADE sparse count: more joins than their capacity");
+        if (n == 0) return true;
+        unsigned end_bit = 32;
+        while (end_bit < 64 && (uint64_t(1) << (end_bit - 32)) < b.cbase_total) ++end_bit;
+        DevBuf uniq(n * 8), counts(n * 4);
+        sparse_sort_rle(keys.as<uint64_t>(), sorted.as<uint64_t>(), n, end_bit, uniq.as<uint64_t>(),
+                        counts.as<uint32_t>(), nruns.as<uint32_t>(), s);
+        // member slot -> counter row (the rows' index in `rows`)
+        std::vector<uint32_t> s2r(size_t(std::max<uint64_t>(b.cbase_total, 1)), kNone);
+        for (size_t q = 0; q < rows.size(); ++q) s2r[b.cls[rows[q].cls].cbase + rows[q].mi] = uint32_t(q);
+        DevBuf d_s2r, flag(n * 4), off((n + 1) * 8);
+        upload(d_s2r, s2r);
+        const unsigned g2 = unsigned(std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192));
+        hipLaunchKernelGGL(k_sparse_flag, dim3(g2), dim3(kBlock), 0, s, counts.as<uint32_t>(), nruns.as<uint32_t>(),
+                           uint32_t(n), minsup, flag.as<uint32_t>());
+        FSM_LAUNCHED("k_sparse_flag", s);
+        scan_exclusive(flag.as<uint32_t>(), off.as<uint64_t>(), n, s);
+        FSM_HIP(hipMemcpyAsync(&pend[3], off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        sync();
+        const uint64_t nrec = pend[3];
+        if (nrec) {
+            DevBuf d_recs(nrec * sizeof(FreqRec));
+            hipLaunchKernelGGL(k_sparse_recs, dim3(g2), dim3(kBlock), 0, s, uniq.as<uint64_t>(), counts.as<uint32_t>(),
+                               nruns.as<uint32_t>(), off.as<uint64_t>(), d_s2r.as<uint32_t>(), minsup,
+                               d_recs.as<FreqRec>());
+            FSM_LAUNCHED("k_sparse_recs", s);
+            recs.resize(nrec);
+            FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, nrec * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
+            sync();
+        }
+        return true;
+    }
+
     void stats_for_class(const Batch& b, const ClassMeta& m) {
         const uint64_t S = m.nS, I = m.nI, sS = m.sS, sI = m.sI;
         fsm_stats& st = ctx->stats;
@@ -2522,6 +2693,12 @@ struct Miner {
         if (b.db_direct && b.E && !root_done)
             throw Error(FSM_EDEVICE, "SPADE internal error: the DB-direct root F2 did not apply");
         if (b.E) st.count_launches += 1;
+        // huge, sparse counter matrices: the joins sorted instead (records in (row, slot) order)
+        const bool sparse_done = !root_done && b.E && sparse_wanted(b) && sparse_count(b, recs, rows);
+        if (sparse_done) {
+            order_recs(recs, uint32_t(rows.size()));
+            return;
+        }
         const bool keyed_done = !root_done && keyed_layout && keyed_count(b, cnt);
         if (!root_done && !keyed_done) {
             cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
@@ -3539,6 +3716,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     std::vector<std::unique_ptr<Batch>> stack;
     if (!freq.empty()) {
         auto root = std::make_unique<Batch>();
+        root->root = true;  // (even if run_root fails below: every rank then takes the root's gather)
         mn.run_or_defer([&] {  // agreed on in the root count
             mn.maybe_inject("root");
             mn.run_root(*root, freq, f1);

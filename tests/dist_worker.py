@@ -29,11 +29,18 @@ def main():
     from spark_fsm_amd import dist as fdist
     # FSM_TEST_CLAIMS=0: no work-stealing counter (the static class plan); "rank0": only rank 0
     # offers one (the ranks must agree on the static plan)
+    # "shm": no callback, but a unique id: the node's shared-memory counters (the RCCL
+    # communicator's) under the host collectives
     cl = os.environ.get("FSM_TEST_CLAIMS", "1")
     hc = fdist.TorchHostComm(claims=cl == "1" or (cl == "rank0" and rank == 0))
     res = {"rank": rank, "world": world, "claims": hc._store is not None}
+    uid = None
+    if cl == "shm":
+        obj = [os.urandom(128) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
     if mode == "selftest":
-        fdist.selftest(world, rank, host_comm=hc)
+        fdist.selftest(world, rank, host_comm=hc, unique_id=uid)
         res["ok"] = True
     elif mode == "spade":
         from tools import gen

@@ -68,13 +68,18 @@ def test_shard_plan_largest_first():
     assert list(shard_plan([5, 3, 9, 1, 1, 7], 3)) == [2, 2, 0, 1, 1, 1]
 
 
-@pytest.mark.parametrize("claims", ["1", "0", "rank0"])
+@pytest.mark.parametrize("claims", ["1", "0", "rank0", "shm"])
 @pytest.mark.parametrize("world", [2, 3])
 def test_host_comm_collectives_gloo(world, claims, tmp_path, monkeypatch):
-    """fsm_comm_selftest over gloo: all-reduce, ragged all-gather and (claims=1) the
-    work-stealing counter: ranks claiming ranges of r + 1 units until it runs out take
-    every unit exactly once (checked inside the self-test)."""
+    """fsm_comm_selftest over gloo: all-reduce, ragged all-gather and the work-stealing
+    counter: ranks claiming ranges of r + 1 units until it runs out take every unit
+    exactly once (checked inside the self-test).  claims=1: the store's counter through
+    fsm_host_comm.fetch_add; shm: the node's shared-memory counters the RCCL
+    communicator uses (a unique id, no callback); 0 / rank0: no common counter, the
+    ranks agree on the static plan."""
     monkeypatch.setenv("FSM_TEST_CLAIMS", claims)
+    if claims in ("1", "shm"):
+        monkeypatch.setenv("FSM_SELFTEST_REQUIRE_CLAIMS", "1")
     res = run_ranks(world, ["selftest"], tmp_path, timeout=180)
     assert [r["rank"] for r in res] == list(range(world)) and all(r["ok"] for r in res)
     assert [r["claims"] for r in res] == [claims == "1" or (claims == "rank0" and r == 0) for r in range(world)]

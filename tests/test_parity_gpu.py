@@ -443,20 +443,25 @@ def test_timestamp_limit(eng, fsm):
     assert ei.value.code == fsm.FSM_ELIMIT and "65536" in str(ei.value)
 
 
-@pytest.mark.parametrize("path", ["keys", "atomic", "atomic-thread", "default"])
+@pytest.mark.parametrize("path", ["keys", "atomic", "atomic-thread", "default", "sparse", "sparse-root"])
 @pytest.mark.parametrize("shape", ["quest", "sign", "bible", "sign-low", "wide"])
 def test_count_paths_agree(eng, path, shape, monkeypatch):
     """Class counting: the keyed count (group-aligned counter layout, u16 keys
     in (group, block) regions, LDS counting, counters written out) forced on
     every batch, the global-atomic count (k_count2's run windows at W = 1, runs
     over 64 entries thread-per-entry; or k_count thread-per-entry throughout,
-    FSM_COUNT_KERNEL=thread), and the default size switch give the oracle's
-    patterns and joins, and the same executed pair tests."""
+    FSM_COUNT_KERNEL=thread), the sparse count (joins as u64 keys, radix sort +
+    run-length encode; sparse-root: the root class too, through its slab) and the
+    default size switch give the oracle's patterns and joins, and the same
+    executed pair tests."""
     from oracle import oracle
     from tools import gen
     if path == "atomic-thread":
         monkeypatch.setenv("FSM_COUNT_PATH", "atomic")
         monkeypatch.setenv("FSM_COUNT_KERNEL", "thread")
+    elif path == "sparse-root":
+        monkeypatch.setenv("FSM_COUNT_PATH", "sparse")
+        monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
     elif path != "default":
         monkeypatch.setenv("FSM_COUNT_PATH", path)
     if shape == "quest":
@@ -472,10 +477,38 @@ def test_count_paths_agree(eng, path, shape, monkeypatch):
     o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
-    if path == "keys":
+    if path in ("keys", "sparse"):
         monkeypatch.setenv("FSM_COUNT_PATH", "atomic")
         _, _, st2 = gpu_spade(eng, None, sup, tokens=ds)
         assert st2["pair_tests"] == st["pair_tests"]
+
+
+def test_class_with_70k_frequent_children(eng):
+    """A prefix class with more than 65,535 frequent children (round 3 returned
+    FSM_ELIMIT): 70,000 sequences <a, b_k> at support 1 make 70,001 frequent items
+    (too many for the root's rank-group F2: the root is counted sparse) and a
+    first-level class [a] of 70,000 members whose dense 140,000 x 140,000 counter
+    matrix (78 GB) would not fit: it is counted sparse too.  Known answer: the
+    1-patterns and the 70,000 patterns a -> b_k, every support by definition."""
+    import numpy as np
+    from spark_fsm_amd import MODE_SPADE
+    from tools import gen
+    n = 70000
+    so = np.arange(0, 5 * (n + 1), 5, dtype=np.int64)
+    tk = np.empty(5 * n, dtype=np.int64)
+    tk[0::5], tk[1::5], tk[2::5], tk[3::5], tk[4::5] = 1, -1, np.arange(2, n + 2), -1, -2
+    ds = gen.DataSet(so, tk, "70k-children")
+    db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_SPADE)
+    try:
+        pats, meta = eng.spade(db, 1.0 / n)
+    finally:
+        db.free()
+    exp = sorted([(((1,),), n)] + [(((b,),), 1) for b in range(2, n + 2)] +
+                 [(((1,), (b,)), 1) for b in range(2, n + 2)])
+    assert meta["minsup"] == 1 and sorted(pats) == exp
+    st = eng.stats()
+    F = n + 1  # SURVEY A.2 joins: root F^2 + F(F-1)/2, class [a]: S^2 + S(S-1)/2 with S = n
+    assert st["joins"] == F * F + F * (F - 1) // 2 + n * n + n * (n - 1) // 2
 
 
 # ------------------------------------------------------ sharded (N > 1)
