@@ -3713,6 +3713,9 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
         }
         if (mn.slice_hi < mn.slice_lo) mn.slice_hi = mn.slice_lo;
     }
+    // the root entries this rank joins as the owner in the F2 (its rank slice; all unsharded)
+    for (size_t k = comm ? mn.slice_lo : 0; k < (comm ? std::min<size_t>(mn.slice_hi, freq.size()) : freq.size()); ++k)
+        ctx->stats.rank_root_owned += int64_t(f1[freq[k]]);
     std::vector<std::unique_ptr<Batch>> stack;
     if (!freq.empty()) {
         auto root = std::make_unique<Batch>();

@@ -1511,6 +1511,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // rows and the domain lists), the results (mapped pinned host memory, at most
     // ecap records per slot) and its own events (completion, per-kernel timing).
     const TsrGrid grid;
+    // Sharded TSR (nranks > 1, bitmap path): each launch's rule slots are split over the
+    // ranks and the slots' results all-gathered once per launch (finish); the replay
+    // stays replicated and deterministic.  FSM_TSR_SHARD=0 replicates the expansions.
+    const bool shard_exp = shard && use_bm && [] {
+        const char* v = std::getenv("FSM_TSR_SHARD");
+        return !(v && v[0] == '0');
+    }();
     struct ExpSet {
         DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part, dom;
         std::unique_ptr<PinnedBuf> stage, pin;
@@ -1523,6 +1530,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         uint32_t *h_rcnt = nullptr, *d_rcnt = nullptr;  // bitmap path: records per reduce block
         std::vector<Rule*> batch;
         std::vector<char> drv_in_x;
+        uint32_t la = 0, lz = 0;  // slot sharding: this rank's slots [la, lz) of the batch (else all)
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
         // the set's own stream: the two sets' launches are independent, so the GPU runs
         // one set's kernels while the other's are in flight (FSM_TSR_STREAMS=1: ctx stream)
@@ -1662,14 +1670,15 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             }
             seg[q].n += 1;
         }
-        const uint32_t nb = uint32_t(x.batch.size());
-        if (use_bm) {
+        const uint32_t nb = x.lz - x.la;  // the slots expanded here (slot sharding: this rank's share)
+        if (use_bm && nb) {
             exp_part_bytes += int64_t(x.blocks * row_bytes);
             seg[1].bytes += int64_t(x.blocks * row_bytes);  // the partial rows the row kernel writes
         }
         uint64_t nout_all = 0;
+        ctx->stats.rank_units += int64_t(nb);
         for (uint32_t k = 0; k < nb; ++k) {
-            Rule* r = x.batch[k];
+            Rule* r = x.batch[x.la + k];
             const ExpHdr h = x.h_hdr[k];
             nout_all += h.nout;
             if (use_bm) {
@@ -1708,6 +1717,50 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
             }
         }
+        if (shard_exp) {
+            // every rank's slots: (nsid, nent, nrec, records) per slot of its share, gathered
+            // once per launch (the failure agreement rides along); the replay then goes on
+            // alike on every rank
+            std::vector<uint8_t> mine;
+            auto put = [&](const void* p, size_t n) {
+                const uint8_t* b = static_cast<const uint8_t*>(p);
+                mine.insert(mine.end(), b, b + n);
+            };
+            for (uint32_t k = 0; k < nb; ++k) {
+                Rule* r = x.batch[x.la + k];
+                const ExpHdr h = x.h_hdr[k];
+                const uint32_t nrec = r->dropped || r->res < 0 ? 0u : uint32_t(res_pool[size_t(r->res)].recs.size());
+                const uint32_t hd[3] = {h.nsid, h.nent, nrec};
+                put(hd, sizeof(hd));
+                if (nrec) put(res_pool[size_t(r->res)].recs.data(), nrec * sizeof(ExpRec));
+            }
+            std::vector<size_t> sizes;
+            const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s, &agr);
+            // the ranks' blobs hold their contiguous slot ranges, in rank and slot order
+            size_t at = 0;
+            uint32_t k = 0;
+            for (int q = 0; q < R; ++q) {
+                const size_t end = at + sizes[size_t(q)];
+                for (; k < x.batch.size() && at < end; ++k) {
+                    uint32_t hd[3];
+                    std::memcpy(hd, all.data() + at, sizeof(hd));
+                    at += sizeof(hd);
+                    Rule* r = x.batch[k];
+                    if (q != comm->rank()) {
+                        exp_domain += hd[0];
+                        exp_entries += hd[1];
+                        r->inset = -1;
+                        if (!r->dropped) {
+                            ExpResult& res = res_get(r);
+                            res.recs.resize(hd[2]);
+                            if (hd[2]) std::memcpy(res.recs.data(), all.data() + at, hd[2] * sizeof(ExpRec));
+                        }
+                    }
+                    at += size_t(hd[2]) * sizeof(ExpRec);
+                }
+            }
+            if (at != all.size()) throw Error(FSM_EDEVICE, "TSR: sharded expansion results out of step");
+        }
         seg[2].bytes += int64_t(nout_all * sizeof(ExpRec));
         x.timed = false;
         spec_todo.emplace_back(std::move(x.batch), x.depth);
@@ -1724,12 +1777,30 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         }
         ExpSet& x = *xp;
         const double tl0 = now_ms();
-        const uint32_t nb = uint32_t(batch.size());
         x.batch = batch;
         x.depth = depth;
         x.seq = seq_next++;
-        gpu_rules += nb;
         for (Rule* r : batch) r->inset = int8_t(xp - xs);
+        // slot sharding: this rank expands only its contiguous share of the batch, split so
+        // that the shares' expected domains (about twice each rule's support) are equal
+        x.la = 0;
+        x.lz = uint32_t(batch.size());
+        if (shard_exp) {
+            uint64_t tot = 0;
+            for (Rule* r : batch) tot += 2ull * r->sup + 1;
+            const uint64_t lo = tot * uint64_t(comm->rank()) / uint64_t(R), hi = tot * uint64_t(comm->rank() + 1) / uint64_t(R);
+            uint64_t acc = 0;
+            x.la = x.lz = uint32_t(batch.size());
+            for (uint32_t k = 0; k < batch.size(); ++k) {  // slot k belongs to the rank whose range holds its start
+                if (acc >= lo && x.la == batch.size()) x.la = k;
+                if (acc >= hi) { x.lz = k; break; }
+                acc += 2ull * batch[k]->sup + 1;
+            }
+            if (x.lz < x.la) x.lz = x.la;
+        }
+        const uint32_t nb = x.lz - x.la;  // slots launched here
+        const Rule* const* bp = batch.data() + x.la;
+        gpu_rules += nb;
         // descriptors written in place into the set's pinned stage (only the used items:
         // the kernels read X[0, nx) and Y[0, ny))
         uint64_t* drv_off = x.h_drv;
@@ -1737,7 +1808,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         drv_off[0] = wave_off[0] = 0;
         x.drv_in_x.assign(nb, 1);
         for (uint32_t k = 0; k < nb; ++k) {
-            const Rule* r = batch[k];
+            const Rule* r = bp[k];
             const uint32_t *rx = rp.st.X(r), *ry = rp.st.Y(r);
             Side& sd = x.h_sides[k];
             sd.nx = r->nx;
@@ -1787,56 +1858,58 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         hipStream_t s = x.st;  // (shadows the context stream for this launch)
         FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, 2 * kOffB + size_t(nb) * sizeof(Side), hipMemcpyHostToDevice,
                                s));
-        x.timed = (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
+        x.timed = nb && (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
         const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
-        if (use_bm && x.alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
-            hipLaunchKernelGGL(k_alive, dim3(unsigned(((K + 15) / 16 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               d_ksup.as<uint32_t>(), K, rp.minsup, x.alive.as<uint32_t>());
-            FSM_LAUNCHED("k_alive", s);
-            x.alive_t = rp.minsup;
-        }
-        if (x.timed) FSM_HIP(hipEventRecord(x.ev[0], s));
-        if (use_bm) {
-            hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads), 0, s,
-                               x.d_sides, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), x.d_drv,
-                               x.dom.as<uint2>(), x.ctl.as<ExpCtl>());
-            FSM_LAUNCHED("k_exp_domain", s);
-            if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
-            hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
-                               x.d_wave, nb, x.d_drv, x.dom.as<uint2>(), k_ent.as<uint2>(), d_kidof.as<uint32_t>(),
-                               x.alive.as<uint32_t>(), geo, x.part.as<uint32_t>(), x.ctl.as<ExpCtl>(),
-                               x.d_ndlw.as<uint32_t>());
-            FSM_LAUNCHED("k_exp_rows", s);
-            if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
-            hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
-                               x.d_wave, geo, d_kept.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_rec, ecap,
-                               x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>(), x.d_rcnt);
-            FSM_LAUNCHED("k_expand_reduce", s);
-            if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
-            hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
-                               d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), x.d_dlw.as<uint4>(),
-                               x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
-            FSM_LAUNCHED("k_dl", s);
-        } else {
-            const uint64_t waves = wave_off[nb];
-            if (waves) {
-                hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                                   x.d_sides, x.d_drv, x.d_wave, nb,
-                                   d->vert_sid.as<uint32_t>(), k_off.as<uint32_t>(), k_item.as<uint32_t>(),
-                                   k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, x.TL.as<uint32_t>(),
-                                   x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(),
-                                   x.list.as<uint32_t>(), x.ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
-                FSM_LAUNCHED("k_expand", s);
+        if (nb) {  // (a rank may get no slot of a small sharded batch)
+            if (use_bm && x.alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
+                hipLaunchKernelGGL(k_alive, dim3(unsigned(((K + 15) / 16 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                                   d_ksup.as<uint32_t>(), K, rp.minsup, x.alive.as<uint32_t>());
+                FSM_LAUNCHED("k_alive", s);
+                x.alive_t = rp.minsup;
             }
-            if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
-            if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
-            hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, x.TL.as<uint32_t>(),
-                               x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
-                               x.ctl.as<ExpCtl>(), U, rp.minsup, x.d_rec, ecap);
-            FSM_LAUNCHED("k_expand_collect", s);
-            if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
-            hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
-            FSM_LAUNCHED("k_publish", s);
+            if (x.timed) FSM_HIP(hipEventRecord(x.ev[0], s));
+            if (use_bm) {
+                hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads), 0, s,
+                                   x.d_sides, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), x.d_drv,
+                                   x.dom.as<uint2>(), x.ctl.as<ExpCtl>());
+                FSM_LAUNCHED("k_exp_domain", s);
+                if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
+                hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
+                                   x.d_wave, nb, x.d_drv, x.dom.as<uint2>(), k_ent.as<uint2>(), d_kidof.as<uint32_t>(),
+                                   x.alive.as<uint32_t>(), geo, x.part.as<uint32_t>(), x.ctl.as<ExpCtl>(),
+                                   x.d_ndlw.as<uint32_t>());
+                FSM_LAUNCHED("k_exp_rows", s);
+                if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
+                hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
+                                   x.d_wave, geo, d_kept.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_rec, ecap,
+                                   x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>(), x.d_rcnt);
+                FSM_LAUNCHED("k_expand_reduce", s);
+                if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
+                hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
+                                   d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), x.d_dlw.as<uint4>(),
+                                   x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
+                FSM_LAUNCHED("k_dl", s);
+            } else {
+                const uint64_t waves = wave_off[nb];
+                if (waves) {
+                    hipLaunchKernelGGL(k_expand, dim3(unsigned((waves * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                                       x.d_sides, x.d_drv, x.d_wave, nb,
+                                       d->vert_sid.as<uint32_t>(), k_off.as<uint32_t>(), k_item.as<uint32_t>(),
+                                       k_first.as<uint32_t>(), k_last.as<uint32_t>(), U, x.TL.as<uint32_t>(),
+                                       x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(),
+                                       x.list.as<uint32_t>(), x.ctl.as<ExpCtl>(), d_sup.as<uint32_t>(), rp.minsup);
+                    FSM_LAUNCHED("k_expand", s);
+                }
+                if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
+                if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
+                hipLaunchKernelGGL(k_expand_collect, dim3(grid.collect, nb), dim3(kBlock), 0, s, x.TL.as<uint32_t>(),
+                                   x.DL.as<uint32_t>(), x.TR.as<uint32_t>(), x.seen.as<uint32_t>(), x.list.as<uint32_t>(),
+                                   x.ctl.as<ExpCtl>(), U, rp.minsup, x.d_rec, ecap);
+                FSM_LAUNCHED("k_expand_collect", s);
+                if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
+                hipLaunchKernelGGL(k_publish, dim3(1), dim3(kBlock), 0, s, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
+                FSM_LAUNCHED("k_publish", s);
+            }
         }
         if (x.timed) FSM_HIP(hipEventRecord(x.ev[4], s));
         FSM_HIP(hipEventRecord(x.ev[5], s));

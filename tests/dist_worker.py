@@ -64,7 +64,22 @@ def main():
             csr, meta = eng.spade_csr(db, sup)
             st = eng.stats()
             db.free()
-        res.update(digest=pattern_digest(*csr), minsup=meta["minsup"], joins=st["joins"])
+        res.update(digest=pattern_digest(*csr), minsup=meta["minsup"], joins=st["joins"],
+                   rank_root_slab=st["rank_root_slab"], rank_root_owned=st["rank_root_owned"],
+                   rank_claims=st["rank_claims"], root_entries=st["root_entries"])
+    elif mode == "tsr_digest":
+        # sharded TSR at the c4 prefix: digest of the rule set, slots expanded here
+        from digest import rule_digest
+        from tools import gen
+        D, k, mc = int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5])
+        ds = gen.kosarak(D=990002, seed=1).head(D)
+        with fsm.Engine(0, nranks=world, rank=rank, host_comm=hc) as eng:
+            db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
+            rules, meta = eng.tsr(db, k, mc)
+            st = eng.stats()
+            db.free()
+        res.update(digest=rule_digest(rules), final_minsup=meta["final_minsup"], units=st["rank_units"],
+                   units_total=st["expansions"])
     elif mode == "tsr":
         # TSR on a Kosarak-shaped DB: pair phase sharded by sequence range (candidate keys
         # exchanged, partial counts summed), expansions on every rank alike

@@ -119,18 +119,42 @@ def test_tsr_c4_fullsize_complete(eng):
     assert not missing, missing[:5]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_tsr_c4_prefix_sharded(world, tmp_path):
+    """Sharded TSR at the c4 20,000-sequence prefix over `world` gloo ranks on this
+    GPU: the pair phase by sequence range and every expansion launch's rule slots
+    split over the ranks (results all-gathered per launch, replay replicated) give
+    the exact prefix digest and final minsup on every rank."""
+    from test_dist import run_ranks
+    if "c4-prefix" not in FULL:
+        pytest.skip("fixture not generated")
+    exp = FULL["c4-prefix"]
+    res = run_ranks(world, ["tsr_digest", str(exp["sequences"]), str(exp["k"]), str(exp["minconf"])], tmp_path,
+                    timeout=110)
+    for r in res:
+        assert r["digest"] == exp["digest"] and r["final_minsup"] == exp["final_minsup"]
+    tot = sum(r["units"] for r in res)
+    assert all(0 < r["units"] < tot for r in res)  # every rank expanded a share of the slots
+
+
 @pytest.mark.parametrize("name,world", [("c3", 2), ("c5-bible", 3)])
 def test_spade_fullsize_sharded(name, world, tmp_path):
-    """The sharded path (F1 all-reduce, root counter rows by rank slice,
-    frequent pairs all-gathered, first-level classes by the LPT plan, patterns
-    all-gathered) at full BASELINE size, `world` ranks on this GPU over gloo
-    host collectives: every rank returns the complete pattern set."""
+    """The sharded path (F1 all-reduce, DB-direct root with the counter rows by rank
+    slice, frequent pairs all-gathered, first-level classes claimed from the shared
+    work-stealing counter, patterns all-gathered) at full BASELINE size, `world`
+    ranks on this GPU over gloo host collectives: every rank returns the complete
+    pattern set, and no rank joins root entries of classes it did not claim."""
     from test_dist import run_ranks
     exp = FULL[name]
     shape, D = SPADE_CFG[name]
     res = run_ranks(world, ["spade_digest", shape, str(D or 0), str(exp["support"])], tmp_path, timeout=110)
     for r in res:
         assert r["digest"] == exp["digest"] and r["joins"] == exp["joins"] and r["minsup"] == exp["minsup"]
+        assert r["rank_root_slab"] == 0  # DB-direct root: no rank writes root entries
+    # the ranks' owned root entries partition the root (F2 slices + claimed classes: each
+    # root entry joined as the owner at most twice, once per phase, by exactly one rank)
+    assert sum(r["rank_root_owned"] for r in res) <= 2 * res[0]["root_entries"]
+    assert sum(r["rank_claims"] for r in res) >= 1
 
 
 def test_bench_two_ranks_dry_run(tmp_path):
