@@ -38,7 +38,7 @@ for p in (ROOT, os.path.join(ROOT, "spark-fsm_amd")):
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
 PMC_FILE = "profiles/pmc_latest.json"  # tools/pmc_summary.py output of the committed rocprofv3 --pmc passes
-ROOT_F2_KERNELS = ("k_f2_plan", "k_f2_keys", "k_f2_count")
+ROOT_F2_KERNELS = ("k_f2_plan", "k_f2_keys", "k_f2_count", "k_f2_vert")
 
 
 def pmc_traffic(kernel):

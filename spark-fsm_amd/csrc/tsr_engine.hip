@@ -212,7 +212,9 @@ __global__ __launch_bounds__(kBlock) void k_pairs_gather(const uint32_t* __restr
 
 struct Side {
     uint32_t nx, ny, doL, doR;
-    uint32_t maxX, maxY, pad0, pad1;
+    uint32_t maxX, maxY;
+    uint32_t drv;    // bitmap path: the rarest item of X u Y
+    uint32_t lmode;  // bitmap path: 1 = the domain from drv's sid list (short) probed in the other bitmaps
     uint32_t X[kMaxSide];
     uint32_t Y[kMaxSide];
 };
@@ -511,11 +513,17 @@ __device__ __forceinline__ void bump(uint32_t c, uint32_t fl, uint32_t fX, uint3
 constexpr uint32_t kDomThreads = 256;
 constexpr uint32_t kDomWords = 4 * kDomThreads;  // bitmap words per domain block
 
+// List mode (Side::lmode, chosen on the host when the rarest item's sid list is shorter than
+// a quarter of a bitmap's words): the slot's blocks split that list, every sid is probed in
+// the other items' bitmaps (one 4-byte read each, L2-resident) and the survivors compacted
+// as above: |L| x |X u Y| probes instead of |X u Y| whole-bitmap operands.
 __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restrict__ sides,
                                                             const uint32_t* __restrict__ bm, uint32_t NW,
                                                             const uint32_t* __restrict__ row_off,
                                                             const uint64_t* __restrict__ dom_off,
-                                                            uint2* __restrict__ dom, ExpCtl* __restrict__ ctlb) {
+                                                            uint2* __restrict__ dom, ExpCtl* __restrict__ ctlb,
+                                                            const uint64_t* __restrict__ vert_off,
+                                                            const uint32_t* __restrict__ vert_sid) {
     __shared__ uint32_t sIt[2 * kMaxSide];
     __shared__ uint32_t wsum[kDomThreads / 64];
     __shared__ uint32_t b_base;
@@ -524,6 +532,44 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
     const uint32_t nxy = side.nx + side.ny;
     for (uint32_t q = threadIdx.x; q < nxy; q += blockDim.x) sIt[q] = q < side.nx ? side.X[q] : side.Y[q - side.nx];
     __syncthreads();
+    if (side.lmode) {
+        const uint32_t drv = side.drv;
+        const uint64_t l0 = vert_off[drv], l1 = vert_off[drv + 1];
+        const uint64_t per = (l1 - l0 + gridDim.x - 1) / gridDim.x;
+        const uint64_t a = l0 + per * blockIdx.x, z = min(l1, a + per);
+        uint2* out = dom + dom_off[k];
+        const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+        for (uint64_t r0 = a; r0 < z; r0 += blockDim.x) {  // block-uniform rounds
+            const uint64_t q = r0 + threadIdx.x;
+            bool keep = false;
+            uint32_t sid = 0;
+            if (q < z) {
+                sid = vert_sid[q];
+                keep = true;
+                for (uint32_t t = 0; t < nxy && keep; ++t) {
+                    const uint32_t it = sIt[t];
+                    if (it != drv) keep = (bm[uint64_t(it) * NW + (sid >> 5)] >> (sid & 31u)) & 1u;
+                }
+            }
+            const uint64_t bal = __ballot(keep);
+            if (lane == 0) wsum[wv] = uint32_t(__popcll(bal));
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t tot = 0;
+                for (uint32_t w = 0; w < kDomThreads / 64; ++w) tot += wsum[w];
+                b_base = tot ? atomicAdd(&ctlb[k].nsid, tot) : 0u;
+            }
+            __syncthreads();
+            if (keep) {
+                uint32_t p = b_base + uint32_t(__popcll(bal & lanemask_lt()));
+                for (uint32_t w = 0; w < wv; ++w) p += wsum[w];
+                const uint32_t rs = row_off[sid];
+                out[p] = make_uint2(rs, row_off[sid + 1] - rs);
+            }
+            __syncthreads();  // wsum / b_base are rewritten next round
+        }
+        return;
+    }
     const uint32_t w = blockIdx.x * kDomWords + 4 * threadIdx.x;  // NW is a multiple of 4
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (w < NW) {
@@ -1385,8 +1431,18 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         if (sup[c] >= rp.minsup) kept_items.push_back(c);
     const uint32_t K = uint32_t(kept_items.size());
     const uint64_t N = uint64_t(d->N);
-    // bitmap path: sid bitmaps built, K <= kMaxKids, itemset indexes < 2^16 (packed rows)
-    bool use_bm = d->bm.p != nullptr && K > 0 && K <= kMaxKids;
+    // bitmap path: sid bitmaps built, K <= kMaxKids, itemset indexes < 2^16 (packed rows);
+    // FSM_TSR_MAX_KIDS / FSM_TSR_MAX_POS lower both caps (test hooks: the list path, taken up
+    // front or after the rows were packed)
+    const uint32_t max_kids = [] {
+        const char* v = std::getenv("FSM_TSR_MAX_KIDS");
+        return v ? std::min<uint32_t>(uint32_t(std::strtoul(v, nullptr, 10)), kMaxKids) : kMaxKids;
+    }();
+    const uint32_t max_pos = [] {
+        const char* v = std::getenv("FSM_TSR_MAX_POS");
+        return v ? std::min<uint32_t>(uint32_t(std::strtoul(v, nullptr, 10)), 0xFFFFu) : 0xFFFFu;
+    }();
+    bool use_bm = d->bm.p != nullptr && K > 0 && K <= max_kids;
     DevBuf k_off, k_item, k_first, k_last, k_sup;  // list path rows (SoA)
     DevBuf k_ent, d_kidof, d_kept, d_ksup;  // bitmap path rows (packed) and kid tables
     uint64_t E2 = 0;
@@ -1417,7 +1473,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         FSM_HIP(hipMemcpyAsync(&E2, off64.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(&maxpos, mpos.p, 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipStreamSynchronize(s));
-        if (maxpos > 0xFFFFu || E2 >= kNone) {
+        if (maxpos > max_pos || E2 >= kNone) {
             use_bm = false;  // an itemset index past 2^16: the list path takes it
         } else {
             k_off.alloc((N + 1) * 4);
@@ -1514,6 +1570,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // Sharded TSR (nranks > 1, bitmap path): each launch's rule slots are split over the
     // ranks and the slots' results all-gathered once per launch (finish); the replay
     // stays replicated and deterministic.  FSM_TSR_SHARD=0 replicates the expansions.
+    // FSM_TSR_DOMAIN=bitmap keeps every domain on the whole-bitmap AND (tests, A/B)
+    const int dom_mode = [] {  // 0 auto (by the rarest item's list length), 1 every slot bitmap, 2 every slot list
+        const char* v = std::getenv("FSM_TSR_DOMAIN");
+        return !v ? 0 : (!std::strcmp(v, "bitmap") ? 1 : (!std::strcmp(v, "list") ? 2 : 0));
+    }();
     const bool shard_exp = shard && use_bm && [] {
         const char* v = std::getenv("FSM_TSR_SHARD");
         return !(v && v[0] == '0');
@@ -1825,10 +1886,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 // domain list holds at most the support of the rarest item of X u Y
                 wave_off[k + 1] = wave_off[k] + std::clamp<uint64_t>((2ull * r->sup + exp_spb - 1) / exp_spb, 1,
                                                                      grid.expand);
-                uint32_t cap = kNone;
-                for (uint32_t q = 0; q < r->nx; ++q) cap = std::min(cap, sup[rx[q]]);
-                for (uint32_t q = 0; q < r->ny; ++q) cap = std::min(cap, sup[ry[q]]);
+                uint32_t cap = kNone, drv = rx[0];
+                for (uint32_t q = 0; q < r->nx; ++q) if (sup[rx[q]] < cap) { cap = sup[rx[q]]; drv = rx[q]; }
+                for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < cap) { cap = sup[ry[q]]; drv = ry[q]; }
                 drv_off[k + 1] = drv_off[k] + cap;
+                sd.drv = drv;
+                sd.lmode = dom_mode == 2 || (dom_mode == 0 && uint64_t(cap) * 4 < d->NW) ? 1u : 0u;
             } else {
                 // list path: one wave per sid of the driver list: the rarest item of X
                 // (expandL needs all of sids(X)), else of X u Y
@@ -1871,7 +1934,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (use_bm) {
                 hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads), 0, s,
                                    x.d_sides, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), x.d_drv,
-                                   x.dom.as<uint2>(), x.ctl.as<ExpCtl>());
+                                   x.dom.as<uint2>(), x.ctl.as<ExpCtl>(), d->vert_off.as<uint64_t>(),
+                                   d->vert_sid.as<uint32_t>());
                 FSM_LAUNCHED("k_exp_domain", s);
                 if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
                 hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,

@@ -360,15 +360,21 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic", "passes-3", "passes-64"])
+@pytest.mark.parametrize("path", ["vert", "group", "group-few-blocks", "atomic", "passes-3", "passes-64",
+                                  "slab-root", "slab-root-keys"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
-    """The root F2 implementations (key runs counted per rank group, at the
-    default and at a small block chunk, in several passes over group ranges;
-    global atomics) give the oracle's patterns and joins."""
+    """The root F2 implementations (the default vertical count from the DB's item
+    lists; key runs counted per rank group, at the default and at a small block
+    chunk, in several passes over group ranges; global atomics; the DB-direct root
+    or the root slab) give the oracle's patterns and joins."""
     from oracle import oracle
     from tools import gen
     if path == "atomic":
         monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
+    if path.startswith("group") or path.startswith("passes") or path == "slab-root-keys":
+        monkeypatch.setenv("FSM_F2_PATH", "keys")
+    if path.startswith("slab-root"):
+        monkeypatch.setenv("FSM_ROOT_DB", "0")
     if path == "group-few-blocks":
         monkeypatch.setenv("FSM_F2_BLOCKS", "3")
     if path.startswith("passes"):
@@ -602,18 +608,28 @@ def test_sharded_tsr_failure_reaches_every_rank(tmp_path, monkeypatch):
     assert "injected" in res[1]["msg"] and "peer rank failed" in res[0]["msg"]
 
 
-@pytest.mark.parametrize("bitmap", ["1", "0", "passes"])
+@pytest.mark.parametrize("bitmap", ["1", "0", "passes", "domain-bitmap", "domain-list", "max-kids", "max-pos"])
 def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
-    """TSR expansions over sid bitmaps (default; "passes": the LDS histograms
-    cover 37 kids per pass, so every expansion runs several kid passes) and
-    over the driver item's sid list (FSM_TSR_BITMAP=0, the over-budget
-    fallback) give the oracle's rules."""
+    """TSR expansions over sid bitmaps (default: each slot's domain from the
+    whole-bitmap AND or, for a rare item, from its sid list probed in the other
+    bitmaps; domain-bitmap / domain-list force either for every slot; "passes":
+    the LDS histograms cover 37 kids per pass, so every expansion runs several kid
+    passes) and over the driver item's sid list (FSM_TSR_BITMAP=0, the over-budget
+    fallback; max-kids: taken up front because the kept items exceed the cap;
+    max-pos: taken after the rows were packed because an itemset index exceeds the
+    cap) give the oracle's rules."""
     from oracle import oracle
     from tools import gen
     from spark_fsm_amd import MODE_TSR
     monkeypatch.setenv("FSM_TSR_BITMAP", "0" if bitmap == "0" else "1")
     if bitmap == "passes":
         monkeypatch.setenv("FSM_TSR_PASS_KIDS", "37")
+    if bitmap.startswith("domain-"):
+        monkeypatch.setenv("FSM_TSR_DOMAIN", bitmap.split("-")[1])
+    if bitmap == "max-kids":
+        monkeypatch.setenv("FSM_TSR_MAX_KIDS", "10")
+    if bitmap == "max-pos":
+        monkeypatch.setenv("FSM_TSR_MAX_POS", "3")
     ds = gen.kosarak(D=6000, seed=3)
     o = oracle.tsr(ds.records(), 300, 0.4)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)  # bitmaps are built at upload

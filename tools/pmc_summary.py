@@ -26,8 +26,10 @@ def kernel_name(demangled):
         return "k_emit<write>" if "true" in targs else "k_emit<count>"
     if base in ("k_emit1", "k_emit2"):  # the emit kernels: fsm_get_kernel_stats times them as "k_emit"
         return "k_emit"
-    if base == "k_count2":  # the window count: timed as "k_count"
+    if base in ("k_count2", "k_sparse_keys"):  # the window / sparse counts: timed as "k_count"
         return "k_count"
+    if base == "k_f2_plan_db":  # the DB-direct root's F2 plan: timed as "k_f2_plan"
+        return "k_f2_plan"
     return base
 
 
