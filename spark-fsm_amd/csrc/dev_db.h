@@ -19,10 +19,6 @@ struct SpadeDevDB {
     // -1 = a row exceeds 65535 entries (that DB keeps the root slab)
     fsm::DevBuf pos;      // u32 [E]
     int pos_state = 0;
-    // the vertical root F2 (W = 1): every dense item's DB entries (any order), made once
-    fsm::DevBuf vert_off;  // u64 [U+1]
-    fsm::DevBuf vert_ent;  // u32 [E]
-    bool vert_made = false;
 };
 
 // TSR: horizontal rows (sid = row) of (item, first, last itemset index),

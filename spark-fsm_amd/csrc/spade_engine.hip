@@ -611,9 +611,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
                                                           uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
                                                           uint32_t mhi, uint32_t* __restrict__ cap,
                                                           unsigned long long* __restrict__ nroot,
-                                                          uint32_t* __restrict__ mem_out,
-                                                          const uint64_t* __restrict__ mask,
-                                                          uint32_t* __restrict__ cv_out) {
+                                                          uint32_t* __restrict__ mem_out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     __shared__ uint32_t blk_root;
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
@@ -630,14 +628,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
         for (uint32_t b0 = rb; b0 < e1; b0 += 64) {
             const uint32_t e = b0 + lane;
             const uint32_t v = e < e1 ? rk2[item[e]] : kNone;
-            if (e < e1) {
-                mem_out[e] = v;  // the entries' member ids, read by the F2 keys and the root emit
-                if (cv_out) {    // (W = 1) rank | first eid | last eid, read by the vertical F2
-                    const uint64_t m = mask[e];
-                    cv_out[e] = ((v & 1u) ? 0xFFFF0000u : ((v >> 1) << 16)) | (uint32_t(__builtin_ctzll(m)) << 8) |
-                                (63u - uint32_t(__builtin_clzll(m)));
-                }
-            }
+            if (e < e1) mem_out[e] = v;  // the entries' member ids, read by the F2 keys and the root emit
             if (b0 == rb) v0 = v;
             len += uint32_t(__popcll(__ballot(e < e1 && !(v & 1u))));
         }
@@ -649,14 +640,13 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
             const bool fr = e < e1 && !(v & 1u);
             const uint64_t bal = __ballot(fr);
             const uint32_t p = k + uint32_t(__popcll(bal & lt));
-            if (cap && fr && v - mlo < mhi - mlo) atomicAdd(&h[group_of(v >> 1, pm)], 2 * len - 1 - p);
+            if (fr && v - mlo < mhi - mlo) atomicAdd(&h[group_of(v >> 1, pm)], 2 * len - 1 - p);
             k += uint32_t(__popcll(bal));
         }
     }
     if (lane == 0) atomicAdd(&blk_root, my_root);
     __syncthreads();
-    if (cap)
-        for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + 7u) & ~7u;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + 7u) & ~7u;
     if (threadIdx.x == 0 && blk_root) atomicAdd(nroot, (unsigned long long)blk_root);
 }
 
@@ -928,125 +918,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
             at = rfl(at) + uint32_t(__popcll(fb & lanemask_lt()));
             if (fr && at < cap) recs[at] = FreqRec{row, c, val, 0u};
         }
-    }
-}
-
-// ---- Vertical root F2 (W = 1, DB-direct root): no key round trip through HBM.  The
-// block of rank group g counts the pairs of its own counter rows x in LDS straight
-// from the DB: for every entry of x (the DB's vertical list of x's item, built once
-// per DB) it walks that entry's row.  The (entry of x, partner) pairs of a wave's 64
-// list entries are flattened over the lanes in entry order (owner by a 6-step
-// shuffle search), each partner read as one packed word cv = rank << 16 | first eid
-// << 8 | last eid (0xFFFF rank: an infrequent item; written by the F2 plan), its
-// mask only for an equality candidate whose eid range meets x's.  The rows (4 B per
-// entry, about 100 MB at D1M) stay on-die: the root F2 writes and reads no keys.
-// The frequent pairs are balloted out of the group's tile as in k_f2_count.
-__global__ __launch_bounds__(kF2Threads) void k_f2_vert(const uint32_t* __restrict__ freq_item,
-                                                       const uint64_t* __restrict__ voff,
-                                                       const uint32_t* __restrict__ vent,
-                                                       const uint32_t* __restrict__ pos,
-                                                       const uint32_t* __restrict__ cv,
-                                                       const uint64_t* __restrict__ mask, uint32_t D, uint32_t per,
-                                                       uint32_t g0, uint32_t rlo, uint32_t rhi, uint32_t minsup,
-                                                       FreqRec* __restrict__ recs, uint32_t cap,
-                                                       uint32_t* __restrict__ nrec,
-                                                       unsigned long long* __restrict__ nkeys) {
-    __shared__ uint32_t h[kGroupCounters];
-    __shared__ uint32_t blk_keys;
-    const uint32_t g = g0 + blockIdx.x;
-    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    for (uint32_t t = threadIdx.x; t < per * D; t += blockDim.x) h[t] = 0;
-    if (threadIdx.x == 0) blk_keys = 0;
-    __syncthreads();
-    const uint32_t ra = max(g * per, rlo), rz = min((g + 1) * per, rhi);
-    uint32_t my_keys = 0;
-    for (uint32_t x = ra; x < rz; ++x) {
-        const uint32_t it = freq_item[x];
-        const uint64_t l0 = voff[it], l1 = voff[it + 1];
-        uint32_t* hx = h + (x - g * per) * D;
-        for (uint64_t c0 = l0 + uint64_t(wave) * 64; c0 < l1; c0 += uint64_t(kF2Waves) * 64) {
-            // this lane's entry of x: its row [rb, rb + rl) and first eid
-            const uint64_t q = c0 + lane;
-            uint32_t e = 0, rb = 0, rl = 0, lo = 0, hi = 0;
-            uint64_t mk = 0;
-            if (q < l1) {
-                e = vent[q];
-                const uint32_t p = pos[e];
-                rb = e - (p >> 16);
-                rl = p & 0xFFFFu;
-                const uint32_t w = cv[e];
-                lo = (w >> 8) & 0xFFu;
-                hi = w & 0xFFu;
-                mk = mask[e];
-            }
-            const uint32_t incl = wave_incl_scan(rl), excl = incl - rl;
-            const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
-            for (uint32_t p0 = 0; p0 < total; p0 += 64) {
-                const uint32_t pp = p0 + lane;
-                uint32_t ow = 0;  // the owner lane: the largest lane whose first pair index <= pp
-#pragma unroll
-                for (uint32_t stp = 32; stp > 0; stp >>= 1) {
-                    const uint32_t cand = ow + stp;
-                    if (uint32_t(__shfl(int(excl), int(cand), 64)) <= pp) ow = cand;
-                }
-                const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
-                const uint32_t o_rb = uint32_t(__shfl(int(rb), int(ow), 64));
-                const uint32_t o_e = uint32_t(__shfl(int(e), int(ow), 64));
-                const uint32_t o_lo = uint32_t(__shfl(int(lo), int(ow), 64));
-                const uint32_t o_hi = uint32_t(__shfl(int(hi), int(ow), 64));
-                const uint64_t o_mk = __shfl(mk, int(ow), 64);
-                if (pp < total) {
-                    const uint32_t j = o_rb + (pp - o_ex);
-                    const uint32_t w = cv[j];
-                    const uint32_t rj = w >> 16, lj = (w >> 8) & 0xFFu, hj = w & 0xFFu;
-                    if (rj != 0xFFFFu) {
-                        // x -> y: bits of L(y) after the first bit of L(x)
-                        if (hj > o_lo) {
-                            atomicAdd(&hx[rj << 1], 1u);
-                            ++my_keys;
-                        }
-                        // (x y), y > x: L(x) & L(y) (only when the eid ranges meet)
-                        if (j > o_e && lj <= o_hi && o_lo <= hj && (mask[j] & o_mk) != 0ull) {
-                            atomicAdd(&hx[(rj << 1) | 1u], 1u);
-                            ++my_keys;
-                        }
-                    }
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) my_keys += uint32_t(__shfl_xor(int(my_keys), d, 64));
-    if (lane == 0 && my_keys) atomicAdd(&blk_keys, my_keys);
-    __syncthreads();
-    for (uint32_t row = ra; row < rz; ++row) {
-        const uint32_t* hr = h + (row - g * per) * D;
-        for (uint32_t cc = wave * 64; cc < D; cc += kF2Threads) {
-            const uint32_t c = cc + lane;
-            const uint32_t val = c < D ? hr[c] : 0u;
-            const bool fr = c < D && val >= minsup;
-            const uint64_t fb = __ballot(fr);
-            if (!fb) continue;
-            uint32_t at = 0;
-            if (lane == 0) at = atomicAdd(nrec, uint32_t(__popcll(fb)));
-            at = rfl(at) + uint32_t(__popcll(fb & lanemask_lt()));
-            if (fr && at < cap) recs[at] = FreqRec{row, c, val, 0u};
-        }
-    }
-    if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys, (unsigned long long)blk_keys);
-}
-
-// the DB's vertical lists (once per DB): entries of every dense item, any order within an item
-__global__ __launch_bounds__(kBlock) void k_db_vhist(const uint32_t* __restrict__ item, uint32_t E,
-                                                     uint32_t* __restrict__ cnt) {
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) atomicAdd(&cnt[item[e]], 1u);
-}
-__global__ __launch_bounds__(kBlock) void k_db_vscatter(const uint32_t* __restrict__ item, uint32_t E,
-                                                        const uint64_t* __restrict__ voff,
-                                                        uint32_t* __restrict__ cur, uint32_t* __restrict__ vent) {
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
-        const uint32_t it = item[e];
-        vent[voff[it] + atomicAdd(&cur[it], 1u)] = e;
     }
 }
 
@@ -2032,8 +1903,6 @@ struct Batch {
     bool db_direct = false;
     DevBuf rk2;
     DevBuf mem_db;  // u32 [DB entries]: each DB entry's member id rk2[item] (written by the F2 plan)
-    bool f2_vert = false;  // the vertical root F2 (k_f2_vert) runs: cv below, no key plan
-    DevBuf cv;             // u32 [DB entries]: rank << 16 | first eid << 8 | last eid (W = 1)
     // sharded root with work stealing: children [0, nshared_children) are the
     // heavy classes every rank mines; the rest, largest first, are claimed in ranges from the
     // shared counter claim_key (-1: no claims; groups fixed)
@@ -2070,8 +1939,6 @@ struct Batch {
         db_direct = false;
         rk2.release();
         mem_db.release();
-        f2_vert = false;
-        cv.release();
         claim_key = -1;
         nshared_children = 0;
         claims_done = false;
@@ -2536,52 +2403,6 @@ struct Miner {
         return g;
     }
 
-    // the vertical root F2 (k_f2_vert, W = 1 DB-direct root): one block per rank group of
-    // this rank's slice counts its rows' pairs in LDS from the DB's vertical lists
-    bool root_f2_vert(Batch& b, std::vector<FreqRec>& recs, const F2Geo& geo, uint32_t rlo, uint32_t rhi) {
-        const uint32_t D = geo.D, F = geo.F, per = geo.per;
-        const uint32_t g0 = rlo / per, g1 = rhi == 0 ? 0u : (rhi - 1) / per + 1;
-        DevBuf d_freq;
-        upload(d_freq, std::vector<uint32_t>(b.rank_item.begin(), b.rank_item.end()));
-        uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * D, uint64_t(1) << 20));
-        DevBuf d_nrec(4), nk(8), d_recs;
-        unsigned long long nkeys = 0;
-        for (int attempt = 0;; ++attempt) {
-            d_recs.alloc(std::max<uint32_t>(cap_recs, 1) * sizeof(FreqRec));
-            FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
-            FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
-            const size_t tk = clk->begin("k_f2_vert");
-            if (g1 > g0)
-                hipLaunchKernelGGL(k_f2_vert, dim3(g1 - g0), dim3(kF2Threads), 0, s, d_freq.as<uint32_t>(),
-                                   db->vert_off.as<uint64_t>(), db->vert_ent.as<uint32_t>(), db->pos.as<uint32_t>(),
-                                   b.cv.as<uint32_t>(), db->mask.as<uint64_t>(), D, per, g0, rlo, rhi, minsup,
-                                   d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), nk.as<unsigned long long>());
-            FSM_LAUNCHED("k_f2_vert", s);
-            // the owned entries' list slots, packed words and masks + one packed word per partner
-            clk->end(tk, int64_t(b.cls[0].cap) * 20, attempt == 0 ? int64_t(b.cls[0].cap) * 8 : 0);
-            uint32_t nrec = 0;
-            FSM_HIP(hipMemcpyAsync(&nrec, d_nrec.p, 4, hipMemcpyDeviceToHost, s));
-            FSM_HIP(hipMemcpyAsync(&nkeys, nk.p, 8, hipMemcpyDeviceToHost, s));
-            sync();
-            clk->add_bytes(tk, int64_t(nkeys) * 4);
-            if (nrec <= cap_recs || attempt > 0) {
-                if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
-                recs.resize(nrec);
-                if (nrec)
-                    FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, size_t(nrec) * sizeof(FreqRec), hipMemcpyDeviceToHost,
-                                           s));
-                sync();
-                break;
-            }
-            cap_recs = nrec;  // rare: more frequent pairs than the first buffer held; count again
-        }
-        ctx->stats.root_keys += int64_t(nkeys);
-        const double th0 = now_ms();
-        order_recs(recs, F);
-        hp[0] += now_ms() - th0;
-        return true;
-    }
-
     bool root_f2(Batch& b, std::vector<FreqRec>& recs) {
         const ClassMeta& m = b.cls[0];
         if (b.root_rows.p == nullptr && !b.db_direct) return false;
@@ -2593,7 +2414,6 @@ struct Miner {
         const uint64_t nd = geo.nd;
         const SlabPtrs sp = b.slab.ptrs();
         const int64_t E0 = int64_t(m.cap);
-        if (b.f2_vert) return root_f2_vert(b, recs, geo, rlo, rhi);
         if (!b.f2_planned) return false;  // the plan is made while the root rows are written
         DevBuf base = std::move(b.f2_base), fill(nd * 4);
         const uint64_t nslots = b.f2_nslots;
@@ -3531,36 +3351,6 @@ struct Miner {
         return db->pos_state > 0;
     }
 
-    // FSM_F2_PATH=keys keeps the key-stream root F2 (k_f2_keys + k_f2_count) at W = 1 (tests, A/B;
-    // default: the vertical k_f2_vert)
-    static bool f2_vert_env() {
-        const char* v = std::getenv("FSM_F2_PATH");
-        return !(v && !std::strcmp(v, "keys"));
-    }
-    // the DB's vertical lists (once per DB): counts, scan, scatter
-    void ensure_db_vert() {
-        if (db->vert_made) return;
-        const uint32_t U = uint32_t(db->U), E = uint32_t(db->E);
-        DevBuf cnt(std::max<uint32_t>(U, 1) * 4), cur(std::max<uint32_t>(U, 1) * 4);
-        db->vert_off.alloc((size_t(U) + 1) * 8);
-        db->vert_ent.alloc(std::max<uint32_t>(E, 1) * 4);
-        FSM_HIP(hipMemsetAsync(cnt.p, 0, size_t(U) * 4, s));
-        FSM_HIP(hipMemsetAsync(cur.p, 0, size_t(U) * 4, s));
-        const unsigned grid = unsigned(std::min<uint64_t>((uint64_t(E) + kBlock - 1) / kBlock, 8192));
-        if (E) {
-            hipLaunchKernelGGL(k_db_vhist, dim3(grid), dim3(kBlock), 0, s, db->item.as<uint32_t>(), E, cnt.as<uint32_t>());
-            FSM_LAUNCHED("k_db_vhist", s);
-        }
-        scan_exclusive(cnt.as<uint32_t>(), db->vert_off.as<uint64_t>(), U, s);
-        if (E) {
-            hipLaunchKernelGGL(k_db_vscatter, dim3(grid), dim3(kBlock), 0, s, db->item.as<uint32_t>(), E,
-                               db->vert_off.as<uint64_t>(), cur.as<uint32_t>(), db->vert_ent.as<uint32_t>());
-            FSM_LAUNCHED("k_db_vscatter", s);
-        }
-        sync();
-        db->vert_made = true;
-    }
-
     // The DB-direct root: no root slab.  The F2 plan (key capacities per rank group and row
     // block, and the root entry count) is made from the DB rows; the F2 keys and the root
     // emit read the same rows.  Returns false (nothing launched that matters) when the
@@ -3588,29 +3378,19 @@ struct Miner {
         }
         upload(root.rk2, rk2);
         root.mem_db.alloc(std::max<int64_t>(db->E, 1) * 4);
-        // W = 1: the vertical F2 (no key plan; the plan pass writes the packed cv words)
-        root.f2_vert = W == 1 && f2_vert_env();
-        if (root.f2_vert) {
-            ensure_db_vert();
-            root.cv.alloc(std::max<int64_t>(db->E, 1) * 4);
-        }
-        DevBuf cap(root.f2_vert ? 4 : geo.nd * 4), nroot(8);
-        if (!root.f2_vert) root.f2_base.alloc((geo.nd + 1) * 8);
+        DevBuf cap(geo.nd * 4), nroot(8);
+        root.f2_base.alloc((geo.nd + 1) * 8);
         FSM_HIP(hipMemsetAsync(nroot.p, 0, 8, s));
         const size_t tk = clk->begin("k_f2_plan");
-        hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), root.f2_vert ? 0 : size_t(geo.G) * 4, s,
+        hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,
                            db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), root.rk2.as<uint32_t>(), geo.R,
-                           geo.rpb, geo.pm, root.f2_vert ? 0u : geo.G, geo.nblk, geo.mlo, geo.mhi,
-                           root.f2_vert ? (uint32_t*)nullptr : cap.as<uint32_t>(), nroot.as<unsigned long long>(),
-                           root.mem_db.as<uint32_t>(), db->mask.as<uint64_t>(),
-                           root.f2_vert ? root.cv.as<uint32_t>() : (uint32_t*)nullptr);
+                           geo.rpb, geo.pm, geo.G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(),
+                           nroot.as<unsigned long long>(), root.mem_db.as<uint32_t>());
         FSM_LAUNCHED("k_f2_plan", s);
-        clk->end(tk, int64_t(db->R) * 4 + db->E * (root.f2_vert ? 20 : 8) + (root.f2_vert ? 0 : int64_t(geo.nd) * 4));
+        clk->end(tk, int64_t(db->R) * 4 + db->E * 8 + int64_t(geo.nd) * 4);
+        scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), geo.nd, s);
         pend[2] = pend[4] = 0;
-        if (!root.f2_vert) {
-            scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), geo.nd, s);
-            FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + geo.nd, 8, hipMemcpyDeviceToHost, s));
-        }
+        FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + geo.nd, 8, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(&pend[4], nroot.p, 8, hipMemcpyDeviceToHost, s));
         root_meta(root, freq_items, f1);
         sync();

@@ -360,20 +360,17 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["vert", "group", "group-few-blocks", "atomic", "passes-3", "passes-64",
-                                  "slab-root", "slab-root-keys"])
+@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic", "passes-3", "passes-64", "slab-root"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
-    """The root F2 implementations (the default vertical count from the DB's item
-    lists; key runs counted per rank group, at the default and at a small block
-    chunk, in several passes over group ranges; global atomics; the DB-direct root
-    or the root slab) give the oracle's patterns and joins."""
+    """The root F2 implementations (key runs counted per rank group, at the
+    default and at a small block chunk, in several passes over group ranges;
+    global atomics; from the DB rows (DB-direct root, default) or from the root
+    slab) give the oracle's patterns and joins."""
     from oracle import oracle
     from tools import gen
     if path == "atomic":
         monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
-    if path.startswith("group") or path.startswith("passes") or path == "slab-root-keys":
-        monkeypatch.setenv("FSM_F2_PATH", "keys")
-    if path.startswith("slab-root"):
+    if path == "slab-root":
         monkeypatch.setenv("FSM_ROOT_DB", "0")
     if path == "group-few-blocks":
         monkeypatch.setenv("FSM_F2_BLOCKS", "3")
