@@ -728,23 +728,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
             const bool vj = j < rl && (ej.x & 0xFFFFu) != 0xFFFFu;
             const uint32_t hi_j = uint32_t(__shfl(int(lh), int(j), 64)) >> 16;
             const uint32_t rj = ej.x & 0xFFFFu;
-            // phase A: lane i counts entry i's keys over the row (partners by shuffle) and
-            // reserves them with one LDS atomic, all entries of the row at once: the key
-            // steps below then take their offsets by shuffle instead of waiting on one
-            // dependent cursor atomic per step
-            uint32_t offi = 0;
-            {
-                const uint32_t lo_i = lh & 0xFFFFu;
-                uint32_t n_i = 0;
-                for (uint32_t q = 0; q < rl; ++q) {  // (wave-uniform trip count)
-                    const uint32_t mq = uint32_t(__shfl(int(me), int(q), 64));
-                    const uint32_t hq = uint32_t(__shfl(int(lh), int(q), 64)) >> 16;
-                    const uint64_t kq = __shfl(mk, int(q), 64);
-                    if (!(mq & 1u)) n_i += (hq > lo_i ? 1u : 0u) + (q > lane && (kq & mk) != 0ull ? 1u : 0u);
-                }
-                if (act && n_i) offi = atomicAdd(&cur[group_of(me >> 1, pm)], n_i);
-                if (act) my_keys += n_i;
-            }
             for (uint32_t i0 = 0; i0 < nact; i0 += k) {
                 const uint32_t ia = i0 + (lane >> lg);  // this segment's active entry
                 const bool vi = ia < nact;
@@ -757,11 +740,14 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                 const bool t_ok = act_i && vj && hi_j > li;
                 const bool e_ok = act_i && vj && j > i && (ej.mask & ei.mask) != 0ull;
                 const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
-                const uint32_t nt = uint32_t(__popcll(tb & segm));
-                const uint32_t off = uint32_t(__shfl(int(offi), int(i), 64));  // entry i's reservation
+                const uint32_t nt = uint32_t(__popcll(tb & segm)), n = nt + uint32_t(__popcll(eb & segm));
+                uint32_t off = 0;
+                if (lane == s0 && n) off = atomicAdd(&cur[gi], n);
+                off = uint32_t(__shfl(int(off), int(s0), 64));
                 const uint32_t key = (ei.y >> 16) + (rj << 1);
                 if (t_ok) keys[off + uint32_t(__popcll(tb & seg_lt))] = uint16_t(key);
                 if (e_ok) keys[off + nt + uint32_t(__popcll(eb & seg_lt))] = uint16_t(key | 1u);
+                if (lane == s0) my_keys += n;
             }
             __builtin_amdgcn_wave_barrier();
         } else {
@@ -1413,9 +1399,6 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                                                     uint32_t rcap, uint32_t* __restrict__ longl,
                                                     uint32_t* __restrict__ nlong) {
     __shared__ uint32_t r_f[kE2Waves][kE2Cap], r_q[kE2Waves][kE2Cap], r_ek[kE2Waves][kE2Cap];
-    // W = 1: a record carries its child entry whole (joined mask, child member id), so the
-    // write phase stores it without loading the kid tables or either mask again
-    __shared__ uint64_t r_m[W == 1 ? kE2Waves : 1][W == 1 ? kE2Cap : 1];
     __shared__ uint32_t i_n[kE2Waves][kE2Own], i_off[kE2Waves][kE2Own], i_cc[kE2Waves][kE2Own], i_lt[kE2Waves][kE2Own];
     __shared__ uint32_t w_tot[kE2Waves];
     __shared__ unsigned long long b_base;
@@ -1504,7 +1487,6 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                     const bool live = pp < total;
                     const uint32_t q = o_k0 + (pp - o_ex);
                     const uint32_t slot = live ? kid_slot[q] : 0u;
-                    const uint32_t kcid = W == 1 && live ? kid_cid[q] : 0u;  // (issued beside the slot load)
                     const uint32_t ct = slot & 1u;
                     const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : (o_lt >> 16));  // partner member id
                     // lower_bound of target in lanes [o_rs, o_re): 6 fixed steps
@@ -1538,14 +1520,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                     const uint64_t succ = __ballot(ok);
                     const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
                     const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
-                    uint64_t jm = 0;  // W = 1: the child entry's mask (the join)
-                    if constexpr (W == 1) {
-                        if (ok) {
-                            const uint32_t lo = o_lt & 0xFFFFu;
-                            jm = ct == kSeq ? (f_mk & (lo >= 63u ? 0ull : (~0ull << (lo + 1u)))) : (o_mk & f_mk);
-                        }
-                    }
-                    on_ok(ok, e0 + f, q, e0 + ow - ef, k, jm, kcid);
+                    on_ok(ok, e0 + f, q, e0 + ow - ef, k);
                     const uint32_t a = (excl > p0 ? excl : p0), bnd = (incl < p0 + 64 ? incl : p0 + 64);
                     if (bnd > a) done += uint32_t(__popcll(succ & lane_range(a - p0, bnd - p0)));
                 }
@@ -1557,18 +1532,13 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                 e0 += cut;
             }
         };
-        walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k, uint64_t jm, uint32_t kcid) {
+        walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k) {
                  const uint64_t b = __ballot(ok);
                  if (ok) {
                      const uint32_t x = nrec + uint32_t(__popcll(b & lt));
                      if (x < rcap) {
-                         if constexpr (W == 1) {
-                             r_m[w][x] = jm;
-                             r_q[w][x] = kcid;
-                         } else {
-                             r_f[w][x] = f;
-                             r_q[w][x] = q;
-                         }
+                         r_f[w][x] = f;
+                         r_q[w][x] = q;
                          r_ek[w][x] = (os << 16) | k;
                      }
                  }
@@ -1595,30 +1565,13 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
         for (uint32_t k = 0; k < w; ++k) wb += w_tot[k];
         if (nrec <= rcap) {
             for (uint32_t x = lane; x < nrec; x += 64) {
-                const uint32_t ek = r_ek[w][x];
+                const uint32_t f = r_f[w][x], q = r_q[w][x], ek = r_ek[w][x];
                 const uint32_t os = ek >> 16, k = ek & 0xFFFFu;
-                if constexpr (W == 1) {
-                    const uint64_t d = wb + i_off[w][os] + k;
-                    const uint32_t n = i_n[w][os];
-                    if (d >= cap) continue;  // a count mismatch: the host reports it
-                    if (n > 0xFFFFu) {       // a run past the 16-bit pos fields: FSM_ELIMIT on the host
-                        atomicOr(o.lim, 1u);
-                        continue;
-                    }
-                    const uint64_t m = r_m[w][x];
-                    o.cid[d] = i_cc[w][os];
-                    o.mem[d] = r_q[w][x];
-                    o.lohi[d] = uint32_t(__builtin_ctzll(m)) | ((63u - uint32_t(__builtin_clzll(m))) << 16);
-                    o.pos[d] = (k << 16) | n;
-                    o.mask[d] = m;
-                } else {
-                    const uint32_t f = r_f[w][x], q = r_q[w][x];
-                    emit_write<W>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
-                                  i_lt[w][os], f, kid_slot[q], lohi, mask, uint32_t(W));
-                }
+                emit_write<W>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
+                              i_lt[w][os], f, kid_slot[q], lohi, mask, uint32_t(W));
             }
         } else {  // the records overflowed: join again, writing at the run bases
-            walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k, uint64_t, uint32_t) {
+            walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k) {
                      if (ok)
                          emit_write<W>(o, cap, wb + i_off[w][os] + k, i_cc[w][os], kid_cid[q], k, i_n[w][os], ef + os,
                                        i_lt[w][os], f, kid_slot[q], lohi, mask, uint32_t(W));
