@@ -456,7 +456,10 @@ __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {  // bit
 //               group g (u16, local to the group's counter tile) into region
 //               (g, b) through an LDS cursor per group.  Rows of <= 64 entries
 //               (W = 1) go lane-per-pair in power-of-two lane segments: a step
-//               evaluates 64 / S entries i at once, S = row length rounded up
+//               evaluates 64 / S entries i at once, S = row length rounded up;
+//               the row's active entries are compacted into LDS (F2Act, one
+//               16-byte read per step, issued a step ahead) and the segment's
+//               cursor offset comes back by readlane when S >= 32
 //   k_f2_count  one block per group: stream the group's regions with 16-byte
 //               loads into LDS counters, then ballot out the frequent pairs
 //               (support >= minsup) - the matrix itself never reaches HBM
@@ -477,13 +480,19 @@ __device__ __forceinline__ uint64_t f2_region(uint32_t g, uint32_t b, uint32_t n
 constexpr uint32_t kF2Threads = 1024;  // k_f2_keys / k_f2_count block
 constexpr uint32_t kF2Waves = kF2Threads / 64;
 
-// row entry staged in LDS for the lane-per-pair path (W = 1)
+// row entry staged in LDS for the lane-per-pair path (W = 1): the partner side
 struct F2Ent {
-    uint32_t x;     // rank | lo << 16
-    uint32_t y;     // group (0xFFFF: entry counted by another rank) | local counter row base << 16
+    uint32_t x;     // rank (0xFFFF: an infrequent DB entry) | lo << 16
+    uint32_t y;     // (unused)
     uint64_t mask;  // eid mask
 };
+// an active entry i of the row (compacted): group | row index << 16, key base | lo << 16, mask
+struct F2Act {
+    uint32_t a, b;
+    uint64_t mask;
+};
 constexpr uint32_t kF2MaxRows = 4096;  // rows per block of k_f2_keys (row offsets staged in LDS)
+constexpr uint32_t kF2RowWords = (kF2MaxRows + 1 + 3) & ~3u;  // their LDS words (what follows stays 16-byte aligned)
 
 // Root rows fused with the F2 plan: block b builds the root runs of its row block
 // (rpb rows, one wave per row in turn, as k_root_write) and histograms the key
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
                                                                uint32_t rpb, const uint64_t* __restrict__ off,
                                                                SlabPtrs o, uint32_t pm, uint32_t G, uint32_t nblk,
                                                                uint32_t mlo, uint32_t mhi,
-                                                               uint32_t* __restrict__ cap, uint32_t wd) {
+                                                               uint32_t* __restrict__ cap, uint32_t amask, uint32_t wd) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
     __syncthreads();
@@ -544,9 +553,9 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
         }
     }
     __syncthreads();
-    // regions start on 16-byte boundaries (8 keys): k_f2_count reads them in aligned chunks
+    // regions start on 16-byte boundaries (amask + 1 >= 8 keys): k_f2_count reads them in aligned chunks
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
-        cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + 7u) & ~7u;
+        cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + amask) & ~amask;
 }
 
 // ---- DB-direct root.  The root class is the DB restricted to the frequent items, so
@@ -609,7 +618,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
                                                           const uint32_t* __restrict__ item,
                                                           const uint32_t* __restrict__ rk2, uint32_t R, uint32_t rpb,
                                                           uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
-                                                          uint32_t mhi, uint32_t* __restrict__ cap,
+                                                          uint32_t mhi, uint32_t* __restrict__ cap, uint32_t amask,
                                                           unsigned long long* __restrict__ nroot,
                                                           uint32_t* __restrict__ mem_out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
@@ -646,7 +655,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
     }
     if (lane == 0) atomicAdd(&blk_root, my_root);
     __syncthreads();
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + 7u) & ~7u;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + amask) & ~amask;
     if (threadIdx.x == 0 && blk_root) atomicAdd(nroot, (unsigned long long)blk_root);
 }
 
@@ -665,8 +674,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     F2Ent* stage_all = reinterpret_cast<F2Ent*>(smem);  // kF2Waves x 64 entries
     uint32_t* srow = smem + kF2Waves * 64 * (sizeof(F2Ent) / 4);  // row offsets of the block [rpb + 1]
-    uint32_t* actx_all = srow + kF2MaxRows + 1;                     // kF2Waves x 64 active entry positions
-    uint32_t* cur = actx_all + kF2Waves * 64;                       // region cursors [G]
+    uint32_t* actx_all = srow + kF2RowWords;                        // kF2Waves x 64 active entries (F2Act)
+    uint32_t* cur = actx_all + kF2Waves * 64 * (sizeof(F2Act) / 4); // region cursors [G]
     __shared__ uint32_t blk_keys;
     const uint32_t b = blockIdx.x;
     const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
@@ -677,7 +686,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     __syncthreads();
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     F2Ent* stage = stage_all + wave * 64;
-    uint32_t* actx = actx_all + wave * 64;
+    F2Act* sact = reinterpret_cast<F2Act*>(actx_all) + wave * 64;
     const uint64_t lt = lanemask_lt();
     uint32_t my_keys = 0;
     // the next row's entries are loaded while the current row is enumerated
@@ -701,53 +710,58 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
         fetch(r + kF2Waves);
         if (rl == 0) continue;
         if (W == 1 && rl <= 64) {
-            // ---- lane-per-pair: segments of S lanes, lane s0 + j tests partner j
-            // entries i are this rank's members only (sharded root: the other
-            // ranks count the rest); every entry of the row is a partner j
-            // (an odd member id: an infrequent DB entry of the DB-direct root, neither i nor j)
+            // ---- lane-per-pair: segments of S lanes, lane s0 + j tests partner j.  The
+            // active entries i are compacted into LDS with all a step needs (one 16-byte read,
+            // issued a step ahead); the segment's cursor offset comes back by readlane (S >= 32)
             const bool act = lane < rl && !(me & 1u) && me - mlo < mhi - mlo;
             const uint64_t actb = __ballot(act);
             const uint32_t nact = uint32_t(__popcll(actb));
+            const uint32_t ri = me >> 1, g = group_of(ri, pm);
             if (lane < rl) {
-                const uint32_t ri = me >> 1, g = group_of(ri, pm);
                 F2Ent en;
                 en.x = ((me & 1u) ? 0xFFFFu : ri) | ((lh & 0xFFFFu) << 16);
-                en.y = (act ? g : 0xFFFFu) | ((ri - g * per) * D << 16);
+                en.y = 0u;
                 en.mask = mk;
                 stage[lane] = en;
             }
-            if (act) actx[__popcll(actb & lt)] = lane;
+            if (act) sact[__popcll(actb & lt)] = F2Act{g | (lane << 16), ((ri - g * per) * D) | ((lh & 0xFFFFu) << 16), mk};
             __builtin_amdgcn_wave_barrier();
-            const uint32_t lg = rl <= 1 ? 0u : 32u - uint32_t(__clz(rl - 1));  // S = 2^lg >= rl
-            const uint32_t S = 1u << lg, k = 64u >> lg;
-            const uint32_t j = lane & (S - 1), s0 = lane & ~(S - 1);
-            const uint64_t segm = S == 64 ? ~0ull : (((1ull << S) - 1ull) << s0);
-            const uint64_t seg_lt = lt & segm;
-            // this lane's partner j (fixed for the row; not an infrequent DB entry)
-            const F2Ent ej = stage[j < rl ? j : 0];
-            const bool vj = j < rl && (ej.x & 0xFFFFu) != 0xFFFFu;
-            const uint32_t hi_j = uint32_t(__shfl(int(lh), int(j), 64)) >> 16;
-            const uint32_t rj = ej.x & 0xFFFFu;
-            for (uint32_t i0 = 0; i0 < nact; i0 += k) {
-                const uint32_t ia = i0 + (lane >> lg);  // this segment's active entry
-                const bool vi = ia < nact;
-                const uint32_t i = vi ? actx[ia] : 0u;
-                const F2Ent ei = stage[i];
-                const uint32_t gi = ei.y & 0xFFFFu;
-                const bool act_i = vi && gi != 0xFFFFu;
-                const uint32_t li = ei.x >> 16;
-                // x -> y: bits of L(j) after the first bit of L(i); (x y), y > x: L(i) & L(j)
-                const bool t_ok = act_i && vj && hi_j > li;
-                const bool e_ok = act_i && vj && j > i && (ej.mask & ei.mask) != 0ull;
-                const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
-                const uint32_t nt = uint32_t(__popcll(tb & segm)), n = nt + uint32_t(__popcll(eb & segm));
-                uint32_t off = 0;
-                if (lane == s0 && n) off = atomicAdd(&cur[gi], n);
-                off = uint32_t(__shfl(int(off), int(s0), 64));
-                const uint32_t key = (ei.y >> 16) + (rj << 1);
-                if (t_ok) keys[off + uint32_t(__popcll(tb & seg_lt))] = uint16_t(key);
-                if (e_ok) keys[off + nt + uint32_t(__popcll(eb & seg_lt))] = uint16_t(key | 1u);
-                if (lane == s0) my_keys += n;
+            if (nact) {
+                const uint32_t lg = rl <= 1 ? 0u : 32u - uint32_t(__clz(rl - 1));  // S = 2^lg >= rl
+                const uint32_t S = 1u << lg, k = 64u >> lg;
+                const uint32_t j = lane & (S - 1), s0 = lane & ~(S - 1), sub = lane >> lg;
+                const uint64_t segm = S == 64 ? ~0ull : (((1ull << S) - 1ull) << s0);
+                const uint64_t seg_lt = lt & segm;
+                const F2Ent ej = stage[j < rl ? j : 0];
+                const bool vj = j < rl && (ej.x & 0xFFFFu) != 0xFFFFu;
+                const uint32_t hi_j = uint32_t(__shfl(int(lh), int(j), 64)) >> 16;
+                const uint32_t rj2 = (ej.x & 0xFFFFu) << 1;
+                F2Act A = sact[min(sub, nact - 1)];
+                for (uint32_t i0 = 0; i0 < nact; i0 += k) {
+                    const uint32_t ia = i0 + sub;
+                    const bool vi = ia < nact;
+                    const F2Act An = sact[min(ia + k, nact - 1)];  // the next step's entry
+                    const uint32_t gi = A.a & 0xFFFFu, i = A.a >> 16, li = A.b >> 16;
+                    const bool t_ok = vi && vj && hi_j > li;
+                    const bool e_ok = vi && vj && j > i && (ej.mask & A.mask) != 0ull;
+                    const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
+                    const uint32_t nt = uint32_t(__popcll(tb & segm)), n = nt + uint32_t(__popcll(eb & segm));
+                    uint32_t off = 0;
+                    if (lane == s0 && n) off = atomicAdd(&cur[gi], n);
+                    if (S == 64)
+                        off = uint32_t(__builtin_amdgcn_readlane(int(off), 0));
+                    else if (S == 32) {
+                        const uint32_t o0 = uint32_t(__builtin_amdgcn_readlane(int(off), 0));
+                        const uint32_t o1 = uint32_t(__builtin_amdgcn_readlane(int(off), 32));
+                        off = lane < 32 ? o0 : o1;
+                    }
+                    else
+                        off = uint32_t(__shfl(int(off), int(s0), 64));
+                    const uint32_t key = (A.b & 0xFFFFu) + rj2;
+                    if (t_ok) keys[off + uint32_t(__popcll(tb & seg_lt))] = uint16_t(key);
+                    if (e_ok) keys[off + nt + uint32_t(__popcll(eb & seg_lt))] = uint16_t(key | 1u);
+                    A = An;
+                }
             }
             __builtin_amdgcn_wave_barrier();
         } else {
@@ -790,18 +804,21 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                     const uint32_t key = kb + (rq << 1);
                     if (t_ok) keys[off + uint32_t(__popcll(tb & lt))] = uint16_t(key);
                     if (e_ok) keys[off + nt + uint32_t(__popcll(eb & lt))] = uint16_t(key | 1u);
-                    if (lane == 0) my_keys += n;
                 }
             }
         }
     }
-    atomicAdd(&blk_keys, my_keys);
     __syncthreads();
     // the fills of the groups of the member range [mlo, mhi) only (a pass over other groups
-    // leaves theirs as an earlier pass wrote them)
+    // leaves theirs as an earlier pass wrote them); the block's key count is their sum
     const uint32_t glo = (mlo >> 1) / per, ghi = mhi == kNone ? G : min(G, ((mhi >> 1) + per - 1) / per);
-    for (uint32_t g = glo + threadIdx.x; g < ghi; g += blockDim.x)
-        fill[uint64_t(g) * nblk + b] = cur[g] - uint32_t(base[f2_region(g, b, nblk)]);
+    for (uint32_t g = glo + threadIdx.x; g < ghi; g += blockDim.x) {
+        const uint32_t f = cur[g] - uint32_t(base[f2_region(g, b, nblk)]);
+        fill[uint64_t(g) * nblk + b] = f;
+        my_keys += f;
+    }
+    atomicAdd(&blk_keys, my_keys);
+    __syncthreads();
     if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
@@ -2363,6 +2380,15 @@ struct Miner {
         const char* v = std::getenv("FSM_F2_PASSES");
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 64)) : 1u;
     }
+    // key alignment of the root F2 regions (a power of two >= 8 keys; FSM_F2_ALIGN overrides, for tuning)
+    static uint32_t f2_align() {
+        static const uint32_t a = [] {
+            const char* v = std::getenv("FSM_F2_ALIGN");
+            const uint64_t x = v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 8, 4096) : 8;
+            return uint32_t(1) << (63 - __builtin_clzll(x));
+        }();
+        return a;
+    }
     // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
     static uint32_t f2_blocks() {
         const char* v = std::getenv("FSM_F2_BLOCKS");
@@ -2422,7 +2448,7 @@ struct Miner {
         // the one enumeration (keys padded: k_f2_count reads whole 16-byte words past a region's end)
         DevBuf keys((nslots + 1024) * 2), nk(8);
         FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
-        const size_t kshm = size_t(kF2Waves) * 64 * (sizeof(F2Ent) + 4) + (size_t(kF2MaxRows) + 1) * 4 + size_t(G) * 4;
+        const size_t kshm = size_t(kF2Waves) * 64 * (sizeof(F2Ent) + sizeof(F2Act)) + size_t(kF2RowWords) * 4 + size_t(G) * 4;
         // count + frequent pairs of this rank's slice
         const uint32_t g0 = rlo / per, g1 = rhi == 0 ? 0u : (rhi - 1) / per + 1;
         uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * D, uint64_t(1) << 20));
@@ -3384,7 +3410,7 @@ struct Miner {
         const size_t tk = clk->begin("k_f2_plan");
         hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,
                            db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), root.rk2.as<uint32_t>(), geo.R,
-                           geo.rpb, geo.pm, geo.G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(),
+                           geo.rpb, geo.pm, geo.G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(), f2_align() - 1,
                            nroot.as<unsigned long long>(), root.mem_db.as<uint32_t>());
         FSM_LAUNCHED("k_f2_plan", s);
         clk->end(tk, int64_t(db->R) * 4 + db->E * 8 + int64_t(geo.nd) * 4);
@@ -3476,7 +3502,7 @@ struct Miner {
     hipLaunchKernelGGL(k_root_write_plan<WW>, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,              \
                        db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), db->mask.as<uint64_t>(),               \
                        d_rank.as<uint32_t>(), geo.R, geo.rpb, roff.as<uint64_t>(), op, geo.pm, geo.G, geo.nblk,    \
-                       geo.mlo, geo.mhi, cap.as<uint32_t>(), uint32_t(W))
+                       geo.mlo, geo.mhi, cap.as<uint32_t>(), f2_align() - 1, uint32_t(W))
             FSM_W_DISPATCH(W, FSM_ROOTWP)
 #undef FSM_ROOTWP
             FSM_LAUNCHED("k_root_write", s);
