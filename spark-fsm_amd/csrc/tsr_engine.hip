@@ -235,7 +235,8 @@ struct ExpCtl {
     uint32_t done;   // collect blocks finished
     uint32_t nsid;   // bitmap path: sids containing X u Y (the expansion domain)
     uint32_t nent;   // bitmap path: row entries read over the domain (algorithmic bytes)
-    uint32_t pad[2];
+    uint32_t nsuf;   // bitmap path (diagnostic): entries past mlo, the only bump candidates
+    uint32_t nval;   // bitmap path (diagnostic): entries in rows where X => Y holds
 };
 
 // histogram bump (no returned value: the lanes' atomics stay in flight) that
@@ -338,7 +339,7 @@ struct ExpRec {
     uint32_t c, tl, dl, tr;
 };
 struct ExpHdr {
-    uint32_t nout, nx, nsid, nent;
+    uint32_t nout, nx, nsid, nent, nsuf, nval, pad[2];
 };
 
 // List path: visit the items this expansion touched, keep the counts >= t
@@ -384,6 +385,10 @@ __device__ __forceinline__ void publish_slots(ExpCtl* __restrict__ ctlb, ExpHdr*
         hdrb[b].nx = c.nx;
         hdrb[b].nsid = c.nsid;
         hdrb[b].nent = c.nent;
+        hdrb[b].nsuf = c.nsuf;
+        hdrb[b].nval = c.nval;
+        c.nsuf = 0;
+        c.nval = 0;
         c.nx = 0;
         c.nlist = 0;
         c.nout = 0;
@@ -695,9 +700,11 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
     }
     const uint32_t maxX = sXY[nx - 1], maxY = sXY[nxy - 1];  // sides ascend by item, so by kid
     uint32_t my_ent = 0;   // row entries of this block (thread 0)
+    uint32_t my_suf = 0, my_val = 0;  // (diagnostics, pass 0: entries past mlo / in rows where X => Y holds)
     uint32_t tag = 0;      // this wave's step tags in wflag
     // bumps of this pass start past min(max X, max Y) (both extensions need c above one of them)
-    const uint32_t mlo = max(doL ? (doR ? min(maxX, maxY) : maxX) : maxY, kid_lo == 0 ? 0u : kid_lo - 1u);
+    const uint32_t mlo0 = doL ? (doR ? min(maxX, maxY) : maxX) : maxY;
+    const uint32_t mlo = max(mlo0, kid_lo == 0 ? 0u : kid_lo - 1u);
     for (uint32_t win = d0; win < d1; win += kExpWin) {
         const uint32_t n = min(kExpWin, d1 - win);
         {   // the window's rows and the exclusive scan of their lengths (rows 2t, 2t + 1 per thread)
@@ -823,6 +830,11 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
             if (qa < qz) {
 #pragma unroll
                 for (int u = 0; u < kEpt; ++u) {
+                    if (pass == 0 && ((codes >> (3 * u)) & 4u)) {
+                        my_suf += e[u].x > mlo0 ? 1u : 0u;
+                        const uint2 fv = sfl[ej[u]];
+                        my_val += fv.x < fv.y ? 1u : 0u;
+                    }
                     if (((codes >> (3 * u)) & 7u) != 5u || e[u].x <= mlo) continue;  // an entry with code 1
                     const uint2 fl = sfl[ej[u]];
                     const uint32_t fX = fl.x, lY = fl.y;
@@ -837,6 +849,14 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
     uint32_t* prow = part + (uint64_t(pass) * geo.nblk + blockIdx.x) * 2 * KP;
     for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) prow[k] = dsm[k];
     if (pass == 0 && threadIdx.x == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
+    if (pass == 0) {
+        for (int d = 32; d > 0; d >>= 1) {
+            my_suf += uint32_t(__shfl_xor(int(my_suf), d, 64));
+            my_val += uint32_t(__shfl_xor(int(my_val), d, 64));
+        }
+        if (lane == 0 && my_suf) atomicAdd(&ctl->nsuf, my_suf);
+        if (lane == 0 && my_val) atomicAdd(&ctl->nval, my_val);
+    }
 }
 
 // Sum each slot's partial rows per kid and keep the counts >= t: block x of
@@ -1714,6 +1734,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     const char* seg_name[4] = {use_bm ? "k_exp_domain" : "k_expand", use_bm ? "k_exp_rows" : "",
                                use_bm ? "k_expand_reduce" : "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
+    int64_t exp_suf = 0, exp_val = 0;  // (diagnostics, verbose: entries past mlo / in rows where X => Y holds)
     int64_t seq_next = 0;
     // Take in the results of set x (waits for its launch): records sorted into the
     // cache, and its batch queued for child speculation.
@@ -1748,6 +1769,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 const uint64_t bmb = uint64_t(r->nx + r->ny) * d->NW * 4;
                 exp_domain += h.nsid;
                 exp_entries += h.nent;
+                exp_suf += h.nsuf;
+                exp_val += h.nval;
                 exp_bitmap_bytes += int64_t(bmb);
                 seg[0].bytes += int64_t(bmb + 16ull * h.nsid);
                 seg[1].bytes += int64_t(8ull * h.nent + 8ull * h.nsid);
@@ -2206,8 +2229,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      (long long)expansions, (long long)launches, (long long)gpu_rules, (long long)spec_pushback, wait_ms,
                      prep_ms, post_ms, commit_ms, pop_ms, rp.st.size());
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB\n",
-                     (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6);
+        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB; row entries "
+                     "%lld, past mlo %lld, in rows where the rule holds %lld (chunked rows)\n",
+                     (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6, (long long)exp_entries,
+                     (long long)exp_suf, (long long)exp_val);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {
