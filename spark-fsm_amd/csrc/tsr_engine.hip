@@ -233,10 +233,10 @@ struct ExpCtl {
     uint32_t nlist;  // items touched (list entries)
     uint32_t nout;   // candidates kept
     uint32_t done;   // collect blocks finished
-    uint32_t nsid;   // bitmap path: sids containing X u Y (the expansion domain)
-    uint32_t nent;   // bitmap path: row entries read over the domain (algorithmic bytes)
-    uint32_t nsuf;   // bitmap path (diagnostic): entries past mlo, the only bump candidates
-    uint32_t nval;   // bitmap path (diagnostic): entries in rows where X => Y holds
+    uint32_t nsid;   // bitmap path: domain sids (holding X u Y: the bitmap AND)
+    uint32_t nent;   // bitmap path: row entries of the domain sids (SURVEY's scan)
+    uint32_t nhold;  // bitmap path: domain rows where X => Y holds (with a candidate past mlo)
+    uint32_t nwalk;  // bitmap path: row entries the row kernel walks (those rows' suffixes)
 };
 
 // histogram bump (no returned value: the lanes' atomics stay in flight) that
@@ -339,7 +339,7 @@ struct ExpRec {
     uint32_t c, tl, dl, tr;
 };
 struct ExpHdr {
-    uint32_t nout, nx, nsid, nent, nsuf, nval, pad[2];
+    uint32_t nout, nx, nsid, nent, nhold, nwalk, pad[2];
 };
 
 // List path: visit the items this expansion touched, keep the counts >= t
@@ -385,10 +385,10 @@ __device__ __forceinline__ void publish_slots(ExpCtl* __restrict__ ctlb, ExpHdr*
         hdrb[b].nx = c.nx;
         hdrb[b].nsid = c.nsid;
         hdrb[b].nent = c.nent;
-        hdrb[b].nsuf = c.nsuf;
-        hdrb[b].nval = c.nval;
-        c.nsuf = 0;
-        c.nval = 0;
+        hdrb[b].nhold = c.nhold;
+        hdrb[b].nwalk = c.nwalk;
+        c.nhold = 0;
+        c.nwalk = 0;
         c.nx = 0;
         c.nlist = 0;
         c.nout = 0;
@@ -509,12 +509,76 @@ __device__ __forceinline__ void bump(uint32_t c, uint32_t fl, uint32_t fX, uint3
     if (doR && c > maxY && (fl >> 16) > fX) atomicAdd(&hR[rel], 1u);
 }
 
+// Rank directory of the kept items' sid bitmaps: rdir[k * NW4 + g] = the sids below
+// 128 g holding kid k's item (exclusive prefix popcount, one entry per 4-word group).
+// One block per kid.
+__global__ __launch_bounds__(kBlock) void k_rank_dir(const uint32_t* __restrict__ bm, uint32_t NW,
+                                                     const uint32_t* __restrict__ kept, uint32_t* __restrict__ rdir) {
+    __shared__ uint32_t wsum[kBlock / 64];
+    const uint32_t k = blockIdx.x, NW4 = NW / 4u;
+    const uint4* row = reinterpret_cast<const uint4*>(bm + uint64_t(kept[k]) * NW);
+    uint32_t* out = rdir + uint64_t(k) * NW4;
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (uint32_t g0 = 0; g0 < NW4; g0 += blockDim.x) {
+        const uint32_t g = g0 + threadIdx.x;
+        uint32_t c = 0;
+        if (g < NW4) {
+            const uint4 v = row[g];
+            c = uint32_t(__popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w));
+        }
+        const uint32_t inc = wave_incl_scan(c);
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+        for (uint32_t w = 0; w < kBlock / 64; ++w) {
+            before += w < wv ? wsum[w] : 0u;
+            tot += wsum[w];
+        }
+        if (g < NW4) out[g] = carry + before + inc - c;
+        carry += tot;
+        __syncthreads();  // wsum is rewritten next round
+    }
+}
+
+// rank of sid in one item's sid bitmap (the sids below it holding the item): the
+// item's rank directory entry + the popcounts of its words before sid
+__device__ __forceinline__ uint32_t bm_rank(const uint32_t* __restrict__ bmrow, const uint32_t* __restrict__ rd,
+                                            uint32_t sid) {
+    const uint32_t g = sid >> 7, wi = (sid >> 5) & 3u, bit = sid & 31u;
+    const uint4 v = reinterpret_cast<const uint4*>(bmrow)[g];
+    uint32_t r = rd[g];
+    r += wi > 0u ? uint32_t(__popc(v.x)) : 0u;
+    r += wi > 1u ? uint32_t(__popc(v.y)) : 0u;
+    r += wi > 2u ? uint32_t(__popc(v.z)) : 0u;
+    const uint32_t cw = wi == 0u ? v.x : (wi == 1u ? v.y : (wi == 2u ? v.z : v.w));
+    return r + uint32_t(__popc(cw & ((1u << bit) - 1u)));
+}
+
+// The kept rows' vertical entries: for the entry of kid k in packed row s,
+// vfl[kvoff[k] + rank of s in k's bitmap] = (first | last << 16, its position in
+// the row), so a sid's entry of any kid is two loads away (bm_rank, vfl).  One
+// thread per row.
+__global__ __launch_bounds__(kBlock) void k_vfl(const uint32_t* __restrict__ k_off, const uint2* __restrict__ ent,
+                                                uint32_t N, const uint32_t* __restrict__ bm, uint32_t NW,
+                                                const uint32_t* __restrict__ kept, const uint32_t* __restrict__ rdir,
+                                                const uint32_t* __restrict__ kvoff, uint2* __restrict__ vfl) {
+    const uint32_t NW4 = NW / 4u;
+    for (uint32_t sid = blockIdx.x * blockDim.x + threadIdx.x; sid < N; sid += gridDim.x * blockDim.x) {
+        const uint32_t rs = k_off[sid], re = k_off[sid + 1];
+        for (uint32_t e = rs; e < re; ++e) {
+            const uint2 v = ent[e];
+            const uint32_t r = bm_rank(bm + uint64_t(kept[v.x]) * NW, rdir + uint64_t(v.x) * NW4, sid);
+            vfl[kvoff[v.x] + r] = make_uint2(v.y, e - rs);
+        }
+    }
+}
+
 // Domain of rule slot k (grid.y): its |X|+|Y| item bitmaps ANDed over this
 // block's kDomWords words (4 consecutive words per thread, 16-byte operand
 // loads, 8 operands in flight), the set sids compacted into the slot's domain
-// list at dom_off[k] (one cursor atomic per block: ExpCtl::nsid) as (row start,
-// row length) pairs of the packed kept rows.  Every pass of the row kernel
-// reads this list; the bitmaps are ANDed once per rule.
+// list at dom_off[k] (one cursor atomic per block: ExpCtl::nsid).  Every pass of
+// the row kernel reads this list; the bitmaps are ANDed once per rule.
 constexpr uint32_t kDomThreads = 256;
 constexpr uint32_t kDomWords = 4 * kDomThreads;  // bitmap words per domain block
 
@@ -524,9 +588,8 @@ constexpr uint32_t kDomWords = 4 * kDomThreads;  // bitmap words per domain bloc
 // as above: |L| x |X u Y| probes instead of |X u Y| whole-bitmap operands.
 __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restrict__ sides,
                                                             const uint32_t* __restrict__ bm, uint32_t NW,
-                                                            const uint32_t* __restrict__ row_off,
                                                             const uint64_t* __restrict__ dom_off,
-                                                            uint2* __restrict__ dom, ExpCtl* __restrict__ ctlb,
+                                                            uint32_t* __restrict__ dom, ExpCtl* __restrict__ ctlb,
                                                             const uint64_t* __restrict__ vert_off,
                                                             const uint32_t* __restrict__ vert_sid) {
     __shared__ uint32_t sIt[2 * kMaxSide];
@@ -537,13 +600,13 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
     const uint32_t nxy = side.nx + side.ny;
     for (uint32_t q = threadIdx.x; q < nxy; q += blockDim.x) sIt[q] = q < side.nx ? side.X[q] : side.Y[q - side.nx];
     __syncthreads();
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    uint32_t* out = dom + dom_off[k];
     if (side.lmode) {
         const uint32_t drv = side.drv;
         const uint64_t l0 = vert_off[drv], l1 = vert_off[drv + 1];
         const uint64_t per = (l1 - l0 + gridDim.x - 1) / gridDim.x;
         const uint64_t a = l0 + per * blockIdx.x, z = min(l1, a + per);
-        uint2* out = dom + dom_off[k];
-        const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
         for (uint64_t r0 = a; r0 < z; r0 += blockDim.x) {  // block-uniform rounds
             const uint64_t q = r0 + threadIdx.x;
             bool keep = false;
@@ -568,8 +631,7 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
             if (keep) {
                 uint32_t p = b_base + uint32_t(__popcll(bal & lanemask_lt()));
                 for (uint32_t w = 0; w < wv; ++w) p += wsum[w];
-                const uint32_t rs = row_off[sid];
-                out[p] = make_uint2(rs, row_off[sid + 1] - rs);
+                out[p] = sid;
             }
             __syncthreads();  // wsum / b_base are rewritten next round
         }
@@ -596,7 +658,6 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
         }
     }
     const uint32_t cnt = uint32_t(__popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w));
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const uint32_t incl = wave_incl_scan(cnt);
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
@@ -609,37 +670,69 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
     if (!cnt) return;
     uint32_t p = b_base + incl - cnt;
     for (uint32_t q = 0; q < wv; ++q) p += wsum[q];
-    uint2* out = dom + dom_off[k];
     const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        for (uint32_t m = ww[h]; m; m &= m - 1u) {
-            const uint32_t sid = (w + uint32_t(h)) * 32u + uint32_t(__builtin_ctz(m));
-            const uint32_t rs = row_off[sid];
-            out[p++] = make_uint2(rs, row_off[sid + 1] - rs);
-        }
-    }
+    for (int h = 0; h < 4; ++h)
+        for (uint32_t m = ww[h]; m; m &= m - 1u) out[p++] = (w + uint32_t(h)) * 32u + uint32_t(__builtin_ctz(m));
 }
 
-// The rows of slot b's domain (k_exp_domain's list, this block's share of it)
-// counted into LDS histograms of the kid range [kid_lo, kid_lo + KP), pass =
-// blockIdx.y.  Windows of kExpWin domain rows: their (start, length) pairs are
-// loaded coalesced and the lengths scanned; the window's rows are then walked
-// FLAT: chunks of whole rows holding at most kChunkEnt entries are spread over
-// every lane of the block (each wave a contiguous stretch of the chunk,
-// lane-interleaved: one coalesced 8-byte load per lane per step, kEpt steps
-// per lane in registers), so a 2,000-entry row is 4 steps of 8 waves instead
-// of one wave's serial chain of dependent loads, and an 8-entry row does not
-// leave 56 lanes idle.  A lane finds its row from the step's row-start mask:
-// the rows starting inside the step flag their offsets in a wave-private LDS
-// word array, one ballot turns the flags into a 64-bit mask and mbcnt counts
-// the starts up to the lane.  Each kid's role comes from one 2-bit code (dead,
-// candidate, in X, in Y; ctab).  Pass 1 (loads in flight together) marks
-// firstX / lastY of each row with LDS atomics; after one barrier pass 2 bumps
-// the candidates from the same registers.  Rows longer than a chunk are walked
-// twice (pass 1, barrier, pass 2).  Each block writes its whole histogram as
-// one dense partial row (plain coalesced stores); k_expand_reduce sums a
-// slot's rows.
+// A domain sid's firstX (max over X of the item's first itemset) and lastY (min over
+// Y of the last), and the row position of side item tm, from the kept items'
+// vertical entries: rank of the sid in the item's bitmap (rank directory +
+// popcounts) -> vfl.  Two dependent loads per item, the items' loads in flight
+// together.
+struct DomProbe {
+    const uint32_t* bm;
+    uint32_t NW, NW4;
+    const uint32_t* rdir;
+    const uint32_t* kvoff;
+    const uint2* vfl;
+    __device__ __forceinline__ bool operator()(uint32_t sid, const uint32_t* sIt, const uint32_t* sKid, uint32_t nx,
+                                               uint32_t nxy, uint32_t tm, uint32_t& fl, uint32_t& pm) const {
+        uint32_t fX = 0, lY = 0xFFFFu;
+        pm = 0;
+        for (uint32_t t0 = 0; t0 < nxy; t0 += 4) {
+            uint2 v[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t t = t0 + u;
+                if (t < nxy) {
+                    const uint32_t kk = sKid[t];
+                    const uint32_t r = bm_rank(bm + uint64_t(sIt[t]) * NW, rdir + uint64_t(kk) * NW4, sid);
+                    v[u] = vfl[kvoff[kk] + r];
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t t = t0 + u;
+                if (t >= nxy) break;
+                if (t < nx) fX = max(fX, v[u].x & 0xFFFFu); else lY = min(lY, v[u].x >> 16);
+                if (t == tm) pm = v[u].y;
+            }
+        }
+        fl = fX | (lY << 16);
+        return fX < lY;
+    }
+};
+
+// The rows of slot b's domain (k_exp_domain's list of row suffixes, this block's
+// share of it) counted into LDS histograms of the kid range [kid_lo, kid_lo + KP),
+// pass = blockIdx.y.  Windows of kExpWin domain rows: their (start, length,
+// firstX | lastY) entries are loaded coalesced and the lengths scanned; the
+// window's rows are then walked FLAT: chunks of whole rows holding at most
+// kChunkEnt entries are spread over every lane of the block (each wave a
+// contiguous stretch of the chunk, lane-interleaved: one coalesced 8-byte load
+// per lane per step, kEpt steps per lane in registers), so a 2,000-entry row is
+// 4 steps of 8 waves instead of one wave's serial chain of dependent loads, and
+// an 8-entry row does not leave 56 lanes idle.  A lane finds its row from the
+// step's row-start mask: the rows starting inside the step flag their offsets in
+// a wave-private LDS word array, one ballot turns the flags into a 64-bit mask
+// and mbcnt counts the starts up to the lane.  Each kid's role comes from one
+// 2-bit code (dead, candidate, in X, in Y; ctab) behind a 64-bit bloom of X u Y;
+// the candidates are bumped straight from the registers (firstX / lastY come with
+// the row: no first walk, no barrier).  Each block writes its whole histogram as
+// one dense partial row (plain coalesced stores); k_expand_reduce sums a slot's
+// rows.
 __device__ __forceinline__ uint32_t kid_code(const uint32_t* ctab, uint32_t c) {
     return (ctab[c >> 4] >> ((c & 15u) * 2u)) & 3u;
 }
@@ -647,21 +740,23 @@ __device__ __forceinline__ uint32_t kid_code(const uint32_t* ctab, uint32_t c) {
 __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ sides,
                                                       const uint64_t* __restrict__ blk_off, uint32_t nslot,
                                                       const uint64_t* __restrict__ dom_off,
-                                                      const uint2* __restrict__ dom,
+                                                      const uint32_t* __restrict__ dom,
+                                                      const uint32_t* __restrict__ row_off,
                                                       const uint2* __restrict__ ent,
                                                       const uint32_t* __restrict__ kid_of,
                                                       const uint32_t* __restrict__ alive, ExpGeo geo,
                                                       uint32_t* __restrict__ part, ExpCtl* __restrict__ ctlb,
-                                                      uint32_t* __restrict__ ndlw) {
+                                                      uint32_t* __restrict__ ndlw, DomProbe probe) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];  // hist L [KP] | hist R [KP] | ctab
     // window rows: x = first flat entry (exclusive scan of the lengths), y = row start in
     // `ent` minus x (u32 wrap: the ent index of flat entry q is y + q)
     __shared__ uint2 rowv[kExpWin + 1];
-    __shared__ uint2 sfl[kExpWin];                   // per row: firstX (x: max over X), lastY (y: min over Y)
+    __shared__ uint32_t sfl[kExpWin];                // per row: firstX | lastY << 16
     __shared__ unsigned long long s_bloom;
     __shared__ uint32_t wflag[kXBlock / 64][64];     // per wave: row-start flags of the current step (tags)
     __shared__ uint32_t sXY[2 * kMaxSide];           // X then Y, as kids
-    __shared__ uint32_t wsum[kXBlock / 64];
+    __shared__ uint32_t sItm[2 * kMaxSide];          // X then Y, as items
+    __shared__ uint32_t wsum[kXBlock / 64], wcnt[kXBlock / 64];
     const uint32_t KP = geo.KP, pass = blockIdx.y, kid_lo = pass * KP;
     uint32_t* hL = dsm;
     uint32_t* hR = dsm + KP;
@@ -681,12 +776,18 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
     const uint32_t wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) dsm[k] = 0;
     for (uint32_t k = threadIdx.x; k < (geo.K + 15) / 16; k += blockDim.x) ctab[k] = alive[k];
-    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) sXY[k] = kid_of[k < nx ? side.X[k] : side.Y[k - nx]];
+    for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) {
+        const uint32_t it = k < nx ? side.X[k] : side.Y[k - nx];
+        sItm[k] = it;
+        sXY[k] = kid_of[it];
+    }
     wflag[wv][lane] = 0;
     // this block's share of the slot's domain
     const uint32_t nd = ctl->nsid;
     const uint32_t d0 = uint32_t(uint64_t(nd) * bx / nbx), d1 = uint32_t(uint64_t(nd) * (bx + 1) / nbx);
-    const uint2* dl = dom + dom_off[b];
+    const uint32_t* dl = dom + dom_off[b];
+    // the side item at min(max X, max Y) (sides ascend by item): a row's candidates lie past it
+    const uint32_t tm = doL ? (doR ? (side.maxX < side.maxY ? nx - 1u : nxy - 1u) : nx - 1u) : nxy - 1u;
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) {  // X -> code 2, Y -> code 3
         const uint32_t c = sXY[k], sh = (c & 15u) * 2u;
@@ -699,39 +800,63 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
         s_bloom = bl;
     }
     const uint32_t maxX = sXY[nx - 1], maxY = sXY[nxy - 1];  // sides ascend by item, so by kid
-    uint32_t my_ent = 0;   // row entries of this block (thread 0)
-    uint32_t my_suf = 0, my_val = 0;  // (diagnostics, pass 0: entries past mlo / in rows where X => Y holds)
+    uint32_t my_ent = 0;   // row entries walked by this block (thread 0)
+    uint32_t my_full = 0, my_hold = 0;  // pass 0: the domain rows' entries, the rows where the rule holds
     uint32_t tag = 0;      // this wave's step tags in wflag
-    // bumps of this pass start past min(max X, max Y) (both extensions need c above one of them)
-    const uint32_t mlo0 = doL ? (doR ? min(maxX, maxY) : maxX) : maxY;
-    const uint32_t mlo = max(mlo0, kid_lo == 0 ? 0u : kid_lo - 1u);
+    // the domain rows start past min(max X, max Y) already; a later pass starts at its kid_lo
+    const uint32_t mlo = kid_lo == 0 ? 0u : kid_lo - 1u;
     for (uint32_t win = d0; win < d1; win += kExpWin) {
-        const uint32_t n = min(kExpWin, d1 - win);
-        {   // the window's rows and the exclusive scan of their lengths (rows 2t, 2t + 1 per thread)
+        const uint32_t n0 = min(kExpWin, d1 - win);
+        uint32_t n;  // the window's rows where X => Y holds (block-uniform)
+        {   // the window's sids probed (2t, 2t + 1 per thread): the rows where X => Y holds with a
+            // non-empty suffix past mlo, compacted, with the exclusive scan of the suffix lengths
             const uint32_t j = 2 * threadIdx.x;
-            const uint2 r0 = j < n ? dl[win + j] : make_uint2(0u, 0u);
-            const uint2 r1 = j + 1 < n ? dl[win + j + 1] : make_uint2(0u, 0u);
-            const uint32_t pr = r0.y + r1.y, inc = wave_incl_scan(pr);
-            if (lane == 63) wsum[wv] = inc;
+            uint32_t st[2] = {0u, 0u}, ln[2] = {0u, 0u}, fv[2] = {0u, 0u}, ok[2] = {0u, 0u};
+#pragma unroll
+            for (uint32_t u = 0; u < 2; ++u) {
+                if (j + u >= n0) continue;
+                const uint32_t sid = dl[win + j + u];
+                const uint32_t rs = row_off[sid], rl = row_off[sid + 1] - rs;
+                uint32_t f, pm;
+                if (pass == 0) my_full += rl;
+                if (probe(sid, sItm, sXY, nx, nxy, tm, f, pm) && pm + 1u < rl) {
+                    ok[u] = 1u;
+                    st[u] = rs + pm + 1u;
+                    ln[u] = rl - pm - 1u;
+                    fv[u] = f;
+                }
+            }
+            const uint32_t c = ok[0] + ok[1], pr = ln[0] + ln[1];
+            const uint32_t cinc = wave_incl_scan(c), inc = wave_incl_scan(pr);
+            if (lane == 63) {
+                wsum[wv] = inc;
+                wcnt[wv] = cinc;
+            }
             __syncthreads();  // (also: the previous window's LDS and the ctab codes are ready)
-            uint32_t bb = 0, tt = 0;
+            uint32_t bb = 0, tt = 0, cb = 0, ct = 0;
             for (uint32_t k = 0; k < wpb; ++k) {
                 bb += k < wv ? wsum[k] : 0u;
                 tt += wsum[k];
+                cb += k < wv ? wcnt[k] : 0u;
+                ct += wcnt[k];
             }
-            const uint32_t ex = bb + inc - pr;
-            if (j < n) {
-                rowv[j] = make_uint2(ex, r0.x - ex);
-                sfl[j] = make_uint2(0u, 0xFFFFFFFFu);
-            }
-            if (j + 1 < n) {
-                rowv[j + 1] = make_uint2(ex + r0.y, r1.x - (ex + r0.y));
-                sfl[j + 1] = make_uint2(0u, 0xFFFFFFFFu);
+            uint32_t ex = bb + inc - pr, ci = cb + cinc - c;
+#pragma unroll
+            for (uint32_t u = 0; u < 2; ++u) {
+                if (!ok[u]) continue;
+                rowv[ci] = make_uint2(ex, st[u] - ex);
+                sfl[ci] = fv[u];
+                ex += ln[u];
+                ++ci;
             }
             if (threadIdx.x == 0) {
-                rowv[n] = make_uint2(tt, 0u);
-                if (pass == 0) my_ent += tt;
+                rowv[ct] = make_uint2(tt, 0u);
+                if (pass == 0) {
+                    my_ent += tt;
+                    my_hold += ct;
+                }
             }
+            n = ct;
         }
         __syncthreads();
         // an entry's kid code: 1 (a candidate) when its bloom bit is clear (not in X u Y;
@@ -739,10 +864,8 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
         // t, so k_expand_reduce drops it), else the exact code from ctab
         const uint64_t bloom = s_bloom;
         auto code_of = [&](uint32_t c) -> uint32_t { return ((bloom >> (c & 63u)) & 1ull) ? kid_code(ctab, c) : 1u; };
-        uint32_t* sflw = reinterpret_cast<uint32_t*>(sfl);  // [2 j] = firstX, [2 j + 1] = lastY
         // chunks of whole rows [j0, j1) with at most kChunkEnt entries (block-uniform loop).
-        // Every domain row holds X u Y (the bitmap AND): at least 2 entries, so the 65
-        // entries from a step's first one span at most 33 rows.
+        // Every domain row suffix holds an entry, so at most 64 rows start inside a step.
         for (uint32_t j0 = 0; j0 < n;) {
             const uint32_t E0 = rowv[j0].x;
             uint32_t j1 = j0;  // the last j in [j0, n] with start(j) - E0 <= kChunkEnt
@@ -751,23 +874,13 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                 if (rowv[mid].x - E0 <= kChunkEnt) j1 = mid; else hi = mid - 1;
             }
             if (j1 == j0) {
-                // one row longer than a chunk: pass 1 over it, barrier, pass 2 reloading it
+                // one row longer than a chunk: the block walks it
                 const uint32_t rs = rowv[j0].y + E0, len = rowv[j0 + 1].x - E0;
+                const uint32_t fl = sfl[j0], fX = fl & 0xFFFFu, lY = fl >> 16;
                 for (uint32_t q = threadIdx.x; q < len; q += blockDim.x) {
                     const uint2 e = ent[rs + q];
-                    const uint32_t cd = code_of(e.x);
-                    if (cd == 2u) atomicMax(&sflw[2 * j0], e.y & 0xFFFFu);
-                    if (cd == 3u) atomicMin(&sflw[2 * j0 + 1], e.y >> 16);
-                }
-                __syncthreads();
-                const uint2 fl = sfl[j0];
-                const uint32_t fX = fl.x, lY = fl.y;
-                if (fX < lY) {
-                    for (uint32_t q = threadIdx.x; q < len; q += blockDim.x) {
-                        const uint2 e = ent[rs + q];
-                        if (e.x > mlo && code_of(e.x) == 1u)
-                            bump(e.x, e.y, fX, lY, false, false, maxX, maxY, doL, doR, kid_lo, KP, hL, hR);
-                    }
+                    if (e.x > mlo && code_of(e.x) == 1u)
+                        bump(e.x, e.y, fX, lY, false, false, maxX, maxY, doL, doR, kid_lo, KP, hL, hR);
                 }
                 ++j0;
                 continue;
@@ -775,9 +888,6 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
             const uint32_t Tc = rowv[j1].x - E0;
             const uint32_t sw = (Tc + wpb * 64 - 1) / (wpb * 64) * 64;  // entries per wave (<= 64 kEpt)
             const uint32_t qa = E0 + wv * sw, qz = min(E0 + Tc, qa + sw);
-            uint32_t ej[kEpt];
-            uint2 e[kEpt];
-            uint32_t codes = 0;  // 2 bits per step: the entry's kid code (0: no entry)
             if (qa < qz) {
                 // the wave's first row: the last j in [j0, j1) with start(j) <= qa (wave-uniform)
                 uint32_t ja = j0;
@@ -785,27 +895,29 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                     const uint32_t mid = (ja + hi + 1) >> 1;
                     if (rowv[mid].x <= qa) ja = mid; else hi = mid - 1;
                 }
-                uint32_t idx[kEpt];
-                // pass 1a: the row of each entry from the step's row-start mask
+                uint32_t idx[kEpt], ej[kEpt];
+                // the row of each entry from the step's row-start mask
 #pragma unroll
                 for (int u = 0; u < kEpt; ++u) {
                     const uint32_t q0 = qa + 64u * uint32_t(u);  // wave-uniform
                     idx[u] = kNone;
                     ej[u] = 0;
                     if (q0 < qz) {
-                        const uint32_t jl = ja + lane;
+                        const uint32_t jl = ja + 1u + lane;  // the rows after ja (non-empty: <= 64 start in the step)
                         const uint2 rl = jl < j1 ? rowv[jl] : make_uint2(0xFFFFFFFFu, 0u);
-                        const uint32_t pp = rl.x - q0;  // row jl starts pp entries into the step (lane 0: <= 0)
+                        const uint32_t pp = rl.x - q0;  // row jl starts pp entries into the step (>= 1)
                         ++tag;
                         if (jl < j1 && pp - 1u < 63u) wflag[wv][pp] = tag;  // a start inside the step
                         const uint64_t nxt = __ballot(jl < j1 && pp - 1u < 64u);  // starts in (q0, q0 + 64]
                         __builtin_amdgcn_wave_barrier();
                         const uint64_t m = __ballot(wflag[wv][lane] == tag);
-                        // row of lane l = ja + starts at offsets 1..l
+                        // row of lane l = ja + starts at offsets 1..l (lane r - 1 holds row ja + r)
                         const uint32_t r = uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))) +
                                            uint32_t((m >> lane) & 1ull);
-                        const uint32_t ab = uint32_t(__shfl(int(rl.y), int(r), 64));
+                        const uint32_t ya = rowv[ja].y;
+                        const uint32_t ys = uint32_t(__shfl(int(rl.y), int(r == 0u ? 0u : r - 1u), 64));
+                        const uint32_t ab = r == 0u ? ya : ys;
                         if (q0 + lane < qz) {
                             idx[u] = ab + q0 + lane;
                             ej[u] = ja + r;
@@ -813,49 +925,31 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                         ja += uint32_t(__popcll(nxt));
                     }
                 }
-                // pass 1b: every load in flight, then firstX / lastY of the rows
+                uint2 e[kEpt];
 #pragma unroll
-                for (int u = 0; u < kEpt; ++u) e[u] = idx[u] != kNone ? ent[idx[u]] : make_uint2(kNone, 0u);
-#pragma unroll
-                for (int u = 0; u < kEpt; ++u) {
-                    if (idx[u] == kNone) continue;
-                    const uint32_t cd = code_of(e[u].x);
-                    codes |= (cd | 4u) << (3 * u);  // bit 2: an entry
-                    if (cd == 2u) atomicMax(&sflw[2 * ej[u]], e[u].y & 0xFFFFu);
-                    if (cd == 3u) atomicMin(&sflw[2 * ej[u] + 1], e[u].y >> 16);
-                }
-            }
-            __syncthreads();
-            // pass 2: the bumps of the candidates in rows where X => Y holds
-            if (qa < qz) {
+                for (int u = 0; u < kEpt; ++u) e[u] = idx[u] != kNone ? ent[idx[u]] : make_uint2(0u, 0u);
 #pragma unroll
                 for (int u = 0; u < kEpt; ++u) {
-                    if (pass == 0 && ((codes >> (3 * u)) & 4u)) {
-                        my_suf += e[u].x > mlo0 ? 1u : 0u;
-                        const uint2 fv = sfl[ej[u]];
-                        my_val += fv.x < fv.y ? 1u : 0u;
-                    }
-                    if (((codes >> (3 * u)) & 7u) != 5u || e[u].x <= mlo) continue;  // an entry with code 1
-                    const uint2 fl = sfl[ej[u]];
-                    const uint32_t fX = fl.x, lY = fl.y;
-                    if (fX < lY) bump(e[u].x, e[u].y, fX, lY, false, false, maxX, maxY, doL, doR, kid_lo, KP, hL, hR);
+                    if (idx[u] == kNone || e[u].x <= mlo || code_of(e[u].x) != 1u) continue;
+                    const uint32_t fl = sfl[ej[u]];
+                    bump(e[u].x, e[u].y, fl & 0xFFFFu, fl >> 16, false, false, maxX, maxY, doL, doR, kid_lo, KP,
+                         hL, hR);
                 }
             }
-            j0 = j1;  // the next chunk's rows are disjoint: no barrier before its pass 1
+            j0 = j1;  // the next chunk's rows are disjoint
         }
     }
     __syncthreads();
     // the block's histograms -> its dense partial rows [L | R] (k_expand_reduce sums a slot's)
     uint32_t* prow = part + (uint64_t(pass) * geo.nblk + blockIdx.x) * 2 * KP;
     for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) prow[k] = dsm[k];
-    if (pass == 0 && threadIdx.x == 0 && my_ent) atomicAdd(&ctl->nent, my_ent);
+    if (pass == 0 && threadIdx.x == 0) {
+        if (my_ent) atomicAdd(&ctl->nwalk, my_ent);
+        if (my_hold) atomicAdd(&ctl->nhold, my_hold);
+    }
     if (pass == 0) {
-        for (int d = 32; d > 0; d >>= 1) {
-            my_suf += uint32_t(__shfl_xor(int(my_suf), d, 64));
-            my_val += uint32_t(__shfl_xor(int(my_val), d, 64));
-        }
-        if (lane == 0 && my_suf) atomicAdd(&ctl->nsuf, my_suf);
-        if (lane == 0 && my_val) atomicAdd(&ctl->nval, my_val);
+        for (int d = 32; d > 0; d >>= 1) my_full += uint32_t(__shfl_xor(int(my_full), d, 64));
+        if (lane == 0 && my_full) atomicAdd(&ctl->nent, my_full);
     }
 }
 
@@ -1465,6 +1559,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     bool use_bm = d->bm.p != nullptr && K > 0 && K <= max_kids;
     DevBuf k_off, k_item, k_first, k_last, k_sup;  // list path rows (SoA)
     DevBuf k_ent, d_kidof, d_kept, d_ksup;  // bitmap path rows (packed) and kid tables
+    DevBuf d_rdir, d_kvoff, d_vfl;          // bitmap path: rank directories and vertical entries of the kids
     uint64_t E2 = 0;
     const unsigned rows_grid = unsigned(std::min<uint64_t>((N * 64 + kBlock - 1) / kBlock, 65536));
     if (use_bm) {
@@ -1507,6 +1602,24 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                    d_kidof.as<uint32_t>(), N, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                    off64.as<uint64_t>(), k_ent.as<uint2>());
                 FSM_LAUNCHED("k_rows_pack", s);
+            }
+            // the kept items' rank directories and vertical entries (k_exp_domain's probes)
+            std::vector<uint32_t> kvoff(size_t(K) + 1, 0);
+            for (uint32_t q = 0; q < K; ++q) kvoff[q + 1] = kvoff[q] + ksup[q];
+            if (kvoff[K] != E2) throw Error(FSM_EDEVICE, "TSR: kept row entries differ from the kept supports");
+            d_kvoff.alloc((size_t(K) + 1) * 4);
+            FSM_HIP(hipMemcpyAsync(d_kvoff.p, kvoff.data(), (size_t(K) + 1) * 4, hipMemcpyHostToDevice, s));
+            d_rdir.alloc(std::max<size_t>(size_t(K) * (d->NW / 4) * 4, 4));
+            hipLaunchKernelGGL(k_rank_dir, dim3(K), dim3(kBlock), 0, s, d->bm.as<uint32_t>(), d->NW,
+                               d_kept.as<uint32_t>(), d_rdir.as<uint32_t>());
+            FSM_LAUNCHED("k_rank_dir", s);
+            d_vfl.alloc(std::max<uint64_t>(E2, 1) * 8);
+            if (N) {
+                hipLaunchKernelGGL(k_vfl, dim3(unsigned(std::min<uint64_t>((N + kBlock - 1) / kBlock, 65536))),
+                                   dim3(kBlock), 0, s, k_off.as<uint32_t>(), k_ent.as<uint2>(), uint32_t(N),
+                                   d->bm.as<uint32_t>(), d->NW, d_kept.as<uint32_t>(), d_rdir.as<uint32_t>(),
+                                   d_kvoff.as<uint32_t>(), d_vfl.as<uint2>());
+                FSM_LAUNCHED("k_vfl", s);
             }
             FSM_HIP(hipStreamSynchronize(s));
         }
@@ -1734,7 +1847,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     const char* seg_name[4] = {use_bm ? "k_exp_domain" : "k_expand", use_bm ? "k_exp_rows" : "",
                                use_bm ? "k_expand_reduce" : "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
-    int64_t exp_suf = 0, exp_val = 0;  // (diagnostics, verbose: entries past mlo / in rows where X => Y holds)
+    int64_t exp_hold = 0, exp_walk = 0;  // domain rows where the rule holds, row entries walked (verbose)
     int64_t seq_next = 0;
     // Take in the results of set x (waits for its launch): records sorted into the
     // cache, and its batch queued for child speculation.
@@ -1764,17 +1877,19 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             const ExpHdr h = x.h_hdr[k];
             nout_all += h.nout;
             if (use_bm) {
-                // algorithmic bytes: domain = the |X|+|Y| bitmap operands + 8 B row bounds read
-                // and 8 B written per domain sid; rows = the domain list + 8 B per row entry
+                // own bytes: domain = the |X|+|Y| bitmap operands + 4 B written per domain sid;
+                // rows = per domain sid its id and row bounds (12 B) and |X u Y| probes (rank
+                // directory 4 B + bitmap words 16 B + vertical entry 8 B) + 8 B per entry walked
                 const uint64_t bmb = uint64_t(r->nx + r->ny) * d->NW * 4;
                 exp_domain += h.nsid;
                 exp_entries += h.nent;
-                exp_suf += h.nsuf;
-                exp_val += h.nval;
+                exp_hold += h.nhold;
+                exp_walk += h.nwalk;
                 exp_bitmap_bytes += int64_t(bmb);
-                seg[0].bytes += int64_t(bmb + 16ull * h.nsid);
-                seg[1].bytes += int64_t(8ull * h.nent + 8ull * h.nsid);
-                // SURVEY: N/8 B per sid-bitmap operand; 4 B token + 4 B first/last per scanned position
+                seg[0].bytes += int64_t(bmb + 4ull * h.nsid);
+                seg[1].bytes += int64_t(8ull * h.nwalk + (12ull + 28ull * (r->nx + r->ny)) * h.nsid);
+                // SURVEY: N/8 B per sid-bitmap operand; 4 B token + 4 B first/last per position of
+                // every row holding X u Y (the reference scans each such sequence whole)
                 seg[0].survey += int64_t(bmb);
                 seg[1].survey += int64_t(8ull * h.nent);
             }
@@ -1939,8 +2054,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             }
         }
         x.blocks = wave_off[nb];
-        if (use_bm && x.dom.bytes < drv_off[nb] * sizeof(uint2))
-            x.dom.alloc(std::max<uint64_t>(drv_off[nb] * sizeof(uint2) * 5 / 4, uint64_t(1) << 20));
+        if (use_bm && x.dom.bytes < drv_off[nb] * 4)
+            x.dom.alloc(std::max<uint64_t>(drv_off[nb] * 4 * 5 / 4, uint64_t(1) << 20));
         hipStream_t s = x.st;  // (shadows the context stream for this launch)
         FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, 2 * kOffB + size_t(nb) * sizeof(Side), hipMemcpyHostToDevice,
                                s));
@@ -1956,15 +2071,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (x.timed) FSM_HIP(hipEventRecord(x.ev[0], s));
             if (use_bm) {
                 hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads), 0, s,
-                                   x.d_sides, d->bm.as<uint32_t>(), d->NW, k_off.as<uint32_t>(), x.d_drv,
-                                   x.dom.as<uint2>(), x.ctl.as<ExpCtl>(), d->vert_off.as<uint64_t>(),
-                                   d->vert_sid.as<uint32_t>());
+                                   x.d_sides, d->bm.as<uint32_t>(), d->NW, x.d_drv, x.dom.as<uint32_t>(),
+                                   x.ctl.as<ExpCtl>(), d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>());
                 FSM_LAUNCHED("k_exp_domain", s);
                 if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
                 hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
-                                   x.d_wave, nb, x.d_drv, x.dom.as<uint2>(), k_ent.as<uint2>(), d_kidof.as<uint32_t>(),
-                                   x.alive.as<uint32_t>(), geo, x.part.as<uint32_t>(), x.ctl.as<ExpCtl>(),
-                                   x.d_ndlw.as<uint32_t>());
+                                   x.d_wave, nb, x.d_drv, x.dom.as<uint32_t>(), k_off.as<uint32_t>(), k_ent.as<uint2>(),
+                                   d_kidof.as<uint32_t>(), x.alive.as<uint32_t>(), geo, x.part.as<uint32_t>(),
+                                   x.ctl.as<ExpCtl>(), x.d_ndlw.as<uint32_t>(),
+                                   DomProbe{d->bm.as<uint32_t>(), d->NW, d->NW / 4, d_rdir.as<uint32_t>(),
+                                            d_kvoff.as<uint32_t>(), d_vfl.as<uint2>()});
                 FSM_LAUNCHED("k_exp_rows", s);
                 if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
                 hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
@@ -2229,10 +2345,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      (long long)expansions, (long long)launches, (long long)gpu_rules, (long long)spec_pushback, wait_ms,
                      prep_ms, post_ms, commit_ms, pop_ms, rp.st.size());
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB; row entries "
-                     "%lld, past mlo %lld, in rows where the rule holds %lld (chunked rows)\n",
-                     (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6, (long long)exp_entries,
-                     (long long)exp_suf, (long long)exp_val);
+        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB; domain sids "
+                     "%lld (row entries %lld), rows where the rule holds %lld, row entries walked %lld\n",
+                     (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6, (long long)exp_domain,
+                     (long long)exp_entries, (long long)exp_hold, (long long)exp_walk);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {
