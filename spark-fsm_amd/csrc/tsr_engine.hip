@@ -48,7 +48,7 @@ constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRI
 constexpr int kExpBatch = 256;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
 constexpr int kMaxBatch = 256;
 constexpr int kExpandBlocks = 4096; // bitmap path: at most this many expansion blocks per rule slot
-constexpr int kExpSpb = 64;         // bitmap path: expected domain sids per expansion block (FSM_TSR_SPB)
+constexpr int kExpSpb = 128;        // bitmap path: expected domain sids per expansion block (FSM_TSR_SPB; swept: 64-512)
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kDlUnroll = 8;        // k_dl: independent words / sids per thread per round
 constexpr int kSpecDepth = 3;       // child speculation: levels per launch
