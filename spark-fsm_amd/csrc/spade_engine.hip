@@ -612,24 +612,19 @@ __global__ __launch_bounds__(kBlock) void k_db_pos(const uint32_t* __restrict__ 
 
 // F2 plan of the DB-direct root: block b histograms, by rank group, the key capacity of
 // the frequent entries of its rpb rows that lie in the member range [mlo, mhi)
-// (temporal <= row's frequent entries, equality <= frequent partners after it) and
-// counts the rows' frequent entries (the root entries, *nroot).
+// (temporal <= row's frequent entries, equality <= frequent partners after it).
 __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __restrict__ row_off,
                                                           const uint32_t* __restrict__ item,
                                                           const uint32_t* __restrict__ rk2, uint32_t R, uint32_t rpb,
                                                           uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
                                                           uint32_t mhi, uint32_t* __restrict__ cap, uint32_t amask,
-                                                          unsigned long long* __restrict__ nroot,
                                                           uint32_t* __restrict__ mem_out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
-    __shared__ uint32_t blk_root;
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
-    if (threadIdx.x == 0) blk_root = 0;
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
     const uint64_t lt = lanemask_lt();
     const uint32_t r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
-    uint32_t my_root = 0;
     for (uint32_t r = r0 + wave; r < r1; r += kF2Waves) {
         const uint32_t rb = row_off[r], e1 = row_off[r + 1];
         // the row's frequent entries (first chunk kept in registers: rows are short)
@@ -641,7 +636,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
             if (b0 == rb) v0 = v;
             len += uint32_t(__popcll(__ballot(e < e1 && !(v & 1u))));
         }
-        my_root += len;
         uint32_t k = 0;
         for (uint32_t b0 = rb; b0 < e1; b0 += 64) {
             const uint32_t e = b0 + lane;
@@ -653,10 +647,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
             k += uint32_t(__popcll(bal));
         }
     }
-    if (lane == 0) atomicAdd(&blk_root, my_root);
     __syncthreads();
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cap[f2_region(g, blockIdx.x, nblk)] = (h[g] + amask) & ~amask;
-    if (threadIdx.x == 0 && blk_root) atomicAdd(nroot, (unsigned long long)blk_root);
 }
 
 // kRoot: the rows are the DB's (row_off32), entries read through rr (DB-direct root)
@@ -2728,9 +2720,11 @@ struct Miner {
             return;
         }
         const bool keyed_done = !root_done && keyed_layout && keyed_count(b, cnt);
+        uint32_t* d_nz = nullptr;  // a zeroed u32 after the counters (the extraction's record count)
         if (!root_done && !keyed_done) {
-            cnt.alloc(std::max<uint64_t>(b.n_cnt, 1) * 4);
-            FSM_HIP(hipMemsetAsync(cnt.p, 0, b.n_cnt * 4, s));
+            cnt.alloc((b.n_cnt + 1) * 4);
+            FSM_HIP(hipMemsetAsync(cnt.p, 0, (b.n_cnt + 1) * 4, s));
+            d_nz = cnt.as<uint32_t>() + b.n_cnt;
         }
         if (!root_done) {
             if (b.E && !keyed_done) {
@@ -2814,17 +2808,22 @@ struct Miner {
             // one pass, unordered records at block cursors; rare overflow: extract again at the exact size
             uint32_t cap_recs = uint32_t(std::min<uint64_t>(std::max<uint64_t>(uint64_t(nrows) * 4, 4096), b.n_cnt));
             // the records land in mapped pinned host memory: one stream sync per batch
-            DevBuf d_n(4);
+            DevBuf d_n;
+            uint32_t* dn = d_nz;  // zeroed with the counters (a retry or the keyed count: its own)
             for (int attempt = 0; nrows; ++attempt) {
                 PinnedBuf* pb = ctx->pinned_big(size_t(std::max<uint32_t>(cap_recs, 1)) * sizeof(FreqRec));
-                FSM_HIP(hipMemsetAsync(d_n.p, 0, 4, s));
+                if (attempt > 0 || dn == nullptr) {
+                    if (d_n.p == nullptr) d_n.alloc(4);
+                    dn = d_n.as<uint32_t>();
+                    FSM_HIP(hipMemsetAsync(dn, 0, 4, s));
+                }
                 const size_t tk = clk->begin("k_freq_recs");
                 hipLaunchKernelGGL(k_freq_recs, dim3(grid), dim3(kBlock), 0, s, d_rows.as<DRow>(), nrows,
                                    b.d_cls.as<DClass>(), cnt.as<uint32_t>(), minsup, rlo,
-                                   static_cast<FreqRec*>(pb->dev), cap_recs, d_n.as<uint32_t>());
+                                   static_cast<FreqRec*>(pb->dev), cap_recs, dn);
                 FSM_LAUNCHED("k_freq_recs", s);
                 clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4));
-                FSM_HIP(hipMemcpyAsync(&pend[1], d_n.p, 4, hipMemcpyDeviceToHost, s));
+                FSM_HIP(hipMemcpyAsync(&pend[1], dn, 4, hipMemcpyDeviceToHost, s));
                 sync();
                 const uint32_t nf = uint32_t(pend[1] & 0xFFFFFFFFu);
                 if (nf <= cap_recs) {
@@ -3277,7 +3276,6 @@ struct Miner {
                 const uint64_t ce = uint64_t(kE2Waves) * kE2Range;
                 const unsigned g2 = unsigned(std::min<uint64_t>((Eg + ce - 1) / ce, emit_grid_cap()));
                 d_long.alloc(std::max<uint64_t>(Eg / 65 + 1, 1) * 4);
-                FSM_HIP(hipMemsetAsync(cursor.as<char>() + 8, 0, 4, s));
 #define FSM_EMIT2(WW, RT)                                                                                       \
     hipLaunchKernelGGL((k_emit2<WW, RT>), dim3(g2), dim3(kE2Block), 0, s, uint32_t(Eg), rr, sp.cid,                  \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
@@ -3329,10 +3327,11 @@ struct Miner {
             // writes every child entry once
             const uint64_t rd = rootdb ? Eg * (8 + 8 * uint64_t(W)) : b.E * entry_bytes();
             clk->end(tk, int64_t(rd + total * entry_bytes()), int64_t((b.E + total) * survey_entry_bytes()));
-            FSM_HIP(hipMemcpyAsync(&pend[0], cursor.p, 8, hipMemcpyDeviceToHost, s));
-            FSM_HIP(hipMemcpyAsync(&pend[7], cursor.as<char>() + 12, 4, hipMemcpyDeviceToHost, s));
+            // the whole cursor block back in one copy: pend[6] = entries written, pend[7] = long
+            // runs | run-length flag << 32
+            FSM_HIP(hipMemcpyAsync(&pend[6], cursor.p, 16, hipMemcpyDeviceToHost, s));
         } else {
-            pend[0] = 0;
+            pend[6] = 0;
             pend[7] = 0;
         }
         // no sync: the host prepares the next count while the emit runs; the runs must add
@@ -3344,8 +3343,8 @@ struct Miner {
     void check_emit() {
         if (!pend_check) return;
         pend_check = false;
-        const uint64_t written = pend[0];
-        if (pend[7] & 0xFFFFFFFFu)
+        const uint64_t written = pend[6];
+        if (pend[7] >> 32)
             throw Error(FSM_ELIMIT, "SPADE: a class holds more than 65535 entries of one sequence");
         if (written != pend_total)
             throw Error(FSM_EDEVICE, "SPADE emit: wrote " + std::to_string(written) + " child entries, expected " +
@@ -3404,23 +3403,23 @@ struct Miner {
         }
         upload(root.rk2, rk2);
         root.mem_db.alloc(std::max<int64_t>(db->E, 1) * 4);
-        DevBuf cap(geo.nd * 4), nroot(8);
+        DevBuf cap(geo.nd * 4);
         root.f2_base.alloc((geo.nd + 1) * 8);
-        FSM_HIP(hipMemsetAsync(nroot.p, 0, 8, s));
         const size_t tk = clk->begin("k_f2_plan");
         hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,
                            db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), root.rk2.as<uint32_t>(), geo.R,
                            geo.rpb, geo.pm, geo.G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(), f2_align() - 1,
-                           nroot.as<unsigned long long>(), root.mem_db.as<uint32_t>());
+                           root.mem_db.as<uint32_t>());
         FSM_LAUNCHED("k_f2_plan", s);
         clk->end(tk, int64_t(db->R) * 4 + db->E * 8 + int64_t(geo.nd) * 4);
         scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), geo.nd, s);
-        pend[2] = pend[4] = 0;
+        pend[2] = 0;
         FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + geo.nd, 8, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipMemcpyAsync(&pend[4], nroot.p, 8, hipMemcpyDeviceToHost, s));
         root_meta(root, freq_items, f1);
+        // the root entries: one per (sequence, frequent item), so the frequent items' supports add up to them
+        uint64_t E0 = 0;
+        for (uint32_t it : freq_items) E0 += f1[it];
         sync();
-        const uint64_t E0 = pend[4];
         if (E0 >= kNone) throw Error(FSM_ELIMIT, "SPADE: more than 2^32 root entries");
         if (pend[2] >= (uint64_t(1) << 32) - 4096) {  // region cursors are u32: the slab path counts it
             root.recycle();
