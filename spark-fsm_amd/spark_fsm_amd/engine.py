@@ -176,13 +176,14 @@ class Engine:
         return MinedRules(self._L, out)
 
     def kernel_stats(self):
-        """[{name, launches, alg_bytes, ms}] of the last mine call (device time, HIP events)."""
+        """[{name, launches, alg_bytes, survey_bytes, ms}] of the last mine call (device time, HIP
+        events; alg_bytes: the kernel's own layout, survey_bytes: SURVEY §8(d) units)."""
         n = ctypes.c_int32()
         check(self._L.fsm_get_kernel_stats(self._ctx, None, 0, ctypes.byref(n)), self._ctx)
         arr = (_lib.KernelStat * max(n.value, 1))()
         check(self._L.fsm_get_kernel_stats(self._ctx, arr, n.value, ctypes.byref(n)), self._ctx)
-        return [{"name": k.name.decode(), "launches": k.launches, "alg_bytes": k.alg_bytes, "ms": k.ms}
-                for k in arr[:n.value]]
+        return [{"name": k.name.decode(), "launches": k.launches, "alg_bytes": k.alg_bytes,
+                 "survey_bytes": k.survey_bytes, "ms": k.ms} for k in arr[:n.value]]
 
     def stats(self):
         st = _lib.Stats()
