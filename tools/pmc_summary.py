@@ -1,7 +1,11 @@
 """Fold rocprofv3 --pmc CSV passes into profiles/pmc_latest.json.
 
-Usage (each pass is its own rocprofv3 run of ONE bench step, see tools/profile.sh):
-    python tools/pmc_summary.py OUT.json DIR_FETCH DIR_WRITE [more dirs...]
+Usage (each pass is its own rocprofv3 run of a bench command, see tools/round_evidence.sh):
+    python tools/pmc_summary.py [--last-mine] OUT.json DIR_FETCH DIR_WRITE [more dirs...]
+
+--last-mine keeps only the dispatches from the last k_f1 on (the last SPADE mine of
+the run: a bench run of a warmup step and one step then reports the steady state,
+without the DB build's one-time kernels and fills).
 
 For every kernel (named as libfsm's fsm_get_kernel_stats names it) the JSON has
 the counter totals over the step's dispatches, in bytes (rocprofv3 reports
@@ -41,11 +45,26 @@ def read_dir(d):
     return rows
 
 
+def last_mine(rows):
+    """the rows of the dispatches from the last k_f1 on (Dispatch_Id order)"""
+    ids = [int(r.get("Dispatch_Id", 0) or 0) for r in rows if kernel_name(r.get("Kernel_Name", "")) == "k_f1"]
+    if not ids:
+        return rows
+    first = max(ids)
+    return [r for r in rows if int(r.get("Dispatch_Id", 0) or 0) >= first]
+
+
 def main():
-    out, dirs = sys.argv[1], sys.argv[2:]
+    args = sys.argv[1:]
+    only_last = "--last-mine" in args
+    args = [a for a in args if a != "--last-mine"]
+    out, dirs = args[0], args[1:]
     kernels = {}
     for d in dirs:
-        for r in read_dir(d):
+        rows = read_dir(d)
+        if only_last:
+            rows = last_mine(rows)
+        for r in rows:
             name = kernel_name(r.get("Kernel_Name", ""))
             ctr = r.get("Counter_Name", "")
             val = float(r.get("Counter_Value", 0) or 0)
@@ -58,7 +77,8 @@ def main():
     for k in kernels.values():
         k["dispatches"] = len(k["dispatches"])
     with open(out, "w") as f:
-        json.dump({"source": "rocprofv3 --pmc, one bench.py step per pass: " + " ".join(dirs),
+        json.dump({"source": "rocprofv3 --pmc, one pass per counter" + (", the last mine of the run" if only_last
+                                                                             else "") + ": " + " ".join(dirs),
                    "note": "bytes summed over the step's dispatches; FETCH_SIZE uncorrected here",
                    "kernels": kernels}, f, indent=1, sort_keys=True)
     print(json.dumps({n: {c: v for c, v in k.items() if c != "dispatches"} for n, k in kernels.items()})[:2000])

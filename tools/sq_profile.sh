@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ / LDS / TCC counter passes over ONE D1M mine (tools/run_one.py), one
+# SQ / LDS / TCC counter passes over D1M mines (tools/run_one.py, the last of 2 summarised), one
 # rocprofv3 --pmc run per counter group (gfx950 slot limits: 8 SQ, 4 TCC per
 # pass), each under its own time limit.  Output: gpurun_out/sq/<pass>/ and
 # gpurun_out/sq/summary.json (tools/pmc_summary.py).
@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/sq
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${*:-"spade quest --D 1000000 --support 0.001"}
+ARGS=${*:-"spade quest --D 1000000 --support 0.001 --reps 2"}
 cd /tmp
 pass() {
     local name=$1; shift
@@ -21,5 +21,5 @@ pass mix SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_IN
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 cd "$R"
-python3 tools/pmc_summary.py "$OUT/summary.json" "$OUT/issue" "$OUT/mix" "$OUT/fetch" "$OUT/write" > /dev/null
+python3 tools/pmc_summary.py --last-mine "$OUT/summary.json" "$OUT/issue" "$OUT/mix" "$OUT/fetch" "$OUT/write" > /dev/null
 echo "sq profile done"
