@@ -1478,15 +1478,29 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                 const uint32_t incl = wave_incl_scan(nk), excl = incl - nk;
                 const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
                 uint32_t done = 0;
-                for (uint32_t p0 = 0; p0 < total; p0 += 64) {
-                    const uint32_t pp = p0 + lane;
-                    uint32_t ow = 0;  // the owner lane: the largest lane whose first pair index <= pp
+                // the owner lane of pair pp: the largest lane whose first pair index <= pp
+                auto owner_of = [&](uint32_t pp) {
+                    uint32_t ow = 0;
 #pragma unroll
                     for (uint32_t stp = 32; stp > 0; stp >>= 1) {
                         const uint32_t cand = ow + stp;
                         if (uint32_t(__shfl(int(excl), int(cand), 64)) <= pp) ow = cand;
                     }
-                    const uint32_t o_k0 = uint32_t(__shfl(int(k0), int(ow), 64));
+                    return ow;
+                };
+                // the kid slot of each step is loaded one step ahead (its owner search needs no
+                // result of the step before), so the load's latency overlaps a step's shuffles
+                uint32_t ow_n = owner_of(lane);
+                uint32_t q_n = uint32_t(__shfl(int(k0), int(ow_n), 64)) + (lane - uint32_t(__shfl(int(excl), int(ow_n), 64)));
+                uint32_t slot_n = lane < total ? kid_slot[q_n] : 0u;
+                for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+                    const uint32_t pp = p0 + lane;
+                    const uint32_t ow = ow_n, q = q_n, slot = slot_n;
+                    if (p0 + 64 < total) {
+                        ow_n = owner_of(pp + 64);
+                        q_n = uint32_t(__shfl(int(k0), int(ow_n), 64)) + (pp + 64 - uint32_t(__shfl(int(excl), int(ow_n), 64)));
+                        slot_n = pp + 64 < total ? kid_slot[q_n] : 0u;
+                    }
                     const uint32_t o_ex = uint32_t(__shfl(int(excl), int(ow), 64));
                     const uint32_t o_rs = uint32_t(__shfl(int(rs), int(ow), 64));
                     const uint32_t o_re = uint32_t(__shfl(int(re), int(ow), 64));
@@ -1494,8 +1508,6 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                     const uint32_t o_done = uint32_t(__shfl(int(done), int(ow), 64));
                     const uint64_t o_mk = W == 1 ? __shfl(mk, int(ow), 64) : 0ull;
                     const bool live = pp < total;
-                    const uint32_t q = o_k0 + (pp - o_ex);
-                    const uint32_t slot = live ? kid_slot[q] : 0u;
                     const uint32_t ct = slot & 1u;
                     const uint32_t target = (slot & ~1u) | (ct == kSeq ? 0u : (o_lt >> 16));  // partner member id
                     // lower_bound of target in lanes [o_rs, o_re): 6 fixed steps
