@@ -214,7 +214,14 @@ struct Side {
     uint32_t nx, ny, doL, doR;
     uint32_t maxX, maxY;
     uint32_t drv;    // bitmap path: the rarest item of X u Y
-    uint32_t lmode;  // bitmap path: 1 = the domain from drv's sid list (short) probed in the other bitmaps
+    uint32_t lmode;  // bitmap path: 1 = the domain from drv's sid list (short) probed in the other bitmaps;
+                     // 2 = the domain from the parent rule's kept rows (pl, pn) and the new item pc
+    uint32_t pc;     // lmode 2: the item the rule added to its parent (to X when pleft, else to Y)
+    uint32_t pleft;
+    uint32_t pn;     // lmode 2: the parent's kept rows
+    uint32_t kb;     // this rule's kept rows: at most kb (its support) ...
+    uint64_t pl;     // lmode 2: the parent's first entry in the kept-rows arena
+    uint64_t ko;     // ... written from arena entry ko (kNoList: none kept)
     uint32_t X[kMaxSide];
     uint32_t Y[kMaxSide];
 };
@@ -237,7 +244,10 @@ struct ExpCtl {
     uint32_t nent;   // bitmap path: row entries of the domain sids (SURVEY's scan)
     uint32_t nhold;  // bitmap path: domain rows where X => Y holds (with a candidate past mlo)
     uint32_t nwalk;  // bitmap path: row entries the row kernel walks (those rows' suffixes)
+    uint32_t nkeep;  // bitmap path: domain rows kept for the rule's children (k_exp_rows, pass 0)
+    uint32_t pad[3];
 };
+constexpr uint64_t kNoList = ~uint64_t(0);
 
 // histogram bump (no returned value: the lanes' atomics stay in flight) that
 // also records the item the first time it is touched in this expansion, so the
@@ -339,7 +349,9 @@ struct ExpRec {
     uint32_t c, tl, dl, tr;
 };
 struct ExpHdr {
-    uint32_t nout, nx, nsid, nent, nhold, nwalk, pad[2];
+    uint32_t nout, nx, nsid, nent, nhold, nwalk;
+    uint32_t ln;  // bitmap path: the rows the rule kept (in the arena at its slot's ko, if <= kb)
+    uint32_t pad;
 };
 
 // List path: visit the items this expansion touched, keep the counts >= t
@@ -381,6 +393,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_collect(uint32_t* __restrict_
 __device__ __forceinline__ void publish_slots(ExpCtl* __restrict__ ctlb, ExpHdr* __restrict__ hdrb, uint32_t nslot) {
     for (uint32_t b = threadIdx.x; b < nslot; b += blockDim.x) {
         ExpCtl& c = ctlb[b];
+        hdrb[b].ln = c.nkeep;
+        c.nkeep = 0;
         hdrb[b].nout = c.nout;
         hdrb[b].nx = c.nx;
         hdrb[b].nsid = c.nsid;
@@ -597,6 +611,7 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
     __shared__ uint32_t b_base;
     const uint32_t k = blockIdx.y;
     const Side& side = sides[k];
+    if (side.lmode == 2) return;  // the domain is the parent's kept rows (k_exp_rows reads them)
     const uint32_t nxy = side.nx + side.ny;
     for (uint32_t q = threadIdx.x; q < nxy; q += blockDim.x) sIt[q] = q < side.nx ? side.X[q] : side.Y[q - side.nx];
     __syncthreads();
@@ -677,10 +692,10 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
 }
 
 // A domain sid's firstX (max over X of the item's first itemset) and lastY (min over
-// Y of the last), and the row position of side item tm, from the kept items'
-// vertical entries: rank of the sid in the item's bitmap (rank directory +
-// popcounts) -> vfl.  Two dependent loads per item, the items' loads in flight
-// together.
+// Y of the last), and the row positions of max X and max Y (the sides' last items),
+// from the kept items' vertical entries: rank of the sid in the item's bitmap (rank
+// directory + popcounts) -> vfl.  Two dependent loads per item, the items' loads in
+// flight together.
 struct DomProbe {
     const uint32_t* bm;
     uint32_t NW, NW4;
@@ -688,9 +703,9 @@ struct DomProbe {
     const uint32_t* kvoff;
     const uint2* vfl;
     __device__ __forceinline__ bool operator()(uint32_t sid, const uint32_t* sIt, const uint32_t* sKid, uint32_t nx,
-                                               uint32_t nxy, uint32_t tm, uint32_t& fl, uint32_t& pm) const {
+                                               uint32_t nxy, uint32_t& fl, uint32_t& pX, uint32_t& pY) const {
         uint32_t fX = 0, lY = 0xFFFFu;
-        pm = 0;
+        pX = pY = 0;
         for (uint32_t t0 = 0; t0 < nxy; t0 += 4) {
             uint2 v[4];
 #pragma unroll
@@ -707,7 +722,8 @@ struct DomProbe {
                 const uint32_t t = t0 + u;
                 if (t >= nxy) break;
                 if (t < nx) fX = max(fX, v[u].x & 0xFFFFu); else lY = min(lY, v[u].x >> 16);
-                if (t == tm) pm = v[u].y;
+                if (t == nx - 1u) pX = v[u].y;
+                if (t == nxy - 1u) pY = v[u].y;
             }
         }
         fl = fX | (lY << 16);
@@ -746,7 +762,7 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                                                       const uint32_t* __restrict__ kid_of,
                                                       const uint32_t* __restrict__ alive, ExpGeo geo,
                                                       uint32_t* __restrict__ part, ExpCtl* __restrict__ ctlb,
-                                                      uint32_t* __restrict__ ndlw, DomProbe probe) {
+                                                      uint32_t* __restrict__ ndlw, DomProbe probe, uint4* arena) {
     extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];  // hist L [KP] | hist R [KP] | ctab
     // window rows: x = first flat entry (exclusive scan of the lengths), y = row start in
     // `ent` minus x (u32 wrap: the ent index of flat entry q is y + q)
@@ -757,6 +773,7 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
     __shared__ uint32_t sXY[2 * kMaxSide];           // X then Y, as kids
     __shared__ uint32_t sItm[2 * kMaxSide];          // X then Y, as items
     __shared__ uint32_t wsum[kXBlock / 64], wcnt[kXBlock / 64];
+    __shared__ uint32_t s_kbase;                     // the window's first kept row (pass 0)
     const uint32_t KP = geo.KP, pass = blockIdx.y, kid_lo = pass * KP;
     uint32_t* hL = dsm;
     uint32_t* hR = dsm + KP;
@@ -782,12 +799,19 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
         sXY[k] = kid_of[it];
     }
     wflag[wv][lane] = 0;
-    // this block's share of the slot's domain
-    const uint32_t nd = ctl->nsid;
+    // this block's share of the slot's domain: the sids of the bitmap AND (k_exp_domain), or the
+    // parent rule's kept rows (lmode 2)
+    const bool pmode = side.lmode == 2;
+    const uint32_t nd = pmode ? side.pn : ctl->nsid;
     const uint32_t d0 = uint32_t(uint64_t(nd) * bx / nbx), d1 = uint32_t(uint64_t(nd) * (bx + 1) / nbx);
     const uint32_t* dl = dom + dom_off[b];
-    // the side item at min(max X, max Y) (sides ascend by item): a row's candidates lie past it
-    const uint32_t tm = doL ? (doR ? (side.maxX < side.maxY ? nx - 1u : nxy - 1u) : nx - 1u) : nxy - 1u;
+    const uint4* dlp = arena + (pmode ? side.pl : 0ull);  // (arena: read here, written below; no restrict)
+    const bool keep = side.ko != kNoList;
+    uint4* kp = arena + (keep ? side.ko : 0ull);  // the rule's kept rows (for its children)
+    // a row's candidates lie past min(max X, max Y) (sides ascend by item): its position is max X's
+    // when max X is the smaller (or only X extends), else max Y's
+    const bool use_px = doL && (!doR || side.maxX < side.maxY);
+    const uint32_t pkid = pmode ? kid_of[side.pc] : 0u;
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nxy; k += blockDim.x) {  // X -> code 2, Y -> code 3
         const uint32_t c = sXY[k], sh = (c & 15u) * 2u;
@@ -809,21 +833,52 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
         const uint32_t n0 = min(kExpWin, d1 - win);
         uint32_t n;  // the window's rows where X => Y holds (block-uniform)
         {   // the window's sids probed (2t, 2t + 1 per thread): the rows where X => Y holds with a
-            // non-empty suffix past mlo, compacted, with the exclusive scan of the suffix lengths
+            // non-empty suffix past mlo, compacted, with the exclusive scan of the suffix lengths.
+            // A parent-list row probes only the added item: X => Y held there for the parent, the
+            // child holds where the item is present and keeps first X before last Y
             const uint32_t j = 2 * threadIdx.x;
             uint32_t st[2] = {0u, 0u}, ln[2] = {0u, 0u}, fv[2] = {0u, 0u}, ok[2] = {0u, 0u};
+            uint4 kv[2];
 #pragma unroll
             for (uint32_t u = 0; u < 2; ++u) {
                 if (j + u >= n0) continue;
-                const uint32_t sid = dl[win + j + u];
+                uint32_t sid, f = 0, pX = 0, pY = 0;
+                bool hold;
+                if (pmode) {
+                    const uint4 pe = dlp[win + j + u];  // (sid, firstX | lastY << 16, pos max X, pos max Y)
+                    sid = pe.x;
+                    const uint32_t* bmc = probe.bm + uint64_t(side.pc) * probe.NW;
+                    hold = (bmc[sid >> 5] >> (sid & 31u)) & 1u;
+                    if (hold) {
+                        const uint32_t r = bm_rank(bmc, probe.rdir + uint64_t(pkid) * probe.NW4, sid);
+                        const uint2 v = probe.vfl[probe.kvoff[pkid] + r];
+                        uint32_t fX = pe.y & 0xFFFFu, lY = pe.y >> 16;
+                        pX = pe.z;
+                        pY = pe.w;
+                        if (side.pleft) {
+                            fX = max(fX, v.x & 0xFFFFu);
+                            pX = v.y;
+                        } else {
+                            lY = min(lY, v.x >> 16);
+                            pY = v.y;
+                        }
+                        f = fX | (lY << 16);
+                        hold = fX < lY;
+                    }
+                } else {
+                    sid = dl[win + j + u];
+                    hold = probe(sid, sItm, sXY, nx, nxy, f, pX, pY);
+                }
+                if (!hold) continue;
                 const uint32_t rs = row_off[sid], rl = row_off[sid + 1] - rs;
-                uint32_t f, pm;
-                if (pass == 0) my_full += rl;
-                if (probe(sid, sItm, sXY, nx, nxy, tm, f, pm) && pm + 1u < rl) {
+                if (pass == 0) my_full += rl;  // (SURVEY basis: the rows where the rule holds, whole)
+                const uint32_t pm = use_px ? pX : pY;
+                if (pm + 1u < rl) {
                     ok[u] = 1u;
                     st[u] = rs + pm + 1u;
                     ln[u] = rl - pm - 1u;
                     fv[u] = f;
+                    kv[u] = make_uint4(sid, f, pX, pY);
                 }
             }
             const uint32_t c = ok[0] + ok[1], pr = ln[0] + ln[1];
@@ -841,6 +896,7 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                 ct += wcnt[k];
             }
             uint32_t ex = bb + inc - pr, ci = cb + cinc - c;
+            const uint32_t ci0 = ci;
 #pragma unroll
             for (uint32_t u = 0; u < 2; ++u) {
                 if (!ok[u]) continue;
@@ -854,9 +910,17 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                 if (pass == 0) {
                     my_ent += tt;
                     my_hold += ct;
+                    s_kbase = ct ? atomicAdd(&ctl->nkeep, ct) : 0u;
                 }
             }
             n = ct;
+            if (pass == 0 && keep) {  // the kept rows, for the rule's children (s_kbase: barrier)
+                __syncthreads();
+                uint32_t kc = s_kbase + ci0;  // (more than kb: the host drops the list)
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u)
+                    if (ok[u] && kc < side.kb) kp[kc++] = kv[u];
+            }
         }
         __syncthreads();
         // an entry's kid code: 1 (a candidate) when its bloom bit is clear (not in X u Y;
@@ -1104,7 +1168,11 @@ struct Rule {
     bool expandLR = false;
     bool dropped = false;  // a speculated child its parent's commit did not register
     int8_t inset = -1;     // replay: the launch set expanding it (results not yet taken in), or -1
+    bool pleft = false;    // derived by adding pc to its parent's X (else to Y)
     int32_t res = -1;      // replay: its expansion results (slot of the result pool), or -1
+    uint32_t ln = 0, pn = 0, pc = 0;
+    uint64_t loff = kNoList;   // its kept domain rows in the arena (ln of them), after its expansion
+    uint64_t ploff = kNoList;  // its parent's (pn of them): its own domain is a subset of those rows
 };
 
 // Rules and their items in large chunks that never move (a c4 replay makes millions
@@ -1283,6 +1351,12 @@ struct Replay {
         const uint32_t* x = st.X(&r);
         r.k1 = uint64_t(sup) << 32 | uint64_t(mx) << 16 | uint64_t(my);
         r.k2 = uint64_t(x[0]) << 32 | (mx > 1 ? x[1] : x[mx]);
+        if (src && src->loff != kNoList) {  // the parent's kept rows: the child's domain probes only pc there
+            r.ploff = src->loff;
+            r.pn = src->ln;
+            r.pc = ax != kNone ? ax : ay;
+            r.pleft = ax != kNone;
+        }
         return &r;
     }
     // AlgoTopSeqRules.save
@@ -1712,6 +1786,33 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const char* v = std::getenv("FSM_TSR_SHARD");
         return !(v && v[0] == '0');
     }();
+    // Kept-row lists (bitmap path, unsharded): an expansion keeps the rows where its rule holds
+    // with a non-empty suffix (sid, firstX | lastY, max X / max Y positions) in a per-mine device
+    // arena; a child rule's domain is then its parent's list with only the added item probed
+    // (a child holds only where its parent does).  Rules whose parent list did not fit the arena
+    // probe the whole bitmap AND.  FSM_TSR_PLIST=0 turns the lists off.
+    const bool plist = use_bm && !shard_exp && [] {
+        const char* v = std::getenv("FSM_TSR_PLIST");
+        return !(v && v[0] == '0');
+    }();
+    // The arena is a ring: a launch writes its rules' lists (each at most the rule's support)
+    // at the head, at most acap / 8 entries (else it keeps none), so two launches in flight
+    // never reach a list within acap / 2 of the head, the lists a child may read.
+    DevBuf arena;
+    uint64_t acap = 0;   // arena entries (16 B)
+    uint64_t ahead = 0;  // the ring's head (entries written, monotonic; a list's position mod acap)
+    if (plist) {
+        size_t fr = 0, tot = 0;
+        FSM_HIP(hipMemGetInfo(&fr, &tot));
+        // lists for about the whole mine: the rows where a rule holds summed over the expansions
+        // reach a few thousand per sequence (c4: 2.0 G entries)
+        acap = std::min<uint64_t>({fr / 4, uint64_t(64) << 30,
+                                   std::max<uint64_t>(uint64_t(64) << 20, uint64_t(d->NW) * 32 * 4096 * sizeof(uint4))}) /
+               sizeof(uint4);
+        if (const char* v = std::getenv("FSM_TSR_ARENA_MB"))
+            acap = (std::strtoull(v, nullptr, 10) << 20) / sizeof(uint4);
+        if (acap) arena.alloc(acap * sizeof(uint4));
+    }
     struct ExpSet {
         DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part, dom;
         std::unique_ptr<PinnedBuf> stage, pin;
@@ -1724,6 +1825,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         uint32_t *h_rcnt = nullptr, *d_rcnt = nullptr;  // bitmap path: records per reduce block
         std::vector<Rule*> batch;
         std::vector<char> drv_in_x;
+        std::vector<uint64_t> kmono;  // bitmap path: each slot's kept-row list (ring position; kNoList: none)
         uint32_t la = 0, lz = 0;  // slot sharding: this rank's slots [la, lz) of the batch (else all)
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
         // the set's own stream: the two sets' launches are independent, so the GPU runs
@@ -1838,6 +1940,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const char* v = std::getenv("FSM_TSR_SPB");
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
     }();
+    const uint64_t pl_spb = [] {  // parent-list rows per row block (one probe each: cheaper than a domain sid)
+        const char* v = std::getenv("FSM_TSR_PLSPB");
+        return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
+    }();
     // per-kernel device time: every 16th launch records one set of events and reads
     // them back when it finishes (ctx->kstats rows)
     struct Seg {
@@ -1848,6 +1954,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                use_bm ? "k_expand_reduce" : "k_expand_collect", use_bm ? "k_dl" : "k_publish"};
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
     int64_t exp_hold = 0, exp_walk = 0;  // domain rows where the rule holds, row entries walked (verbose)
+    int64_t exp_plist = 0;               // expansions whose domain came from the parent's kept rows (verbose)
     int64_t seq_next = 0;
     // Take in the results of set x (waits for its launch): records sorted into the
     // cache, and its batch queued for child speculation.
@@ -1879,19 +1986,27 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             if (use_bm) {
                 // own bytes: domain = the |X|+|Y| bitmap operands + 4 B written per domain sid;
                 // rows = per domain sid its id and row bounds (12 B) and |X u Y| probes (rank
-                // directory 4 B + bitmap words 16 B + vertical entry 8 B) + 8 B per entry walked
-                const uint64_t bmb = uint64_t(r->nx + r->ny) * d->NW * 4;
-                exp_domain += h.nsid;
+                // directory 4 B + bitmap words 16 B + vertical entry 8 B), or per parent row 16 B
+                // and one probe (plist), + 8 B per entry walked + 16 B per kept row written
+                const bool pm = x.h_sides[k].lmode == 2;
+                const uint64_t bmb = pm ? 0ull : uint64_t(r->nx + r->ny) * d->NW * 4;
+                const uint64_t ndom = pm ? r->pn : h.nsid;
+                exp_domain += ndom;
                 exp_entries += h.nent;
                 exp_hold += h.nhold;
                 exp_walk += h.nwalk;
+                exp_plist += pm ? 1 : 0;
                 exp_bitmap_bytes += int64_t(bmb);
-                seg[0].bytes += int64_t(bmb + 4ull * h.nsid);
-                seg[1].bytes += int64_t(8ull * h.nwalk + (12ull + 28ull * (r->nx + r->ny)) * h.nsid);
+                seg[0].bytes += int64_t(bmb + 4ull * (pm ? 0ull : h.nsid));
+                seg[1].bytes += int64_t(8ull * h.nwalk + (pm ? 44ull : 12ull + 28ull * (r->nx + r->ny)) * ndom +
+                                        (x.kmono[k] != kNoList ? 16ull * h.ln : 0ull));
                 // SURVEY: N/8 B per sid-bitmap operand; 4 B token + 4 B first/last per position of
-                // every row holding X u Y (the reference scans each such sequence whole)
+                // every sequence where the rule holds (the reference scans each of them whole)
                 seg[0].survey += int64_t(bmb);
                 seg[1].survey += int64_t(8ull * h.nent);
+                // the rule's kept rows (more than its support: the list was cut, none kept)
+                r->loff = x.kmono[k] != kNoList && h.ln <= x.h_sides[k].kb ? x.kmono[k] : kNoList;
+                r->ln = h.ln;
             }
             if (h.nout > ecap) throw Error(FSM_ELIMIT, "TSR: expansion candidate buffer overflow");
             if (!use_bm && x.drv_in_x[k] && h.nx != r->nX)
@@ -2018,7 +2133,22 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             sd.maxY = ry[r->ny - 1];
             std::copy(rx, rx + r->nx, sd.X);
             std::copy(ry, ry + r->ny, sd.Y);
-            if (use_bm) {
+            sd.pc = sd.pleft = sd.pn = sd.kb = 0;
+            sd.pl = 0;
+            sd.ko = kNoList;
+            if (use_bm && plist && r->ploff != kNoList && r->ploff + acap / 2 >= ahead) {
+                // the parent's kept rows (still in the ring) are the domain: only the added item is
+                // probed there
+                wave_off[k + 1] = wave_off[k] + std::clamp<uint64_t>((uint64_t(r->pn) + pl_spb - 1) / pl_spb, 1,
+                                                                     grid.expand);
+                drv_off[k + 1] = drv_off[k];
+                sd.drv = 0;
+                sd.lmode = 2;
+                sd.pc = r->pc;
+                sd.pleft = r->pleft ? 1u : 0u;
+                sd.pn = r->pn;
+                sd.pl = r->ploff % acap;
+            } else if (use_bm) {
                 // bitmap path: row blocks sized by the expected domain (about twice the rule's
                 // support: sids holding X u Y in either order), exp_spb sids per block; the
                 // domain list holds at most the support of the rarest item of X u Y
@@ -2039,6 +2169,20 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                     for (uint32_t q = 0; q < r->ny; ++q) if (sup[ry[q]] < sup[drv]) { drv = ry[q]; x.drv_in_x[k] = 0; }
                 drv_off[k] = voff[drv];
                 wave_off[k + 1] = wave_off[k] + (voff[drv + 1] - voff[drv]);
+            }
+        }
+        x.kmono.assign(nb, kNoList);
+        if (plist && acap) {  // the slots' kept-row lists at the ring's head, each at most the rule's support
+            uint64_t need = 0;
+            for (uint32_t k = 0; k < nb; ++k) need += bp[k]->sup;
+            if (need && need <= acap / 8) {
+                if (ahead % acap + need > acap) ahead += acap - ahead % acap;  // (a list never wraps)
+                for (uint32_t k = 0; k < nb; ++k) {
+                    x.h_sides[k].ko = ahead % acap;
+                    x.h_sides[k].kb = bp[k]->sup;
+                    x.kmono[k] = ahead;
+                    ahead += bp[k]->sup;
+                }
             }
         }
         if (use_bm && wave_off[nb] > max_blocks) {
@@ -2080,7 +2224,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                                    d_kidof.as<uint32_t>(), x.alive.as<uint32_t>(), geo, x.part.as<uint32_t>(),
                                    x.ctl.as<ExpCtl>(), x.d_ndlw.as<uint32_t>(),
                                    DomProbe{d->bm.as<uint32_t>(), d->NW, d->NW / 4, d_rdir.as<uint32_t>(),
-                                            d_kvoff.as<uint32_t>(), d_vfl.as<uint2>()});
+                                            d_kvoff.as<uint32_t>(), d_vfl.as<uint2>()},
+                                   arena.as<uint4>());
                 FSM_LAUNCHED("k_exp_rows", s);
                 if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
                 hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
@@ -2346,9 +2491,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      prep_ms, post_ms, commit_ms, pop_ms, rp.st.size());
     if (ctx->opts.verbose)
         std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB; domain sids "
-                     "%lld (row entries %lld), rows where the rule holds %lld, row entries walked %lld\n",
+                     "%lld (row entries %lld), rows where the rule holds %lld, row entries walked %lld; "
+                     "rules on their parent's kept rows %lld\n",
                      (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6, (long long)exp_domain,
-                     (long long)exp_entries, (long long)exp_hold, (long long)exp_walk);
+                     (long long)exp_entries, (long long)exp_hold, (long long)exp_walk, (long long)exp_plist);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {
