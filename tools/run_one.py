@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--minconf", type=float, default=0.5)
     ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--head", type=int, default=0, help="mine only the first HEAD sequences")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime per process, see _lib.py)
@@ -37,6 +38,8 @@ def main():
         ds = gen.quest(a.D or 100000, seed=1)
     else:
         ds = getattr(gen, a.shape)(seed=1, **kw)
+    if a.head:
+        ds = ds.head(a.head)
     mode = fsm.MODE_SPADE if a.algo == "spade" else fsm.MODE_TSR
     with fsm.Engine(0, verbose=a.verbose) as eng:
         db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, mode)
