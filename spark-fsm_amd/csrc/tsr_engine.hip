@@ -53,6 +53,7 @@ constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kDlUnroll = 8;        // k_dl: independent words / sids per thread per round
 constexpr int kSpecDepth = 6;       // child speculation: levels per launch
 constexpr int kSpecMax = 512;       // child speculation: rules per level
+constexpr int kExpSets = 2;         // launch sets (buffers, stream, events) in flight
 // FSM_TSR_GRID="expand,collect,dl" overrides the per-launch grids (tuning sweeps)
 struct TsrGrid {
     unsigned expand = kExpandBlocks, collect = kCollectBlocks, dl = kDlBlocks;
@@ -1796,8 +1797,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         return !(v && v[0] == '0');
     }();
     // The arena is a ring: a launch writes its rules' lists (each at most the rule's support)
-    // at the head, at most acap / 8 entries (else it keeps none), so two launches in flight
-    // never reach a list within acap / 2 of the head, the lists a child may read.
+    // at the head, at most acap / (4 nsets) entries (else it keeps none), so the launches in
+    // flight never reach a list within acap / 2 of the head, the lists a child may read.
     DevBuf arena;
     uint64_t acap = 0;   // arena entries (16 B)
     uint64_t ahead = 0;  // the ring's head (entries written, monotonic; a list's position mod acap)
@@ -1847,9 +1848,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 (void)hipStreamDestroy(st);
             }
         }
-    } xs[2];
+    };
+    const int nsets = [] {  // launch sets in flight (FSM_TSR_SETS, 2-4)
+        const char* v = std::getenv("FSM_TSR_SETS");
+        return v ? std::clamp(std::atoi(v), 2, 4) : kExpSets;
+    }();
+    std::unique_ptr<ExpSet[]> xs_own(new ExpSet[nsets]);
+    ExpSet* const xs = xs_own.get();
     const bool set_streams = [] { const char* v = std::getenv("FSM_TSR_STREAMS"); return !(v && v[0] == '1'); }();
-    for (ExpSet& x : xs) {
+    for (int xi = 0; xi < nsets; ++xi) {
+        ExpSet& x = xs[xi];
         if (set_streams) {
             FSM_HIP(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
             x.own_stream = true;
@@ -1935,6 +1943,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     double last_log_ms = now_ms();  // verbose progress line every 20 s
     double prep_ms = 0, post_ms = 0, commit_ms = 0, pop_ms = 0;  // host time split (verbose summary)
+    double fill_ms = 0;  // launch prep: descriptor fill (the rest is the HIP calls)
 
     const uint64_t exp_spb = [] {  // bitmap path: target domain sids per expansion block (FSM_TSR_SPB, tuning)
         const char* v = std::getenv("FSM_TSR_SPB");
@@ -2084,9 +2093,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // expand `batch` on a free set (finishing the older busy one first when both are
     // busy): enqueue the launch and return; finish() takes the results in
     auto launch = [&](const std::vector<Rule*>& batch, int depth) {
-        ExpSet* xp = !xs[0].busy ? &xs[0] : (!xs[1].busy ? &xs[1] : nullptr);
-        if (!xp) {
-            xp = xs[0].seq < xs[1].seq ? &xs[0] : &xs[1];
+        ExpSet* xp = nullptr;
+        for (int xi = 0; xi < nsets && !xp; ++xi)
+            if (!xs[xi].busy) xp = &xs[xi];
+        if (!xp) {  // every set busy: the oldest launch finishes first
+            xp = &xs[0];
+            for (int xi = 1; xi < nsets; ++xi)
+                if (xs[xi].seq < xp->seq) xp = &xs[xi];
             finish(*xp);
         }
         ExpSet& x = *xp;
@@ -2175,7 +2188,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         if (plist && acap) {  // the slots' kept-row lists at the ring's head, each at most the rule's support
             uint64_t need = 0;
             for (uint32_t k = 0; k < nb; ++k) need += bp[k]->sup;
-            if (need && need <= acap / 8) {
+            if (need && need <= acap / (4 * uint64_t(nsets))) {
                 if (ahead % acap + need > acap) ahead += acap - ahead % acap;  // (a list never wraps)
                 for (uint32_t k = 0; k < nb; ++k) {
                     x.h_sides[k].ko = ahead % acap;
@@ -2200,6 +2213,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.blocks = wave_off[nb];
         if (use_bm && x.dom.bytes < drv_off[nb] * 4)
             x.dom.alloc(std::max<uint64_t>(drv_off[nb] * 4 * 5 / 4, uint64_t(1) << 20));
+        fill_ms += now_ms() - tl0;
         hipStream_t s = x.st;  // (shadows the context stream for this launch)
         FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, 2 * kOffB + size_t(nb) * sizeof(Side), hipMemcpyHostToDevice,
                                s));
@@ -2480,15 +2494,15 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         launch(batch, 0);
         spec_pushback += int64_t(batch.size()) - 1;
     }
-    for (ExpSet& x : xs)  // speculation still in flight when the replay ended
-        if (x.busy) finish(x);
+    for (int xi = 0; xi < nsets; ++xi)  // speculation still in flight when the replay ended
+        if (xs[xi].busy) finish(xs[xi]);
     if (ctx->opts.verbose)
         std::fprintf(stderr,
                      "[fsm tsr] expansions %lld in %lld launches (%lld rules expanded, %lld pushed back), %.0f ms waiting on the "
-                     "GPU; host: %.0f ms launch prep, %.0f ms result intake, %.0f ms commit, %.0f ms batch pops; %zu rules "
+                     "GPU; host: %.0f ms launch prep (%.0f descriptors), %.0f ms result intake, %.0f ms commit, %.0f ms batch pops; %zu rules "
                      "made\n",
                      (long long)expansions, (long long)launches, (long long)gpu_rules, (long long)spec_pushback, wait_ms,
-                     prep_ms, post_ms, commit_ms, pop_ms, rp.st.size());
+                     prep_ms, fill_ms, post_ms, commit_ms, pop_ms, rp.st.size());
     if (ctx->opts.verbose)
         std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB; domain sids "
                      "%lld (row entries %lld), rows where the rule holds %lld, row entries walked %lld; "
