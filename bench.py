@@ -157,8 +157,9 @@ def c2_leg(fsm, gen, cpu_reps, steps=20):
 def tsr_leg(fsm, gen, cpu_seconds, cpu_reps, cpu):
     """BASELINE config 4 (TSR, 990,002 Kosarak-shaped sequences, k = 1000,
     minconf 0.5): one mine after a warmup mine, expansions/s, the roofline of
-    its dominant kernel (SURVEY §8(d) TSR unit: 12 B per row entry scanned +
-    the sid-bitmap operands, per k_expand_bm launch) and the CPU restatement
+    its dominant kernel (SURVEY §8(d) TSR unit: 8 B per position of every
+    sequence where the expanded rule holds, whole rows, summed over the
+    kernel's timed launches) and the CPU restatement
     on a bounded sample of the same DB (expansions/s)."""
     k, minconf = 1000, 0.5
     ds = gen.kosarak(D=990002, seed=1)
@@ -181,13 +182,16 @@ def tsr_leg(fsm, gen, cpu_seconds, cpu_reps, cpu):
            "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": ach, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "kernel_ms": dom["ms"],
                         "alg_bytes": dom["survey_bytes"], "launches": dom["launches"],
-                        "bytes_basis": "SURVEY §8(d) TSR unit for the row kernel: 4 B token + 4 B first/last per "
-                                       "scanned row position (8 B per packed (kid, first|last) entry); the sid-bitmap "
-                                       "operands (N/8 B each) are k_exp_domain's; kernel time sampled every 16th "
-                                       "launch with HIP events",
+                        "bytes_basis": "SURVEY §8(d) TSR unit for the row kernel: 4 B token + 4 B first/last "
+                                       "per position of every sequence where the expanded rule holds, whole rows (the "
+                                       "reference scans each such sequence); the sid-bitmap operands (N/8 B each) are "
+                                       "k_exp_domain's; kernel time sampled every 16th launch with HIP events",
                         "own_bytes": dom["alg_bytes"], "own_frac": ach_own / HBM_PEAK_GBS,
-                        "own_bytes_basis": "tsr_engine.hip: 8 B per scanned row entry + 8 B per domain sid + "
-                                           "the partial histogram rows written"},
+                        "own_bytes_basis": "tsr_engine.hip k_exp_rows: 8 B per row entry walked (the suffix past "
+                                           "min(max X, max Y) of the rows where the rule holds) + per domain sid 12 B "
+                                           "and 28 B per item of X u Y probed (rank directory, bitmap words, vertical "
+                                           "entry), or 44 B per parent kept row (one probe) + 16 B per kept row "
+                                           "written + the partial histogram rows written"},
            "kernels": [{"name": q["name"], "launches": q["launches"], "ms": round(q["ms"], 1)} for q in ks]}
     if cpu:
         # the restatement needs hours at 990K sequences, so both sides run the same
