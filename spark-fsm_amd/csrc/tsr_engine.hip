@@ -223,6 +223,8 @@ struct Side {
     uint32_t kb;     // this rule's kept rows: at most kb (its support) ...
     uint64_t pl;     // lmode 2: the parent's first entry in the kept-rows arena
     uint64_t ko;     // ... written from arena entry ko (kNoList: none kept)
+    uint64_t hx;     // hashes of the item set X (the |sids(X u {c})| memo's keys)
+    uint32_t hx2, pad2;
     uint32_t X[kMaxSide];
     uint32_t Y[kMaxSide];
 };
@@ -504,6 +506,46 @@ constexpr int kEpt = FSM_TSR_EPT;           // row entries per lane per chunk (r
 constexpr uint32_t kChunkEnt = uint32_t(kXBlock) * kEpt;  // entries of one flat chunk
 constexpr uint32_t kPassKids = 4096;        // kids per LDS histogram pass (2 x 16 KiB)
 constexpr uint32_t kMaxKids = 65536;        // bitmap path: kept items (kid codes 16 KiB of LDS)
+
+// |sids(X u {c})| memo (bitmap path): open addressing over uint4 entries (64-bit key of the
+// item set X u {c}, 32-bit check, count), written by k_dl, read by k_expand_reduce of later
+// launches.  An entry is written once (key by CAS, then check and count in one 8-byte store)
+// and every count is final, so a reader sees either a miss or the exact count.
+struct DlMemo {
+    uint4* tab;     // nullptr: no memo
+    uint32_t mask;  // entries - 1 (a power of two)
+};
+constexpr uint32_t kMemoProbe = 8;
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ void memo_key(uint64_t hx, uint32_t hx2, uint32_t c, uint64_t& key, uint32_t& chk) {
+    key = mix64(hx ^ ((uint64_t(c) + 1ull) * 0x9E3779B97F4A7C15ull)) | 1ull;
+    chk = uint32_t(mix64(uint64_t(hx2) << 32 | c) >> 32) | 1u;
+}
+__device__ __forceinline__ uint32_t memo_find(const DlMemo& m, uint64_t key, uint32_t chk) {
+    uint32_t h = uint32_t(key >> 20) & m.mask;
+    for (uint32_t k = 0; k < kMemoProbe; ++k, h = (h + 1) & m.mask) {
+        const uint4 e = m.tab[h];
+        const uint64_t ek = uint64_t(e.x) | (uint64_t(e.y) << 32);
+        if (ek == 0) return 0u;
+        if (ek == key) return e.z == chk ? e.w : 0u;
+    }
+    return 0u;
+}
+__device__ __forceinline__ void memo_put(const DlMemo& m, uint64_t key, uint32_t chk, uint32_t v) {
+    uint32_t h = uint32_t(key >> 20) & m.mask;
+    for (uint32_t k = 0; k < kMemoProbe; ++k, h = (h + 1) & m.mask) {
+        unsigned long long* kp = reinterpret_cast<unsigned long long*>(&m.tab[h].x);
+        const unsigned long long old = atomicCAS(kp, 0ull, (unsigned long long)key);
+        if (old == 0ull || old == key) {
+            *reinterpret_cast<unsigned long long*>(&m.tab[h].z) = uint64_t(chk) | (uint64_t(v) << 32);
+            return;
+        }
+    }
+}
 
 struct ExpGeo {       // kernel view of one launch's geometry
     uint32_t K, KP;   // kept items, kids per pass
@@ -1029,7 +1071,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __rest
                                                           const uint32_t* __restrict__ kept,
                                                           ExpCtl* __restrict__ ctlb, ExpRec* __restrict__ outb,
                                                           uint32_t cap, uint4* __restrict__ dlw,
-                                                          uint32_t* __restrict__ ndlw, uint32_t* __restrict__ rcnt) {
+                                                          uint32_t* __restrict__ ndlw, uint32_t* __restrict__ rcnt,
+                                                          const Side* __restrict__ sides, DlMemo memo) {
     __shared__ uint32_t wsum[kBlock / 64];
     const uint32_t b = blockIdx.y, pass = blockIdx.z, KP = geo.KP, kid_lo = pass * KP;
     const uint64_t r0 = blk_off[b], r1 = blk_off[b + 1];
@@ -1061,9 +1104,16 @@ __global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __rest
         if (keep) {
             const uint32_t idx = at + uint32_t(__popcll(bal & lanemask_lt()));
             const uint32_t it = kept[kid_lo + c];
-            out[idx] = ExpRec{it, tl, 0u, tr};
-            // |sids(X u {c})| of a left extension comes from k_dl
-            if (tl >= geo.t) dlw[atomicAdd(ndlw, 1u)] = make_uint4(b, it, kid_lo + c0 + idx, 0u);
+            // |sids(X u {c})| of a left extension: from the memo, else from k_dl
+            uint32_t dl = 0;
+            if (tl >= geo.t && memo.tab) {
+                uint64_t key;
+                uint32_t chk;
+                memo_key(sides[b].hx, sides[b].hx2, it, key, chk);
+                dl = memo_find(memo, key, chk);
+            }
+            out[idx] = ExpRec{it, tl, dl, tr};
+            if (tl >= geo.t && !dl) dlw[atomicAdd(ndlw, 1u)] = make_uint4(b, it, kid_lo + c0 + idx, 0u);
         }
         n += tot;
         __syncthreads();  // wsum is rewritten next round
@@ -1083,7 +1133,7 @@ __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, c
                                                const uint32_t* __restrict__ vert_sid, const uint4* __restrict__ dlw,
                                                const uint32_t* __restrict__ ndlw, ExpRec* __restrict__ outb,
                                                uint32_t cap, ExpCtl* __restrict__ ctlb, ExpHdr* __restrict__ hdrb,
-                                               uint32_t nslot) {
+                                               uint32_t nslot, DlMemo memo) {
     __shared__ uint32_t red[kBlock / 64];
     if (blockIdx.x == 0) publish_slots(ctlb, hdrb, nslot);
     const uint32_t n = *ndlw;
@@ -1149,6 +1199,12 @@ __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, c
             uint32_t tot = 0;
             for (uint32_t k = 0; k < blockDim.x / 64; ++k) tot += red[k];
             outb[uint64_t(wk.x) * cap + wk.z].dl = tot;
+            if (memo.tab && tot) {
+                uint64_t key;
+                uint32_t chk;
+                memo_key(side.hx, side.hx2, wk.y, key, chk);
+                memo_put(memo, key, chk, tot);
+            }
         }
         __syncthreads();
     }
@@ -1814,6 +1870,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             acap = (std::strtoull(v, nullptr, 10) << 20) / sizeof(uint4);
         if (acap) arena.alloc(acap * sizeof(uint4));
     }
+    // |sids(X u {c})| memo (bitmap path; FSM_TSR_DLMEMO=0 turns it off): zeroed once per mine
+    DevBuf memo_buf;
+    DlMemo memo{nullptr, 0u};
+    if (use_bm && [] { const char* v = std::getenv("FSM_TSR_DLMEMO"); return !(v && v[0] == '0'); }()) {
+        const uint32_t ent = 1u << 24;  // 256 MiB
+        memo_buf.alloc(size_t(ent) * sizeof(uint4));
+        FSM_HIP(hipMemsetAsync(memo_buf.p, 0, size_t(ent) * sizeof(uint4), s));
+        FSM_HIP(hipStreamSynchronize(s));  // (the launches run on the sets' own streams)
+        memo = DlMemo{memo_buf.as<uint4>(), ent - 1u};
+    }
     struct ExpSet {
         DevBuf TL, DL, TR, seen, list, ctl, d_stage, d_dlw, d_ndlw, part, dom;
         std::unique_ptr<PinnedBuf> stage, pin;
@@ -2149,6 +2215,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             sd.pc = sd.pleft = sd.pn = sd.kb = 0;
             sd.pl = 0;
             sd.ko = kNoList;
+            {  // X's hashes (the memo keys of its left extensions)
+                uint64_t h1 = 0x243F6A8885A308D3ull ^ r->nx, h2 = 0x13198A2E03707344ull ^ r->nx;
+                for (uint32_t q = 0; q < r->nx; ++q) {
+                    h1 = mix64(h1 ^ (uint64_t(rx[q]) + 0x9E3779B97F4A7C15ull));
+                    h2 = mix64(h2 + uint64_t(rx[q]) * 0xD6E8FEB86659FD93ull);
+                }
+                sd.hx = h1;
+                sd.hx2 = uint32_t(h2 >> 32);
+                sd.pad2 = 0;
+            }
             if (use_bm && plist && r->ploff != kNoList && r->ploff + acap / 2 >= ahead) {
                 // the parent's kept rows (still in the ring) are the domain: only the added item is
                 // probed there
@@ -2244,12 +2320,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 if (x.timed) FSM_HIP(hipEventRecord(x.ev[2], s));
                 hipLaunchKernelGGL(k_expand_reduce, dim3(grid.collect, nb, P), dim3(kBlock), 0, s, x.part.as<uint32_t>(),
                                    x.d_wave, geo, d_kept.as<uint32_t>(), x.ctl.as<ExpCtl>(), x.d_rec, ecap,
-                                   x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>(), x.d_rcnt);
+                                   x.d_dlw.as<uint4>(), x.d_ndlw.as<uint32_t>(), x.d_rcnt, x.d_sides, memo);
                 FSM_LAUNCHED("k_expand_reduce", s);
                 if (x.timed) FSM_HIP(hipEventRecord(x.ev[3], s));
                 hipLaunchKernelGGL(k_dl, dim3(grid.dl), dim3(kBlock), 0, s, x.d_sides, d->bm.as<uint32_t>(),
                                    d->NW, d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>(), x.d_dlw.as<uint4>(),
-                                   x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb);
+                                   x.d_ndlw.as<uint32_t>(), x.d_rec, ecap, x.ctl.as<ExpCtl>(), x.d_hdr, nb, memo);
                 FSM_LAUNCHED("k_dl", s);
             } else {
                 const uint64_t waves = wave_off[nb];
