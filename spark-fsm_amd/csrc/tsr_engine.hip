@@ -2303,11 +2303,15 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 x.alive_t = rp.minsup;
             }
             if (x.timed) FSM_HIP(hipEventRecord(x.ev[0], s));
+            bool any_dom = false;  // (every slot on its parent's kept rows: no domain kernel)
+            for (uint32_t k = 0; k < nb && !any_dom; ++k) any_dom = x.h_sides[k].lmode != 2;
             if (use_bm) {
-                hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads), 0, s,
-                                   x.d_sides, d->bm.as<uint32_t>(), d->NW, x.d_drv, x.dom.as<uint32_t>(),
-                                   x.ctl.as<ExpCtl>(), d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>());
-                FSM_LAUNCHED("k_exp_domain", s);
+                if (any_dom) {
+                    hipLaunchKernelGGL(k_exp_domain, dim3((d->NW + kDomWords - 1) / kDomWords, nb), dim3(kDomThreads),
+                                       0, s, x.d_sides, d->bm.as<uint32_t>(), d->NW, x.d_drv, x.dom.as<uint32_t>(),
+                                       x.ctl.as<ExpCtl>(), d->vert_off.as<uint64_t>(), d->vert_sid.as<uint32_t>());
+                    FSM_LAUNCHED("k_exp_domain", s);
+                }
                 if (x.timed) FSM_HIP(hipEventRecord(x.ev[1], s));
                 hipLaunchKernelGGL(k_exp_rows, dim3(unsigned(wave_off[nb]), P), dim3(kXBlock), xlds, s, x.d_sides,
                                    x.d_wave, nb, x.d_drv, x.dom.as<uint32_t>(), k_off.as<uint32_t>(), k_ent.as<uint2>(),
