@@ -1304,17 +1304,27 @@ struct Replay {
             return rule_cmp(*st, a.r, b.r) < 0;
         }
     };
-    // candidates: one max-heap per support value (the comparator's first key),
-    // so a pop sifts through the rules of one support only, and the buckets
-    // below minsup (never expandable: minsup only rises) are freed as it rises.
-    // The heaps are 4-ary (half the levels of a binary heap, a node's children
-    // side by side): the same pop order, the comparator being a total order.
+    // candidates: one bucket per support value (the comparator's first key), so
+    // the buckets below minsup (never expandable: minsup only rises) are freed as
+    // it rises.  A bucket is an unsorted append-only array until it first becomes
+    // the top: it is then sorted once (ascending: the maximum at the back, popped
+    // in O(1) with sequential memory), and later arrivals into it go to a small
+    // side heap.  A pop takes the larger of the sorted back and the side heap's
+    // top: the same order as one heap, the comparator being a total order.
+    // (FSM_TSR_CANDQ=heap: every bucket a 4-ary heap, as in round 3; A/B.)
     struct CandQueue {
-        std::vector<std::vector<HeapEnt>> bucket;
+        struct Bucket {
+            std::vector<HeapEnt> v;     // unsorted, or sorted ascending (sorted = true)
+            std::vector<HeapEnt> side;  // sorted buckets: later arrivals, a binary max-heap
+            bool sorted = false;
+            bool empty() const { return v.empty() && side.empty(); }
+        };
+        std::vector<Bucket> bucket;
         std::vector<uint64_t> occ;  // bit s: bucket[s] non-empty (the next lower bucket is a word scan away)
         uint32_t top_sup = 0, floor = 0;  // buckets < floor are dropped
         size_t n = 0;
         MaxFirst cmp;
+        const bool heap_mode = [] { const char* v = std::getenv("FSM_TSR_CANDQ"); return v && !std::strcmp(v, "heap"); }();
         explicit CandQueue(MaxFirst c) : cmp(c) {}
         bool empty() const { return n == 0; }
         size_t size() const { return n; }
@@ -1325,7 +1335,71 @@ struct Replay {
                 bucket.resize(size_t(sp) + 1);
                 occ.resize(size_t(sp) / 64 + 1, 0);
             }
-            std::vector<HeapEnt>& b = bucket[sp];
+            Bucket& b = bucket[sp];
+            if (heap_mode) {
+                heap4_push(b.v, e);
+            } else if (b.sorted) {
+                b.side.push_back(e);
+                std::push_heap(b.side.begin(), b.side.end(), cmp);
+            } else {
+                b.v.push_back(e);
+            }
+            occ[sp >> 6] |= 1ull << (sp & 63u);
+            if (n == 0 || sp > top_sup) top_sup = sp;
+            ++n;
+        }
+        Bucket& settle() {  // n > 0: move top_sup down to the highest non-empty bucket (sorted)
+            if (bucket[top_sup].empty()) {
+                size_t w = top_sup >> 6;
+                uint64_t m = occ[w] & ((top_sup & 63u) ? ((1ull << (top_sup & 63u)) - 1ull) : 0ull);
+                while (!m) m = occ[--w];
+                top_sup = uint32_t(w * 64 + 63 - size_t(__builtin_clzll(m)));
+            }
+            Bucket& b = bucket[top_sup];
+            if (!heap_mode && !b.sorted) {
+                std::sort(b.v.begin(), b.v.end(), cmp);
+                b.sorted = true;
+            }
+            return b;
+        }
+        // in a sorted bucket: the side heap's top is the maximum
+        bool side_first(const Bucket& b) const { return !b.side.empty() && (b.v.empty() || cmp(b.v.back(), b.side.front())); }
+        const HeapEnt& top() {
+            Bucket& b = settle();
+            if (heap_mode) return b.v.front();
+            return side_first(b) ? b.side.front() : b.v.back();
+        }
+        void pop() {
+            Bucket& b = settle();
+            if (heap_mode) {
+                heap4_pop(b.v);
+            } else if (side_first(b)) {
+                std::pop_heap(b.side.begin(), b.side.end(), cmp);
+                b.side.pop_back();
+            } else {
+                b.v.pop_back();
+            }
+            if (b.empty()) {
+                occ[top_sup >> 6] &= ~(1ull << (top_sup & 63u));
+                std::vector<HeapEnt>().swap(b.v);
+                std::vector<HeapEnt>().swap(b.side);
+                b.sorted = false;
+            }
+            --n;
+        }
+        void drop_below(uint32_t ms) {
+            for (; floor < ms && floor < bucket.size(); ++floor) {
+                Bucket& b = bucket[floor];
+                n -= b.v.size() + b.side.size();
+                std::vector<HeapEnt>().swap(b.v);
+                std::vector<HeapEnt>().swap(b.side);
+                b.sorted = false;
+                occ[floor >> 6] &= ~(1ull << (floor & 63u));
+            }
+            if (floor < ms) floor = ms;
+        }
+        // 4-ary max-heap (FSM_TSR_CANDQ=heap)
+        void heap4_push(std::vector<HeapEnt>& b, const HeapEnt& e) {
             size_t i = b.size();
             b.push_back(e);
             while (i > 0) {
@@ -1335,50 +1409,25 @@ struct Replay {
                 i = up;
             }
             b[i] = e;
-            occ[sp >> 6] |= 1ull << (sp & 63u);
-            if (n == 0 || sp > top_sup) top_sup = sp;
-            ++n;
         }
-        std::vector<HeapEnt>& settle() {  // n > 0: move top_sup down to the highest non-empty bucket
-            if (bucket[top_sup].empty()) {
-                size_t w = top_sup >> 6;
-                uint64_t m = occ[w] & ((top_sup & 63u) ? ((1ull << (top_sup & 63u)) - 1ull) : 0ull);
-                while (!m) m = occ[--w];
-                top_sup = uint32_t(w * 64 + 63 - size_t(__builtin_clzll(m)));
-            }
-            return bucket[top_sup];
-        }
-        const HeapEnt& top() { return settle().front(); }
-        void pop() {
-            std::vector<HeapEnt>& b = settle();
+        void heap4_pop(std::vector<HeapEnt>& b) {
             const HeapEnt last = b.back();
             b.pop_back();
             const size_t m = b.size();
-            if (m) {
-                size_t i = 0;
-                for (;;) {
-                    const size_t c = 4 * i + 1;
-                    if (c >= m) break;
-                    size_t best = c;
-                    const size_t ce = std::min(c + 4, m);
-                    for (size_t j = c + 1; j < ce; ++j)
-                        if (cmp(b[best], b[j])) best = j;
-                    if (!cmp(last, b[best])) break;
-                    b[i] = b[best];
-                    i = best;
-                }
-                b[i] = last;
+            if (!m) return;
+            size_t i = 0;
+            for (;;) {
+                const size_t c = 4 * i + 1;
+                if (c >= m) break;
+                size_t best = c;
+                const size_t ce = std::min(c + 4, m);
+                for (size_t j = c + 1; j < ce; ++j)
+                    if (cmp(b[best], b[j])) best = j;
+                if (!cmp(last, b[best])) break;
+                b[i] = b[best];
+                i = best;
             }
-            if (b.empty()) occ[top_sup >> 6] &= ~(1ull << (top_sup & 63u));
-            --n;
-        }
-        void drop_below(uint32_t ms) {
-            for (; floor < ms && floor < bucket.size(); ++floor) {
-                n -= bucket[floor].size();
-                std::vector<HeapEnt>().swap(bucket[floor]);
-                occ[floor >> 6] &= ~(1ull << (floor & 63u));
-            }
-            if (floor < ms) floor = ms;
+            b[i] = last;
         }
     };
     std::priority_queue<HeapEnt, std::vector<HeapEnt>, MinFirst> krules;
