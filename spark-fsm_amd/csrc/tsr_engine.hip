@@ -224,7 +224,8 @@ struct Side {
     uint64_t pl;     // lmode 2: the parent's first entry in the kept-rows arena
     uint64_t ko;     // ... written from arena entry ko (kNoList: none kept)
     uint64_t hx;     // hashes of the item set X (the |sids(X u {c})| memo's keys)
-    uint32_t hx2, pad2;
+    uint32_t hx2;
+    uint32_t klo;    // bitmap path: the lowest kid ever counted, min(max X, max Y) + 1 (as kids)
     uint32_t X[kMaxSide];
     uint32_t Y[kMaxSide];
 };
@@ -1047,9 +1048,16 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
         }
     }
     __syncthreads();
-    // the block's histograms -> its dense partial rows [L | R] (k_expand_reduce sums a slot's)
+    // the block's histograms -> its partial rows [L | R] (k_expand_reduce sums a slot's).  No kid at
+    // or below min(max X, max Y) is ever counted (candidates lie past it): only the kids above it
+    // are written, and the reduce reads no others
     uint32_t* prow = part + (uint64_t(pass) * geo.nblk + blockIdx.x) * 2 * KP;
-    for (uint32_t k = threadIdx.x; k < 2 * KP; k += blockDim.x) prow[k] = dsm[k];
+    const uint32_t lo_abs = min(maxX, maxY) + 1u;
+    const uint32_t klo = lo_abs > kid_lo ? min(lo_abs - kid_lo, KP) : 0u;
+    for (uint32_t k = klo + threadIdx.x; k < KP; k += blockDim.x) {
+        prow[k] = hL[k];
+        prow[KP + k] = hR[k];
+    }
     if (pass == 0 && threadIdx.x == 0) {
         if (my_ent) atomicAdd(&ctl->nwalk, my_ent);
         if (my_hold) atomicAdd(&ctl->nhold, my_hold);
@@ -1075,6 +1083,8 @@ __global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __rest
                                                           const Side* __restrict__ sides, DlMemo memo) {
     __shared__ uint32_t wsum[kBlock / 64];
     const uint32_t b = blockIdx.y, pass = blockIdx.z, KP = geo.KP, kid_lo = pass * KP;
+    // kids at or below min(max X, max Y) are never counted (k_exp_rows writes none of them)
+    const uint32_t lo_abs = sides[b].klo;
     const uint64_t r0 = blk_off[b], r1 = blk_off[b + 1];
     const uint32_t q = (KP + gridDim.x - 1) / gridDim.x;
     const uint32_t c0 = blockIdx.x * q, c1 = min(KP, c0 + q);
@@ -1086,7 +1096,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __rest
         const uint32_t c = cb + threadIdx.x;
         uint32_t tl = 0, tr = 0;
         bool keep = false;
-        if (c < c1 && kid_lo + c < geo.K) {
+        if (c < c1 && kid_lo + c < geo.K && kid_lo + c >= lo_abs) {
             for (uint64_t r = r0; r < r1; ++r) {
                 tl += rows[r * 2 * KP + c];
                 tr += rows[r * 2 * KP + KP + c];
@@ -1737,13 +1747,16 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         return v ? std::min<uint32_t>(uint32_t(std::strtoul(v, nullptr, 10)), 0xFFFFu) : 0xFFFFu;
     }();
     bool use_bm = d->bm.p != nullptr && K > 0 && K <= max_kids;
+    std::vector<uint32_t> h_kid_of;  // bitmap path: item -> kid (host copy)
     DevBuf k_off, k_item, k_first, k_last, k_sup;  // list path rows (SoA)
     DevBuf k_ent, d_kidof, d_kept, d_ksup;  // bitmap path rows (packed) and kid tables
     DevBuf d_rdir, d_kvoff, d_vfl;          // bitmap path: rank directories and vertical entries of the kids
     uint64_t E2 = 0;
     const unsigned rows_grid = unsigned(std::min<uint64_t>((N * 64 + kBlock - 1) / kBlock, 65536));
     if (use_bm) {
-        std::vector<uint32_t> kid_of(U, kNone), ksup(K);
+        std::vector<uint32_t>& kid_of = h_kid_of;
+        kid_of.assign(U, kNone);
+        std::vector<uint32_t> ksup(K);
         for (uint32_t q = 0; q < K; ++q) {
             kid_of[kept_items[q]] = q;
             ksup[q] = sup[kept_items[q]];
@@ -2272,7 +2285,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 }
                 sd.hx = h1;
                 sd.hx2 = uint32_t(h2 >> 32);
-                sd.pad2 = 0;
+                sd.klo = use_bm ? std::min(h_kid_of[rx[r->nx - 1]], h_kid_of[ry[r->ny - 1]]) + 1u : 0u;
             }
             if (use_bm && plist && r->ploff != kNoList && r->ploff + acap / 2 >= ahead) {
                 // the parent's kept rows (still in the ring) are the domain: only the added item is
