@@ -45,14 +45,14 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxSide = 64;
 constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRID sweep: 4-8 best)
-constexpr int kExpBatch = 256;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
+constexpr int kExpBatch = 384;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
 constexpr int kMaxBatch = 1024;  // FSM_TSR_BATCH ceiling (the slot searches of the kernels)
 constexpr int kExpandBlocks = 4096; // bitmap path: at most this many expansion blocks per rule slot
 constexpr int kExpSpb = 128;        // bitmap path: expected domain sids per expansion block (FSM_TSR_SPB; swept: 64-512)
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kDlUnroll = 8;        // k_dl: independent words / sids per thread per round
 constexpr int kSpecDepth = 6;       // child speculation: levels per launch
-constexpr int kSpecMax = 512;       // child speculation: rules per level
+constexpr int kSpecMax = 768;       // child speculation: rules per level
 constexpr int kExpSets = 2;         // launch sets (buffers, stream, events) in flight
 // FSM_TSR_GRID="expand,collect,dl" overrides the per-launch grids (tuning sweeps)
 struct TsrGrid {
