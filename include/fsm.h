@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FSM_ABI_VERSION 5
+#define FSM_ABI_VERSION 6
 
 /* status codes */
 #define FSM_OK 0
@@ -69,15 +69,29 @@ typedef struct {
     int64_t (*fetch_add)(void* user, int64_t key, int64_t inc);
 } fsm_host_comm;
 
+#define FSM_MAX_DEVICES 16
+
+/* Device selection (1, 2, 4 or 8 GPUs).  Two ways to shard a mine:
+ *  - in-process (the drop-in's way: SPADE.scala:132-133 and TSR.scala:102-103 run on
+ *    one driver thread): ndevices > 1 makes ONE context that drives ndevices ranks,
+ *    rank r on HIP device devices[r] with its own stream, pool and DB replica, one host
+ *    thread per rank, collectives through host memory inside the library.  Every call
+ *    on the context is one call for the caller; the result is the whole mine's.  A
+ *    device may repeat (several ranks on one GPU);
+ *  - one process per GPU (torch.distributed launches): nranks > 1, rank, and RCCL over
+ *    unique_id or host_comm callbacks; each process gets the complete result.
+ * ndevices <= 1 with nranks <= 1 is the single-GPU context on `device`. */
 typedef struct {
-    int32_t device;          /* local HIP device ordinal */
-    int32_t nranks;          /* 1: single GPU; >1: SPADE sharded over ranks (one process per GPU) */
+    int32_t device;          /* local HIP device ordinal (ndevices <= 1) */
+    int32_t nranks;          /* 1: single GPU; >1: sharded over ranks, one process per GPU */
     int32_t rank;            /* this process's rank in [0, nranks) */
     int32_t verbose;         /* 1: per-level trace on stderr */
     uint8_t unique_id[128];  /* RCCL unique id (fsm_comm_unique_id on rank 0), nranks > 1 */
     int64_t mem_budget;      /* device bytes for lattice frontier slabs; 0 = 1/2 of free HBM */
     const fsm_host_comm* host_comm; /* nranks > 1: NULL = RCCL over unique_id, else these callbacks
                                        (must outlive the context) */
+    int32_t ndevices;        /* > 1: in-process ranks on devices[0..ndevices) (nranks must be <= 1) */
+    int32_t devices[FSM_MAX_DEVICES]; /* HIP ordinals of the in-process ranks */
 } fsm_opts;
 
 /* SPADE result: the patterns of List[Pattern] in CSR form.  Pattern p has
@@ -169,8 +183,10 @@ int fsm_comm_unique_id(uint8_t out[128]);
  * The engine shards SPADE's first-level prefix classes with it. */
 int fsm_shard_plan(const uint64_t* volume, int64_t n, int32_t nranks, int32_t* owner);
 /* Collective self-test of the nranks > 1 plumbing (all-reduce, all-gather of
- * ragged blobs) on the context-free transport of opts; no GPU compute when
- * opts->host_comm is set.  0 = every rank saw the expected data. */
+ * ragged blobs, the work-stealing counter) on the context-free transport of opts;
+ * no GPU compute when opts->host_comm is set.  With opts->ndevices > 1 the test runs
+ * the in-process transport on ndevices host threads (no GPU at all).  0 = every rank
+ * saw the expected data. */
 int fsm_comm_selftest(const fsm_opts* opts);
 
 int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out);

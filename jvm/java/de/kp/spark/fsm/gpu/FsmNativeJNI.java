@@ -10,10 +10,12 @@ package de.kp.spark.fsm.gpu;
 public final class FsmNativeJNI {
     private FsmNativeJNI() {}
 
-    /** [support int[], patOff long[], setOff long[], items int[], {total, minsup} long[]] */
-    public static native Object[] spade(int[] sids, String[] lines, double support, int device);
+    /** [support int[], patOff long[], setOff long[], items int[], {total, minsup} long[]].
+     *  devices: the HIP ordinals of the mine's ranks (one: a single GPU; more: one call sharded
+     *  over in-process ranks, rank r on devices[r]). */
+    public static native Object[] spade(int[] sids, String[] lines, double support, boolean dfs, int[] devices);
 
     /** [support int[], confidence double[], anteOff long[], ante int[], consOff long[], cons int[],
      *  {total, finalMinsup} long[]] */
-    public static native Object[] tsr(int[] sids, String[] lines, int k, double minconf, int device);
+    public static native Object[] tsr(int[] sids, String[] lines, int k, double minconf, int[] devices);
 }

@@ -77,11 +77,33 @@ static fsm_db* make_db(JNIEnv* env, fsm_ctx* ctx, int32_t mode, jintArray jsids,
     return db;
 }
 
-static fsm_ctx* make_ctx(JNIEnv* env, jint device) {
+/* devices: the HIP ordinals of the request's ranks (FsmNative.devices, -Dfsm.devices).
+ * One entry: the single-GPU context on that device.  More: ONE context that shards
+ * the mine over in-process ranks, rank r on devices[r] (fsm_opts.ndevices, DESIGN.md
+ * §6): the Spark driver thread (SPADE.scala:132-133, TSR.scala:102-103) makes one
+ * call and gets the whole result back. */
+static fsm_ctx* make_ctx(JNIEnv* env, jintArray jdevices) {
     fsm_opts o;
     memset(&o, 0, sizeof o);
-    o.device = device;
     o.nranks = 1;
+    const jsize nd = jdevices ? (*env)->GetArrayLength(env, jdevices) : 0;
+    if (nd > FSM_MAX_DEVICES) {
+        throw_exception(env, "fsm_ctx_create", FSM_EINVAL, "more devices than FSM_MAX_DEVICES");
+        return NULL;
+    }
+    if (nd > 0) {
+        jint* dv = (*env)->GetIntArrayElements(env, jdevices, NULL);
+        if (!dv) {
+            throw_exception(env, "fsm_ctx_create", FSM_ENOMEM, "device list unavailable");
+            return NULL;
+        }
+        o.device = dv[0];
+        if (nd > 1) {
+            o.ndevices = nd;
+            for (jsize r = 0; r < nd; ++r) o.devices[r] = dv[r];
+        }
+        (*env)->ReleaseIntArrayElements(env, jdevices, dv, JNI_ABORT);
+    }
     fsm_ctx* ctx = NULL;
     const int rc = fsm_ctx_create(&o, &ctx);
     if (rc != FSM_OK) {
@@ -91,20 +113,22 @@ static fsm_ctx* make_ctx(JNIEnv* env, jint device) {
     return ctx;
 }
 
-/* de.kp.spark.fsm.gpu.FsmNativeJNI.spade(int[] sids, String[] lines, double support, int device): Object[] =
+/* de.kp.spark.fsm.gpu.FsmNativeJNI.spade(int[] sids, String[] lines, double support, boolean dfs,
+ *                                        int[] devices): Object[] =
  *   [support: Array[Int], patOff: Array[Long], setOff: Array[Long], items: Array[Int], total+minsup: Array[Long]] */
 JNIEXPORT jobjectArray JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(JNIEnv* env, jclass cls, jintArray jsids,
                                                                        jobjectArray jlines, jdouble support,
-                                                                       jint device) {
+                                                                       jboolean dfs, jintArray jdevices) {
     (void)cls;
-    fsm_ctx* ctx = make_ctx(env, device);
+    fsm_ctx* ctx = make_ctx(env, jdevices);
     if (!ctx) return NULL;
     jobjectArray res = NULL;
     fsm_db* db = make_db(env, ctx, FSM_MODE_SPADE, jsids, jlines);
     fsm_patterns* p = NULL;
     if (db) {
-        /* dfs = 1: SPADEActor calls extractRDDPatterns(dataset, support) with the defaults (SPADE.scala:36) */
-        const int rc = fsm_spade_mine(ctx, db, support, 1, &p);
+        /* dfs as SpadeAlgorithm(support, dfs) takes it (SPADE.scala:132); SPADEActor passes the
+         * default true (SPADE.scala:36, SPADEActor.scala:47) */
+        const int rc = fsm_spade_mine(ctx, db, support, dfs ? 1 : 0, &p);
         if (rc != FSM_OK) throw_exception(env, "fsm_spade_mine", rc, fsm_last_error(ctx));
     }
     if (p) {
@@ -136,14 +160,14 @@ JNIEXPORT jobjectArray JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(JNIEn
     return res;
 }
 
-/* FsmNativeJNI.tsr(int[] sids, String[] lines, int k, double minconf, int device): Object[] =
+/* FsmNativeJNI.tsr(int[] sids, String[] lines, int k, double minconf, int[] devices): Object[] =
  *   [support: Array[Int], confidence: Array[Double], anteOff: Array[Long], ante: Array[Int],
  *    consOff: Array[Long], cons: Array[Int], total+finalMinsup: Array[Long]] */
 JNIEXPORT jobjectArray JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr(JNIEnv* env, jclass cls, jintArray jsids,
                                                                      jobjectArray jlines, jint k, jdouble minconf,
-                                                                     jint device) {
+                                                                     jintArray jdevices) {
     (void)cls;
-    fsm_ctx* ctx = make_ctx(env, device);
+    fsm_ctx* ctx = make_ctx(env, jdevices);
     if (!ctx) return NULL;
     jobjectArray res = NULL;
     fsm_db* db = make_db(env, ctx, FSM_MODE_TSR, jsids, jlines);

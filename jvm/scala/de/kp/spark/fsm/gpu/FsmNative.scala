@@ -30,16 +30,35 @@ object FsmNative {
     }
   }
 
-  /** The GPU device of this JVM's requests: -Dfsm.device=N (default 0). */
+  /** The first GPU device of this JVM's requests: -Dfsm.device=N (default 0). */
   def device: Int = Integer.getInteger("fsm.device", 0)
 
-  def spade(sids: Array[Int], lines: Array[String], support: Double, device: Int): Array[AnyRef] = {
-    ensureLoaded()
-    FsmNativeJNI.spade(sids, lines, support, device)
+  /**
+   * The GPUs one request shards over (SURVEY §8(b): 1, 2, 4 or 8), from -Dfsm.devices:
+   *   absent or "1"  -> Array(device)                   one GPU
+   *   "N"            -> device, device+1, ..., device+N-1
+   *   "0,1,2,3"      -> exactly these ordinals (one may repeat: several ranks on one GPU)
+   * A malformed value surfaces as java.lang.Exception from the call (TrainActor.scala:66).
+   */
+  def devices: Array[Int] = {
+    val v = System.getProperty("fsm.devices", "").trim
+    try {
+      if (v.isEmpty) Array(device)
+      else if (v.contains(",")) v.split(",").map(_.trim.toInt)
+      else (0 until math.max(1, v.toInt)).map(device + _).toArray
+    } catch {
+      case e: NumberFormatException => throw new Exception("bad -Dfsm.devices value: " + v, e)
+    }
   }
 
-  def tsr(sids: Array[Int], lines: Array[String], k: Int, minconf: Double, device: Int): Array[AnyRef] = {
+  def spade(sids: Array[Int], lines: Array[String], support: Double, dfs: Boolean,
+            devices: Array[Int]): Array[AnyRef] = {
     ensureLoaded()
-    FsmNativeJNI.tsr(sids, lines, k, minconf, device)
+    FsmNativeJNI.spade(sids, lines, support, dfs, devices)
+  }
+
+  def tsr(sids: Array[Int], lines: Array[String], k: Int, minconf: Double, devices: Array[Int]): Array[AnyRef] = {
+    ensureLoaded()
+    FsmNativeJNI.tsr(sids, lines, k, minconf, devices)
   }
 }

@@ -18,7 +18,7 @@ object GpuSPADE {
   def extractRDDPatterns(dataset: RDD[(Int, String)], support: Double, dfs: Boolean = true,
                          stats: Boolean = true): List[GpuPattern] = {
     val recs = dataset.collect()
-    val res = FsmNative.spade(recs.map(_._1), recs.map(_._2), support, FsmNative.device)
+    val res = FsmNative.spade(recs.map(_._1), recs.map(_._2), support, dfs, FsmNative.devices)
     val sup = res(0).asInstanceOf[Array[Int]]
     val patOff = res(1).asInstanceOf[Array[Long]]
     val setOff = res(2).asInstanceOf[Array[Long]]

@@ -17,7 +17,7 @@ object GpuTSR {
 
   def extractRDDRules(dataset: RDD[(Int, String)], k: Int, minconf: Double): List[GpuRule] = {
     val recs = dataset.collect()
-    val res = FsmNative.tsr(recs.map(_._1), recs.map(_._2), k, minconf, FsmNative.device)
+    val res = FsmNative.tsr(recs.map(_._1), recs.map(_._2), k, minconf, FsmNative.devices)
     val sup = res(0).asInstanceOf[Array[Int]]
     val conf = res(1).asInstanceOf[Array[Double]]
     val anteOff = res(2).asInstanceOf[Array[Long]]

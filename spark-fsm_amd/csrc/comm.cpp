@@ -19,6 +19,9 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 
@@ -89,21 +92,21 @@ void nccl_check(ncclResult_t r, const char* what) {
 // collective that precedes its first claim.
 class ShmCounters {
   public:
-    static constexpr size_t kSlots = 512;
+    static constexpr size_t kSlots = 512;  // + 1 probe slot (counters_shared)
     explicit ShmCounters(const uint8_t id[128]) {
         uint64_t h = 1469598103934665603ull;  // FNV-1a of the unique id
         for (int k = 0; k < 128; ++k) h = (h ^ id[k]) * 1099511628211ull;
         std::snprintf(name_, sizeof(name_), "/fsm-claims-%016llx", (unsigned long long)h);
         const int fd = shm_open(name_, O_CREAT | O_RDWR, 0600);
         if (fd < 0) return;
-        if (ftruncate(fd, off_t(kSlots * sizeof(int64_t))) == 0) {
-            void* p = mmap(nullptr, kSlots * sizeof(int64_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (ftruncate(fd, off_t((kSlots + 1) * sizeof(int64_t))) == 0) {
+            void* p = mmap(nullptr, (kSlots + 1) * sizeof(int64_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
             if (p != MAP_FAILED) ctr_ = static_cast<int64_t*>(p);
         }
         close(fd);
     }
     ~ShmCounters() {
-        if (ctr_) munmap(ctr_, kSlots * sizeof(int64_t));
+        if (ctr_) munmap(ctr_, (kSlots + 1) * sizeof(int64_t));
     }
     ShmCounters(const ShmCounters&) = delete;
     ShmCounters& operator=(const ShmCounters&) = delete;
@@ -116,11 +119,40 @@ class ShmCounters {
         // slot key % kSlots was last used kSlots keys ago, long past that mine's final gather
         if (ctr_) __atomic_store_n(&ctr_[size_t(key) % kSlots], int64_t(0), __ATOMIC_SEQ_CST);
     }
+    void set_probe(int64_t v) {
+        if (ctr_) __atomic_store_n(&ctr_[kSlots], v, __ATOMIC_SEQ_CST);
+    }
+    int64_t probe() const { return ctr_ ? __atomic_load_n(&ctr_[kSlots], __ATOMIC_SEQ_CST) : 0; }
 
   private:
     char name_[64] = {0};
     int64_t* ctr_ = nullptr;
 };
+
+double comm_timeout_ms(const char* var) {
+    const char* tv = std::getenv(var);
+    return 1000.0 * (tv ? std::max(1.0, std::atof(tv)) : 300.0);
+}
+
+// Whether every rank's ShmCounters are ONE segment (ranks on one node sharing /dev/shm):
+// rank 0 stores a nonce in the probe slot, the nonce is all-gathered, every rank reads
+// the slot back, and the ranks all-reduce whether they saw it.  Ranks on another node
+// (or in a container with its own /dev/shm) have a segment of their own under the same
+// name; without this check each such group would claim every class and the gathered
+// output would hold duplicates.  Collective; false on every rank unless all agree.
+bool counters_shared(Comm& c, ShmCounters& shm) {
+    int64_t nonce = 0;
+    if (c.rank() == 0) {
+        nonce = int64_t((uint64_t(std::chrono::steady_clock::now().time_since_epoch().count()) * 0x9E3779B97F4A7C15ull ^
+                         (uint64_t(getpid()) << 20)) | 1u) & INT64_MAX;
+        shm.set_probe(nonce);
+    }
+    std::vector<int64_t> all(size_t(c.nranks()), 0);
+    c.host_allgather(&nonce, all.data(), sizeof(int64_t), nullptr);
+    uint32_t ok = shm.ok() && shm.probe() == all[0] ? 1u : 0u;
+    c.host_allreduce_u32(&ok, 1, nullptr);
+    return ok == uint32_t(c.nranks());
+}
 
 bool id_set(const uint8_t id[128]) {
     for (int k = 0; k < 128; ++k)
@@ -141,23 +173,42 @@ class RcclComm final : public Comm {
             comm_ = nullptr;
             nccl_check(r, "ncclCommInitRankConfig");
         }
-        const char* tv = std::getenv("FSM_COMM_INIT_TIMEOUT_S");
-        const double limit_ms = 1000.0 * (tv ? std::max(1.0, std::atof(tv)) : 300.0);
         try {
-            wait("ncclCommInitRankConfig", limit_ms);
+            wait("ncclCommInitRankConfig", comm_timeout_ms("FSM_COMM_INIT_TIMEOUT_S"));
         } catch (...) {
-            if (rank == 0) shm_.unlink_name();
+            shm_.unlink_name();
             throw;
         }
-        if (rank == 0) shm_.unlink_name();
+        // every rank has the segment open once the setup completed: each unlinks the name (the
+        // first call removes it; on a multi-node job every node's segment goes)
+        shm_.unlink_name();
+        shared_ = counters_shared(*this, shm_);
     }
     ~RcclComm() override {
         if (comm_) (void)rccl().comm_destroy(comm_);
     }
-    bool has_fetch_add() const override { return shm_.ok(); }
+    bool has_fetch_add() const override { return shared_; }
     int64_t fetch_add(int64_t key, int64_t inc) override { return shm_.fetch_add(key, inc); }
     void reset_counter(int64_t key) override {
         if (rank() == 0) shm_.reset(key);
+    }
+    void host_allreduce_u32(uint32_t* h, size_t n, hipStream_t s) override {
+        if (!n) return;
+        auto* d = static_cast<uint32_t*>(staging(n * 4));
+        FSM_HIP(hipMemcpyAsync(d, h, n * 4, hipMemcpyHostToDevice, s));
+        allreduce_u32(d, n, s);
+        FSM_HIP(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+    }
+    void host_allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        if (!bytes) return;
+        const size_t all = bytes * size_t(nranks());
+        auto* d = static_cast<uint8_t*>(staging(all + ((bytes + 255) & ~size_t(255))));
+        uint8_t* ds = d + all;  // the send block after the receive blocks
+        FSM_HIP(hipMemcpyAsync(ds, send, bytes, hipMemcpyHostToDevice, s));
+        allgather(ds, d, bytes, s);
+        FSM_HIP(hipMemcpyAsync(recv, d, all, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
     }
     void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
         if (n) enqueued(rccl().all_reduce(dev, dev, n, ncclUint32, ncclSum, comm_, s), "ncclAllReduce");
@@ -168,13 +219,13 @@ class RcclComm final : public Comm {
 
   private:
     void enqueued(ncclResult_t r, const char* what) {
-        if (r == ncclInProgress) wait(what, 1e300);
+        if (r == ncclInProgress) wait(what, comm_timeout_ms("FSM_COMM_TIMEOUT_S"));
         else nccl_check(r, what);
     }
     // poll until the communicator leaves ncclInProgress (abort past limit_ms)
     void wait(const char* what, double limit_ms) {
         const double t0 = now_ms();
-        for (;;) {
+        for (int polls = 0;; ) {
             ncclResult_t st = ncclSuccess;
             nccl_check(rccl().comm_get_async_error(comm_, &st), "ncclCommGetAsyncError");
             if (st == ncclSuccess) return;
@@ -187,13 +238,23 @@ class RcclComm final : public Comm {
                 (void)rccl().comm_abort(comm_);
                 comm_ = nullptr;
                 throw Error(FSM_ECOMM, std::string(what) + ": timed out waiting for the peer ranks "
-                                                           "(FSM_COMM_INIT_TIMEOUT_S)");
+                                                           "(FSM_COMM_INIT_TIMEOUT_S / FSM_COMM_TIMEOUT_S)");
             }
-            std::this_thread::yield();
+            // a short spin first (a collective's enqueue normally completes within microseconds),
+            // then 100 us sleeps: a rank whose peer died does not burn a core until the limit
+            if (++polls > 64) std::this_thread::sleep_for(std::chrono::microseconds(100));
+            else std::this_thread::yield();
         }
     }
+    // persistent device staging of the host-memory collectives (grown on demand)
+    void* staging(size_t bytes) {
+        if (stage_.bytes < bytes) stage_.alloc(std::max(bytes, std::max<size_t>(2 * stage_.bytes, size_t(1) << 16)));
+        return stage_.p;
+    }
     ShmCounters shm_;
+    bool shared_ = false;
     ncclComm_t comm_ = nullptr;
+    DevBuf stage_;
 };
 
 // Host callbacks.  Without a fetch_add callback but with a unique id in fsm_opts, the
@@ -207,7 +268,8 @@ class HostComm final : public Comm {
             shm_ = std::make_unique<ShmCounters>(id);
             uint32_t one = 1;
             host_allreduce_u32(&one, 1, nullptr);  // every rank has the segment open
-            if (rank == 0) shm_->unlink_name();
+            shm_->unlink_name();
+            shared_ = counters_shared(*this, *shm_);
         }
     }
     void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
@@ -235,7 +297,7 @@ class HostComm final : public Comm {
         if (cb_.allgather(cb_.user, send, recv, int64_t(bytes)) != 0)
             throw Error(FSM_ECOMM, "host all-gather callback failed");
     }
-    bool has_fetch_add() const override { return cb_.fetch_add != nullptr || (shm_ && shm_->ok()); }
+    bool has_fetch_add() const override { return cb_.fetch_add != nullptr || shared_; }
     int64_t fetch_add(int64_t key, int64_t inc) override {
         if (cb_.fetch_add) return cb_.fetch_add(cb_.user, key, inc);  // (keys are never reused: no reset)
         return shm_ ? shm_->fetch_add(key, inc) : -1;
@@ -247,6 +309,7 @@ class HostComm final : public Comm {
   private:
     fsm_host_comm cb_;
     std::unique_ptr<ShmCounters> shm_;
+    bool shared_ = false;
 };
 
 }  // namespace
@@ -268,7 +331,7 @@ void Comm::host_allgather(const void* send, void* recv, size_t bytes, hipStream_
 }
 
 std::vector<uint8_t> Comm::gather_blobs(const std::vector<uint8_t>& mine, std::vector<size_t>& sizes, hipStream_t s,
-                                        Agreement* agr, uint32_t* extra, size_t n_extra) {
+                                        Agreement* agr, uint32_t* extra, size_t n_extra, bool root_only) {
     const int N = nranks();
     // (lo, hi) u32 halves of each rank's size | 8 failure flags | the caller's extra values
     std::vector<uint32_t> sz(size_t(N) * 2 + 8 + n_extra, 0);
@@ -280,11 +343,15 @@ std::vector<uint8_t> Comm::gather_blobs(const std::vector<uint8_t>& mine, std::v
     if (agr) agr->check(sz.data() + size_t(N) * 2);
     for (size_t k = 0; k < n_extra; ++k) extra[k] = sz[size_t(N) * 2 + 8 + k];
     sizes.assign(size_t(N), 0);
+    for (int r = 0; r < N; ++r) sizes[size_t(r)] = size_t(sz[size_t(r) * 2]) | (size_t(sz[size_t(r) * 2 + 1]) << 32);
+    return gather_var(mine, sizes, s, root_only);
+}
+
+std::vector<uint8_t> Comm::gather_var(const std::vector<uint8_t>& mine, const std::vector<size_t>& sizes,
+                                      hipStream_t s, bool /*root_only*/) {
+    const int N = nranks();
     size_t mx = 0;
-    for (int r = 0; r < N; ++r) {
-        sizes[size_t(r)] = size_t(sz[size_t(r) * 2]) | (size_t(sz[size_t(r) * 2 + 1]) << 32);
-        mx = std::max(mx, sizes[size_t(r)]);
-    }
+    for (size_t v : sizes) mx = std::max(mx, v);
     mx = (mx + 7) & ~size_t(7);
     std::vector<uint8_t> snd(mx, 0), all(mx * size_t(N));
     if (!mine.empty()) std::memcpy(snd.data(), mine.data(), mine.size());
@@ -354,5 +421,161 @@ void Agreement::maybe_inject(const char* phase) const {
     if (std::sscanf(v, "%d,%15s", &r, ph) == 2 && r == comm->rank() && !std::strcmp(ph, phase))
         throw Error(FSM_ELIMIT, std::string(what) + ": injected failure (FSM_INJECT_FAIL, " + phase + ")");
 }
+
+}  // namespace fsm
+
+// ------------------------------------------------------------------ in-process ranks
+namespace fsm {
+
+class InProcHub {
+  public:
+    explicit InProcHub(int n) : n_(n), post_(size_t(n), nullptr) {
+        for (auto& c : ctr_) c.store(0);
+    }
+    int n() const { return n_; }
+    // every rank's pointer of the current exchange (valid between the two barriers)
+    void post(int rank, const void* p) { post_[size_t(rank)] = p; }
+    const void* posted(int rank) const { return post_[size_t(rank)]; }
+    // Generation barrier: a short spin (the ranks usually arrive within microseconds of
+    // each other), then a condition-variable wait.  Throws FSM_ECOMM once aborted.
+    void barrier() {
+        std::unique_lock<std::mutex> g(mu_);
+        if (broken_) throw broken_error();
+        const uint64_t my = gen_;
+        if (++arrived_ == n_) {
+            arrived_ = 0;
+            gen_ = my + 1;
+            agen_.store(my + 1, std::memory_order_release);
+            g.unlock();
+            cv_.notify_all();
+            return;
+        }
+        g.unlock();
+        for (int i = 0; i < 4000; ++i) {
+            if (agen_.load(std::memory_order_acquire) != my) return;
+            if (abroken_.load(std::memory_order_relaxed)) break;
+            if (i > 256) std::this_thread::yield();
+        }
+        g.lock();
+        cv_.wait(g, [&] { return gen_ != my || broken_; });
+        if (gen_ == my) throw broken_error();
+    }
+    void abort() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            broken_ = true;
+            abroken_.store(true);
+        }
+        cv_.notify_all();
+    }
+    bool aborted() {
+        std::lock_guard<std::mutex> g(mu_);
+        return broken_;
+    }
+    void reset() {  // every rank has returned from its call
+        std::lock_guard<std::mutex> g(mu_);
+        broken_ = false;
+        abroken_.store(false);
+        arrived_ = 0;
+    }
+    std::atomic<int64_t>& counter(int64_t key) { return ctr_[size_t(key) % kSlots]; }
+
+  private:
+    static Error broken_error() {
+        return Error(FSM_ECOMM, "in-process rank group: a peer rank failed; the call is aborted on every rank");
+    }
+    static constexpr size_t kSlots = 512;
+    const int n_;
+    std::vector<const void*> post_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int arrived_ = 0;
+    uint64_t gen_ = 0;
+    bool broken_ = false;
+    std::atomic<uint64_t> agen_{0};
+    std::atomic<bool> abroken_{false};
+    std::atomic<int64_t> ctr_[kSlots];
+};
+
+namespace {
+
+class InProcComm final : public Comm {
+  public:
+    InProcComm(std::shared_ptr<InProcHub> hub, int rank) : Comm(hub->n(), rank), hub_(std::move(hub)) {}
+    bool has_fetch_add() const override { return true; }
+    int64_t fetch_add(int64_t key, int64_t inc) override { return hub_->counter(key).fetch_add(inc); }
+    void reset_counter(int64_t key) override {
+        // (the collective that follows on every rank orders this before any claim)
+        if (rank() == 0) hub_->counter(key).store(0);
+    }
+    void host_allreduce_u32(uint32_t* h, size_t n, hipStream_t) override {
+        std::vector<uint32_t> sum(n, 0u);
+        hub_->post(rank(), h);
+        hub_->barrier();
+        for (int r = 0; r < nranks(); ++r) {
+            const auto* v = static_cast<const uint32_t*>(hub_->posted(r));
+            for (size_t i = 0; i < n; ++i) sum[i] += v[i];
+        }
+        hub_->barrier();  // every rank has read every buffer before any is overwritten
+        if (n) std::memcpy(h, sum.data(), n * 4);
+    }
+    void host_allgather(const void* send, void* recv, size_t bytes, hipStream_t) override {
+        hub_->post(rank(), send);
+        hub_->barrier();
+        for (int r = 0; r < nranks(); ++r)
+            if (bytes) std::memcpy(static_cast<uint8_t*>(recv) + size_t(r) * bytes, hub_->posted(r), bytes);
+        hub_->barrier();
+    }
+    void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
+        std::vector<uint32_t> h(n);
+        if (n) FSM_HIP(hipMemcpyAsync(h.data(), dev, n * 4, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        host_allreduce_u32(h.data(), n, s);
+        if (n) FSM_HIP(hipMemcpyAsync(dev, h.data(), n * 4, hipMemcpyHostToDevice, s));
+        FSM_HIP(hipStreamSynchronize(s));
+    }
+    void allgather(const void* dev_send, void* dev_recv, size_t bytes, hipStream_t s) override {
+        std::vector<uint8_t> snd(bytes), rcv(bytes * size_t(nranks()));
+        if (bytes) FSM_HIP(hipMemcpyAsync(snd.data(), dev_send, bytes, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipStreamSynchronize(s));
+        host_allgather(snd.data(), rcv.data(), bytes, s);
+        if (bytes) FSM_HIP(hipMemcpyAsync(dev_recv, rcv.data(), rcv.size(), hipMemcpyHostToDevice, s));
+        FSM_HIP(hipStreamSynchronize(s));
+    }
+
+  protected:
+    // blobs read in place from the posting ranks (no padding); with root_only only rank 0 copies
+    std::vector<uint8_t> gather_var(const std::vector<uint8_t>& mine, const std::vector<size_t>& sizes, hipStream_t,
+                                    bool root_only) override {
+        std::vector<uint8_t> out;
+        hub_->post(rank(), mine.data());
+        hub_->barrier();
+        if (!root_only || rank() == 0) {
+            size_t tot = 0;
+            for (size_t v : sizes) tot += v;
+            out.resize(tot);
+            size_t at = 0;
+            for (int r = 0; r < nranks(); ++r) {
+                if (sizes[size_t(r)]) std::memcpy(out.data() + at, hub_->posted(r), sizes[size_t(r)]);
+                at += sizes[size_t(r)];
+            }
+        }
+        hub_->barrier();
+        return out;
+    }
+
+  private:
+    std::shared_ptr<InProcHub> hub_;
+};
+
+}  // namespace
+
+std::shared_ptr<InProcHub> make_inproc_hub(int nranks) { return std::make_shared<InProcHub>(nranks); }
+std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<InProcHub>& hub, int rank) {
+    return std::make_unique<InProcComm>(hub, rank);
+}
+void inproc_abort(InProcHub& hub) { hub.abort(); }
+bool inproc_aborted(InProcHub& hub) { return hub.aborted(); }
+void inproc_reset(InProcHub& hub) { hub.reset(); }
 
 }  // namespace fsm

@@ -39,8 +39,17 @@ class Comm {
     // agr: the failure agreement rides on the size all-reduce (no round trip of its own):
     // if any rank failed, every rank throws its FSM_E* before the blobs move.  extra[0..n):
     // u32 values summed over the ranks in the same all-reduce.
+    // root_only: only rank 0 needs the concatenation (the others may get an empty result;
+    // the in-process communicator then copies nothing on them).
     std::vector<uint8_t> gather_blobs(const std::vector<uint8_t>& mine, std::vector<size_t>& sizes, hipStream_t s,
-                                      Agreement* agr = nullptr, uint32_t* extra = nullptr, size_t n_extra = 0);
+                                      Agreement* agr = nullptr, uint32_t* extra = nullptr, size_t n_extra = 0,
+                                      bool root_only = false);
+
+  protected:
+    // the blob exchange of gather_blobs once every rank's size is known (sizes[r]):
+    // the default pads every blob to the largest and all-gathers them
+    virtual std::vector<uint8_t> gather_var(const std::vector<uint8_t>& mine, const std::vector<size_t>& sizes,
+                                            hipStream_t s, bool root_only);
 
   private:
     int nranks_, rank_;
@@ -90,6 +99,21 @@ struct Agreement {
 
 std::unique_ptr<Comm> make_comm(const fsm_opts& o);
 void rccl_unique_id(uint8_t out[128]);
+
+// In-process ranks: one fsm_ctx driving fsm_opts.ndevices ranks, one host thread
+// per rank (fsm_api.cpp, Group).  The ranks' collectives meet in a hub in host
+// memory: each rank posts a pointer to its buffer, a barrier, every rank reads the
+// others' buffers, a barrier.  Device buffers are staged through host memory (the
+// exchanged data are KB-sized: F1 histograms, frequent-pair records, per-launch TSR
+// results).  abort() breaks every current and later barrier with FSM_ECOMM, so a
+// rank that fails outside a failure agreement cannot leave its peers blocked;
+// reset() re-arms the hub once every rank has returned.
+class InProcHub;
+std::shared_ptr<InProcHub> make_inproc_hub(int nranks);
+std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<InProcHub>& hub, int rank);
+void inproc_abort(InProcHub& hub);
+bool inproc_aborted(InProcHub& hub);
+void inproc_reset(InProcHub& hub);
 
 // Longest-processing-time assignment of `n` work units with estimated volumes
 // to `nranks` ranks (largest first, ties by index, to the least-loaded rank,

@@ -2,10 +2,18 @@
 // catches everything: no C++ exception crosses the ABI, failures come back as
 // FSM_E* codes with the message in fsm_last_error (the Scala shim turns them
 // into java.lang.Exception so TrainActor records FAILURE, TrainActor.scala:65-67).
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <new>
+#include <thread>
 
 #include "comm.h"
 #include "dev_db.h"
@@ -18,6 +26,30 @@ using fsm::Error;
 namespace {
 
 thread_local std::string g_err;  // errors before a context exists
+
+// FSM_SEGV_TRACE=1: a host fault prints the faulting thread's native backtrace to stderr
+// before the default action (debugging aid for the host code; resolve with addr2line)
+void segv_trace(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    const char msg[] = "[fsm] fatal signal; native backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+void maybe_install_segv_trace() {
+    static const bool once = [] {
+        const char* v = std::getenv("FSM_SEGV_TRACE");
+        if (v && v[0] == '1') {
+            signal(SIGSEGV, segv_trace);
+            signal(SIGBUS, segv_trace);
+            signal(SIGABRT, segv_trace);
+        }
+        return true;
+    }();
+    (void)once;
+}
 
 int fail(fsm_ctx* ctx, int code, const std::string& msg) {
     if (ctx) ctx->err = msg; else g_err = msg;
@@ -64,11 +96,14 @@ template <class T> T* host_copy(const fsm::DevBuf& d, size_t n, hipStream_t s) {
     return h;
 }
 
+int group_make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out);
+
 int make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out) {
     if (!ctx || !out) return fail(ctx, FSM_EINVAL, "null argument");
     *out = nullptr;
     if (src.n < 0 || (src.n > 0 && !src.sids)) return fail(ctx, FSM_EINVAL, "bad record arrays");
     if (mode != FSM_MODE_SPADE && mode != FSM_MODE_TSR) return fail(ctx, FSM_EINVAL, "mode must be SPADE(0) or TSR(1)");
+    if (ctx->group) return group_make_db(ctx, mode, src, out);
     fsm_db* db = new (std::nothrow) fsm_db();
     if (!db) return fail(ctx, FSM_ENOMEM, "host allocation failed");
     db->ctx = ctx;
@@ -86,6 +121,219 @@ int make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out) {
         ctx->stats.ms_flatten = t1 - t0;
         ctx->stats.ms_upload = fsm::now_ms() - t1;
     });
+    if (rc != FSM_OK) {
+        fsm_db_free(db);
+        return rc;
+    }
+    *out = db;
+    return FSM_OK;
+}
+
+}  // namespace
+
+
+// ------------------------------------------------------------------ in-process rank groups
+// fsm_opts.ndevices > 1: one context drives N rank contexts (rank r on devices[r]), each
+// with its own stream, pool, DB replica and an in-process communicator (comm.cpp).  The
+// engines run unchanged on the rank contexts: the sharded mine of DESIGN.md §6, with
+// the ranks as threads of the caller's process instead of processes.  Rank 0 runs on the
+// calling thread, ranks 1..N-1 on persistent worker threads (each keeps its device
+// current), so one call on the group context is one call for the caller.
+namespace fsm {
+
+struct Group {
+    std::shared_ptr<InProcHub> hub;
+    std::vector<fsm_ctx*> ranks;
+    std::vector<int> rc;
+
+    explicit Group(int n) : hub(make_inproc_hub(n)), ranks(size_t(n), nullptr), rc(size_t(n), 0) {
+        for (int r = 1; r < n; ++r) th_.emplace_back([this, r] { work(r); });
+    }
+    ~Group() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    Group(const Group&) = delete;
+    Group& operator=(const Group&) = delete;
+    int n() const { return int(ranks.size()); }
+
+    // fn(r) on every rank at once (rank 0 on the caller); a rank that fails aborts the hub so
+    // that no peer stays blocked in a collective.  Returns the rank whose error to report
+    // (the first one that did not fail only because a peer did), or -1.
+    int run(const std::function<int(int)>& fn) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &fn;
+            left_ = n() - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        one(fn, 0);
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            done_.wait(g, [&] { return left_ == 0; });
+            job_ = nullptr;
+        }
+        inproc_reset(*hub);
+        // the failing rank to report: one whose own message is not a peer's failure, preferably
+        // one that failed before the hub was aborted
+        int first = -1, best = 4;
+        for (int r = 0; r < n(); ++r) {
+            if (rc[size_t(r)] == FSM_OK) continue;
+            const bool msg_peer =
+                ranks[size_t(r)] && ranks[size_t(r)]->err.find("peer rank failed") != std::string::npos;
+            const int score = (msg_peer ? 2 : 0) + (after_abort_[size_t(r)] ? 1 : 0);
+            if (score < best) {
+                best = score;
+                first = r;
+            }
+        }
+        return first;
+    }
+
+  private:
+    void one(const std::function<int(int)>& fn, int r) {
+        int c;
+        try {
+            c = fn(r);
+        } catch (...) {
+            c = FSM_EDEVICE;
+        }
+        rc[size_t(r)] = c;
+        // a rank that fails once the hub is already aborted failed because a peer did
+        after_abort_[size_t(r)] = c != FSM_OK && inproc_aborted(*hub);
+        if (c != FSM_OK) inproc_abort(*hub);
+    }
+    void work(int r) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<int(int)>* job;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                job = job_;
+            }
+            one(*job, r);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<int(int)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int left_ = 0;
+    bool stop_ = false;
+    std::vector<char> after_abort_ = std::vector<char>(size_t(FSM_MAX_DEVICES), 0);
+};
+
+}  // namespace fsm
+
+namespace {
+
+// the group's result: rank `who`'s error (message and code) on the group context,
+// its statistics otherwise
+int group_finish(fsm_ctx* ctx, int who) {
+    fsm::Group& g = *ctx->group;
+    fsm_ctx* r0 = g.ranks[0];
+    if (r0) {
+        ctx->stats = r0->stats;
+        ctx->kstats = r0->kstats;
+    }
+    if (who < 0) {
+        ctx->err.clear();
+        return FSM_OK;
+    }
+    ctx->err = g.ranks[size_t(who)] ? g.ranks[size_t(who)]->err : std::string("rank context creation failed");
+    if (ctx->err.empty()) ctx->err = "rank " + std::to_string(who) + " failed";
+    return g.rc[size_t(who)];
+}
+
+// the collective checks of fsm_comm_selftest on one rank's communicator
+void comm_selftest(fsm::Comm& comm) {
+    const uint32_t N = uint32_t(comm.nranks()), r = uint32_t(comm.rank());
+    {
+        // FSM_INJECT_FAIL="<rank>,selftest": that rank fails before its first collective (the
+        // in-process transport must then release its peers with FSM_ECOMM, not leave them blocked)
+        const char* v = std::getenv("FSM_INJECT_FAIL");
+        char ph[16] = {0};
+        int fr = -1;
+        if (v && std::sscanf(v, "%d,%15s", &fr, ph) == 2 && fr == int(r) && !std::strcmp(ph, "selftest"))
+            throw Error(FSM_ELIMIT, "selftest: injected failure (FSM_INJECT_FAIL)");
+    }
+    std::vector<uint32_t> v(1000);
+    for (uint32_t i = 0; i < v.size(); ++i) v[i] = r + i;
+    comm.host_allreduce_u32(v.data(), v.size(), nullptr);
+    for (uint32_t i = 0; i < v.size(); ++i)
+        if (v[i] != N * i + N * (N - 1) / 2) throw Error(FSM_ECOMM, "selftest: all-reduce mismatch");
+    std::vector<uint8_t> mine(size_t(r) * 3 + 1);
+    for (size_t j = 0; j < mine.size(); ++j) mine[j] = uint8_t(r * 7 + j);
+    std::vector<size_t> sizes;
+    // (the work-stealing counter of the claim test below is reset before this gather, which
+    // also agrees on whether every rank has the shared counters)
+    const int64_t key = comm.next_key();
+    comm.reset_counter(key);
+    uint32_t ex = comm.has_fetch_add() ? 1u : 0u;
+    const std::vector<uint8_t> all = comm.gather_blobs(mine, sizes, nullptr, nullptr, &ex, 1);
+    size_t at = 0;
+    for (uint32_t q = 0; q < N; ++q) {
+        if (sizes[q] != size_t(q) * 3 + 1) throw Error(FSM_ECOMM, "selftest: gather size mismatch");
+        for (size_t j = 0; j < sizes[q]; ++j)
+            if (all[at + j] != uint8_t(q * 7 + j)) throw Error(FSM_ECOMM, "selftest: gather data mismatch");
+        at += sizes[q];
+    }
+    if (at != all.size()) throw Error(FSM_ECOMM, "selftest: gather length mismatch");
+    if (ex != N && std::getenv("FSM_SELFTEST_REQUIRE_CLAIMS"))
+        throw Error(FSM_ECOMM, "selftest: the ranks have no common work-stealing counter");
+    if (ex == N) {
+        // claims: the ranks take ranges of r + 1 units of [0, 997) from the shared counter
+        // until it runs out; every unit must be claimed exactly once
+        constexpr int64_t kUnits = 997;
+        std::vector<uint8_t> got;
+        for (;;) {
+            const int64_t old = comm.fetch_add(key, int64_t(r) + 1);
+            if (old < 0) throw Error(FSM_ECOMM, "selftest: fetch_add failed");
+            if (old >= kUnits) break;
+            for (int64_t u = old; u < std::min<int64_t>(old + r + 1, kUnits); ++u) {
+                const uint16_t v16 = uint16_t(u);
+                got.push_back(uint8_t(v16 & 0xFF));
+                got.push_back(uint8_t(v16 >> 8));
+            }
+        }
+        std::vector<size_t> csz;
+        const std::vector<uint8_t> claimed = comm.gather_blobs(got, csz, nullptr);
+        std::vector<int> seen(kUnits, 0);
+        for (size_t j = 0; j + 1 < claimed.size(); j += 2) {
+            const size_t u = size_t(claimed[j]) | (size_t(claimed[j + 1]) << 8);
+            if (u >= size_t(kUnits)) throw Error(FSM_ECOMM, "selftest: claimed unit out of range");
+            ++seen[u];
+        }
+        for (int64_t u = 0; u < kUnits; ++u)
+            if (seen[size_t(u)] != 1) throw Error(FSM_ECOMM, "selftest: a unit was claimed " +
+                                                                 std::to_string(seen[size_t(u)]) + " times");
+    }
+    // a root-only gather: rank 0 gets every blob in rank order (the others may get nothing)
+    std::vector<size_t> rsz;
+    const std::vector<uint8_t> root = comm.gather_blobs(mine, rsz, nullptr, nullptr, nullptr, 0, true);
+    if (r == 0 && root != all) throw Error(FSM_ECOMM, "selftest: root-only gather mismatch");
+}
+
+int group_make_db(fsm_ctx* ctx, int32_t mode, const fsm::Source& src, fsm_db** out) {
+    fsm::Group& g = *ctx->group;
+    fsm_db* db = new (std::nothrow) fsm_db();
+    if (!db) return fail(ctx, FSM_ENOMEM, "host allocation failed");
+    db->ctx = ctx;
+    db->mode = mode;
+    db->parts.assign(size_t(g.n()), nullptr);
+    const int who = g.run([&](int r) { return make_db(g.ranks[size_t(r)], mode, src, &db->parts[size_t(r)]); });
+    const int rc = group_finish(ctx, who);
     if (rc != FSM_OK) {
         fsm_db_free(db);
         return rc;
@@ -114,71 +362,42 @@ int fsm_shard_plan(const uint64_t* volume, int64_t n, int32_t nranks, int32_t* o
 }
 
 int fsm_comm_selftest(const fsm_opts* opts) {
-    if (!opts || opts->nranks < 2) return fail(nullptr, FSM_EINVAL, "selftest needs nranks >= 2");
+    if (opts && opts->ndevices > 1 && opts->nranks <= 1) {
+        // the in-process transport on ndevices host threads (no GPU)
+        if (opts->ndevices > FSM_MAX_DEVICES) return fail(nullptr, FSM_EINVAL, "ndevices exceeds FSM_MAX_DEVICES");
+        const int N = opts->ndevices;
+        fsm::Group g(N);
+        std::vector<std::string> errs(static_cast<size_t>(N));
+        const int who = g.run([&](int r) {
+            const int c = guarded(nullptr, [&] {
+                auto comm = fsm::make_inproc_comm(g.hub, r);
+                comm_selftest(*comm);
+            });
+            if (c != FSM_OK) errs[size_t(r)] = g_err;
+            return c;
+        });
+        if (who < 0) return FSM_OK;
+        return fail(nullptr, g.rc[size_t(who)], "rank " + std::to_string(who) + ": " + errs[size_t(who)]);
+    }
+    if (!opts || opts->nranks < 2) return fail(nullptr, FSM_EINVAL, "selftest needs nranks >= 2 or ndevices >= 2");
     return guarded(nullptr, [&] {
         if (!opts->host_comm) FSM_HIP(hipSetDevice(opts->device));
         auto comm = fsm::make_comm(*opts);
-        const uint32_t N = uint32_t(opts->nranks), r = uint32_t(opts->rank);
-        std::vector<uint32_t> v(1000);
-        for (uint32_t i = 0; i < v.size(); ++i) v[i] = r + i;
-        comm->host_allreduce_u32(v.data(), v.size(), nullptr);
-        for (uint32_t i = 0; i < v.size(); ++i)
-            if (v[i] != N * i + N * (N - 1) / 2) throw Error(FSM_ECOMM, "selftest: all-reduce mismatch");
-        std::vector<uint8_t> mine(size_t(r) * 3 + 1);
-        for (size_t j = 0; j < mine.size(); ++j) mine[j] = uint8_t(r * 7 + j);
-        std::vector<size_t> sizes;
-        // (the work-stealing counter of the claim test below is reset before this gather, which
-        // also agrees on whether every rank has the shared counters)
-        const int64_t key = comm->next_key();
-        comm->reset_counter(key);
-        uint32_t ex = comm->has_fetch_add() ? 1u : 0u;
-        const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, nullptr, nullptr, &ex, 1);
-        size_t at = 0;
-        for (uint32_t q = 0; q < N; ++q) {
-            if (sizes[q] != size_t(q) * 3 + 1) throw Error(FSM_ECOMM, "selftest: gather size mismatch");
-            for (size_t j = 0; j < sizes[q]; ++j)
-                if (all[at + j] != uint8_t(q * 7 + j)) throw Error(FSM_ECOMM, "selftest: gather data mismatch");
-            at += sizes[q];
-        }
-        if (at != all.size()) throw Error(FSM_ECOMM, "selftest: gather length mismatch");
-        if (ex != N && std::getenv("FSM_SELFTEST_REQUIRE_CLAIMS"))
-            throw Error(FSM_ECOMM, "selftest: the ranks have no common work-stealing counter");
-        if (ex == N) {
-            // claims: the ranks take ranges of r + 1 units of [0, 997) from the shared counter
-            // until it runs out; every unit must be claimed exactly once
-            constexpr int64_t kUnits = 997;
-            std::vector<uint8_t> got;
-            for (;;) {
-                const int64_t old = comm->fetch_add(key, int64_t(r) + 1);
-                if (old < 0) throw Error(FSM_ECOMM, "selftest: fetch_add failed");
-                if (old >= kUnits) break;
-                for (int64_t u = old; u < std::min<int64_t>(old + r + 1, kUnits); ++u) {
-                    const uint16_t v16 = uint16_t(u);
-                    got.push_back(uint8_t(v16 & 0xFF));
-                    got.push_back(uint8_t(v16 >> 8));
-                }
-            }
-            std::vector<size_t> csz;
-            const std::vector<uint8_t> claimed = comm->gather_blobs(got, csz, nullptr);
-            std::vector<int> seen(kUnits, 0);
-            for (size_t j = 0; j + 1 < claimed.size(); j += 2) {
-                const size_t u = size_t(claimed[j]) | (size_t(claimed[j + 1]) << 8);
-                if (u >= size_t(kUnits)) throw Error(FSM_ECOMM, "selftest: claimed unit out of range");
-                ++seen[u];
-            }
-            for (int64_t u = 0; u < kUnits; ++u)
-                if (seen[size_t(u)] != 1) throw Error(FSM_ECOMM, "selftest: a unit was claimed " +
-                                                                     std::to_string(seen[size_t(u)]) + " times");
-        }
+        comm_selftest(*comm);
     });
 }
 
-int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
-    if (!out) return FSM_EINVAL;
+}  // extern "C"
+
+namespace {
+
+// one context on one device; comm: the in-process communicator of a group's rank
+// (nullptr: make_comm from the options)
+int create_one(const fsm_opts& opts, std::unique_ptr<fsm::Comm> comm, fsm_ctx** out) {
     *out = nullptr;
     fsm_ctx* ctx = new (std::nothrow) fsm_ctx();
     if (!ctx) return fail(nullptr, FSM_ENOMEM, "host allocation failed");
-    if (opts) ctx->opts = *opts;
+    ctx->opts = opts;
     if (ctx->opts.nranks <= 0) ctx->opts.nranks = 1;
     const int rc = guarded(ctx, [&] {
         int ndev = 0;
@@ -193,7 +412,7 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
             throw Error(FSM_EDEVICE, std::string("libfsm is built for gfx950; device is ") + prop.gcnArchName);
         FSM_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
         ctx->pool = std::make_shared<fsm::Pool>(ctx->opts.device);
-        ctx->comm = fsm::make_comm(ctx->opts).release();
+        ctx->comm = comm ? comm.release() : fsm::make_comm(ctx->opts).release();
         // the host side a DB build and a mine use from their first call: the staging
         // ring (two 4 MiB pinned slots, each DMA'd once: the first DMA from a pinned
         // buffer is slow) and the host thread pool's workers
@@ -219,8 +438,79 @@ int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
     return FSM_OK;
 }
 
+// fsm_opts.ndevices > 1: the group context and its rank contexts, each made on its own
+// thread (its device current there from then on)
+int create_group(const fsm_opts& opts, fsm_ctx** out) {
+    const int N = opts.ndevices;
+    if (N > FSM_MAX_DEVICES) return fail(nullptr, FSM_EINVAL, "ndevices exceeds FSM_MAX_DEVICES");
+    if (opts.nranks > 1) return fail(nullptr, FSM_EINVAL, "ndevices > 1 (in-process ranks) excludes nranks > 1");
+    fsm_ctx* ctx = new (std::nothrow) fsm_ctx();
+    if (!ctx) return fail(nullptr, FSM_ENOMEM, "host allocation failed");
+    ctx->opts = opts;
+    ctx->opts.device = opts.devices[0];
+    ctx->opts.nranks = 1;
+    int rc = FSM_OK;
+    try {
+        ctx->group = std::make_unique<fsm::Group>(N);
+    } catch (const std::exception& e) {
+        rc = fail(nullptr, FSM_ENOMEM, std::string("cannot start the rank threads: ") + e.what());
+    }
+    if (rc == FSM_OK) {
+        fsm::Group& g = *ctx->group;
+        std::vector<std::string> errs(static_cast<size_t>(N));
+        const int who = g.run([&](int r) {
+            fsm_opts o = opts;
+            o.ndevices = 0;
+            o.device = opts.devices[r];
+            o.nranks = N;
+            o.rank = r;
+            o.host_comm = nullptr;
+            const int c = create_one(o, fsm::make_inproc_comm(g.hub, r), &g.ranks[size_t(r)]);
+            if (c != FSM_OK) errs[size_t(r)] = g_err;  // (thread-local on this rank's thread)
+            else g.ranks[size_t(r)]->result_root_only = true;
+            return c;
+        });
+        if (who >= 0) rc = fail(nullptr, g.rc[size_t(who)], "rank " + std::to_string(who) + " (device " +
+                                                                 std::to_string(opts.devices[who]) + "): " + errs[size_t(who)]);
+    }
+    if (rc != FSM_OK) {
+        const std::string keep = g_err;
+        fsm_ctx_destroy(ctx);
+        g_err = keep;
+        return rc;
+    }
+    *out = ctx;
+    return FSM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fsm_ctx_create(const fsm_opts* opts, fsm_ctx** out) {
+    maybe_install_segv_trace();
+    if (!out) return FSM_EINVAL;
+    *out = nullptr;
+    fsm_opts o{};
+    if (opts) o = *opts;
+    if (o.ndevices > 1) return create_group(o, out);
+    return create_one(o, nullptr, out);
+}
+
 void fsm_ctx_destroy(fsm_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->group) {
+        // each rank context is destroyed on its own thread (its device current there)
+        fsm::Group& g = *ctx->group;
+        (void)g.run([&](int r) {
+            fsm_ctx_destroy(g.ranks[size_t(r)]);
+            g.ranks[size_t(r)] = nullptr;
+            return FSM_OK;
+        });
+        ctx->group.reset();
+        delete ctx;
+        return;
+    }
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (hipEvent_t e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
@@ -277,6 +567,11 @@ int fsm_db_export(fsm_ctx* ctx, const fsm_db* db, fsm_db_image** out) {
     if (!ctx || !db || !out) return fail(ctx, FSM_EINVAL, "null argument");
     *out = nullptr;
     if (db->ctx != ctx) return fail(ctx, FSM_EINVAL, "db belongs to another context");
+    if (ctx->group) {  // rank 0's replica (every rank holds the same DB)
+        const int rc = fsm_db_export(ctx->group->ranks[0], db->parts[0], out);
+        if (rc != FSM_OK) ctx->err = ctx->group->ranks[0]->err;
+        return rc;
+    }
     auto* img = static_cast<fsm_db_image*>(std::calloc(1, sizeof(fsm_db_image)));
     if (!img) return fail(ctx, FSM_ENOMEM, "calloc failed");
     const int rc = guarded(ctx, [&] {
@@ -332,6 +627,7 @@ void fsm_db_image_free(fsm_db_image* img) {
 
 void fsm_db_free(fsm_db* db) {
     if (!db) return;
+    for (fsm_db* p : db->parts) fsm_db_free(p);
     fsm::spade_release(db);
     fsm::tsr_release(db);
     delete db;
@@ -343,6 +639,18 @@ int fsm_spade_mine(fsm_ctx* ctx, fsm_db* db, double support, int32_t dfs, fsm_pa
     *out = nullptr;
     if (db->ctx != ctx) return fail(ctx, FSM_EINVAL, "db belongs to another context");
     if (db->mode != FSM_MODE_SPADE) return fail(ctx, FSM_EINVAL, "db was not flattened for SPADE");
+    if (ctx->group) {
+        fsm::Group& g = *ctx->group;
+        std::vector<fsm_patterns*> res(size_t(g.n()), nullptr);
+        const int who = g.run([&](int r) {
+            return fsm_spade_mine(g.ranks[size_t(r)], db->parts[size_t(r)], support, dfs, &res[size_t(r)]);
+        });
+        for (size_t r = 1; r < res.size(); ++r) fsm_patterns_free(res[r]);  // (empty: root-only output)
+        const int rc = group_finish(ctx, who);
+        if (rc != FSM_OK) fsm_patterns_free(res[0]);
+        else *out = res[0];
+        return rc;
+    }
     return guarded(ctx, [&] {
         FSM_HIP(hipSetDevice(ctx->opts.device));
         reset_stats(ctx);
@@ -363,6 +671,18 @@ int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules*
     if (db->ctx != ctx) return fail(ctx, FSM_EINVAL, "db belongs to another context");
     if (db->mode != FSM_MODE_TSR) return fail(ctx, FSM_EINVAL, "db was not flattened for TSR");
     if (k < 1) return fail(ctx, FSM_EINVAL, "TSR: k must be >= 1 (got " + std::to_string(k) + ")");
+    if (ctx->group) {
+        fsm::Group& g = *ctx->group;
+        std::vector<fsm_rules*> res(size_t(g.n()), nullptr);
+        const int who = g.run([&](int r) {
+            return fsm_tsr_mine(g.ranks[size_t(r)], db->parts[size_t(r)], k, minconf, &res[size_t(r)]);
+        });
+        for (size_t r = 1; r < res.size(); ++r) fsm_rules_free(res[r]);  // (the replay is replicated)
+        const int rc = group_finish(ctx, who);
+        if (rc != FSM_OK) fsm_rules_free(res[0]);
+        else *out = res[0];
+        return rc;
+    }
     return guarded(ctx, [&] {
         FSM_HIP(hipSetDevice(ctx->opts.device));
         reset_stats(ctx);

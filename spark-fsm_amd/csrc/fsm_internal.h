@@ -216,6 +216,7 @@ struct SpadeDevDB;
 struct TsrDevDB;
 namespace fsm {
 class Comm;
+struct Group;
 }
 
 struct fsm_ctx {
@@ -225,6 +226,9 @@ struct fsm_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     fsm::Comm* comm = nullptr;  // nranks > 1 (owned)
+    // fsm_opts.ndevices > 1: the rank contexts this context drives in-process (fsm_api.cpp)
+    std::unique_ptr<fsm::Group> group;
+    bool result_root_only = false;  // a rank context of a group: only rank 0's result is returned
     std::shared_ptr<fsm::Pool> pool;  // device blocks of this context (see fsm::Pool)
     std::vector<fsm_kernel_stat> kstats;  // of the last mine call
     std::unique_ptr<fsm::PinnedBuf> pin;  // small mapped readback slots, made on first use
@@ -277,6 +281,7 @@ struct fsm_ctx {
 struct fsm_db {
     fsm_ctx* ctx = nullptr;
     int mode = 0;
+    std::vector<fsm_db*> parts;  // a group context's DB: one replica per rank context (owned)
     fsm::FlatSpade spade;
     fsm::FlatTsr tsr;
     SpadeDevDB* spade_dev = nullptr;

@@ -3195,7 +3195,9 @@ struct Miner {
             for (size_t k = ga; k < gb; ++k) ctx->stats.rank_root_owned += int64_t(b.children[k].psup);
         // the only group: the children and their member tables move over whole (swapped:
         // the parent, released after this emit and recycled, keeps nb's old capacity)
-        const bool whole = ga == 0 && gb == b.children.size() && b.groups.size() == 1;
+        // (not a claiming root: it stays on the stack for its next claim, which reads its children;
+        // a first claim covering every class would otherwise leave it with nb's old ones)
+        const bool whole = ga == 0 && gb == b.children.size() && b.groups.size() == 1 && b.claim_key < 0;
         if (whole) {
             nb.cls.clear();
             nb.rank_item.clear();
@@ -3606,8 +3608,11 @@ void sum_stats_fields(fsm_stats& st, int64_t* f[kSumStats]) {
 
 // every rank's pattern CSR, concatenated in rank order, on every rank, with the summed work
 // counters; one gather, which also carries the failure agreement of the mine (agr)
+// root_only (ranks of one in-process group): only rank 0's result is returned, the others
+// get an empty CSR and copy nothing
 void gather_patterns(Comm* comm, hipStream_t s, std::vector<int32_t>& sup, std::vector<int64_t>& pat_off,
-                     std::vector<int64_t>& set_off, std::vector<int32_t>& items, fsm_stats& st, Agreement* agr) {
+                     std::vector<int64_t>& set_off, std::vector<int32_t>& items, fsm_stats& st, Agreement* agr,
+                     bool root_only) {
     // blob (int32): stats (2 x kSumStats), n, n_sets, n_items, sup[n], sets-per-pattern[n],
     // set sizes[n_sets], items[n_items]
     const size_t n = sup.size(), ns = set_off.size() - 1, ni = items.size();
@@ -3633,11 +3638,12 @@ void gather_patterns(Comm* comm, hipStream_t s, std::vector<int32_t>& sup, std::
     std::vector<uint8_t> mine(b.size() * 4);
     std::memcpy(mine.data(), b.data(), mine.size());
     std::vector<size_t> sizes;
-    const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s, agr);
+    const std::vector<uint8_t> all = comm->gather_blobs(mine, sizes, s, agr, nullptr, 0, root_only);
     sup.clear();
     items.clear();
     pat_off.assign(1, 0);
     set_off.assign(1, 0);
+    if (root_only && comm->rank() != 0) return;
     for (size_t k = 0; k < kSumStats; ++k) *f[k] = 0;
     size_t at = 0;
     for (size_t r = 0; r < sizes.size(); ++r) {
@@ -3989,7 +3995,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             vp.assign(pat_off.p, pat_off.p + pat_off.n);
             vo.assign(set_off.p, set_off.p + set_off.n);
         }
-        gather_patterns(comm, ctx->stream, vs, vp, vo, vi, ctx->stats, &mn.agr);
+        gather_patterns(comm, ctx->stream, vs, vp, vo, vi, ctx->stats, &mn.agr, ctx->result_root_only);
         n = int64_t(vs.size());
         p->n_sets = int64_t(vo.size()) - 1;
         p->n_items = int64_t(vi.size());

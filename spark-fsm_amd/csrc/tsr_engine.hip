@@ -223,8 +223,7 @@ struct Side {
     uint32_t kb;     // this rule's kept rows: at most kb (its support) ...
     uint64_t pl;     // lmode 2: the parent's first entry in the kept-rows arena
     uint64_t ko;     // ... written from arena entry ko (kNoList: none kept)
-    uint64_t hx;     // hashes of the item set X (the |sids(X u {c})| memo's keys)
-    uint32_t hx2;
+    uint32_t xid;    // the item set X's interned id (Replay::XIntern: the |sids(X u {c})| memo's exact key)
     uint32_t klo;    // bitmap path: the lowest kid ever counted, min(max X, max Y) + 1 (as kids)
     uint32_t X[kMaxSide];
     uint32_t Y[kMaxSide];
@@ -508,10 +507,12 @@ constexpr uint32_t kChunkEnt = uint32_t(kXBlock) * kEpt;  // entries of one flat
 constexpr uint32_t kPassKids = 4096;        // kids per LDS histogram pass (2 x 16 KiB)
 constexpr uint32_t kMaxKids = 65536;        // bitmap path: kept items (kid codes 16 KiB of LDS)
 
-// |sids(X u {c})| memo (bitmap path): open addressing over uint4 entries (64-bit key of the
-// item set X u {c}, 32-bit check, count), written by k_dl, read by k_expand_reduce of later
-// launches.  An entry is written once (key by CAS, then check and count in one 8-byte store)
-// and every count is final, so a reader sees either a miss or the exact count.
+// |sids(X u {c})| memo (bitmap path): open addressing over uint4 entries (64-bit key, the
+// count), written by k_dl, read by k_expand_reduce of later launches.  The key is the item
+// set's identity, not a hash of it: (id(X) + 1) << 32 | c, with id(X) the host's interned id
+// of the item set X (Replay::XIntern), so two different sets never share a key.  An entry is
+// written once (key by CAS, then the count in one 8-byte store with a written flag) and every
+// count is final, so a reader sees either a miss or the exact count.
 struct DlMemo {
     uint4* tab;     // nullptr: no memo
     uint32_t mask;  // entries - 1 (a power of two)
@@ -522,27 +523,25 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ void memo_key(uint64_t hx, uint32_t hx2, uint32_t c, uint64_t& key, uint32_t& chk) {
-    key = mix64(hx ^ ((uint64_t(c) + 1ull) * 0x9E3779B97F4A7C15ull)) | 1ull;
-    chk = uint32_t(mix64(uint64_t(hx2) << 32 | c) >> 32) | 1u;
-}
-__device__ __forceinline__ uint32_t memo_find(const DlMemo& m, uint64_t key, uint32_t chk) {
-    uint32_t h = uint32_t(key >> 20) & m.mask;
+__device__ __forceinline__ uint64_t memo_key(uint32_t xid, uint32_t c) { return (uint64_t(xid) + 1ull) << 32 | c; }
+__device__ __forceinline__ uint32_t memo_slot(const DlMemo& m, uint64_t key) { return uint32_t(mix64(key)) & m.mask; }
+__device__ __forceinline__ uint32_t memo_find(const DlMemo& m, uint64_t key) {
+    uint32_t h = memo_slot(m, key);
     for (uint32_t k = 0; k < kMemoProbe; ++k, h = (h + 1) & m.mask) {
         const uint4 e = m.tab[h];
         const uint64_t ek = uint64_t(e.x) | (uint64_t(e.y) << 32);
         if (ek == 0) return 0u;
-        if (ek == key) return e.z == chk ? e.w : 0u;
+        if (ek == key) return e.z ? e.w : 0u;  // (z = 0: claimed, count not yet written)
     }
     return 0u;
 }
-__device__ __forceinline__ void memo_put(const DlMemo& m, uint64_t key, uint32_t chk, uint32_t v) {
-    uint32_t h = uint32_t(key >> 20) & m.mask;
+__device__ __forceinline__ void memo_put(const DlMemo& m, uint64_t key, uint32_t v) {
+    uint32_t h = memo_slot(m, key);
     for (uint32_t k = 0; k < kMemoProbe; ++k, h = (h + 1) & m.mask) {
         unsigned long long* kp = reinterpret_cast<unsigned long long*>(&m.tab[h].x);
         const unsigned long long old = atomicCAS(kp, 0ull, (unsigned long long)key);
         if (old == 0ull || old == key) {
-            *reinterpret_cast<unsigned long long*>(&m.tab[h].z) = uint64_t(chk) | (uint64_t(v) << 32);
+            *reinterpret_cast<unsigned long long*>(&m.tab[h].z) = 1ull | (uint64_t(v) << 32);
             return;
         }
     }
@@ -1116,12 +1115,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __rest
             const uint32_t it = kept[kid_lo + c];
             // |sids(X u {c})| of a left extension: from the memo, else from k_dl
             uint32_t dl = 0;
-            if (tl >= geo.t && memo.tab) {
-                uint64_t key;
-                uint32_t chk;
-                memo_key(sides[b].hx, sides[b].hx2, it, key, chk);
-                dl = memo_find(memo, key, chk);
-            }
+            if (tl >= geo.t && memo.tab) dl = memo_find(memo, memo_key(sides[b].xid, it));
             out[idx] = ExpRec{it, tl, dl, tr};
             if (tl >= geo.t && !dl) dlw[atomicAdd(ndlw, 1u)] = make_uint4(b, it, kid_lo + c0 + idx, 0u);
         }
@@ -1209,12 +1203,7 @@ __global__ __launch_bounds__(kBlock) void k_dl(const Side* __restrict__ sides, c
             uint32_t tot = 0;
             for (uint32_t k = 0; k < blockDim.x / 64; ++k) tot += red[k];
             outb[uint64_t(wk.x) * cap + wk.z].dl = tot;
-            if (memo.tab && tot) {
-                uint64_t key;
-                uint32_t chk;
-                memo_key(side.hx, side.hx2, wk.y, key, chk);
-                memo_put(memo, key, chk, tot);
-            }
+            if (memo.tab && tot) memo_put(memo, memo_key(side.xid, wk.y), tot);
         }
         __syncthreads();
     }
@@ -1240,6 +1229,52 @@ struct Rule {
     uint32_t ln = 0, pn = 0, pc = 0;
     uint64_t loff = kNoList;   // its kept domain rows in the arena (ln of them), after its expansion
     uint64_t ploff = kNoList;  // its parent's (pn of them): its own domain is a subset of those rows
+    uint32_t xid = 0;          // its item set X, interned (XIntern)
+};
+
+// The item sets X of the rules, interned: the |sids(X u {c})| memo's exact keys (DlMemo).  A
+// single item is its own id; X u {c} gets the id of the pair (id(X), c), numbered from U up.
+// A left extension only adds an item above every item of X (TopSeqRules' expandLeft
+// candidates), so a set has exactly one chain of prefixes and one id whatever
+// rule it appears in.
+struct XIntern {
+    uint32_t next = 0;
+    std::vector<uint64_t> key;
+    std::vector<uint32_t> val;
+    size_t used = 0;
+    void init(uint32_t U) {
+        next = U;
+        key.assign(size_t(1) << 16, 0ull);
+        val.assign(key.size(), 0u);
+        used = 0;
+    }
+    uint32_t get(uint32_t xid, uint32_t c) {
+        const uint64_t k = (uint64_t(xid) + 1ull) << 32 | c;
+        size_t m = key.size() - 1, h = size_t(mix64(k)) & m;
+        for (; key[h]; h = (h + 1) & m)
+            if (key[h] == k) return val[h];
+        if (next >= 0xFFFFFFFEu) throw Error(FSM_ELIMIT, "TSR: more than 2^32 distinct rule antecedents");
+        key[h] = k;
+        val[h] = next;
+        if (++used * 2 > key.size()) grow();
+        return next++;
+    }
+
+  private:
+    void grow() {
+        std::vector<uint64_t> ok(key.size() * 2, 0ull);
+        std::vector<uint32_t> ov(ok.size(), 0u);
+        ok.swap(key);
+        ov.swap(val);
+        const size_t m = key.size() - 1;
+        for (size_t q = 0; q < ok.size(); ++q)
+            if (ok[q]) {
+                size_t h = size_t(mix64(ok[q])) & m;
+                while (key[h]) h = (h + 1) & m;
+                key[h] = ok[q];
+                val[h] = ov[q];
+            }
+    }
 };
 
 // Rules and their items in large chunks that never move (a c4 replay makes millions
@@ -1442,6 +1477,7 @@ struct Replay {
     };
     std::priority_queue<HeapEnt, std::vector<HeapEnt>, MinFirst> krules;
     CandQueue cand;
+    XIntern xin;
 
     Replay(int32_t k_, double mc) : k(k_), minconf(mc), krules(MinFirst{&st}), cand(MaxFirst{&st}) {}
 
@@ -1467,6 +1503,7 @@ struct Replay {
         const uint32_t* x = st.X(&r);
         r.k1 = uint64_t(sup) << 32 | uint64_t(mx) << 16 | uint64_t(my);
         r.k2 = uint64_t(x[0]) << 32 | (mx > 1 ? x[1] : x[mx]);
+        r.xid = !src ? ax : (ax != kNone ? xin.get(src->xid, ax) : src->xid);
         if (src && src->loff != kNoList) {  // the parent's kept rows: the child's domain probes only pc there
             r.ploff = src->loff;
             r.pn = src->ln;
@@ -1574,6 +1611,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     hipStream_t s = ctx->stream;
     const uint32_t U = uint32_t(d->U);
     Replay rp{k, minconf};
+    rp.xin.init(U);
     std::vector<uint64_t> voff(size_t(U) + 1);
     FSM_HIP(hipMemcpyAsync(voff.data(), d->vert_off.p, (size_t(U) + 1) * 8, hipMemcpyDeviceToHost, s));
     DevBuf d_sup(size_t(std::max<uint32_t>(U, 1)) * 4);
@@ -1915,8 +1953,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         return !(v && v[0] == '0');
     }();
     // The arena is a ring: a launch writes its rules' lists (each at most the rule's support)
-    // at the head, at most acap / (4 nsets) entries (else it keeps none), so the launches in
-    // flight never reach a list within acap / 2 of the head, the lists a child may read.
+    // at the head, at most acap / (4 nsets) entries (else it keeps none); a child reads its
+    // parent's list only while it lies within acap / 2 of the head.  A launch may stay in
+    // flight (its set not yet finished by the replay) while later launches advance the head,
+    // so each set records the oldest ring position it reads or writes (ExpSet::amin), and a
+    // launch that would overwrite that position finishes the set first (launch()).
     DevBuf arena;
     uint64_t acap = 0;   // arena entries (16 B)
     uint64_t ahead = 0;  // the ring's head (entries written, monotonic; a list's position mod acap)
@@ -1936,7 +1977,9 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     DevBuf memo_buf;
     DlMemo memo{nullptr, 0u};
     if (use_bm && [] { const char* v = std::getenv("FSM_TSR_DLMEMO"); return !(v && v[0] == '0'); }()) {
-        const uint32_t ent = 1u << 24;  // 256 MiB
+        // 2^24 entries (256 MiB); FSM_TSR_DLMEMO_LOG2 (tests: a tiny table fills, probes run out)
+        const char* lv = std::getenv("FSM_TSR_DLMEMO_LOG2");
+        const uint32_t ent = 1u << (lv ? std::clamp(std::atoi(lv), 4, 28) : 24);
         memo_buf.alloc(size_t(ent) * sizeof(uint4));
         FSM_HIP(hipMemsetAsync(memo_buf.p, 0, size_t(ent) * sizeof(uint4), s));
         FSM_HIP(hipStreamSynchronize(s));  // (the launches run on the sets' own streams)
@@ -1955,6 +1998,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         std::vector<Rule*> batch;
         std::vector<char> drv_in_x;
         std::vector<uint64_t> kmono;  // bitmap path: each slot's kept-row list (ring position; kNoList: none)
+        uint64_t amin = kNoList;      // the oldest ring position the launch reads or writes (kNoList: none)
         uint32_t la = 0, lz = 0;  // slot sharding: this rank's slots [la, lz) of the batch (else all)
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
         // the set's own stream: the two sets' launches are independent, so the GPU runs
@@ -2092,6 +2136,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     int64_t exp_domain = 0, exp_entries = 0, exp_bitmap_bytes = 0, exp_part_bytes = 0;
     int64_t exp_hold = 0, exp_walk = 0;  // domain rows where the rule holds, row entries walked (verbose)
     int64_t exp_plist = 0;               // expansions whose domain came from the parent's kept rows (verbose)
+    int64_t ring_waits = 0;              // launches in flight finished early to free their ring positions
     int64_t seq_next = 0;
     // Take in the results of set x (waits for its launch): records sorted into the
     // cache, and its batch queued for child speculation.
@@ -2277,16 +2322,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             sd.pc = sd.pleft = sd.pn = sd.kb = 0;
             sd.pl = 0;
             sd.ko = kNoList;
-            {  // X's hashes (the memo keys of its left extensions)
-                uint64_t h1 = 0x243F6A8885A308D3ull ^ r->nx, h2 = 0x13198A2E03707344ull ^ r->nx;
-                for (uint32_t q = 0; q < r->nx; ++q) {
-                    h1 = mix64(h1 ^ (uint64_t(rx[q]) + 0x9E3779B97F4A7C15ull));
-                    h2 = mix64(h2 + uint64_t(rx[q]) * 0xD6E8FEB86659FD93ull);
-                }
-                sd.hx = h1;
-                sd.hx2 = uint32_t(h2 >> 32);
-                sd.klo = use_bm ? std::min(h_kid_of[rx[r->nx - 1]], h_kid_of[ry[r->ny - 1]]) + 1u : 0u;
-            }
+            sd.xid = r->xid;  // (the memo key of its left extensions)
+            sd.klo = use_bm ? std::min(h_kid_of[rx[r->nx - 1]], h_kid_of[ry[r->ny - 1]]) + 1u : 0u;
             if (use_bm && plist && r->ploff != kNoList && r->ploff + acap / 2 >= ahead) {
                 // the parent's kept rows (still in the ring) are the domain: only the added item is
                 // probed there
@@ -2323,11 +2360,24 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             }
         }
         x.kmono.assign(nb, kNoList);
+        x.amin = kNoList;
+        for (uint32_t k = 0; k < nb; ++k)
+            if (x.h_sides[k].lmode == 2) x.amin = std::min(x.amin, bp[k]->ploff);
         if (plist && acap) {  // the slots' kept-row lists at the ring's head, each at most the rule's support
             uint64_t need = 0;
             for (uint32_t k = 0; k < nb; ++k) need += bp[k]->sup;
             if (need && need <= acap / (4 * uint64_t(nsets))) {
                 if (ahead % acap + need > acap) ahead += acap - ahead % acap;  // (a list never wraps)
+                // positions below ahead + need - acap are overwritten now: a set still in flight
+                // that reads or writes one of them is finished first (its results are taken in)
+                for (int xi = 0; xi < nsets; ++xi) {
+                    ExpSet& o = xs[xi];
+                    if (&o != &x && o.busy && o.amin != kNoList && o.amin + acap < ahead + need) {
+                        finish(o);
+                        ++ring_waits;
+                    }
+                }
+                x.amin = std::min(x.amin, ahead);
                 for (uint32_t k = 0; k < nb; ++k) {
                     x.h_sides[k].ko = ahead % acap;
                     x.h_sides[k].kb = bp[k]->sup;
@@ -2648,9 +2698,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     if (ctx->opts.verbose)
         std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB; domain sids "
                      "%lld (row entries %lld), rows where the rule holds %lld, row entries walked %lld; "
-                     "rules on their parent's kept rows %lld\n",
+                     "rules on their parent's kept rows %lld (ring: %llu entries written, %lld early finishes)\n",
                      (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6, (long long)exp_domain,
-                     (long long)exp_entries, (long long)exp_hold, (long long)exp_walk, (long long)exp_plist);
+                     (long long)exp_entries, (long long)exp_hold, (long long)exp_walk, (long long)exp_plist,
+                     (unsigned long long)ahead, (long long)ring_waits);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {

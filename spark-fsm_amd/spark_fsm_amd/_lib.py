@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("FSM_LIB_PATH") or os.path.join(HERE, "libfsm.so")  # 
 
 FSM_OK, FSM_EINVAL, FSM_EPARSE, FSM_EDEVICE, FSM_ENOMEM, FSM_ECOMM, FSM_ELIMIT = range(7)
 MODE_SPADE, MODE_TSR = 0, 1
+MAX_DEVICES = 16  # FSM_MAX_DEVICES
 
 
 class FsmError(RuntimeError):
@@ -51,6 +52,8 @@ class Opts(ctypes.Structure):
         ("unique_id", ctypes.c_uint8 * 128),
         ("mem_budget", ctypes.c_int64),
         ("host_comm", ctypes.POINTER(HostComm)),
+        ("ndevices", ctypes.c_int32),
+        ("devices", ctypes.c_int32 * MAX_DEVICES),
     ]
 
 

@@ -123,3 +123,14 @@ def selftest(nranks, rank, host_comm=None, unique_id=None, device=0):
     if host_comm is not None:
         o.host_comm = ctypes.pointer(host_comm.struct)
     _lib.check(L.fsm_comm_selftest(ctypes.byref(o)))
+
+
+def selftest_inproc(ndevices):
+    """fsm_comm_selftest of the in-process transport (fsm_opts.ndevices ranks as host
+    threads of this process, no GPU): all-reduce, ragged and root-only gathers, the
+    work-stealing counter."""
+    L = _lib.load()
+    o = _lib.Opts()
+    o.nranks = 1
+    o.ndevices = int(ndevices)
+    _lib.check(L.fsm_comm_selftest(ctypes.byref(o)))

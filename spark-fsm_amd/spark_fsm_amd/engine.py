@@ -30,13 +30,25 @@ class _ResultOwner:
 class Engine:
     """Owns a libfsm context on one gfx950 device."""
 
-    def __init__(self, device=0, verbose=False, mem_budget=0, nranks=1, rank=0, unique_id=None, host_comm=None):
+    def __init__(self, device=0, verbose=False, mem_budget=0, nranks=1, rank=0, unique_id=None, host_comm=None,
+                 devices=None):
         """nranks > 1: sharded SPADE, one Engine per rank, collectives over RCCL
         (unique_id from dist.comm_unique_id() on rank 0) or over host_comm
-        (a dist.TorchHostComm; kept alive by this Engine)."""
+        (a dist.TorchHostComm; kept alive by this Engine).
+        devices=[d0, d1, ...] (more than one): ONE Engine whose calls shard over
+        in-process ranks, rank r on HIP device d_r (a device may repeat), the way the
+        JVM drop-in shards (fsm_opts.ndevices); every call returns the whole result."""
         L = _lib.load()
         opts = _lib.Opts()
         opts.device = device
+        if devices is not None and len(devices) > 1:
+            if len(devices) > _lib.MAX_DEVICES:
+                raise ValueError("at most %d in-process ranks" % _lib.MAX_DEVICES)
+            opts.ndevices = len(devices)
+            for r, d in enumerate(devices):
+                opts.devices[r] = int(d)
+        elif devices is not None and len(devices) == 1:
+            opts.device = int(devices[0])
         opts.nranks = int(nranks)
         opts.rank = int(rank)
         opts.verbose = 1 if verbose else 0

@@ -84,8 +84,16 @@ static const struct JNINativeInterface_ g_table = {
     NewLongArray, NewDoubleArray, NewObjectArray, SetIntArrayRegion, SetLongArrayRegion, SetDoubleArrayRegion};
 static JNIEnv g_env = &g_table;
 
-jobjectArray Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(JNIEnv*, jclass, jintArray, jobjectArray, jdouble, jint);
-jobjectArray Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr(JNIEnv*, jclass, jintArray, jobjectArray, jint, jdouble, jint);
+jobjectArray Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(JNIEnv*, jclass, jintArray, jobjectArray, jdouble, jboolean,
+                                                        jintArray);
+jobjectArray Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr(JNIEnv*, jclass, jintArray, jobjectArray, jint, jdouble, jintArray);
+
+/* FsmNative.devices as the Scala side passes it: ndev ordinals */
+static jintArray device_list(int ndev, const int* devs) {
+    jintArray a = NewIntArray(&g_env, ndev);
+    SetIntArrayRegion(&g_env, a, 0, ndev, devs);
+    return a;
+}
 
 static void inputs(int n, const int* sids, const char** lines, jintArray* js, jobjectArray* jl) {
     *js = NewIntArray(&g_env, n);
@@ -120,12 +128,13 @@ static void put(buf_t* b, const char* fmt, ...) {
 }
 
 /* GpuSPADE.extractRDDPatterns' mapping, rendered as GpuPattern.serialize() lines */
-char* harness_spade(int n, const int* sids, const char** lines, double support, int device) {
+char* harness_spade(int n, const int* sids, const char** lines, double support, int ndev, const int* devs) {
     jintArray js;
     jobjectArray jl;
     inputs(n, sids, lines, &js, &jl);
     g_has_exc = 0;
-    jobjectArray res = Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(&g_env, NULL, js, jl, support, device);
+    jobjectArray res =
+        Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(&g_env, NULL, js, jl, support, 1, device_list(ndev, devs));
     buf_t b = {malloc(256), 0, 256};
     b.p[0] = 0;
     if (g_has_exc || !res) {
@@ -147,12 +156,12 @@ char* harness_spade(int n, const int* sids, const char** lines, double support, 
 }
 
 /* GpuTSR.extractRDDRules' mapping, one GpuRule.toString line per rule (%.17g confidence) */
-char* harness_tsr(int n, const int* sids, const char** lines, int k, double minconf, int device) {
+char* harness_tsr(int n, const int* sids, const char** lines, int k, double minconf, int ndev, const int* devs) {
     jintArray js;
     jobjectArray jl;
     inputs(n, sids, lines, &js, &jl);
     g_has_exc = 0;
-    jobjectArray res = Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr(&g_env, NULL, js, jl, k, minconf, device);
+    jobjectArray res = Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr(&g_env, NULL, js, jl, k, minconf, device_list(ndev, devs));
     buf_t b = {malloc(256), 0, 256};
     b.p[0] = 0;
     if (g_has_exc || !res) {

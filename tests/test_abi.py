@@ -38,8 +38,8 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_sizes():
     L = _lib.load()
-    assert L.fsm_abi_version() == 5
-    assert ctypes.sizeof(_lib.Opts) == 4 * 4 + 128 + 8 + 8
+    assert L.fsm_abi_version() == 6
+    assert ctypes.sizeof(_lib.Opts) == 4 * 4 + 128 + 8 + 8 + 4 + 16 * 4 + 4  # (+4: tail padding)
     assert ctypes.sizeof(_lib.Patterns) == 9 * 8  # 8 x 8-byte fields + int32 padded
     assert ctypes.sizeof(_lib.Stats) == 9 * 8 + 8 * 8 + 3 * 8 + 2 * 8 + 8 * 8 + 4 * 8
     assert ctypes.sizeof(_lib.KernelStat) == 40 + 4 * 8
@@ -98,12 +98,13 @@ def test_struct_layout_matches_c_compiler(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "fsm.h"\nint main(void){\n'
                    'printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(fsm_opts), sizeof(fsm_patterns),'
                    ' sizeof(fsm_rules), sizeof(fsm_stats), sizeof(fsm_host_comm), sizeof(fsm_kernel_stat),'
-                   ' offsetof(fsm_opts, host_comm), offsetof(fsm_stats, bytes_count_alg));\nreturn 0;}\n')
+                   ' offsetof(fsm_opts, host_comm), offsetof(fsm_stats, bytes_count_alg));\n'
+                   'printf("%zu %zu\\n", offsetof(fsm_opts, ndevices), offsetof(fsm_opts, devices));\nreturn 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     exp = [ctypes.sizeof(_lib.Opts), ctypes.sizeof(_lib.Patterns), ctypes.sizeof(_lib.Rules),
            ctypes.sizeof(_lib.Stats), ctypes.sizeof(_lib.HostComm), ctypes.sizeof(_lib.KernelStat),
            _lib.Opts.host_comm.offset,
-           _lib.Stats.bytes_count_alg.offset]
+           _lib.Stats.bytes_count_alg.offset, _lib.Opts.ndevices.offset, _lib.Opts.devices.offset]
     assert got == exp

@@ -3,6 +3,7 @@ prefix classes, and the host-callback collectives (all-reduce, ragged
 all-gather) between world_size-2 gloo processes through libfsm's own
 fsm_comm_selftest.  The sharded mining itself runs on the GPU in
 tests/test_parity_gpu.py::test_sharded_spade_two_ranks."""
+import ctypes
 import json
 import os
 import random
@@ -102,3 +103,38 @@ def test_rccl_unique_id():
     except FsmError as e:  # pragma: no cover - image without librccl
         pytest.skip(str(e))
     assert isinstance(uid, bytes) and len(uid) == 128 and any(uid)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8, 16])
+def test_inproc_comm_selftest(n):
+    """The in-process transport of a multi-device context (fsm_opts.ndevices): n host
+    threads run the collectives and the claim counter (every unit claimed once)."""
+    from spark_fsm_amd import dist as fdist
+    for _ in range(5):  # the hub is re-armed between calls
+        fdist.selftest_inproc(n)
+
+
+def test_inproc_comm_failure_releases_peers(monkeypatch):
+    """A rank that fails before its first collective aborts the hub: the peers leave their
+    barrier with FSM_ECOMM instead of blocking, the caller sees the failing rank's own
+    error, and the next call on a fresh group works."""
+    from spark_fsm_amd import FsmError, _lib
+    from spark_fsm_amd import dist as fdist
+    for r in (0, 2):
+        monkeypatch.setenv("FSM_INJECT_FAIL", "%d,selftest" % r)
+        with pytest.raises(FsmError) as ei:
+            fdist.selftest_inproc(4)
+        assert ei.value.code == _lib.FSM_ELIMIT and "injected" in ei.value.msg
+    monkeypatch.delenv("FSM_INJECT_FAIL")
+    fdist.selftest_inproc(4)
+
+
+def test_inproc_rejects_bad_device_lists():
+    from spark_fsm_amd import FsmError, _lib
+    L = _lib.load()
+    o = _lib.Opts()
+    o.ndevices = _lib.MAX_DEVICES + 1
+    assert L.fsm_comm_selftest(ctypes.byref(o)) == _lib.FSM_EINVAL
+    o.ndevices, o.nranks = 2, 2
+    ctx = ctypes.c_void_p()
+    assert L.fsm_ctx_create(ctypes.byref(o), ctypes.byref(ctx)) == _lib.FSM_EINVAL

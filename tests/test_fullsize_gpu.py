@@ -181,3 +181,71 @@ def test_bench_two_ranks_dry_run(tmp_path):
     pr = d["extra"]["per_rank"]  # the per-rank trace: each rank mined its share of the classes
     assert [r["rank"] for r in pr] == [0, 1] and all(r["classes"] > 0 for r in pr)
     assert sum(r["classes"] for r in pr) > max(r["classes"] for r in pr)
+
+
+# ---------------------------------------------------------------- in-process ranks
+# The drop-in's way to shard (fsm_opts.ndevices; the JVM caller is one driver thread,
+# SPADE.scala:132-133 / TSR.scala:102-103): ONE context whose calls run rank r on
+# devices[r] as threads of this process.  On the one-GPU box every rank is device 0.
+
+@pytest.mark.parametrize("name,devices", [("c3", (0, 0)), ("c3", (0, 0, 0)), ("c5-bible", (0, 0)),
+                                          ("c5-bible", (0, 0, 0))])
+def test_spade_fullsize_inproc(name, devices):
+    import spark_fsm_amd as fsm
+    exp = FULL[name]
+    ds = dataset(*SPADE_CFG[name])
+    with fsm.Engine(devices=list(devices)) as e:
+        db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+        try:
+            for _ in range(2):  # the group is re-armed between calls (counters, hub)
+                csr, meta = e.spade_csr(db, exp["support"])
+                st = e.stats()
+                assert meta["minsup"] == exp["minsup"]
+                assert st["joins"] == exp["joins"]
+                assert pattern_digest(*csr) == exp["digest"]
+                assert st["rank_root_slab"] == 0 and st["rank_claims"] >= 1
+                # rank 0 owned only part of the root (the rest went to its peers)
+                assert 0 < st["rank_root_owned"] < 2 * st["root_entries"]
+        finally:
+            db.free()
+
+
+@pytest.mark.parametrize("devices", [(0, 0), (0, 0, 0)])
+def test_tsr_c4_prefix_inproc(devices):
+    import spark_fsm_amd as fsm
+    from tools import gen
+    exp = FULL["c4-prefix"]
+    ds = gen.kosarak(D=990002, seed=1).head(exp["sequences"])
+    with fsm.Engine(devices=list(devices)) as e:
+        db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
+        try:
+            rules, meta = e.tsr(db, exp["k"], exp["minconf"])
+        finally:
+            db.free()
+        st = e.stats()
+    assert meta["final_minsup"] == exp["final_minsup"]
+    assert rule_digest(rules) == exp["digest"]
+    assert 0 < st["rank_units"] < st["expansions"]  # rank 0 counted a share of the rule slots
+
+
+def test_inproc_failure_agreement():
+    """A failure injected on one in-process rank comes back as that rank's error from the one
+    call (no rank left blocked), and the same context mines correctly afterwards."""
+    import spark_fsm_amd as fsm
+    exp = FULL["c1"]
+    ds = dataset(*SPADE_CFG["c1"])
+    with fsm.Engine(devices=[0, 0, 0]) as e:
+        db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+        try:
+            for phase in ("root", "lattice"):
+                os.environ["FSM_INJECT_FAIL"] = "1," + phase
+                try:
+                    with pytest.raises(fsm.FsmError) as ei:
+                        e.spade_csr(db, exp["support"])
+                finally:
+                    del os.environ["FSM_INJECT_FAIL"]
+                assert ei.value.code == 6 and "injected" in ei.value.msg, ei.value.msg
+            csr, meta = e.spade_csr(db, exp["support"])
+            assert pattern_digest(*csr) == exp["digest"]
+        finally:
+            db.free()

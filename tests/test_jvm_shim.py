@@ -32,20 +32,22 @@ def harness(tmp_path_factory):
     L = ctypes.CDLL(out)
     for name in ("harness_spade", "harness_tsr"):
         getattr(L, name).restype = ctypes.c_void_p
-    L.harness_spade.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
-                                ctypes.c_double, ctypes.c_int]
-    L.harness_tsr.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
-                              ctypes.c_int, ctypes.c_double, ctypes.c_int]
+    IP = ctypes.POINTER(ctypes.c_int)
+    L.harness_spade.argtypes = [ctypes.c_int, IP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_double, ctypes.c_int, IP]
+    L.harness_tsr.argtypes = [ctypes.c_int, IP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_double,
+                              ctypes.c_int, IP]
     L.harness_free.argtypes = [ctypes.c_void_p]
     L.path = out
     return L
 
 
-def call(L, fn, records, *args):
+def call(L, fn, records, *args, devices=(0,)):
+    """devices: FsmNative.devices as the Scala side passes it (-Dfsm.devices)."""
     n = len(records)
     sids = (ctypes.c_int * max(n, 1))(*[s for s, _ in records])
     lines = (ctypes.c_char_p * max(n, 1))(*[l.encode() for _, l in records])
-    p = getattr(L, fn)(n, sids, lines, *args)
+    devs = (ctypes.c_int * max(len(devices), 1))(*devices)
+    p = getattr(L, fn)(n, sids, lines, *args, len(devices), devs)
     try:
         return ctypes.string_at(p).decode()
     finally:
@@ -70,43 +72,58 @@ def test_shim_exports_the_bound_symbols(harness):
 
 @pytest.mark.skipif(gpu_present(), reason="the no-device failure path needs a machine without a GPU")
 def test_shim_turns_failures_into_exceptions(harness):
-    s = call(harness, "harness_spade", [(0, "1 -1 2 -1")], 0.5, 0)
+    s = call(harness, "harness_spade", [(0, "1 -1 2 -1")], 0.5)
     assert s.startswith("EXCEPTION java/lang/Exception: libfsm fsm_ctx_create failed (FSM error 3)")
-    t = call(harness, "harness_tsr", [(0, "1 -1 2 -1")], 3, 0.5, 0)
+    t = call(harness, "harness_tsr", [(0, "1 -1 2 -1")], 3, 0.5)
     assert t.startswith("EXCEPTION java/lang/Exception: libfsm fsm_ctx_create failed")
+    # a multi-device request fails the same way (every rank context needs a GPU)
+    s = call(harness, "harness_spade", [(0, "1 -1 2 -1")], 0.5, devices=(0, 1))
+    assert s.startswith("EXCEPTION java/lang/Exception: libfsm fsm_ctx_create failed (FSM error 3)")
+
+
+def test_shim_rejects_too_many_devices(harness):
+    s = call(harness, "harness_spade", [(0, "1 -1 2 -1")], 0.5, devices=tuple(range(17)))
+    assert s.startswith("EXCEPTION java/lang/Exception: libfsm fsm_ctx_create failed (FSM error 1)")
 
 
 GOLD = os.path.join(ROOT, "tests", "golden")
 
 
+# FsmNative.devices of the cases: one GPU, and in-process ranks on the one GPU of the box
+# (-Dfsm.devices=0,0 / 0,0,0: the sharded engine reached from the drop-in)
+DEVICE_LISTS = [(0,), (0, 0), (0, 0, 0)]
+
+
 @pytest.mark.gpu
-def test_shim_spade_matches_golden(harness):
+@pytest.mark.parametrize("devices", DEVICE_LISTS)
+def test_shim_spade_matches_golden(harness, devices):
     """The JNI shim's Pattern.serialize() lines (SPADEActor.scala:49-50) equal
     the committed fixtures' patterns rendered the same way: every golden case,
     not a comparison with the engine's own Python path."""
     from spark_fsm_amd.api import Pattern
     for case in json.load(open(os.path.join(GOLD, "spade_cases.json"))):
         recs = [tuple(r) for r in case["records"]]
-        got = call(harness, "harness_spade", recs, case["support"], 0)
+        got = call(harness, "harness_spade", recs, case["support"], devices=devices)
         exp = [Pattern([list(x) for x in sets], sup).serialize() for sets, sup in case["patterns"]]
         assert sorted(got.splitlines()) == sorted(exp), case["name"]
     err = json.load(open(os.path.join(GOLD, "error_cases.json")))["spade"][0]
-    assert call(harness, "harness_spade", [tuple(r) for r in err["records"]], 0.5, 0).startswith(
+    assert call(harness, "harness_spade", [tuple(r) for r in err["records"]], 0.5, devices=devices).startswith(
         "EXCEPTION java/lang/Exception: libfsm fsm_db_from_spmf failed (FSM error 2)")
 
 
 @pytest.mark.gpu
-def test_shim_tsr_matches_golden(harness):
+@pytest.mark.parametrize("devices", DEVICE_LISTS)
+def test_shim_tsr_matches_golden(harness, devices):
     """The JNI shim's Rule accessors (TSRActor.scala:55-59) equal the committed
     fixtures' rules: antecedent, consequent, support and the confidence as the
     same IEEE double (the shim prints Double.toString's shortest form)."""
     for case in json.load(open(os.path.join(GOLD, "tsr_cases.json"))):
         recs = [tuple(r) for r in case["records"]]
-        got = call(harness, "harness_tsr", recs, case["k"], case["minconf"], 0)
+        got = call(harness, "harness_tsr", recs, case["k"], case["minconf"], devices=devices)
         exp = ["%s ==> %s #SUP: %d #CONF: %s" % (",".join(map(str, x)), ",".join(map(str, y)), sup, repr(float(c)))
                for x, y, sup, c in case["rules"]]
         norm = lambda lines: sorted((l.rsplit(" ", 1)[0], float(l.rsplit(" ", 1)[1])) for l in lines)
         assert norm(got.splitlines()) == norm(exp), case["name"]
     for err in json.load(open(os.path.join(GOLD, "error_cases.json")))["tsr"]:
-        out = call(harness, "harness_tsr", [tuple(r) for r in err["records"]], 3, 0.5, 0)
+        out = call(harness, "harness_tsr", [tuple(r) for r in err["records"]], 3, 0.5, devices=devices)
         assert out.startswith("EXCEPTION java/lang/Exception: libfsm ") and "(FSM error 2)" in out, err["name"]

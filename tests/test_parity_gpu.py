@@ -605,7 +605,9 @@ def test_sharded_tsr_failure_reaches_every_rank(tmp_path, monkeypatch):
     assert "injected" in res[1]["msg"] and "peer rank failed" in res[0]["msg"]
 
 
-@pytest.mark.parametrize("bitmap", ["1", "0", "passes", "domain-bitmap", "domain-list", "max-kids", "max-pos"])
+@pytest.mark.parametrize("bitmap", ["1", "0", "passes", "domain-bitmap", "domain-list", "max-kids", "max-pos",
+                                    "plist-off", "dlmemo-off", "dlmemo-tiny", "candq-heap", "ring-wrap",
+                                    "ring-wrap-2sets"])
 def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
     """TSR expansions over sid bitmaps (default: each slot's domain from the
     whole-bitmap AND or, for a rare item, from its sid list probed in the other
@@ -627,6 +629,22 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
         monkeypatch.setenv("FSM_TSR_MAX_KIDS", "10")
     if bitmap == "max-pos":
         monkeypatch.setenv("FSM_TSR_MAX_POS", "3")
+    # the replay's default-on features against the oracle, each off or at its edge: the kept-row
+    # lists off; the |sids(X u {c})| memo off, or 16 entries (full after a few counts: probes run
+    # out, most lookups miss); the candidate buckets as 4-ary heaps; a 1 MiB kept-row ring
+    # (65,536 entries) with 4 (or 2) launch sets in flight, so the head wraps the ring many times
+    # and launches still in flight hold ring positions (finished early before an overwrite)
+    if bitmap == "plist-off":
+        monkeypatch.setenv("FSM_TSR_PLIST", "0")
+    if bitmap == "dlmemo-off":
+        monkeypatch.setenv("FSM_TSR_DLMEMO", "0")
+    if bitmap == "dlmemo-tiny":
+        monkeypatch.setenv("FSM_TSR_DLMEMO_LOG2", "4")
+    if bitmap == "candq-heap":
+        monkeypatch.setenv("FSM_TSR_CANDQ", "heap")
+    if bitmap.startswith("ring-wrap"):
+        monkeypatch.setenv("FSM_TSR_ARENA_MB", "1")
+        monkeypatch.setenv("FSM_TSR_SETS", "2" if bitmap.endswith("2sets") else "4")
     ds = gen.kosarak(D=6000, seed=3)
     o = oracle.tsr(ds.records(), 300, 0.4)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)  # bitmaps are built at upload
@@ -750,3 +768,34 @@ def test_rule_queries_on_gpu_mined_rules(eng):
     assert hits > 0  # the queries do select rules
     assert mr.query(0, []) == [] and mr.query(1, items) == list(range(len(rules)))
     assert mr.to_json() == ref.rules_json(rules, mr.total)
+
+
+@pytest.mark.parametrize("devices", [(0, 0), (0, 0, 0)])
+def test_inproc_ranks_random_vs_oracle(fsm, devices):
+    """In-process ranks (fsm_opts.ndevices: one context, rank r on devices[r] as a thread of
+    this process, the drop-in's way to shard) on random SPMF-text DBs and Quest tokens:
+    the patterns / rules and thresholds of the oracle, and the join count."""
+    from oracle import oracle
+    from tools import gen
+    rng = random.Random(31 + len(devices))
+    with fsm.Engine(devices=list(devices)) as e:
+        for it in range(20):
+            recs = rand_records(rng, rng.randint(8, 60), rng.randint(2, 12), 6, 3, ts=it % 2 == 0)
+            sup = rng.choice([0.15, 0.2, 0.3, 0.5])
+            o = oracle.spade(recs, sup)
+            pats, _, st = gpu_spade(e, recs, sup)
+            assert pats == o["patterns"], (it, recs, sup)
+            assert st["joins"] == o["joins"]
+        for it in range(10):
+            recs = rand_records(rng, rng.randint(2, 60), rng.randint(2, 12), 6, 3, ts=False)
+            if not any(t not in ("-1", "-2") for _, l in recs for t in l.split(" ")):
+                continue
+            k, mc = rng.randint(1, 40), rng.choice([0.0, 0.2, 0.5, 0.9])
+            o = oracle.tsr(recs, k, mc)
+            rules, meta, _ = gpu_tsr(e, recs, k, mc)
+            assert rules == o["rules"], (it, recs, k, mc)
+            assert meta["final_minsup"] == o["final_minsup"]
+        ds = gen.quest(20000, seed=2)
+        o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
+        pats, meta, st = gpu_spade(e, None, 0.003, tokens=ds)
+        assert meta["minsup"] == o["minsup"] and pats == o["patterns"] and st["joins"] == o["joins"]
