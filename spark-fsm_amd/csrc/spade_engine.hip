@@ -613,12 +613,15 @@ __global__ __launch_bounds__(kBlock) void k_db_pos(const uint32_t* __restrict__ 
 // F2 plan of the DB-direct root: block b histograms, by rank group, the key capacity of
 // the frequent entries of its rpb rows that lie in the member range [mlo, mhi)
 // (temporal <= row's frequent entries, equality <= frequent partners after it).
+// tri (the unordered-pair layout below, gtab != nullptr): capacity 1 + 3 (partners after it),
+// the group from the rank's table entry.
 __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __restrict__ row_off,
                                                           const uint32_t* __restrict__ item,
                                                           const uint32_t* __restrict__ rk2, uint32_t R, uint32_t rpb,
                                                           uint32_t pm, uint32_t G, uint32_t nblk, uint32_t mlo,
                                                           uint32_t mhi, uint32_t* __restrict__ cap, uint32_t amask,
-                                                          uint32_t* __restrict__ mem_out) {
+                                                          uint32_t* __restrict__ mem_out,
+                                                          const uint32_t* __restrict__ gtab) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) h[g] = 0;
     __syncthreads();
@@ -643,7 +646,10 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
             const bool fr = e < e1 && !(v & 1u);
             const uint64_t bal = __ballot(fr);
             const uint32_t p = k + uint32_t(__popcll(bal & lt));
-            if (fr && v - mlo < mhi - mlo) atomicAdd(&h[group_of(v >> 1, pm)], 2 * len - 1 - p);
+            if (fr && v - mlo < mhi - mlo) {
+                if (gtab) atomicAdd(&h[gtab[v >> 1] >> kGroupShift], 1 + 3 * (len - 1 - p));
+                else atomicAdd(&h[group_of(v >> 1, pm)], 2 * len - 1 - p);
+            }
             k += uint32_t(__popcll(bal));
         }
     }
@@ -814,6 +820,193 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
 }
 
+// ---- Root F2 over unordered pairs (the "tri" layout, DB-direct root, W = 1).  The counts
+// of the ordered pairs (i -> j) and (j -> i), of the itemset pair (i, j), i < j by rank, and of
+// the repeat (i -> i) all sit in the counter tile of the lower rank i: row i holds
+// tri_len(i) = 1 + 3 (F - 1 - i) counters [t_ii | for j = i+1 .. F-1: t_ij, t_ji, e_ij].
+// Groups are contiguous rank ranges whose rows fit kGroupCounters (gtab[rank] = group << 15 |
+// the row's first counter in the group tile).  One test of an unordered pair of a row then
+// yields all three of its keys, every key goes to the group of the lower rank, and the
+// pairs of a row are folded: a lane segment of S >= n + 1 lanes holds the partners j >= i of
+// entry i and those of entry n - 1 - i together, so the enumeration evaluates each unordered
+// pair once (half the tests of the ordered scheme) on (nearly) every lane.  A lane takes its
+// key slots with one LDS atomic on its group's cursor (the lanes of one entry share it).
+__host__ __device__ __forceinline__ uint32_t tri_len(uint32_t F, uint32_t i) { return 1u + 3u * (F - 1u - i); }
+// the first counter of row i in a group that starts at row a (rows a .. i - 1 before it)
+__host__ __device__ __forceinline__ uint32_t tri_base(uint32_t F, uint32_t a, uint32_t i) {
+    const uint32_t m = i - a;
+    // sum_{r=a}^{i-1} (1 + 3 (F - 1 - r)); (a + i - 1) m is even (the two factors' sum is odd)
+    return m + 3u * (m * (F - 1u) - (a + i - 1u) * m / 2u);
+}
+
+// The keys of the unordered pairs (ie, je) of one wave step, je == ie the repeat.  The lanes of
+// one entry ie form a contiguous run [st, en] (a sub-segment); its keys take one region cursor
+// reservation (the run's first lane), and are written per kind in contiguous blocks: the
+// (i -> j) keys of the run, then its (j -> i), then its (i, j) keys.  Lane offsets come from
+// mbcnt prefixes packed three to a word (byte fields), the run's totals from the prefixes at
+// its ends (two bpermutes), the reserved offset back from the first lane (one bpermute).
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src) {
+    return uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(v)));
+}
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+}
+__device__ __forceinline__ void tri_keys(bool t0, bool t1, bool t2, uint32_t key0, uint32_t grp, uint32_t st,
+                                         uint32_t en, uint32_t* __restrict__ cur, uint16_t* __restrict__ keys) {
+    const uint64_t M0 = __ballot(t0), M1 = __ballot(t1), M2 = __ballot(t2);
+    if (!(M0 | M1 | M2)) return;  // (wave-uniform)
+    const uint32_t pk = mbcnt64(M0) | (mbcnt64(M1) << 8) | (mbcnt64(M2) << 16);
+    const uint32_t qk = pk + (uint32_t(t0) | (uint32_t(t1) << 8) | (uint32_t(t2) << 16));
+    const uint32_t ps = bperm(pk, st), tot = bperm(qk, en) - ps;
+    const uint32_t T0 = tot & 0xFFu, T1 = (tot >> 8) & 0xFFu, T2 = tot >> 16;
+    uint32_t off = 0;
+    if (lane_id() == st && (T0 | T1 | T2)) off = atomicAdd(&cur[grp], T0 + T1 + T2);
+    off = bperm(off, st);
+    const uint32_t loc = pk - ps;
+    if (t0) keys[off + (loc & 0xFFu)] = uint16_t(key0);
+    if (t1) keys[off + T0 + ((loc >> 8) & 0xFFu)] = uint16_t(key0 + 1u);
+    if (t2) keys[off + T0 + T1 + (loc >> 16)] = uint16_t(key0 + 2u);
+}
+
+// the pair (ie, je) of a row staged in LDS (je == ie: the repeat), lanes [st, en] sharing ie
+__device__ __forceinline__ void tri_pair(bool ok, uint32_t ie, uint32_t je, uint32_t st, uint32_t en,
+                                         const uint4* __restrict__ stage, const uint32_t* __restrict__ sgt,
+                                         uint32_t* __restrict__ cur, uint16_t* __restrict__ keys) {
+    const uint4 Ei = stage[ok ? ie : 0], Ej = stage[ok ? je : 0];
+    const uint32_t gt = sgt[ok ? ie : 0];
+    const uint32_t lo_i = Ei.y & 0xFFFFu, hi_i = Ei.y >> 16, lo_j = Ej.y & 0xFFFFu, hi_j = Ej.y >> 16;
+    const bool self = je == ie;
+    const bool t0 = ok && lo_i < (self ? hi_i : hi_j);
+    const bool t1 = ok && !self && lo_j < hi_i;
+    const bool t2 = ok && !self && ((Ei.z & Ej.z) | (Ei.w & Ej.w)) != 0u;
+    const uint32_t key0 = (gt & (kGroupCounters - 1u)) + (self ? 0u : 1u + 3u * (Ej.x - Ei.x - 1u));
+    tri_keys(t0, t1, t2, key0, gt >> kGroupShift, st, en, cur, keys);
+}
+
+__global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restrict__ row_off32,
+                                                      const uint32_t* __restrict__ mem,
+                                                      const uint64_t* __restrict__ mask, uint32_t R, uint32_t rpb,
+                                                      const uint32_t* __restrict__ gtab, uint32_t G, uint32_t nblk,
+                                                      uint32_t mlo, uint32_t mhi, const uint64_t* __restrict__ base,
+                                                      uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
+                                                      unsigned long long* __restrict__ nkeys_total) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint4* stage_all = reinterpret_cast<uint4*>(smem);            // kF2Waves x 64: rank, lo | hi << 16, mask
+    uint32_t* sgt_all = smem + kF2Waves * 64 * 4;                  // kF2Waves x 64: gtab of the active entries
+    uint32_t* srow = sgt_all + kF2Waves * 64;                      // row offsets of the block [rpb + 1]
+    uint32_t* cur = srow + kF2RowWords;                            // region cursors [G]
+    __shared__ uint32_t blk_keys;
+    const uint32_t b = blockIdx.x;
+    const uint32_t r0 = b * rpb, r1 = min(R, r0 + rpb);
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[f2_region(g, b, nblk)]);
+    for (uint32_t r = r0 + threadIdx.x; r <= r1; r += blockDim.x) srow[r - r0] = row_off32[r];
+    if (threadIdx.x == 0) blk_keys = 0;
+    __syncthreads();
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    uint4* stage = stage_all + wave * 64;
+    uint32_t* sgt = sgt_all + wave * 64;
+    const uint64_t lt = lanemask_lt();
+    // the next row's entries are loaded while the current row is enumerated
+    uint32_t nrb = 0, nrl = 0, nme = 0;
+    uint64_t nmk = 0;
+    auto fetch = [&](uint32_t rr) {
+        if (rr >= r1) return;
+        nrb = srow[rr - r0];
+        nrl = srow[rr - r0 + 1] - nrb;
+        if (nrl <= 64 && lane < nrl) {
+            nme = mem[nrb + lane];
+            nmk = mask[nrb + lane];
+        }
+    };
+    fetch(r0 + wave);
+    for (uint32_t r = r0 + wave; r < r1; r += kF2Waves) {
+        const uint32_t rb = rfl(nrb), rl = rfl(nrl), me = nme;
+        const uint64_t mk = nmk;
+        fetch(r + kF2Waves);
+        if (rl == 0) continue;
+        if (rl <= 64) {
+            // the row's frequent entries, compacted (positions ascend with the rank); the active
+            // ones (this rank's member range) are a contiguous run [a0, a1) of them
+            const bool fr = lane < rl && !(me & 1u);
+            const bool act = fr && me - mlo < mhi - mlo;
+            const uint64_t fb = __ballot(fr), ab = __ballot(act);
+            if (!ab) continue;
+            const uint32_t n = uint32_t(__popcll(fb));
+            const uint32_t a0 = uint32_t(__popcll(fb & ((1ull << __builtin_ctzll(ab)) - 1ull)));
+            const uint32_t a1 = a0 + uint32_t(__popcll(ab));
+            if (fr) {
+                const uint32_t p = uint32_t(__popcll(fb & lt));
+                const uint32_t lh = uint32_t(__builtin_ctzll(mk)) | ((63u - uint32_t(__builtin_clzll(mk))) << 16);
+                stage[p] = make_uint4(me >> 1, lh, uint32_t(mk), uint32_t(mk >> 32));
+                if (act) sgt[p] = gtab[me >> 1];
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t need = 2u * n + 1u - a0 - a1;  // partners of a folded pair of entries
+            if (need <= 64u) {
+                const uint32_t npairs = (a1 - a0 + 1u) >> 1;
+                const uint32_t lg = need <= 1u ? 0u : 32u - uint32_t(__clz(need - 1u));  // S = 2^lg >= need
+                const uint32_t k = 64u >> lg, l = lane & ((1u << lg) - 1u), sub = lane >> lg;
+                const uint32_t s0 = lane & ~((1u << lg) - 1u), S = 1u << lg;
+                for (uint32_t f0 = 0; f0 < npairs; f0 += k) {
+                    const uint32_t fp = f0 + sub;
+                    const uint32_t iA = a0 + fp, iB = a1 - 1u - fp, cA = min(n - iA, S);
+                    const bool second = l >= cA;
+                    const uint32_t ie = second ? iB : iA, je = ie + (second ? l - cA : l);
+                    const bool ok = fp < npairs && je < n && (!second || iB > iA);
+                    // the run of lanes of ie: [s0, s0 + cA) for iA, [s0 + cA, s0 + S) for iB
+                    const uint32_t st = second ? s0 + cA : s0, en = second ? s0 + S - 1u : s0 + cA - 1u;
+                    tri_pair(ok, ie, je, st, en, stage, sgt, cur, keys);
+                }
+            } else {
+                for (uint32_t i = a0; i < a1; ++i)
+                    for (uint32_t c0 = 0; i + c0 < n; c0 += 64) {
+                        const uint32_t je = i + c0 + lane;
+                        tri_pair(je < n, i, je, 0u, 63u, stage, sgt, cur, keys);
+                    }
+            }
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            // a row of more than 64 entries: entry i wave-uniform, its partners j >= i in chunks
+            // of 64 lanes, read from the DB
+            for (uint32_t ip = 0; ip < rl; ++ip) {
+                const uint32_t mi = rfl(mem[rb + ip]);
+                if ((mi & 1u) || !(mi - mlo < mhi - mlo)) continue;
+                const uint64_t mki = mask[rb + ip];
+                const uint32_t lo_i = uint32_t(__builtin_ctzll(mki)), hi_i = 63u - uint32_t(__builtin_clzll(mki));
+                const uint32_t gt = gtab[mi >> 1], ri = mi >> 1;
+                for (uint32_t c0 = ip; c0 < rl; c0 += 64) {
+                    const uint32_t jp = c0 + lane;
+                    bool ok = jp < rl;
+                    uint32_t mj = 1u;
+                    uint64_t mkj = 1ull;
+                    if (ok) {
+                        mj = mem[rb + jp];
+                        mkj = mask[rb + jp];
+                    }
+                    ok = ok && !(mj & 1u);
+                    const uint32_t lo_j = uint32_t(__builtin_ctzll(mkj)), hi_j = 63u - uint32_t(__builtin_clzll(mkj));
+                    const bool self = jp == ip;
+                    const bool t0 = ok && lo_i < (self ? hi_i : hi_j);
+                    const bool t1 = ok && !self && lo_j < hi_i;
+                    const bool t2 = ok && !self && (mki & mkj) != 0ull;
+                    const uint32_t key0 = (gt & (kGroupCounters - 1u)) + (self ? 0u : 1u + 3u * ((mj >> 1) - ri - 1u));
+                    tri_keys(t0, t1, t2, key0, gt >> kGroupShift, 0u, 63u, cur, keys);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t my_keys = 0;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
+        const uint32_t f = cur[g] - uint32_t(base[f2_region(g, b, nblk)]);
+        fill[uint64_t(g) * nblk + b] = f;
+        my_keys += f;
+    }
+    atomicAdd(&blk_keys, my_keys);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk_keys) atomicAdd(nkeys_total, (unsigned long long)blk_keys);
+}
+
 // One block per rank group.  The group's regions (one per row block, each
 // starting on a 16-byte boundary, holes after their fills) are read as one
 // logical stream of 8-key chunks: the block loads the regions' fills and
@@ -826,14 +1019,17 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
 // kOut (the keyed class count): the group's kGroupCounters counters are written
 // out to cnt_out[g * kGroupCounters ...] instead of extracted.
 constexpr uint32_t kF2MaxBlocks = 2048;  // row blocks (regions per group) k_f2_count can index in LDS
-template <bool kOut>
+// kTri: the unordered-pair layout (k_f2_tri): group g holds rows tri_gr[g] .. tri_gr[g + 1] of
+// tri_len(F, i) counters each, decoded back to ordered (row, slot) records at the extraction.
+template <bool kOut, bool kTri = false>
 __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restrict__ base,
                                                          const uint32_t* __restrict__ fill, uint32_t nblk,
                                                          const uint16_t* __restrict__ keys, uint32_t D, uint32_t per,
                                                          uint32_t g0, uint32_t rlo, uint32_t rhi, uint32_t minsup,
                                                          FreqRec* __restrict__ recs, uint32_t cap,
                                                          uint32_t* __restrict__ nrec, uint32_t* __restrict__ cnt_out,
-                                                         uint32_t parts) {
+                                                         uint32_t parts, const uint32_t* __restrict__ tri_gr = nullptr,
+                                                         uint32_t triF = 0) {
     __shared__ uint32_t h[kGroupCounters];
     __shared__ uint32_t cpre[kF2MaxBlocks + 1];  // first logical chunk of each region
     __shared__ uint32_t cst[kF2MaxBlocks];       // first physical chunk of each region
@@ -844,7 +1040,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
     const uint32_t rb0 = uint32_t(uint64_t(nblk) * part / parts), rb1 = uint32_t(uint64_t(nblk) * (part + 1) / parts);
     const uint32_t nr = rb1 - rb0;
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    const uint32_t nz = kOut ? kGroupCounters : per * D;
+    const uint32_t nz = kOut ? kGroupCounters : (kTri ? tri_base(triF, tri_gr[g], tri_gr[g + 1]) : per * D);
     for (uint32_t t = threadIdx.x; t < nz; t += blockDim.x) h[t] = 0;
     // region chunk counts -> exclusive prefix (nblk <= 2 * blockDim.x: two per thread)
     const uint64_t gi = uint64_t(g) * nblk + rb0;
@@ -910,6 +1106,37 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
         } else {  // shared group (zeroed beforehand): contiguous adds of the non-zero counters
             for (uint32_t t = threadIdx.x; t < kGroupCounters; t += blockDim.x)
                 if (h[t]) atomicAdd(o + t, h[t]);
+        }
+        return;
+    }
+    if constexpr (kTri) {
+        // counter c of the tile: row i = the last row whose first counter is <= c; then the repeat
+        // (i -> i) or, for the partner j = i + 1 + q / 3, (i -> j), (j -> i), (i, j) by q % 3
+        const uint32_t a = tri_gr[g], z = tri_gr[g + 1];
+        for (uint32_t c0 = wave * 64; c0 < nz; c0 += kF2Threads) {
+            const uint32_t c = c0 + lane;
+            const uint32_t val = c < nz ? h[c] : 0u;
+            const bool fr = c < nz && val >= minsup;
+            const uint64_t fb = __ballot(fr);
+            if (!fb) continue;
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(nrec, uint32_t(__popcll(fb)));
+            at = rfl(at) + uint32_t(__popcll(fb & lanemask_lt()));
+            if (fr && at < cap) {
+                uint32_t lo = a, hi = z;  // tri_base(F, a, lo) <= c < tri_base(F, a, hi)
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (tri_base(triF, a, mid) <= c) lo = mid; else hi = mid;
+                }
+                const uint32_t off = c - tri_base(triF, a, lo);
+                FreqRec rc{lo, 2u * lo, val, 0u};  // the repeat: (i -> i), a sequence-extension
+                if (off) {
+                    const uint32_t q = off - 1u, j = lo + 1u + q / 3u, code = q % 3u;
+                    rc = code == 0 ? FreqRec{lo, 2u * j, val, 0u}
+                                   : (code == 1 ? FreqRec{j, 2u * lo, val, 0u} : FreqRec{lo, 2u * j + 1u, val, 0u});
+                }
+                recs[at] = rc;
+            }
         }
         return;
     }
@@ -1919,6 +2146,10 @@ struct Batch {
     bool f2_planned = false;
     DevBuf f2_base;
     uint64_t f2_nslots = 0;
+    // the root F2 in the unordered-pair layout (k_f2_tri): [gtab: F | group start ranks: G + 1]
+    bool f2_tri = false;
+    DevBuf f2_tri_tab;
+    uint32_t f2_tri_G = 0;
     // DB-direct root (no root slab): its kernels read the DB rows through rk2 (dense item ->
     // member id, odd for an infrequent item)
     bool db_direct = false;
@@ -1957,6 +2188,9 @@ struct Batch {
         f2_planned = false;
         f2_base.release();
         f2_nslots = 0;
+        f2_tri = false;
+        f2_tri_tab.release();
+        f2_tri_G = 0;
         db_direct = false;
         rk2.release();
         mem_db.release();
@@ -2393,6 +2627,34 @@ struct Miner {
         }();
         return a;
     }
+    // the root F2 in the unordered-pair layout (k_f2_tri; FSM_F2_TRI=0: the ordered layout)
+    static bool f2_tri_env() {
+        const char* v = std::getenv("FSM_F2_TRI");
+        return !(v && v[0] == '0');
+    }
+    // groups of the unordered-pair layout over the rows [rlo, rhi) of F ranks: gtab[i] = group <<
+    // kGroupShift | first counter of row i; gr = the groups' first rows (G + 1).  0 groups: a
+    // row does not fit a tile, or too many groups (the ordered layout runs)
+    static uint32_t tri_tables(uint32_t F, uint32_t rlo, uint32_t rhi, std::vector<uint32_t>& tab) {
+        if (F == 0 || tri_len(F, 0) > kGroupCounters || rlo >= rhi) return 0;
+        tab.assign(size_t(F), 0u);
+        std::vector<uint32_t> gr{rlo};
+        uint32_t acc = 0;
+        for (uint32_t i = rlo; i < rhi; ++i) {
+            const uint32_t L = tri_len(F, i);
+            if (acc + L > kGroupCounters) {
+                gr.push_back(i);
+                acc = 0;
+            }
+            tab[i] = uint32_t(gr.size() - 1) << kGroupShift | acc;
+            acc += L;
+        }
+        gr.push_back(rhi);
+        const uint32_t G = uint32_t(gr.size() - 1);
+        if (G > kMaxGroups || G >= (1u << (32 - kGroupShift))) return 0;
+        tab.insert(tab.end(), gr.begin(), gr.end());
+        return G;
+    }
     // row blocks of the root F2 (FSM_F2_BLOCKS overrides the target count, for tuning)
     static uint32_t f2_blocks() {
         const char* v = std::getenv("FSM_F2_BLOCKS");
@@ -2441,6 +2703,7 @@ struct Miner {
         const uint32_t D = geo.D, F = geo.F, per = geo.per, G = geo.G, pm = geo.pm, mlo = geo.mlo, mhi = geo.mhi;
         const uint32_t rlo = comm ? slice_lo : 0u, rhi = comm ? std::min(slice_hi, F) : F;
         const uint32_t R = geo.R, rpb = geo.rpb, nblk = geo.nblk;
+        if (b.f2_tri) return root_f2_tri(b, recs, geo, rlo, rhi);
         const uint64_t nd = geo.nd;
         const SlabPtrs sp = b.slab.ptrs();
         const int64_t E0 = int64_t(m.cap);
@@ -2532,6 +2795,64 @@ struct Miner {
         ctx->stats.root_keys += int64_t(nkeys);
         // (row, slot) order and child member ids: rank among the row's slots with a frequent
         // temporal or equality candidate, << 1 | type (as k_freq_write assigns them)
+        const double th0 = now_ms();
+        order_recs(recs, F);
+        hp[0] += now_ms() - th0;
+        return true;
+    }
+    // The root F2 in the unordered-pair layout (k_f2_plan_db with the group table, k_f2_tri,
+    // k_f2_count<false, true>): the frequent ordered pairs of the rows [rlo, rhi), as records
+    // in (row, slot) order.  A pair (i, j) counts where the lower rank i is owned, so a rank's
+    // records also hold rows j above its slice (the sharded gather orders them again).
+    bool root_f2_tri(Batch& b, std::vector<FreqRec>& recs, const F2Geo& geo, uint32_t rlo, uint32_t rhi) {
+        const uint32_t F = geo.F, G = b.f2_tri_G, R = geo.R, rpb = geo.rpb, nblk = geo.nblk;
+        const uint64_t nd = uint64_t(G) * nblk;
+        DevBuf base = std::move(b.f2_base), fill(nd * 4);
+        const uint64_t nslots = b.f2_nslots;
+        if (nslots >= (uint64_t(1) << 32) - 4096) return false;
+        DevBuf keys((nslots + 1024) * 2), nk(8);
+        FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
+        const uint32_t* gtab = b.f2_tri_tab.as<uint32_t>();
+        const uint32_t* gr = gtab + F;
+        const size_t kshm = size_t(kF2Waves) * 64 * 20 + size_t(kF2RowWords) * 4 + size_t(G) * 4;
+        const size_t tk_keys = clk->begin("k_f2_keys");
+        hipLaunchKernelGGL(k_f2_tri, dim3(nblk), dim3(kF2Threads), kshm, s, db->row_off.as<uint32_t>(),
+                           b.mem_db.as<uint32_t>(), db->mask.as<uint64_t>(), R, rpb, gtab, G, nblk, geo.mlo, geo.mhi,
+                           base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>());
+        FSM_LAUNCHED("k_f2_tri", s);
+        clk->end(tk_keys, db->E * 12 + int64_t(nd) * 12, int64_t(b.cls[0].cap) * 8);
+        // count + frequent pairs (a retry when the first record buffer was too small)
+        uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * 2 * F, uint64_t(1) << 20));
+        DevBuf d_nrec(4), d_recs;
+        size_t tk_cnt = 0;
+        unsigned long long nkeys = 0;
+        for (int attempt = 0;; ++attempt) {
+            d_recs.alloc(std::max<uint32_t>(cap_recs, 1) * sizeof(FreqRec));
+            FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
+            tk_cnt = clk->begin("k_f2_count");
+            hipLaunchKernelGGL((k_f2_count<false, true>), dim3(G), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
+                               fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), 2 * F, 0u, 0u, rlo, rhi, minsup,
+                               d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u, gr, F);
+            FSM_LAUNCHED("k_f2_count", s);
+            clk->end(tk_cnt, int64_t(G) * nblk * 12);
+            uint32_t nrec = 0;
+            FSM_HIP(hipMemcpyAsync(&nrec, d_nrec.p, 4, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&nkeys, nk.p, 8, hipMemcpyDeviceToHost, s));
+            sync();
+            if (nrec <= cap_recs || attempt > 0) {
+                if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
+                recs.resize(nrec);
+                if (nrec)
+                    FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, size_t(nrec) * sizeof(FreqRec), hipMemcpyDeviceToHost,
+                                           s));
+                sync();
+                break;
+            }
+            cap_recs = nrec;
+        }
+        clk->add_bytes(tk_keys, int64_t(nkeys) * 2);
+        clk->add_bytes(tk_cnt, int64_t(nkeys) * 2 + int64_t(recs.size() * sizeof(FreqRec)));
+        ctx->stats.root_keys += int64_t(nkeys);
         const double th0 = now_ms();
         order_recs(recs, F);
         hp[0] += now_ms() - th0;
@@ -2875,6 +3196,9 @@ struct Miner {
             nfreq = all.size() / sizeof(FreqRec);
             recs.resize(nfreq);
             if (nfreq) std::memcpy(recs.data(), all.data(), all.size());
+            // the unordered-pair F2 gives a rank records of rows above its slice: (row, slot)
+            // order and the child ids over the whole set
+            if (b.f2_tri) order_recs(recs, uint32_t(rows.size()));
             R = recs.data();
         }
         double th = now_ms();
@@ -3416,19 +3740,35 @@ struct Miner {
             }
         }
         upload(root.rk2, rk2);
+        // the unordered-pair layout (W = 1): its own groups over this rank's rows
+        uint32_t G = geo.G;
+        uint64_t nd = geo.nd;
+        root.f2_tri = false;
+        if (W == 1 && f2_tri_env() && f2_passes() == 1) {
+            std::vector<uint32_t> tab;
+            const uint32_t rlo = geo.mlo / 2, rhi = geo.mhi == kNone ? F : std::min(geo.mhi / 2, F);
+            const uint32_t TG = tri_tables(F, rlo, rhi, tab);
+            if (TG) {
+                upload(root.f2_tri_tab, tab);
+                root.f2_tri = true;
+                root.f2_tri_G = TG;
+                G = TG;
+                nd = uint64_t(TG) * geo.nblk;
+            }
+        }
         root.mem_db.alloc(std::max<int64_t>(db->E, 1) * 4);
-        DevBuf cap(geo.nd * 4);
-        root.f2_base.alloc((geo.nd + 1) * 8);
+        DevBuf cap(nd * 4);
+        root.f2_base.alloc((nd + 1) * 8);
         const size_t tk = clk->begin("k_f2_plan");
-        hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,
+        hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), size_t(G) * 4, s,
                            db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), root.rk2.as<uint32_t>(), geo.R,
-                           geo.rpb, geo.pm, geo.G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(), f2_align() - 1,
-                           root.mem_db.as<uint32_t>());
+                           geo.rpb, geo.pm, G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(), f2_align() - 1,
+                           root.mem_db.as<uint32_t>(), root.f2_tri ? root.f2_tri_tab.as<uint32_t>() : nullptr);
         FSM_LAUNCHED("k_f2_plan", s);
-        clk->end(tk, int64_t(db->R) * 4 + db->E * 8 + int64_t(geo.nd) * 4);
-        scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), geo.nd, s);
+        clk->end(tk, int64_t(db->R) * 4 + db->E * 8 + int64_t(nd) * 4);
+        scan_exclusive(cap.as<uint32_t>(), root.f2_base.as<uint64_t>(), nd, s);
         pend[2] = 0;
-        FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + geo.nd, 8, hipMemcpyDeviceToHost, s));
+        FSM_HIP(hipMemcpyAsync(&pend[2], root.f2_base.as<uint64_t>() + nd, 8, hipMemcpyDeviceToHost, s));
         root_meta(root, freq_items, f1);
         // the root entries: one per (sequence, frequent item), so the frequent items' supports add up to them
         uint64_t E0 = 0;
