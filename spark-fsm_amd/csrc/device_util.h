@@ -15,6 +15,11 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 __device__ __forceinline__ unsigned lane_id() { return threadIdx.x & 63u; }
 
+// wave64 ballot of a condition.  HIP's __ballot(int) turns the condition into an int
+// first (v_cndmask 0/1, then v_cmp_ne on it: two VALU per ballot on gfx950); the
+// builtin takes the i1 and reads the compare's lane mask (SGPR pair) directly.
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const unsigned l = lane_id();
     return l ? (~0ull >> (64u - l)) : 0ull;

@@ -93,7 +93,7 @@ __device__ __forceinline__ void k0_wave_row(const int32_t* __restrict__ tok, uin
     const int64_t v64 = valid ? tok[t0 + lane] : -2;
     const int32_t v = int32_t(v64);
     const bool sep = v64 == -1, itm = valid && v64 != -1 && v64 != -2;
-    const uint64_t sepb = __ballot(sep), itb = __ballot(itm);
+    const uint64_t sepb = ballot(sep), itb = ballot(itm);
     const uint32_t k = uint32_t(__popcll(sepb & lt));  // itemset index
     const uint32_t nsep = uint32_t(__popcll(sepb));
     const bool closed = itm && k < nsep;  // items after the last -1 are dropped
@@ -104,7 +104,7 @@ __device__ __forceinline__ void k0_wave_row(const int32_t* __restrict__ tok, uin
         const uint64_t prev = sepb & lt;
         const uint64_t after_prev = prev ? ~((2ull << (63 - __clzll(prev))) - 1ull) : ~0ull;
         const bool ne = sep && (itb & lt & after_prev) != 0ull;
-        const uint64_t neb = __ballot(ne);
+        const uint64_t neb = ballot(ne);
         pay = uint32_t(__popcll(neb & lt));  // eid: non-empty closed itemsets before this item
         neids = uint32_t(__popcll(neb));
     }
@@ -127,15 +127,15 @@ __device__ __forceinline__ void k0_wave_row(const int32_t* __restrict__ tok, uin
     const bool vk_next = __shfl_down(int(vk), 1, 64) != 0 && lane < 63;
     const bool head = vk && (lane == 0 || hv_prev != hv);
     const bool tail = vk && (!vk_next || hv_next != hv);
-    const uint64_t headb = __ballot(head);
+    const uint64_t headb = ballot(head);
     const uint32_t nent = uint32_t(__popcll(headb));
     const int32_t val = int32_t(hv ^ 0x80000000u);
     if (!kWrite) {
         if (lane == 0) cnt[r] = nent;
         if (kMode == kSpade) {
             st.max_eids = max(st.max_eids, neids);
-            st.max_occ = max(st.max_occ, uint32_t(__popcll(__ballot(closed))));
-        } else if (__ballot(head && val < 0)) {
+            st.max_occ = max(st.max_occ, uint32_t(__popcll(ballot(closed))));
+        } else if (ballot(head && val < 0)) {
             st.neg_item = 1;
         }
         if (head) {

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_root_write(const uint32_t* __restric
         const uint32_t e = b + lane_id();
         const uint32_t rk = e < e1 ? rank[item[e]] : kNone;
         const bool fr = rk != kNone;
-        const uint64_t bal = __ballot(fr);
+        const uint64_t bal = ballot(fr);
         if (fr) {
             const uint32_t p = k + uint32_t(__popcll(bal & lanemask_lt()));
             const uint64_t d = ob + p;
@@ -311,11 +311,11 @@ __global__ __launch_bounds__(1024) void k_cnt_keys(uint32_t E, uint32_t epb, con
         // cursors, so the wave reserves once per distinct group among its lanes
         uint32_t at = 0;
         if (G <= 64) {
-            for (uint64_t todo = __ballot(n > 0); todo;) {
+            for (uint64_t todo = ballot(n > 0); todo;) {
                 const int lead = __ffsll((unsigned long long)todo) - 1;
                 const uint32_t lg = uint32_t(__shfl(int(g), lead, 64));
                 const bool in = n > 0 && g == lg;
-                const uint64_t m = __ballot(in);
+                const uint64_t m = ballot(in);
                 const uint32_t v = in ? n : 0u;
                 const uint32_t incl = wave_incl_scan(v);
                 const uint32_t tot = uint32_t(__shfl(int(incl), 63, 64));
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
             const uint32_t e = b0 + lane;
             const uint32_t rk = b0 == rb ? rk0 : (e < e1 ? rank[item[e]] : kNone);
             const bool fr = rk != kNone;
-            const uint64_t bal = __ballot(fr);
+            const uint64_t bal = ballot(fr);
             if (fr) {
                 const uint32_t p = k + uint32_t(__popcll(bal & lanemask_lt()));
                 const uint64_t d = ob + p;
@@ -637,14 +637,14 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_plan_db(const uint32_t* __res
             const uint32_t v = e < e1 ? rk2[item[e]] : kNone;
             if (e < e1) mem_out[e] = v;  // the entries' member ids, read by the F2 keys and the root emit
             if (b0 == rb) v0 = v;
-            len += uint32_t(__popcll(__ballot(e < e1 && !(v & 1u))));
+            len += uint32_t(__popcll(ballot(e < e1 && !(v & 1u))));
         }
         uint32_t k = 0;
         for (uint32_t b0 = rb; b0 < e1; b0 += 64) {
             const uint32_t e = b0 + lane;
             const uint32_t v = b0 == rb ? v0 : (e < e1 ? rk2[item[e]] : kNone);
             const bool fr = e < e1 && !(v & 1u);
-            const uint64_t bal = __ballot(fr);
+            const uint64_t bal = ballot(fr);
             const uint32_t p = k + uint32_t(__popcll(bal & lt));
             if (fr && v - mlo < mhi - mlo) {
                 if (gtab) atomicAdd(&h[gtab[v >> 1] >> kGroupShift], 1 + 3 * (len - 1 - p));
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
             // active entries i are compacted into LDS with all a step needs (one 16-byte read,
             // issued a step ahead); the segment's cursor offset comes back by readlane (S >= 32)
             const bool act = lane < rl && !(me & 1u) && me - mlo < mhi - mlo;
-            const uint64_t actb = __ballot(act);
+            const uint64_t actb = ballot(act);
             const uint32_t nact = uint32_t(__popcll(actb));
             const uint32_t ri = me >> 1, g = group_of(ri, pm);
             if (lane < rl) {
@@ -742,7 +742,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                     const uint32_t gi = A.a & 0xFFFFu, i = A.a >> 16, li = A.b >> 16;
                     const bool t_ok = vi && vj && hi_j > li;
                     const bool e_ok = vi && vj && j > i && (ej.mask & A.mask) != 0ull;
-                    const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
+                    const uint64_t tb = ballot(t_ok), eb = ballot(e_ok);
                     const uint32_t nt = uint32_t(__popcll(tb & segm)), n = nt + uint32_t(__popcll(eb & segm));
                     uint32_t off = 0;
                     if (lane == s0 && n) off = atomicAdd(&cur[gi], n);
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                             if (q > i) e_ok = mi.and_any(mask + size_t(rb + q) * mask_words<W>(wd), wd);
                         }
                     }
-                    const uint64_t tb = __ballot(t_ok), eb = __ballot(e_ok);
+                    const uint64_t tb = ballot(t_ok), eb = ballot(e_ok);
                     const uint32_t nt = uint32_t(__popcll(tb)), n = nt + uint32_t(__popcll(eb));
                     if (n == 0) continue;
                     uint32_t off = 0;
@@ -851,9 +851,17 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src) {
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
 }
-__device__ __forceinline__ void tri_keys(bool t0, bool t1, bool t2, uint32_t key0, uint32_t grp, uint32_t st,
-                                         uint32_t en, uint32_t* __restrict__ cur, uint16_t* __restrict__ keys) {
-    const uint64_t M0 = __ballot(t0), M1 = __ballot(t1), M2 = __ballot(t2);
+// compare lane masks straight from v_cmp (a ballot of a combined bool is materialised as
+// v_cndmask + v_cmp first); predicates: LLVM's ICMP_EQ 32, NE 33, ULT 36
+__device__ __forceinline__ uint64_t lt_mask(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 36); }
+__device__ __forceinline__ uint64_t eq_mask(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 32); }
+__device__ __forceinline__ uint64_t nz_mask(uint64_t a) { return __builtin_amdgcn_uicmpl(a, 0ull, 33); }
+
+// M0 / M1 / M2: the lanes with an (i -> j) / (j -> i) / (i, j) key (masks), t0..t2 the same as
+// the lane's own conditions
+__device__ __forceinline__ void tri_keys(uint64_t M0, uint64_t M1, uint64_t M2, bool t0, bool t1, bool t2,
+                                         uint32_t key0, uint32_t grp, uint32_t st, uint32_t en,
+                                         uint32_t* __restrict__ cur, uint16_t* __restrict__ keys) {
     if (!(M0 | M1 | M2)) return;  // (wave-uniform)
     const uint32_t pk = mbcnt64(M0) | (mbcnt64(M1) << 8) | (mbcnt64(M2) << 16);
     const uint32_t qk = pk + (uint32_t(t0) | (uint32_t(t1) << 8) | (uint32_t(t2) << 16));
@@ -868,19 +876,27 @@ __device__ __forceinline__ void tri_keys(bool t0, bool t1, bool t2, uint32_t key
     if (t2) keys[off + T0 + T1 + (loc >> 16)] = uint16_t(key0 + 2u);
 }
 
-// the pair (ie, je) of a row staged in LDS (je == ie: the repeat), lanes [st, en] sharing ie
-__device__ __forceinline__ void tri_pair(bool ok, uint32_t ie, uint32_t je, uint32_t st, uint32_t en,
-                                         const uint4* __restrict__ stage, const uint32_t* __restrict__ sgt,
-                                         uint32_t* __restrict__ cur, uint16_t* __restrict__ keys) {
+// The pair (ie, je) of a row staged in LDS (je == ie: the repeat), okm the lanes with a pair,
+// lanes [st, en] sharing ie.  A staged entry: x = 3 rank | group << 16, y = lo | hi << 8 |
+// (A + kTriA) << 16 with A = (first counter of its row) - 3 rank - 2, z / w its mask: the key of
+// (i -> j) is then A_i + 3 rank_j, that of the repeat A_i + 3 rank_i + 2 (the row's first counter).
+constexpr uint32_t kTriA = 32770u;
+__device__ __forceinline__ void tri_pair(uint64_t okm, uint32_t ie, uint32_t je, uint32_t st, uint32_t en,
+                                         const uint4* __restrict__ stage, uint32_t* __restrict__ cur,
+                                         uint16_t* __restrict__ keys) {
+    const bool ok = (okm >> lane_id()) & 1ull;
     const uint4 Ei = stage[ok ? ie : 0], Ej = stage[ok ? je : 0];
-    const uint32_t gt = sgt[ok ? ie : 0];
-    const uint32_t lo_i = Ei.y & 0xFFFFu, hi_i = Ei.y >> 16, lo_j = Ej.y & 0xFFFFu, hi_j = Ej.y >> 16;
+    const uint32_t lo_i = Ei.y & 0xFFu, hi_i = (Ei.y >> 8) & 0xFFu, lo_j = Ej.y & 0xFFu, hi_j = (Ej.y >> 8) & 0xFFu;
     const bool self = je == ie;
-    const bool t0 = ok && lo_i < (self ? hi_i : hi_j);
-    const bool t1 = ok && !self && lo_j < hi_i;
-    const bool t2 = ok && !self && ((Ei.z & Ej.z) | (Ei.w & Ej.w)) != 0u;
-    const uint32_t key0 = (gt & (kGroupCounters - 1u)) + (self ? 0u : 1u + 3u * (Ej.x - Ei.x - 1u));
-    tri_keys(t0, t1, t2, key0, gt >> kGroupShift, st, en, cur, keys);
+    const uint64_t sm = eq_mask(je, ie);
+    const uint32_t hs = self ? hi_i : hi_j;
+    const uint64_t mm = Ei.z | (uint64_t(Ei.w) << 32), mj = Ej.z | (uint64_t(Ej.w) << 32);
+    const uint64_t M0 = okm & lt_mask(lo_i, hs);
+    const uint64_t M1 = okm & ~sm & lt_mask(lo_j, hi_i);
+    const uint64_t M2 = okm & ~sm & nz_mask(mm & mj);
+    const bool t0 = ok && lo_i < hs, t1 = ok && !self && lo_j < hi_i, t2 = ok && !self && (mm & mj) != 0ull;
+    const uint32_t key0 = (Ei.y >> 16) - kTriA + (Ej.x & 0xFFFFu) + (self ? 2u : 0u);
+    tri_keys(M0, M1, M2, t0, t1, t2, key0, Ei.x >> 16, st, en, cur, keys);
 }
 
 __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restrict__ row_off32,
@@ -891,9 +907,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
                                                       uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
                                                       unsigned long long* __restrict__ nkeys_total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint4* stage_all = reinterpret_cast<uint4*>(smem);            // kF2Waves x 64: rank, lo | hi << 16, mask
-    uint32_t* sgt_all = smem + kF2Waves * 64 * 4;                  // kF2Waves x 64: gtab of the active entries
-    uint32_t* srow = sgt_all + kF2Waves * 64;                      // row offsets of the block [rpb + 1]
+    uint4* stage_all = reinterpret_cast<uint4*>(smem);            // kF2Waves x 64 staged entries (tri_pair)
+    uint32_t* srow = smem + kF2Waves * 64 * 4;                     // row offsets of the block [rpb + 1]
     uint32_t* cur = srow + kF2RowWords;                            // region cursors [G]
     __shared__ uint32_t blk_keys;
     const uint32_t b = blockIdx.x;
@@ -904,7 +919,6 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
     __syncthreads();
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     uint4* stage = stage_all + wave * 64;
-    uint32_t* sgt = sgt_all + wave * 64;
     const uint64_t lt = lanemask_lt();
     // the next row's entries are loaded while the current row is enumerated
     uint32_t nrb = 0, nrl = 0, nme = 0;
@@ -929,16 +943,18 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
             // ones (this rank's member range) are a contiguous run [a0, a1) of them
             const bool fr = lane < rl && !(me & 1u);
             const bool act = fr && me - mlo < mhi - mlo;
-            const uint64_t fb = __ballot(fr), ab = __ballot(act);
+            const uint64_t fb = ballot(fr), ab = ballot(act);
             if (!ab) continue;
             const uint32_t n = uint32_t(__popcll(fb));
             const uint32_t a0 = uint32_t(__popcll(fb & ((1ull << __builtin_ctzll(ab)) - 1ull)));
             const uint32_t a1 = a0 + uint32_t(__popcll(ab));
             if (fr) {
-                const uint32_t p = uint32_t(__popcll(fb & lt));
-                const uint32_t lh = uint32_t(__builtin_ctzll(mk)) | ((63u - uint32_t(__builtin_clzll(mk))) << 16);
-                stage[p] = make_uint4(me >> 1, lh, uint32_t(mk), uint32_t(mk >> 32));
-                if (act) sgt[p] = gtab[me >> 1];
+                const uint32_t p = uint32_t(__popcll(fb & lt)), rk = me >> 1;
+                const uint32_t gt = act ? gtab[rk] : 0u;
+                const uint32_t A = (gt & (kGroupCounters - 1u)) - 3u * rk - 2u + kTriA;  // (active entries only)
+                const uint32_t lh = uint32_t(__builtin_ctzll(mk)) | ((63u - uint32_t(__builtin_clzll(mk))) << 8);
+                stage[p] = make_uint4(3u * rk | ((gt >> kGroupShift) << 16), lh | (A << 16), uint32_t(mk),
+                                      uint32_t(mk >> 32));
             }
             __builtin_amdgcn_wave_barrier();
             const uint32_t need = 2u * n + 1u - a0 - a1;  // partners of a folded pair of entries
@@ -952,16 +968,17 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
                     const uint32_t iA = a0 + fp, iB = a1 - 1u - fp, cA = min(n - iA, S);
                     const bool second = l >= cA;
                     const uint32_t ie = second ? iB : iA, je = ie + (second ? l - cA : l);
-                    const bool ok = fp < npairs && je < n && (!second || iB > iA);
+                    const uint64_t sec = ~lt_mask(l, cA);
+                    const uint64_t okm = lt_mask(fp, npairs) & lt_mask(je, n) & (~sec | lt_mask(iA, iB));
                     // the run of lanes of ie: [s0, s0 + cA) for iA, [s0 + cA, s0 + S) for iB
                     const uint32_t st = second ? s0 + cA : s0, en = second ? s0 + S - 1u : s0 + cA - 1u;
-                    tri_pair(ok, ie, je, st, en, stage, sgt, cur, keys);
+                    tri_pair(okm, ie, je, st, en, stage, cur, keys);
                 }
             } else {
                 for (uint32_t i = a0; i < a1; ++i)
                     for (uint32_t c0 = 0; i + c0 < n; c0 += 64) {
                         const uint32_t je = i + c0 + lane;
-                        tri_pair(je < n, i, je, 0u, 63u, stage, sgt, cur, keys);
+                        tri_pair(lt_mask(je, n), i, je, 0u, 63u, stage, cur, keys);
                     }
             }
             __builtin_amdgcn_wave_barrier();
@@ -990,7 +1007,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
                     const bool t1 = ok && !self && lo_j < hi_i;
                     const bool t2 = ok && !self && (mki & mkj) != 0ull;
                     const uint32_t key0 = (gt & (kGroupCounters - 1u)) + (self ? 0u : 1u + 3u * ((mj >> 1) - ri - 1u));
-                    tri_keys(t0, t1, t2, key0, gt >> kGroupShift, 0u, 63u, cur, keys);
+                    tri_keys(ballot(t0), ballot(t1), ballot(t2), t0, t1, t2, key0, gt >> kGroupShift, 0u, 63u, cur, keys);
                 }
             }
         }
@@ -1117,7 +1134,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
             const uint32_t c = c0 + lane;
             const uint32_t val = c < nz ? h[c] : 0u;
             const bool fr = c < nz && val >= minsup;
-            const uint64_t fb = __ballot(fr);
+            const uint64_t fb = ballot(fr);
             if (!fb) continue;
             uint32_t at = 0;
             if (lane == 0) at = atomicAdd(nrec, uint32_t(__popcll(fb)));
@@ -1147,7 +1164,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_count(const uint64_t* __restr
             const uint32_t c = cc + lane;
             const uint32_t val = c < D ? hr[c] : 0u;
             const bool fr = c < D && val >= minsup;
-            const uint64_t fb = __ballot(fr);
+            const uint64_t fb = ballot(fr);
             if (!fb) continue;
             uint32_t at = 0;
             if (lane == 0) at = atomicAdd(nrec, uint32_t(__popcll(fb)));
@@ -1198,7 +1215,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_count(const DRow* __restrict__ 
     for (uint32_t s = 0; s < c.D; s += 64) {
         const uint32_t slot = s + lane_id();
         const uint32_t v = slot < c.D ? base[slot] : 0u;
-        n += __popcll(__ballot(v >= minsup));
+        n += __popcll(ballot(v >= minsup));
     }
     if (lane_id() == 0) rowcnt[g] = n;
 }
@@ -1222,9 +1239,9 @@ __global__ __launch_bounds__(kBlock) void k_freq_write(const DRow* __restrict__ 
         const uint32_t v = slot < c.D ? base[slot] : 0u;
         const bool fr = slot < c.D && v >= minsup;
         const bool partner = __shfl_xor(int(fr), 1, 64) != 0;
-        const uint64_t lead = __ballot((fr || partner) && !(lane & 1u));
+        const uint64_t lead = ballot((fr || partner) && !(lane & 1u));
         const uint32_t crank = nrank + uint32_t(__popcll(lead & lead_lt));
-        const uint64_t fb = __ballot(fr);
+        const uint64_t fb = ballot(fr);
         if (fr) {
             const uint64_t q = o + __popcll(fb & lanemask_lt());
             out[q] = FreqRec{row_base + g, slot, v, crank << 1 | (slot & 1u)};
@@ -1284,7 +1301,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_recs(const DRow* __restrict__ r
         base = cnt + c.cnt_off + uint64_t(r.mi >> c.mshift) * c.rstride;
         for (uint32_t s0 = 0; s0 < c.D; s0 += 64) {
             const uint32_t slot = s0 + lane;
-            n += uint32_t(__popcll(__ballot(slot < c.D && base[slot] >= minsup)));
+            n += uint32_t(__popcll(ballot(slot < c.D && base[slot] >= minsup)));
         }
     }
     if (lane == 0) w_n[wv] = n;
@@ -1302,7 +1319,7 @@ __global__ __launch_bounds__(kBlock) void k_freq_recs(const DRow* __restrict__ r
         const uint32_t slot = s0 + lane;
         const uint32_t v = slot < c.D ? base[slot] : 0u;
         const bool fr = slot < c.D && v >= minsup;
-        const uint64_t fb = __ballot(fr);
+        const uint64_t fb = ballot(fr);
         const uint32_t x = at + uint32_t(__popcll(fb & lanemask_lt()));
         if (fr && x < cap) out[x] = FreqRec{row_base + g, slot, v, 0u};
         at += uint32_t(__popcll(fb));
@@ -1403,7 +1420,7 @@ __device__ __forceinline__ uint32_t emit_pairs(const EmitEnt& t, uint64_t w0, co
                 }
             }
         }
-        const uint64_t succ = __ballot(ok);
+        const uint64_t succ = ballot(ok);
         const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
         const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
         on_ok(ok, ow, o_e, o_lt, q, f, slot, k);
@@ -1534,7 +1551,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, RootRef rr, co
             const uint32_t done = emit_pairs<W>(
                 t, w0, en, mask, kid_slot, wd,
                 [&](bool ok, uint32_t ow, uint64_t, uint32_t, uint32_t q, uint32_t f, uint32_t, uint32_t k) {
-                    const uint64_t b = __ballot(ok);
+                    const uint64_t b = ballot(ok);
                     if (ok) {
                         const uint32_t x = nrec + uint32_t(__popcll(b & lanemask_lt()));
                         if (x < rcap) {
@@ -1648,7 +1665,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
         uint32_t ef = wz;
         for (uint32_t b0 = wa; b0 < wz; b0 += 64) {
             const uint32_t e = b0 + lane;
-            const uint64_t st = __ballot(e < wz && (pos[e] >> 16) == 0u);
+            const uint64_t st = ballot(e < wz && (pos[e] >> 16) == 0u);
             if (st) {
                 ef = b0 + uint32_t(__ffsll((unsigned long long)st)) - 1u;
                 break;
@@ -1665,8 +1682,8 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                 const uint32_t len = p & 0xFFFFu;
                 const bool st = e < E && (p >> 16) == 0u;
                 // a run starting at lane s is in this window iff it starts in [e0, wz) and fits
-                const uint64_t bad = __ballot(st && (e >= wz || lane + len > 64u));
-                const uint64_t sts = __ballot(st);
+                const uint64_t bad = ballot(st && (e >= wz || lane + len > 64u));
+                const uint64_t sts = ballot(st);
                 uint32_t cut;
                 if (bad & 1ull) {  // lane 0 starts a run of more than 64 entries: k_emit1's list
                     if (keep && lane == 0) longl[atomicAdd(nlong, 1u)] = e0;
@@ -1765,7 +1782,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                             }
                         }
                     }
-                    const uint64_t succ = __ballot(ok);
+                    const uint64_t succ = ballot(ok);
                     const uint32_t first = (o_ex > p0 ? o_ex : p0) - p0;  // owner's first lane in this step
                     const uint32_t k = o_done + uint32_t(__popcll(succ & lane_range(first, lane)));
                     on_ok(ok, e0 + f, q, e0 + ow - ef, k);
@@ -1781,7 +1798,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
             }
         };
         walk([&](bool ok, uint32_t f, uint32_t q, uint32_t os, uint32_t k) {
-                 const uint64_t b = __ballot(ok);
+                 const uint64_t b = ballot(ok);
                  if (ok) {
                      const uint32_t x = nrec + uint32_t(__popcll(b & lt));
                      if (x < rcap) {
@@ -1860,7 +1877,7 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
         uint32_t e0 = wz;  // the first run start in [wa, wz)
         for (uint32_t b0 = wa; b0 < wz; b0 += 64) {
             const uint32_t e = b0 + lane;
-            const uint64_t st = __ballot(e < wz && (pos[e] >> 16) == 0u);
+            const uint64_t st = ballot(e < wz && (pos[e] >> 16) == 0u);
             if (st) {
                 e0 = b0 + uint32_t(__ffsll((unsigned long long)st)) - 1u;
                 break;
@@ -1871,8 +1888,8 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
             const uint32_t p = e < E ? pos[e] : 0u;
             const uint32_t len = p & 0xFFFFu;
             const bool st = e < E && (p >> 16) == 0u;
-            const uint64_t bad = __ballot(st && (e >= wz || lane + len > 64u));
-            const uint64_t sts = __ballot(st);
+            const uint64_t bad = ballot(st && (e >= wz || lane + len > 64u));
+            const uint64_t sts = ballot(st);
             if (bad & 1ull) {  // lane 0 starts a run of more than 64 entries: thread per entry
                 const uint32_t rl = uint32_t(__shfl(int(len), 0, 64));
                 for (uint32_t i0 = e0; i0 < e0 + rl; i0 += 64) {
@@ -2814,7 +2831,7 @@ struct Miner {
         FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
         const uint32_t* gtab = b.f2_tri_tab.as<uint32_t>();
         const uint32_t* gr = gtab + F;
-        const size_t kshm = size_t(kF2Waves) * 64 * 20 + size_t(kF2RowWords) * 4 + size_t(G) * 4;
+        const size_t kshm = size_t(kF2Waves) * 64 * 16 + size_t(kF2RowWords) * 4 + size_t(G) * 4;
         const size_t tk_keys = clk->begin("k_f2_keys");
         hipLaunchKernelGGL(k_f2_tri, dim3(nblk), dim3(kF2Threads), kshm, s, db->row_off.as<uint32_t>(),
                            b.mem_db.as<uint32_t>(), db->mask.as<uint64_t>(), R, rpb, gtab, G, nblk, geo.mlo, geo.mhi,

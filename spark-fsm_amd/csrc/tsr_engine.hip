@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_keep(const uint32_t* __restrict
             const uint32_t c = e < re ? item[e] : 0u;
             const uint32_t sp = e < re ? isup[c] : 0u;
             const bool keep = e < re && sp >= t;
-            const uint64_t b = __ballot(keep);
+            const uint64_t b = ballot(keep);
             if (off && keep) {
                 const uint64_t d = o + uint32_t(__popcll(b & lanemask_lt()));
                 o_item[d] = c;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_pairs_compact(uint32_t* __restrict__
         uint32_t ij = 0, ji = 0;
         if (j < U) { ij = row[2 * j]; ji = row[2 * j + 1]; }
         const bool keep = j < U && (ij >= t || ji >= t);
-        const uint64_t b = __ballot(keep);
+        const uint64_t b = ballot(keep);
         if (out) {
             if (keep) out[o + __popcll(b & lanemask_lt())] = PairRec{i, j, ij, ji};
             if (zero && j < U && (ij | ji)) { row[2 * j] = 0; row[2 * j + 1] = 0; }
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(const Side* __restrict__ side
         if (q >= re || item[q] != side.X[k]) ok = false;
         else fX = max(fX, first[q]);
     }
-    if (__ballot(!ok)) return;  // s not in sids(X)
+    if (ballot(!ok)) return;  // s not in sids(X)
     fX = wave_max(fX);
     if (lane == 0) atomicAdd(&ctl->nx, 1u);
     if (side.doL) {  // |sids(X u {c})| for candidate left extensions
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(const Side* __restrict__ side
         if (q >= re || item[q] != side.Y[k]) ok = false;
         else lY = min(lY, last[q]);
     }
-    if (__ballot(!ok)) return;  // s not in sids(Y)
+    if (ballot(!ok)) return;  // s not in sids(Y)
     lY = wave_min(lY);
     if (fX >= lY) return;  // X => Y does not hold in s
     if (side.doL) {        // expandL: c > max(X), c not in Y, c before lastY(s)
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_pack(const uint32_t* __restrict
             const uint32_t e = e0 + lane_id();
             const uint32_t k = e < re ? kid_of[item[e]] : kNone;
             const bool keep = k != kNone;
-            const uint64_t b = __ballot(keep);
+            const uint64_t b = ballot(keep);
             if (keep) {
                 const uint32_t la = last[e];
                 mp = max(mp, la);
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(kDomThreads) void k_exp_domain(const Side* __restri
                     if (it != drv) keep = (bm[uint64_t(it) * NW + (sid >> 5)] >> (sid & 31u)) & 1u;
                 }
             }
-            const uint64_t bal = __ballot(keep);
+            const uint64_t bal = ballot(keep);
             if (lane == 0) wsum[wv] = uint32_t(__popcll(bal));
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -1015,9 +1015,9 @@ __global__ __launch_bounds__(kXBlock) void k_exp_rows(const Side* __restrict__ s
                         const uint32_t pp = rl.x - q0;  // row jl starts pp entries into the step (>= 1)
                         ++tag;
                         if (jl < j1 && pp - 1u < 63u) wflag[wv][pp] = tag;  // a start inside the step
-                        const uint64_t nxt = __ballot(jl < j1 && pp - 1u < 64u);  // starts in (q0, q0 + 64]
+                        const uint64_t nxt = ballot(jl < j1 && pp - 1u < 64u);  // starts in (q0, q0 + 64]
                         __builtin_amdgcn_wave_barrier();
-                        const uint64_t m = __ballot(wflag[wv][lane] == tag);
+                        const uint64_t m = ballot(wflag[wv][lane] == tag);
                         // row of lane l = ja + starts at offsets 1..l (lane r - 1 holds row ja + r)
                         const uint32_t r = uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))) +
@@ -1102,7 +1102,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_reduce(const uint32_t* __rest
             }
             keep = tl >= geo.t || tr >= geo.t;
         }
-        const uint64_t bal = __ballot(keep);
+        const uint64_t bal = ballot(keep);
         if (lane == 0) wsum[wv] = uint32_t(__popcll(bal));
         __syncthreads();
         uint32_t at = n, tot = 0;

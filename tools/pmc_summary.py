@@ -34,6 +34,8 @@ def kernel_name(demangled):
         return "k_count"
     if base == "k_f2_plan_db":  # the DB-direct root's F2 plan: timed as "k_f2_plan"
         return "k_f2_plan"
+    if base == "k_f2_tri":  # the unordered-pair F2 key enumeration: timed as "k_f2_keys"
+        return "k_f2_keys"
     return base
 
 
