@@ -1229,7 +1229,8 @@ struct Rule {
     uint32_t ln = 0, pn = 0, pc = 0;
     uint64_t loff = kNoList;   // its kept domain rows in the arena (ln of them), after its expansion
     uint64_t ploff = kNoList;  // its parent's (pn of them): its own domain is a subset of those rows
-    uint32_t xid = 0;          // its item set X, interned (XIntern)
+    uint32_t xid = 0;          // its item set X, interned (XIntern); kNone until first needed
+    uint32_t pxid = 0;         // a left extension's parent X (X = X(parent) + its last item)
 };
 
 // The item sets X of the rules, interned: the |sids(X u {c})| memo's exact keys (DlMemo).  A
@@ -1503,7 +1504,10 @@ struct Replay {
         const uint32_t* x = st.X(&r);
         r.k1 = uint64_t(sup) << 32 | uint64_t(mx) << 16 | uint64_t(my);
         r.k2 = uint64_t(x[0]) << 32 | (mx > 1 ? x[1] : x[mx]);
-        r.xid = !src ? ax : (ax != kNone ? xin.get(src->xid, ax) : src->xid);
+        // a left extension's X is interned when the rule is first launched (most derived rules
+        // never are); a right extension shares its parent's X
+        r.xid = !src ? ax : (ax != kNone ? kNone : src->xid);
+        r.pxid = src ? src->xid : 0u;
         if (src && src->loff != kNoList) {  // the parent's kept rows: the child's domain probes only pc there
             r.ploff = src->loff;
             r.pn = src->ln;
@@ -2280,7 +2284,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         x.batch = batch;
         x.depth = depth;
         x.seq = seq_next++;
-        for (Rule* r : batch) r->inset = int8_t(xp - xs);
+        for (Rule* r : batch) {
+            r->inset = int8_t(xp - xs);
+            // every rule of the batch (not only this rank's slots): its children's X ids derive from it
+            if (r->xid == kNone) r->xid = rp.xin.get(r->pxid, rp.st.X(r)[r->nx - 1]);
+        }
         // slot sharding: this rank expands only its contiguous share of the batch, split so
         // that the shares' expected domains (about twice each rule's support) are equal
         x.la = 0;
@@ -2659,10 +2667,11 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         if (r->res >= 0) {  // results at hand: commit now
             if (from_p) pending.pop();
             else rp.cand.pop();
-            const double tc0 = now_ms();
+            // (the host-time split is taken only when verbose: a clock read costs as much as a commit)
+            const double tc0 = ctx->opts.verbose ? now_ms() : 0.0;
             commit(r, res_pool[size_t(r->res)]);
             if (r->res >= 0) res_release(r);
-            commit_ms += now_ms() - tc0;
+            if (ctx->opts.verbose) commit_ms += now_ms() - tc0;
             if (res_live > sweep_at) {  // results of rules now below minsup can never be committed
                 for (ExpResult& e : res_pool)
                     if (e.owner && e.owner->sup < rp.minsup) res_release(e.owner);
