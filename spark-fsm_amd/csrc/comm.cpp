@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -431,6 +432,7 @@ class InProcHub {
   public:
     explicit InProcHub(int n) : n_(n), post_(size_t(n), nullptr) {
         for (auto& c : ctr_) c.store(0);
+        for (auto& b : in_bar_) b.store(-1);
     }
     int n() const { return n_; }
     // every rank's pointer of the current exchange (valid between the two barriers)
@@ -438,10 +440,17 @@ class InProcHub {
     const void* posted(int rank) const { return post_[size_t(rank)]; }
     // Generation barrier: a short spin (the ranks usually arrive within microseconds of
     // each other), then a condition-variable wait.  Throws FSM_ECOMM once aborted.
-    void barrier() {
+    // the generation a rank waits in (-1: not in a barrier), for the group's hang report
+    struct InBar {
+        std::atomic<int64_t>& a;
+        InBar(std::atomic<int64_t>& x, int64_t v) : a(x) { a.store(v); }
+        ~InBar() { a.store(-1); }
+    };
+    void barrier(int rank) {
         std::unique_lock<std::mutex> g(mu_);
         if (broken_) throw broken_error();
         const uint64_t my = gen_;
+        InBar ib(in_bar_[size_t(rank) % in_bar_.size()], int64_t(my));
         if (++arrived_ == n_) {
             arrived_ = 0;
             gen_ = my + 1;
@@ -479,6 +488,12 @@ class InProcHub {
         arrived_ = 0;
     }
     std::atomic<int64_t>& counter(int64_t key) { return ctr_[size_t(key) % kSlots]; }
+    std::string state() {
+        std::string s = "hub: " + std::to_string(n_) + " ranks, barrier generation " + std::to_string(gen_) + ", " +
+                        std::to_string(arrived_) + " arrived, broken " + std::to_string(int(broken_)) + "; in barrier:";
+        for (int r = 0; r < n_; ++r) s += " " + std::to_string(in_bar_[size_t(r) % in_bar_.size()].load());
+        return s;
+    }
 
   private:
     static Error broken_error() {
@@ -495,6 +510,7 @@ class InProcHub {
     std::atomic<uint64_t> agen_{0};
     std::atomic<bool> abroken_{false};
     std::atomic<int64_t> ctr_[kSlots];
+    std::array<std::atomic<int64_t>, 64> in_bar_;
 };
 
 namespace {
@@ -511,20 +527,20 @@ class InProcComm final : public Comm {
     void host_allreduce_u32(uint32_t* h, size_t n, hipStream_t) override {
         std::vector<uint32_t> sum(n, 0u);
         hub_->post(rank(), h);
-        hub_->barrier();
+        hub_->barrier(rank());
         for (int r = 0; r < nranks(); ++r) {
             const auto* v = static_cast<const uint32_t*>(hub_->posted(r));
             for (size_t i = 0; i < n; ++i) sum[i] += v[i];
         }
-        hub_->barrier();  // every rank has read every buffer before any is overwritten
+        hub_->barrier(rank());  // every rank has read every buffer before any is overwritten
         if (n) std::memcpy(h, sum.data(), n * 4);
     }
     void host_allgather(const void* send, void* recv, size_t bytes, hipStream_t) override {
         hub_->post(rank(), send);
-        hub_->barrier();
+        hub_->barrier(rank());
         for (int r = 0; r < nranks(); ++r)
             if (bytes) std::memcpy(static_cast<uint8_t*>(recv) + size_t(r) * bytes, hub_->posted(r), bytes);
-        hub_->barrier();
+        hub_->barrier(rank());
     }
     void allreduce_u32(uint32_t* dev, size_t n, hipStream_t s) override {
         std::vector<uint32_t> h(n);
@@ -549,7 +565,7 @@ class InProcComm final : public Comm {
                                     bool root_only) override {
         std::vector<uint8_t> out;
         hub_->post(rank(), mine.data());
-        hub_->barrier();
+        hub_->barrier(rank());
         if (!root_only || rank() == 0) {
             size_t tot = 0;
             for (size_t v : sizes) tot += v;
@@ -560,7 +576,7 @@ class InProcComm final : public Comm {
                 at += sizes[size_t(r)];
             }
         }
-        hub_->barrier();
+        hub_->barrier(rank());
         return out;
     }
 
@@ -575,6 +591,7 @@ std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<InProcHub>& hub, in
     return std::make_unique<InProcComm>(hub, rank);
 }
 void inproc_abort(InProcHub& hub) { hub.abort(); }
+std::string inproc_state(InProcHub& hub) { return hub.state(); }
 bool inproc_aborted(InProcHub& hub) { return hub.aborted(); }
 void inproc_reset(InProcHub& hub) { hub.reset(); }
 

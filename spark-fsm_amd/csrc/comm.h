@@ -113,6 +113,7 @@ std::shared_ptr<InProcHub> make_inproc_hub(int nranks);
 std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<InProcHub>& hub, int rank);
 void inproc_abort(InProcHub& hub);
 bool inproc_aborted(InProcHub& hub);
+std::string inproc_state(InProcHub& hub);  // (diagnostics: the group's hang report)
 void inproc_reset(InProcHub& hub);
 
 // Longest-processing-time assignment of `n` work units with estimated volumes

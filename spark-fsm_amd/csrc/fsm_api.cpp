@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -175,9 +176,17 @@ struct Group {
         one(fn, 0);
         {
             std::unique_lock<std::mutex> g(mu_);
-            done_.wait(g, [&] { return left_ == 0; });
+            // a call still waiting for its ranks after 60 s reports where they are (stderr, once)
+            if (!done_.wait_for(g, std::chrono::seconds(60), [&] { return left_ == 0; })) {
+                std::string st;
+                for (int r = 0; r < n(); ++r) st += " " + std::to_string(done_r_[size_t(r)]);
+                std::fprintf(stderr, "[fsm] rank group: %d of %d ranks still running after 60 s (done:%s); %s\n",
+                             left_, n(), st.c_str(), inproc_state(*hub).c_str());
+                done_.wait(g, [&] { return left_ == 0; });
+            }
             job_ = nullptr;
         }
+        std::fill(done_r_.begin(), done_r_.end(), 0);
         inproc_reset(*hub);
         // the failing rank to report: one whose own message is not a peer's failure, preferably
         // one that failed before the hub was aborted
@@ -204,6 +213,7 @@ struct Group {
             c = FSM_EDEVICE;
         }
         rc[size_t(r)] = c;
+        done_r_[size_t(r)] = 1;
         // a rank that fails once the hub is already aborted failed because a peer did
         after_abort_[size_t(r)] = c != FSM_OK && inproc_aborted(*hub);
         if (c != FSM_OK) inproc_abort(*hub);
@@ -232,6 +242,7 @@ struct Group {
     int left_ = 0;
     bool stop_ = false;
     std::vector<char> after_abort_ = std::vector<char>(size_t(FSM_MAX_DEVICES), 0);
+    std::vector<int> done_r_ = std::vector<int>(size_t(FSM_MAX_DEVICES), 0);
 };
 
 }  // namespace fsm

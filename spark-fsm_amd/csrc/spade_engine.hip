@@ -3214,8 +3214,10 @@ struct Miner {
             recs.resize(nfreq);
             if (nfreq) std::memcpy(recs.data(), all.data(), all.size());
             // the unordered-pair F2 gives a rank records of rows above its slice: (row, slot)
-            // order and the child ids over the whole set
-            if (b.f2_tri) order_recs(recs, uint32_t(rows.size()));
+            // order and the child ids over the whole set.  Every rank orders them, whatever its
+            // own F2 layout (a rank with an empty slice runs the ordered one): the ranks must
+            // derive identical children, or their collective sequences part
+            order_recs(recs, uint32_t(rows.size()));
             R = recs.data();
         }
         double th = now_ms();
