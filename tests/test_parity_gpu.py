@@ -360,7 +360,33 @@ def test_spade_quest_d1m_properties(eng):
     assert st["joins"] > 4.0e7
 
 
-@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic", "passes-3", "passes-64", "slab-root"])
+_CASES = {}
+
+
+def shape_case(shape):
+    """(dataset, support, oracle result) of a path-agreement shape, computed once per test session:
+    the path variants of one shape share the dataset and the oracle's answer."""
+    if shape not in _CASES:
+        from oracle import oracle
+        from tools import gen
+        if shape == "quest":
+            ds, sup = gen.quest(20000, seed=9), 0.003
+        elif shape == "quest4":
+            ds, sup = gen.quest(20000, seed=4), 0.003
+        elif shape == "sign":
+            ds, sup = gen.sign(seed=2).head(400), 0.3
+        elif shape == "bible":
+            ds, sup = gen.bible(seed=2).head(1500), 0.03
+        elif shape == "wide":  # runs of more than 64 entries at W = 1
+            ds, sup = _wide_runs_db(), 0.05
+        else:  # sign-low: first-level classes whose counter matrix spans several groups
+            ds, sup = gen.sign(seed=3).head(60), 0.08
+        _CASES[shape] = (ds, sup, oracle.spade_tokens(ds.seq_off, ds.tokens, sup))
+    return _CASES[shape]
+
+
+@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic", "passes-3", "passes-64", "slab-root",
+                                  "ordered"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
     """The root F2 implementations (key runs counted per rank group, at the
     default and at a small block chunk, in several passes over group ranges;
@@ -376,9 +402,10 @@ def test_root_f2_paths_agree(eng, path, monkeypatch):
         monkeypatch.setenv("FSM_F2_BLOCKS", "3")
     if path.startswith("passes"):
         monkeypatch.setenv("FSM_F2_PASSES", path.split("-")[1])
-    ds = gen.quest(20000, seed=4)
-    o = oracle.spade_tokens(ds.seq_off, ds.tokens, 0.003)
-    pats, meta, st = gpu_spade(eng, None, 0.003, tokens=ds)
+    if path == "ordered":  # the ordered-pair enumeration (k_f2_keys) instead of the unordered one (k_f2_tri)
+        monkeypatch.setenv("FSM_F2_TRI", "0")
+    ds, sup, o = shape_case("quest4")
+    pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
 
 
@@ -424,15 +451,7 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
         monkeypatch.setenv("FSM_CHILD_OF", "device")
     elif path == "host-kids":  # the kid table from the host records (default: k_freq_write + k_kid_off)
         monkeypatch.setenv("FSM_KIDS", "host")
-    if shape == "quest":
-        ds, sup = gen.quest(20000, seed=9), 0.003
-    elif shape == "sign":
-        ds, sup = gen.sign(seed=2).head(400), 0.3
-    elif shape == "wide":
-        ds, sup = _wide_runs_db(), 0.05
-    else:
-        ds, sup = gen.bible(seed=2).head(1500), 0.03
-    o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
+    ds, sup, o = shape_case(shape)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
 
@@ -467,17 +486,7 @@ def test_count_paths_agree(eng, path, shape, monkeypatch):
         monkeypatch.setenv("FSM_ROOT_PATH", "atomic")
     elif path != "default":
         monkeypatch.setenv("FSM_COUNT_PATH", path)
-    if shape == "quest":
-        ds, sup = gen.quest(20000, seed=9), 0.003
-    elif shape == "sign":
-        ds, sup = gen.sign(seed=2).head(400), 0.3
-    elif shape == "bible":
-        ds, sup = gen.bible(seed=2).head(1500), 0.03
-    elif shape == "wide":  # runs of more than 64 entries at W = 1
-        ds, sup = _wide_runs_db(), 0.05
-    else:  # low support: first-level classes whose counter matrix spans several groups
-        ds, sup = gen.sign(seed=3).head(60), 0.08
-    o = oracle.spade_tokens(ds.seq_off, ds.tokens, sup)
+    ds, sup, o = shape_case(shape)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
     if path in ("keys", "sparse"):
