@@ -2644,6 +2644,21 @@ struct Miner {
         }();
         return a;
     }
+    // records from which the kid table and the children of a batch are built on the host
+    // thread pool (below: one thread); FSM_HOST_PAR_MIN overrides (tuning)
+    static uint64_t par_min() {
+        static const uint64_t v = [] {
+            const char* e = std::getenv("FSM_HOST_PAR_MIN");
+            return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : uint64_t(1) << 16;
+        }();
+        return v;
+    }
+    // whether the DB-direct root's F2 takes the unordered-pair layout (run_root_db decides it the
+    // same way, unless the rank's own slice is empty)
+    bool tri_expected(uint32_t F) const {
+        return W == 1 && f2_tri_env() && f2_passes() == 1 && F > 0 && tri_len(F, 0) <= kGroupCounters &&
+               root_db_env() && !root_atomic();
+    }
     // the root F2 in the unordered-pair layout (k_f2_tri; FSM_F2_TRI=0: the ordered layout)
     static bool f2_tri_env() {
         const char* v = std::getenv("FSM_F2_TRI");
@@ -3240,7 +3255,7 @@ struct Miner {
         // records are in (row, slot) order, and a row's member slot cbase + mi ascends
         // with the row: koff[x] = records of slots < x, by a merge (threads split x)
         auto slot_of = [&](uint64_t q) { return uint64_t(b.cls[rows[R[q].row].cls].cbase) + rows[R[q].row].mi; };
-        const int64_t nthk = nfreq >= (uint64_t(1) << 16) ? host_threads() : 1;
+        const int64_t nthk = nfreq >= par_min() ? host_threads() : 1;
         par_slices(nthk, int64_t(nko), [&](int64_t, int64_t x0, int64_t x1) {
             uint64_t lo = 0, hi = nfreq;  // first record with slot >= x0
             while (lo < hi) {
@@ -3275,7 +3290,7 @@ struct Miner {
         b.children.reserve(nfreq);
         b.child_rank_item.reserve(nfreq + 16);
         b.child_node_of.reserve(2 * nfreq + 16);
-        if (!comm && nfreq >= (uint64_t(1) << 16)) {
+        if (!comm && nfreq >= par_min()) {
             children_parallel(b, R, nfreq, rows);
         } else
         for (size_t q = 0; q < nfreq;) {
@@ -3345,7 +3360,13 @@ struct Miner {
                 b.children[k].split = heavy[k] != 0;
                 nheavy += heavy[k];
             }
-            if (comm->claim_mode == 1) {
+            // Claims pay where a static plan balances badly: few first-level classes per rank
+            // (deep, skewed lattices: BIBLE / SIGN shapes).  With many small classes (Quest D1M:
+            // about 5,000) the largest-first plan is within a few percent, and every claim costs
+            // an emit pass over all the DB rows (0.3 ms at D1M), so the static plan runs (one
+            // pass per rank).  FSM_SPADE_CLAIMS=1 forces claims, =0 the static plan.
+            const bool claims_pay = claims_forced() || nc < kClaimClassesPerRank * uint64_t(comm->nranks());
+            if (comm->claim_mode == 1 && claims_pay) {
                 // work stealing: heavy classes first (every rank), then the rest largest first;
                 // the groups after the shared ones are claimed from the shared counter
                 std::vector<size_t> ord(idx);
@@ -3371,7 +3392,7 @@ struct Miner {
             }
             if (ctx->opts.verbose)
                 std::fprintf(stderr, "[fsm] rank %d: %zu first-level classes, %zu %s, %zu heavy (split)\n",
-                             comm->rank(), nc, b.children.size(), comm->claim_mode == 1 ? "claimable" : "kept", nheavy);
+                             comm->rank(), nc, b.children.size(), b.claim_key >= 0 ? "claimable" : "kept", nheavy);
         } else if (comm) {
             // sub-classes of a split class: LPT over that class's sub-classes alone
             // (the same on every rank whatever the batching), this rank keeps its share
@@ -3482,6 +3503,12 @@ struct Miner {
         const char* v = std::getenv("FSM_SPADE_CLAIMS");
         return !(v && v[0] == '0');
     }
+    static bool claims_forced() {
+        const char* v = std::getenv("FSM_SPADE_CLAIMS");
+        return v && v[0] == '1';
+    }
+    // below this many first-level classes per rank the sharded lattice claims its classes
+    static constexpr uint64_t kClaimClassesPerRank = 64;
     // a rank's first claim takes this fraction of its fair share of the claimable volume
     // (FSM_CLAIM_FIRST); later claims half of the remaining volume's fair share, at least
     // 1/8 of the fair share (guided self-scheduling: few claims, each an emit pass over the DB)
@@ -4107,15 +4134,28 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             if (f1[size_t(i)] >= mn.minsup) freq.push_back(uint32_t(i));
 
     if (comm && !freq.empty()) {
-        // root counter rows: contiguous rank slices of about equal entry counts
-        uint64_t tot = 0, acc = 0;
-        for (uint32_t it : freq) tot += f1[it];
+        // root counter rows: contiguous rank slices of about equal F2 work.  The ordered
+        // enumeration tests every entry against its whole row (work ~ the entry count); the
+        // unordered one (k_f2_tri) only against the partners above it, so an entry of rank k
+        // weighs sup(k) x (the root entries of ranks >= k): rows are sorted by rank
+        const bool tri = mn.tri_expected(uint32_t(freq.size()));
+        uint64_t tot_e = 0;
+        for (uint32_t it : freq) tot_e += f1[it];
+        std::vector<uint64_t> w(freq.size());
+        uint64_t tot = 0, above = tot_e;
+        for (size_t k = 0; k < freq.size(); ++k) {
+            const uint64_t e = f1[freq[k]];
+            w[k] = tri ? e * ((above + (e + 1) / 2) >> 4) + 1 : e;  // (>> 4: the sum stays in 64 bits)
+            above -= e;
+            tot += w[k];
+        }
         const uint64_t N = uint64_t(comm->nranks()), r = uint64_t(comm->rank());
+        uint64_t acc = 0;
         mn.slice_lo = mn.slice_hi = uint32_t(freq.size());
         for (size_t k = 0; k < freq.size(); ++k) {
             if (mn.slice_lo == freq.size() && acc * N >= tot * r) mn.slice_lo = uint32_t(k);
             if (acc * N >= tot * (r + 1)) { mn.slice_hi = uint32_t(k); break; }
-            acc += f1[freq[k]];
+            acc += w[k];
         }
         if (mn.slice_hi < mn.slice_lo) mn.slice_hi = mn.slice_lo;
     }

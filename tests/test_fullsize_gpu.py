@@ -137,14 +137,18 @@ def test_tsr_c4_prefix_sharded(world, tmp_path):
     assert all(0 < r["units"] < tot for r in res)  # every rank expanded a share of the slots
 
 
+@pytest.mark.parametrize("claims", ["auto", "forced"])
 @pytest.mark.parametrize("name,world", [("c3", 2), ("c5-bible", 3)])
-def test_spade_fullsize_sharded(name, world, tmp_path):
+def test_spade_fullsize_sharded(name, world, claims, tmp_path, monkeypatch):
     """The sharded path (F1 all-reduce, DB-direct root with the counter rows by rank
-    slice, frequent pairs all-gathered, first-level classes claimed from the shared
-    work-stealing counter, patterns all-gathered) at full BASELINE size, `world`
-    ranks on this GPU over gloo host collectives: every rank returns the complete
-    pattern set, and no rank joins root entries of classes it did not claim."""
+    slice, frequent pairs all-gathered, first-level classes by the static largest-first
+    plan or, forced here, claimed from the shared work-stealing counter, patterns
+    all-gathered) at full BASELINE size, `world` ranks on this GPU over gloo host
+    collectives: every rank returns the complete pattern set, and no rank joins root
+    entries of classes it did not own."""
     from test_dist import run_ranks
+    if claims == "forced":
+        monkeypatch.setenv("FSM_SPADE_CLAIMS", "1")
     exp = FULL[name]
     shape, D = SPADE_CFG[name]
     res = run_ranks(world, ["spade_digest", shape, str(D or 0), str(exp["support"])], tmp_path, timeout=110)
@@ -154,7 +158,8 @@ def test_spade_fullsize_sharded(name, world, tmp_path):
     # the ranks' owned root entries partition the root (F2 slices + claimed classes: each
     # root entry joined as the owner at most twice, once per phase, by exactly one rank)
     assert sum(r["rank_root_owned"] for r in res) <= 2 * res[0]["root_entries"]
-    assert sum(r["rank_claims"] for r in res) >= 1
+    if claims == "forced":
+        assert sum(r["rank_claims"] for r in res) >= 1
 
 
 def test_bench_two_ranks_dry_run(tmp_path):
@@ -188,10 +193,12 @@ def test_bench_two_ranks_dry_run(tmp_path):
 # SPADE.scala:132-133 / TSR.scala:102-103): ONE context whose calls run rank r on
 # devices[r] as threads of this process.  On the one-GPU box every rank is device 0.
 
-@pytest.mark.parametrize("name,devices", [("c3", (0, 0)), ("c3", (0, 0, 0)), ("c5-bible", (0, 0)),
-                                          ("c5-bible", (0, 0, 0))])
-def test_spade_fullsize_inproc(name, devices):
+@pytest.mark.parametrize("name,devices,claims", [("c3", (0, 0), "auto"), ("c3", (0, 0, 0), "forced"),
+                                                 ("c5-bible", (0, 0), "forced"), ("c5-bible", (0, 0, 0), "auto")])
+def test_spade_fullsize_inproc(name, devices, claims, monkeypatch):
     import spark_fsm_amd as fsm
+    if claims == "forced":
+        monkeypatch.setenv("FSM_SPADE_CLAIMS", "1")
     exp = FULL[name]
     ds = dataset(*SPADE_CFG[name])
     with fsm.Engine(devices=list(devices)) as e:
@@ -203,7 +210,9 @@ def test_spade_fullsize_inproc(name, devices):
                 assert meta["minsup"] == exp["minsup"]
                 assert st["joins"] == exp["joins"]
                 assert pattern_digest(*csr) == exp["digest"]
-                assert st["rank_root_slab"] == 0 and st["rank_claims"] >= 1
+                assert st["rank_root_slab"] == 0
+                if claims == "forced":
+                    assert st["rank_claims"] >= 1
                 # rank 0 owned only part of the root (the rest went to its peers)
                 assert 0 < st["rank_root_owned"] < 2 * st["root_entries"]
         finally:
