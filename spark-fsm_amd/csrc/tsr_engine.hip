@@ -1952,7 +1952,17 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // arena; a child rule's domain is then its parent's list with only the added item probed
     // (a child holds only where its parent does).  Rules whose parent list did not fit the arena
     // probe the whole bitmap AND.  FSM_TSR_PLIST=0 turns the lists off.
-    const bool plist = use_bm && !shard_exp && [] {
+    // A launch is sharded only when its expected domain (sum of 2 sup + 1 over its rules) reaches
+    // FSM_TSR_SHARD_MIN (default 256K sids: about 60 us of kernels at c4, the break-even of a
+    // per-launch gather); smaller launches run replicated on every rank (no gather), so the many
+    // small speculation launches of a c4-sized mine cost no exchange
+    const uint64_t shard_min = [] {
+        const char* v = std::getenv("FSM_TSR_SHARD_MIN");
+        return v ? std::strtoull(v, nullptr, 10) : uint64_t(1) << 18;
+    }();
+    // (the lists are rank-local: a rank keeps the lists of the slots it expanded, a child of
+    // another rank's slot probes the bitmaps; the counts are the same either way)
+    const bool plist = use_bm && [] {
         const char* v = std::getenv("FSM_TSR_PLIST");
         return !(v && v[0] == '0');
     }();
@@ -2003,6 +2013,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         std::vector<char> drv_in_x;
         std::vector<uint64_t> kmono;  // bitmap path: each slot's kept-row list (ring position; kNoList: none)
         uint64_t amin = kNoList;      // the oldest ring position the launch reads or writes (kNoList: none)
+        bool sharded = false;         // this launch's slots split over the ranks (results gathered)
         uint32_t la = 0, lz = 0;  // slot sharding: this rank's slots [la, lz) of the batch (else all)
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
         // the set's own stream: the two sets' launches are independent, so the GPU runs
@@ -2217,7 +2228,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 std::sort(res.recs.begin(), res.recs.end(), [](const ExpRec& a, const ExpRec& c) { return a.c < c.c; });
             }
         }
-        if (shard_exp) {
+        if (x.sharded) {
             // every rank's slots: (nsid, nent, nrec, records) per slot of its share, gathered
             // once per launch (the failure agreement rides along); the replay then goes on
             // alike on every rank
@@ -2293,9 +2304,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         // that the shares' expected domains (about twice each rule's support) are equal
         x.la = 0;
         x.lz = uint32_t(batch.size());
-        if (shard_exp) {
-            uint64_t tot = 0;
+        x.sharded = false;
+        uint64_t tot = 0;
+        if (shard_exp)
             for (Rule* r : batch) tot += 2ull * r->sup + 1;
+        if (shard_exp && tot >= shard_min) {
+            x.sharded = true;
             const uint64_t lo = tot * uint64_t(comm->rank()) / uint64_t(R), hi = tot * uint64_t(comm->rank() + 1) / uint64_t(R);
             uint64_t acc = 0;
             x.la = x.lz = uint32_t(batch.size());
@@ -2381,7 +2395,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 for (int xi = 0; xi < nsets; ++xi) {
                     ExpSet& o = xs[xi];
                     if (&o != &x && o.busy && o.amin != kNoList && o.amin + acap < ahead + need) {
-                        finish(o);
+                        // its kernels completed is all the ring needs (its results are taken in at
+                        // their turn: a finish here would be a rank-local collective when sharded)
+                        FSM_HIP(hipEventSynchronize(o.ev[5]));
+                        o.amin = kNoList;
                         ++ring_waits;
                     }
                 }

@@ -119,15 +119,20 @@ def test_tsr_c4_fullsize_complete(eng):
     assert not missing, missing[:5]
 
 
+@pytest.mark.parametrize("shard_min", ["0", "default"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_tsr_c4_prefix_sharded(world, tmp_path):
+def test_tsr_c4_prefix_sharded(world, shard_min, tmp_path, monkeypatch):
     """Sharded TSR at the c4 20,000-sequence prefix over `world` gloo ranks on this
-    GPU: the pair phase by sequence range and every expansion launch's rule slots
-    split over the ranks (results all-gathered per launch, replay replicated) give
-    the exact prefix digest and final minsup on every rank."""
+    GPU: the pair phase by sequence range and the expansion launches' rule slots
+    split over the ranks (results all-gathered per launch, replay replicated; every
+    launch with FSM_TSR_SHARD_MIN=0, by default only those whose expected domain pays
+    for the gather, the rest replicated) give the exact prefix digest and final minsup
+    on every rank."""
     from test_dist import run_ranks
     if "c4-prefix" not in FULL:
         pytest.skip("fixture not generated")
+    if shard_min != "default":
+        monkeypatch.setenv("FSM_TSR_SHARD_MIN", shard_min)
     exp = FULL["c4-prefix"]
     res = run_ranks(world, ["tsr_digest", str(exp["sequences"]), str(exp["k"]), str(exp["minconf"])], tmp_path,
                     timeout=110)
@@ -219,10 +224,12 @@ def test_spade_fullsize_inproc(name, devices, claims, monkeypatch):
             db.free()
 
 
-@pytest.mark.parametrize("devices", [(0, 0), (0, 0, 0)])
-def test_tsr_c4_prefix_inproc(devices):
+@pytest.mark.parametrize("devices,shard_min", [((0, 0), "0"), ((0, 0, 0), "0"), ((0, 0, 0), "default")])
+def test_tsr_c4_prefix_inproc(devices, shard_min, monkeypatch):
     import spark_fsm_amd as fsm
     from tools import gen
+    if shard_min != "default":
+        monkeypatch.setenv("FSM_TSR_SHARD_MIN", shard_min)
     exp = FULL["c4-prefix"]
     ds = gen.kosarak(D=990002, seed=1).head(exp["sequences"])
     with fsm.Engine(devices=list(devices)) as e:
@@ -234,7 +241,8 @@ def test_tsr_c4_prefix_inproc(devices):
         st = e.stats()
     assert meta["final_minsup"] == exp["final_minsup"]
     assert rule_digest(rules) == exp["digest"]
-    assert 0 < st["rank_units"] < st["expansions"]  # rank 0 counted a share of the rule slots
+    if shard_min == "0":
+        assert 0 < st["rank_units"] < st["expansions"]  # rank 0 counted a share of the rule slots
 
 
 def test_inproc_failure_agreement():
