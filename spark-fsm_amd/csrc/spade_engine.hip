@@ -2630,20 +2630,9 @@ struct Miner {
         const char* v = std::getenv("FSM_COUNT_CHUNK");
         return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 256, 1u << 20)) : kChunk;
     }
-    // passes of the root F2 over ranges of rank groups (FSM_F2_PASSES overrides, for tuning)
-    static uint32_t f2_passes() {
-        const char* v = std::getenv("FSM_F2_PASSES");
-        return v ? uint32_t(std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 64)) : 1u;
-    }
-    // key alignment of the root F2 regions (a power of two >= 8 keys; FSM_F2_ALIGN overrides, for tuning)
-    static uint32_t f2_align() {
-        static const uint32_t a = [] {
-            const char* v = std::getenv("FSM_F2_ALIGN");
-            const uint64_t x = v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 8, 4096) : 8;
-            return uint32_t(1) << (63 - __builtin_clzll(x));
-        }();
-        return a;
-    }
+    // key alignment of the root F2 regions: 8 keys, so k_f2_count reads them in 16-byte words (64 or 256
+    // measured no different in round 4)
+    static constexpr uint32_t kF2Align = 8;
     // records from which the kid table and the children of a batch are built on the host
     // thread pool (below: one thread); FSM_HOST_PAR_MIN overrides (tuning)
     static uint64_t par_min() {
@@ -2656,7 +2645,7 @@ struct Miner {
     // whether the DB-direct root's F2 takes the unordered-pair layout (run_root_db decides it the
     // same way, unless the rank's own slice is empty)
     bool tri_expected(uint32_t F) const {
-        return W == 1 && f2_tri_env() && f2_passes() == 1 && F > 0 && tri_len(F, 0) <= kGroupCounters &&
+        return W == 1 && f2_tri_env() && F > 0 && tri_len(F, 0) <= kGroupCounters &&
                root_db_env() && !root_atomic();
     }
     // the root F2 in the unordered-pair layout (k_f2_tri; FSM_F2_TRI=0: the ordered layout)
@@ -2755,19 +2744,16 @@ struct Miner {
         DevBuf d_recs;
         unsigned long long nkeys = 0;
         size_t tk_cnt = 0, tk_keys = 0;
-        // passes over ranges of whole rank groups: each pass enumerates only the entries of its
-        // groups, so the keys it writes (and k_f2_count reads right after) stay on-die
-        const uint32_t npass = std::max<uint32_t>(1, std::min<uint32_t>(f2_passes(), g1 > g0 ? g1 - g0 : 1));
+        // (one pass over every group of the slice: passes over group ranges, which keep a pass's
+        // keys on-die, measured slower in round 4: each pass enumerates the rows again)
         for (int attempt = 0;; ++attempt) {
             d_recs.alloc(std::max<uint32_t>(cap_recs, 1) * sizeof(FreqRec));
             FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
             if (attempt == 0) FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
-            for (uint32_t ps = 0; ps < npass; ++ps) {
-                const uint32_t pg0 = g0 + uint32_t(uint64_t(g1 - g0) * ps / npass);
-                const uint32_t pg1 = g0 + uint32_t(uint64_t(g1 - g0) * (ps + 1) / npass);
-                const uint32_t prlo = std::max(rlo, pg0 * per), prhi = std::min(rhi, pg1 * per);
+            {
+                const uint32_t pg0 = g0, pg1 = g1, prlo = rlo, prhi = rhi;
                 if (attempt == 0) {  // a retry (record overflow) counts from the keys already written
-                    const uint32_t pmlo = npass == 1 ? mlo : 2 * prlo, pmhi = npass == 1 ? mhi : 2 * prhi;
+                    const uint32_t pmlo = mlo, pmhi = mhi;
                     tk_keys = clk->begin("k_f2_keys");
 #define FSM_F2K(WW)                                                                                                   \
     hipLaunchKernelGGL((k_f2_keys<WW, false>), dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(),      \
@@ -2797,7 +2783,7 @@ struct Miner {
                     // + 2 B per key actually written, added once the count is back
                     // DB-direct: the DB rows (item + mask per entry) instead of the slab's (mem, lohi, mask)
                     const int64_t rowb = b.db_direct ? db->E * int64_t(4 + 8 * W) : E0 * int64_t(8 + 8 * W);
-                    clk->end(tk_keys, rowb + int64_t(nd) * 12, ps == 0 ? E0 * 8 : 0);
+                    clk->end(tk_keys, rowb + int64_t(nd) * 12, E0 * 8);
                 }
                 tk_cnt = clk->begin("k_f2_count");
                 if (pg1 > pg0)
@@ -3790,7 +3776,7 @@ struct Miner {
         uint32_t G = geo.G;
         uint64_t nd = geo.nd;
         root.f2_tri = false;
-        if (W == 1 && f2_tri_env() && f2_passes() == 1) {
+        if (W == 1 && f2_tri_env()) {
             std::vector<uint32_t> tab;
             const uint32_t rlo = geo.mlo / 2, rhi = geo.mhi == kNone ? F : std::min(geo.mhi / 2, F);
             const uint32_t TG = tri_tables(F, rlo, rhi, tab);
@@ -3808,7 +3794,7 @@ struct Miner {
         const size_t tk = clk->begin("k_f2_plan");
         hipLaunchKernelGGL(k_f2_plan_db, dim3(geo.nblk), dim3(kF2Threads), size_t(G) * 4, s,
                            db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), root.rk2.as<uint32_t>(), geo.R,
-                           geo.rpb, geo.pm, G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(), f2_align() - 1,
+                           geo.rpb, geo.pm, G, geo.nblk, geo.mlo, geo.mhi, cap.as<uint32_t>(), kF2Align - 1,
                            root.mem_db.as<uint32_t>(), root.f2_tri ? root.f2_tri_tab.as<uint32_t>() : nullptr);
         FSM_LAUNCHED("k_f2_plan", s);
         clk->end(tk, int64_t(db->R) * 4 + db->E * 8 + int64_t(nd) * 4);
@@ -3901,7 +3887,7 @@ struct Miner {
     hipLaunchKernelGGL(k_root_write_plan<WW>, dim3(geo.nblk), dim3(kF2Threads), size_t(geo.G) * 4, s,              \
                        db->row_off.as<uint32_t>(), db->item.as<uint32_t>(), db->mask.as<uint64_t>(),               \
                        d_rank.as<uint32_t>(), geo.R, geo.rpb, roff.as<uint64_t>(), op, geo.pm, geo.G, geo.nblk,    \
-                       geo.mlo, geo.mhi, cap.as<uint32_t>(), f2_align() - 1, uint32_t(W))
+                       geo.mlo, geo.mhi, cap.as<uint32_t>(), kF2Align - 1, uint32_t(W))
             FSM_W_DISPATCH(W, FSM_ROOTWP)
 #undef FSM_ROOTWP
             FSM_LAUNCHED("k_root_write", s);
@@ -4294,8 +4280,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     pat_off[size_t(n)] = tsets[size_t(nthr)];
     set_off[set_off.n - 1] = titems[size_t(nthr)];
     const int32_t* ival = db->spade.item_val.data();
-    static const bool walk = [] { const char* v = std::getenv("FSM_OUTPUT_WALK"); return v && v[0] == '1'; }();
-    if (first == 0 && !any_dup && nthr > 1 && !walk) {
+    if (first == 0 && !any_dup && nthr > 1) {
         // Every node is output at its own index and its parent precedes it, so a pattern
         // is its parent's pattern plus one item: offsets first, then one parallel pass per
         // pattern length copying the parent's items and itemset starts (written by the

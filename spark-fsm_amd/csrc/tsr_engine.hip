@@ -1357,7 +1357,7 @@ struct Replay {
     // in O(1) with sequential memory), and later arrivals into it go to a small
     // side heap.  A pop takes the larger of the sorted back and the side heap's
     // top: the same order as one heap, the comparator being a total order.
-    // (FSM_TSR_CANDQ=heap: every bucket a 4-ary heap, as in round 3; A/B.)
+    // (Round 3's 4-ary heap per bucket measured 2-4 % slower on c4 and was retired in round 5.)
     struct CandQueue {
         struct Bucket {
             std::vector<HeapEnt> v;     // unsorted, or sorted ascending (sorted = true)
@@ -1370,7 +1370,6 @@ struct Replay {
         uint32_t top_sup = 0, floor = 0;  // buckets < floor are dropped
         size_t n = 0;
         MaxFirst cmp;
-        const bool heap_mode = [] { const char* v = std::getenv("FSM_TSR_CANDQ"); return v && !std::strcmp(v, "heap"); }();
         explicit CandQueue(MaxFirst c) : cmp(c) {}
         bool empty() const { return n == 0; }
         size_t size() const { return n; }
@@ -1382,9 +1381,7 @@ struct Replay {
                 occ.resize(size_t(sp) / 64 + 1, 0);
             }
             Bucket& b = bucket[sp];
-            if (heap_mode) {
-                heap4_push(b.v, e);
-            } else if (b.sorted) {
+            if (b.sorted) {
                 b.side.push_back(e);
                 std::push_heap(b.side.begin(), b.side.end(), cmp);
             } else {
@@ -1402,7 +1399,7 @@ struct Replay {
                 top_sup = uint32_t(w * 64 + 63 - size_t(__builtin_clzll(m)));
             }
             Bucket& b = bucket[top_sup];
-            if (!heap_mode && !b.sorted) {
+            if (!b.sorted) {
                 std::sort(b.v.begin(), b.v.end(), cmp);
                 b.sorted = true;
             }
@@ -1412,14 +1409,11 @@ struct Replay {
         bool side_first(const Bucket& b) const { return !b.side.empty() && (b.v.empty() || cmp(b.v.back(), b.side.front())); }
         const HeapEnt& top() {
             Bucket& b = settle();
-            if (heap_mode) return b.v.front();
             return side_first(b) ? b.side.front() : b.v.back();
         }
         void pop() {
             Bucket& b = settle();
-            if (heap_mode) {
-                heap4_pop(b.v);
-            } else if (side_first(b)) {
+            if (side_first(b)) {
                 std::pop_heap(b.side.begin(), b.side.end(), cmp);
                 b.side.pop_back();
             } else {
@@ -1443,37 +1437,6 @@ struct Replay {
                 occ[floor >> 6] &= ~(1ull << (floor & 63u));
             }
             if (floor < ms) floor = ms;
-        }
-        // 4-ary max-heap (FSM_TSR_CANDQ=heap)
-        void heap4_push(std::vector<HeapEnt>& b, const HeapEnt& e) {
-            size_t i = b.size();
-            b.push_back(e);
-            while (i > 0) {
-                const size_t up = (i - 1) >> 2;
-                if (!cmp(b[up], e)) break;
-                b[i] = b[up];
-                i = up;
-            }
-            b[i] = e;
-        }
-        void heap4_pop(std::vector<HeapEnt>& b) {
-            const HeapEnt last = b.back();
-            b.pop_back();
-            const size_t m = b.size();
-            if (!m) return;
-            size_t i = 0;
-            for (;;) {
-                const size_t c = 4 * i + 1;
-                if (c >= m) break;
-                size_t best = c;
-                const size_t ce = std::min(c + 4, m);
-                for (size_t j = c + 1; j < ce; ++j)
-                    if (cmp(b[best], b[j])) best = j;
-                if (!cmp(last, b[best])) break;
-                b[i] = b[best];
-                i = best;
-            }
-            b[i] = last;
         }
     };
     std::priority_queue<HeapEnt, std::vector<HeapEnt>, MinFirst> krules;
@@ -2017,7 +1980,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         uint32_t la = 0, lz = 0;  // slot sharding: this rank's slots [la, lz) of the batch (else all)
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // 0-4 timing, 5 done
         // the set's own stream: the two sets' launches are independent, so the GPU runs
-        // one set's kernels while the other's are in flight (FSM_TSR_STREAMS=1: ctx stream)
+        // one set's kernels while the other's are in flight
         hipStream_t st = nullptr;
         bool own_stream = false;
         DevBuf alive;          // kid codes for alive_t (each set its own: k_alive never races a launch)
@@ -2042,15 +2005,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     }();
     std::unique_ptr<ExpSet[]> xs_own(new ExpSet[nsets]);
     ExpSet* const xs = xs_own.get();
-    const bool set_streams = [] { const char* v = std::getenv("FSM_TSR_STREAMS"); return !(v && v[0] == '1'); }();
     for (int xi = 0; xi < nsets; ++xi) {
         ExpSet& x = xs[xi];
-        if (set_streams) {
-            FSM_HIP(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
-            x.own_stream = true;
-        } else {
-            x.st = s;
-        }
+        FSM_HIP(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
+        x.own_stream = true;
         if (use_bm) x.alive.alloc(size_t((K + 15) / 16) * 4);
         x.ctl.alloc(B * sizeof(ExpCtl));
         FSM_HIP(hipMemsetAsync(x.ctl.p, 0, B * sizeof(ExpCtl), s));

@@ -385,12 +385,10 @@ def shape_case(shape):
     return _CASES[shape]
 
 
-@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic", "passes-3", "passes-64", "slab-root",
-                                  "ordered"])
+@pytest.mark.parametrize("path", ["group", "group-few-blocks", "atomic", "slab-root", "ordered"])
 def test_root_f2_paths_agree(eng, path, monkeypatch):
     """The root F2 implementations (key runs counted per rank group, at the
-    default and at a small block chunk, in several passes over group ranges;
-    global atomics; from the DB rows (DB-direct root, default) or from the root
+    default and at a small block chunk; global atomics; from the DB rows (DB-direct root, default) or from the root
     slab) give the oracle's patterns and joins."""
     from oracle import oracle
     from tools import gen
@@ -400,8 +398,6 @@ def test_root_f2_paths_agree(eng, path, monkeypatch):
         monkeypatch.setenv("FSM_ROOT_DB", "0")
     if path == "group-few-blocks":
         monkeypatch.setenv("FSM_F2_BLOCKS", "3")
-    if path.startswith("passes"):
-        monkeypatch.setenv("FSM_F2_PASSES", path.split("-")[1])
     if path == "ordered":  # the ordered-pair enumeration (k_f2_keys) instead of the unordered one (k_f2_tri)
         monkeypatch.setenv("FSM_F2_TRI", "0")
     ds, sup, o = shape_case("quest4")
@@ -615,7 +611,7 @@ def test_sharded_tsr_failure_reaches_every_rank(tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("bitmap", ["1", "0", "passes", "domain-bitmap", "domain-list", "max-kids", "max-pos",
-                                    "plist-off", "dlmemo-off", "dlmemo-tiny", "candq-heap", "ring-wrap",
+                                    "plist-off", "dlmemo-off", "dlmemo-tiny", "ring-wrap",
                                     "ring-wrap-2sets"])
 def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
     """TSR expansions over sid bitmaps (default: each slot's domain from the
@@ -640,7 +636,7 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
         monkeypatch.setenv("FSM_TSR_MAX_POS", "3")
     # the replay's default-on features against the oracle, each off or at its edge: the kept-row
     # lists off; the |sids(X u {c})| memo off, or 16 entries (full after a few counts: probes run
-    # out, most lookups miss); the candidate buckets as 4-ary heaps; a 1 MiB kept-row ring
+    # out, most lookups miss); a 1 MiB kept-row ring
     # (65,536 entries) with 4 (or 2) launch sets in flight, so the head wraps the ring many times
     # and launches still in flight hold ring positions (finished early before an overwrite)
     if bitmap == "plist-off":
@@ -649,8 +645,6 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
         monkeypatch.setenv("FSM_TSR_DLMEMO", "0")
     if bitmap == "dlmemo-tiny":
         monkeypatch.setenv("FSM_TSR_DLMEMO_LOG2", "4")
-    if bitmap == "candq-heap":
-        monkeypatch.setenv("FSM_TSR_CANDQ", "heap")
     if bitmap.startswith("ring-wrap"):
         monkeypatch.setenv("FSM_TSR_ARENA_MB", "1")
         monkeypatch.setenv("FSM_TSR_SETS", "2" if bitmap.endswith("2sets") else "4")
