@@ -46,13 +46,15 @@ constexpr int kBlock = 256;
 constexpr int kMaxSide = 64;
 constexpr int kCollectBlocks = 8;   // collect blocks per rule slot (FSM_TSR_GRID sweep: 4-8 best)
 constexpr int kExpBatch = 384;      // rules expanded per launch (speculative, committed in order; FSM_TSR_BATCH; swept on MI355X)
+constexpr int kExpBatchWide = 768;  // the same when the pair phase ends at minsup >= kWideMinsup (swept on MI355X)
+constexpr uint32_t kWideMinsup = 32;
 constexpr int kMaxBatch = 1024;  // FSM_TSR_BATCH ceiling (the slot searches of the kernels)
 constexpr int kExpandBlocks = 4096; // bitmap path: at most this many expansion blocks per rule slot
 constexpr int kExpSpb = 128;        // bitmap path: expected domain sids per expansion block (FSM_TSR_SPB; swept: 64-512)
 constexpr int kDlBlocks = 512;      // bitmap path: |sids(X u {c})| blocks
 constexpr int kDlUnroll = 8;        // k_dl: independent words / sids per thread per round
 constexpr int kSpecDepth = 6;       // child speculation: levels per launch
-constexpr int kSpecMax = 768;       // child speculation: rules per level
+constexpr int kSpecMax = 2;         // child speculation: rules per level, in batches (2 x B)
 constexpr int kExpSets = 2;         // launch sets (buffers, stream, events) in flight
 // FSM_TSR_GRID="expand,collect,dl" overrides the per-launch grids (tuning sweeps)
 struct TsrGrid {
@@ -1225,6 +1227,7 @@ struct Rule {
     bool dropped = false;  // a speculated child its parent's commit did not register
     int8_t inset = -1;     // replay: the launch set expanding it (results not yet taken in), or -1
     bool pleft = false;    // derived by adding pc to its parent's X (else to Y)
+    bool spec = false;     // made by child speculation
     int32_t res = -1;      // replay: its expansion results (slot of the result pool), or -1
     uint32_t ln = 0, pn = 0, pc = 0;
     uint64_t loff = kNoList;   // its kept domain rows in the arena (ln of them), after its expansion
@@ -1867,9 +1870,17 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // heap with their results cached (results are minsup-independent supersets,
     // re-filtered against the current minsup at commit), so no expansion is
     // computed twice and the outcome equals the one-at-a-time replay.
-    const uint32_t B = [] {  // rules per launch (FSM_TSR_BATCH overrides, for tuning)
+    // Rules per launch (FSM_TSR_BATCH overrides, for tuning).  Wide batches halve the launches
+    // (round trips) where supports are coarse: at c4 (pair-phase minsup in the hundreds) every
+    // speculated rule is committed, and 768 rules per launch take 12,973 launches down to 7,179
+    // (2.76 -> 2.39 s).  Where supports are a few units (the 5K prefix ends at minsup 2) a wide
+    // batch's lowest rules sit at the threshold, their speculated children mostly fall below the
+    // rising minsup (1.45M speculated, 0.22M committed) and the launches multiply (2.6K -> 15K):
+    // those mines keep kExpBatch.
+    const uint32_t B = [&] {
         const char* v = std::getenv("FSM_TSR_BATCH");
-        return v ? uint32_t(std::clamp<long>(std::strtol(v, nullptr, 10), 1, kMaxBatch)) : uint32_t(kExpBatch);
+        if (v) return uint32_t(std::clamp<long>(std::strtol(v, nullptr, 10), 1, kMaxBatch));
+        return uint32_t(rp.minsup >= kWideMinsup ? kExpBatchWide : kExpBatch);
     }();
     const uint64_t SU = uint64_t(B) * std::max<uint32_t>(U, 1);
     const size_t kSidesB = B * sizeof(Side), kOffB = (B + 1) * 8;
@@ -2084,6 +2095,8 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         --res_live;
     };
     std::vector<std::pair<std::vector<Rule*>, int>> spec_todo;  // finished launches whose children to speculate
+    // speculated rules committed, and dropped at their parent's commit (verbose)
+    int64_t spec_hit = 0, spec_waste = 0;
     int64_t expansions = 0, launches = 0, spec_pushback = 0, gpu_rules = 0;
     double wait_ms = 0;  // host time blocked on the GPU in the expansion loop
     double last_log_ms = now_ms();  // verbose progress line every 20 s
@@ -2518,6 +2531,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // recursively, those of its own speculated children
     std::function<void(Rule*)> drop_spec = [&](Rule* x) {
         x->dropped = true;
+        spec_waste += x->spec;
         if (x->res < 0) return;
         std::vector<Rule*> kids;
         {
@@ -2569,7 +2583,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     // while the host commits; the commit then registers the pre-built rule
     // (results cached or in flight) instead of deriving it again.
     int64_t spec_made = 0, spec_launches = 0;
-    int spec_depth = kSpecDepth, spec_max = kSpecMax;  // FSM_TSR_SPEC="depth,max" (tuning; "0" disables)
+    int spec_depth = kSpecDepth, spec_max = kSpecMax * int(B);  // FSM_TSR_SPEC="depth,max" (tuning; "0" disables)
     double spec_frac = 1.0;  // FSM_TSR_SPEC_FRAC: speculate children with sup >= frac * T (tuning)
     if (const char* v = std::getenv("FSM_TSR_SPEC_FRAC")) {
         const double f = std::atof(v);
@@ -2602,12 +2616,14 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                 if (x->expandLR && e.tl >= T) {
                     Rule* c = rp.derive(x, e.c, kNone, e.tl, e.dl);
                     c->expandLR = true;
+                    c->spec = true;
                     res.preL[i] = c;
                     next.push_back(c);
                 }
                 if (e.tr >= T && next.size() < size_t(spec_max)) {
                     Rule* c = rp.derive(x, kNone, e.c, e.tr, x->nX);
                     c->expandLR = false;
+                    c->spec = true;
                     res.preR[i] = c;
                     next.push_back(c);
                 }
@@ -2645,6 +2661,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             // (the host-time split is taken only when verbose: a clock read costs as much as a commit)
             const double tc0 = ctx->opts.verbose ? now_ms() : 0.0;
             commit(r, res_pool[size_t(r->res)]);
+            spec_hit += r->spec;
             if (r->res >= 0) res_release(r);
             if (ctx->opts.verbose) commit_ms += now_ms() - tc0;
             if (res_live > sweep_at) {  // results of rules now below minsup can never be committed
@@ -2680,10 +2697,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
                      (long long)expansions, (long long)launches, (long long)gpu_rules, (long long)spec_pushback, wait_ms,
                      prep_ms, fill_ms, post_ms, commit_ms, pop_ms, rp.st.size());
     if (ctx->opts.verbose)
-        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches; partial rows %.1f MB; domain sids "
+        std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches (%lld committed, %lld dropped); partial rows %.1f MB; domain sids "
                      "%lld (row entries %lld), rows where the rule holds %lld, row entries walked %lld; "
                      "rules on their parent's kept rows %lld (ring: %llu entries written, %lld early finishes)\n",
-                     (long long)spec_made, (long long)spec_launches, double(exp_part_bytes) / 1e6, (long long)exp_domain,
+                     (long long)spec_made, (long long)spec_launches, (long long)spec_hit, (long long)spec_waste, double(exp_part_bytes) / 1e6, (long long)exp_domain,
                      (long long)exp_entries, (long long)exp_hold, (long long)exp_walk, (long long)exp_plist,
                      (unsigned long long)ahead, (long long)ring_waits);
     // ---------------- result = kRules

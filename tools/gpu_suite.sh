@@ -6,8 +6,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out"
 ( while true; do sleep 50; date +%s >> "$R/gpurun_out/heartbeat.txt"; done ) &
 HB=$!
-K=${1:+-k "$1"}
-timeout -k 10 1000 python -u -m pytest -v -m gpu --timeout 240 --timeout-method thread --durations=40 $K tests \
+K=()
+[ -n "$1" ] && K=(-k "$1")
+timeout -k 10 1000 python -u -m pytest -v -m gpu --timeout 240 --timeout-method thread --durations=40 "${K[@]}" tests \
     > "$R/gpurun_out/suite.log" 2>&1
 rc=$?
 kill $HB

@@ -1,6 +1,12 @@
+# TSR defaults (rules per launch by the pair-phase minsup) on c4 and its 5K / 50K / 250K prefixes
 set -o pipefail
 mkdir -p gpurun_out
-FSM_HOST_TRACE=1 timeout -k 10 200 python tools/run_one.py spade quest --D 1000000 --support 0.001 --reps 5 > gpurun_out/d1m_host.log 2>&1 || exit 1
-C4_ENVS="- FSM_TSR_BATCH=512+FSM_TSR_SPEC=6,1024 FSM_TSR_BATCH=448+FSM_TSR_SPEC=6,896 FSM_TSR_BATCH=512+FSM_TSR_SPEC=8,1024" REPS=3 bash tools/c4_ab.sh > gpurun_out/c4ab.txt || exit 1
-C4_ARGS="--head 5000" C4_ENVS="- FSM_TSR_BATCH=512+FSM_TSR_SPEC=6,1024 FSM_TSR_BATCH=448+FSM_TSR_SPEC=6,896 FSM_TSR_BATCH=512+FSM_TSR_SPEC=8,1024" REPS=3 bash tools/c4_ab.sh >> gpurun_out/c4ab.txt || exit 1
+: > gpurun_out/c4ab.txt
+for H in 5000 50000 250000; do
+  C4_ARGS="--head $H" REPS=3 bash tools/c4_ab.sh >> gpurun_out/c4ab.txt || exit 1
+done
+REPS=3 bash tools/c4_ab.sh >> gpurun_out/c4ab.txt || exit 1
+for H in 5000 50000 990002; do
+  timeout -k 10 100 python tools/run_one.py tsr kosarak --D 990002 --k 1000 --minconf 0.5 --head $H --reps 1 --verbose 2>&1 | grep -E "pair phase|child spec" | cut -c1-200 >> gpurun_out/c4ab.txt || exit 1
+done
 cat gpurun_out/c4ab.txt
