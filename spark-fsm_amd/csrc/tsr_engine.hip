@@ -1372,6 +1372,7 @@ struct Replay {
         std::vector<uint64_t> occ;  // bit s: bucket[s] non-empty (the next lower bucket is a word scan away)
         uint32_t top_sup = 0, floor = 0;  // buckets < floor are dropped
         size_t n = 0;
+        size_t n_sorted = 0, n_popped = 0;  // entries sorted, and popped (verbose)
         MaxFirst cmp;
         explicit CandQueue(MaxFirst c) : cmp(c) {}
         bool empty() const { return n == 0; }
@@ -1403,7 +1404,8 @@ struct Replay {
             }
             Bucket& b = bucket[top_sup];
             if (!b.sorted) {
-                std::sort(b.v.begin(), b.v.end(), cmp);
+                n_sorted += b.v.size();
+                std::sort(b.v.begin(), b.v.end(), cmp);  // (a parallel merge sort on the host pool measured no faster at c4)
                 b.sorted = true;
             }
             return b;
@@ -1416,6 +1418,7 @@ struct Replay {
         }
         void pop() {
             Bucket& b = settle();
+            ++n_popped;
             if (side_first(b)) {
                 std::pop_heap(b.side.begin(), b.side.end(), cmp);
                 b.side.pop_back();
@@ -2676,7 +2679,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         const double tp0 = now_ms();
         batch.clear();
         popped.clear();
-        while (batch.size() < size_t(B) && !rp.cand.empty() && rp.cand.top().r->sup >= rp.minsup) {
+        while (batch.size() < size_t(B) && !rp.cand.empty() && uint32_t(rp.cand.top().k1 >> 32) >= rp.minsup) {
             Rule* x = rp.cand.top().r;
             rp.cand.pop();
             popped.push_back(x);
@@ -2699,10 +2702,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     if (ctx->opts.verbose)
         std::fprintf(stderr, "[fsm tsr] child speculation: %lld rules in %lld launches (%lld committed, %lld dropped); partial rows %.1f MB; domain sids "
                      "%lld (row entries %lld), rows where the rule holds %lld, row entries walked %lld; "
-                     "rules on their parent's kept rows %lld (ring: %llu entries written, %lld early finishes)\n",
+                     "rules on their parent's kept rows %lld (ring: %llu entries written, %lld early finishes); candidates sorted %zu, popped %zu\n",
                      (long long)spec_made, (long long)spec_launches, (long long)spec_hit, (long long)spec_waste, double(exp_part_bytes) / 1e6, (long long)exp_domain,
                      (long long)exp_entries, (long long)exp_hold, (long long)exp_walk, (long long)exp_plist,
-                     (unsigned long long)ahead, (long long)ring_waits);
+                     (unsigned long long)ahead, (long long)ring_waits, rp.cand.n_sorted, rp.cand.n_popped);
     // ---------------- result = kRules
     std::vector<const Rule*> res;
     while (!rp.krules.empty()) {

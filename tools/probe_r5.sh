@@ -1,12 +1,6 @@
-# TSR defaults (rules per launch by the pair-phase minsup) on c4 and its 5K / 50K / 250K prefixes
+# c4: in-tree libfsm.so (candidate buckets sorted on the host pool) against the serial-sort build
 set -o pipefail
 mkdir -p gpurun_out
-: > gpurun_out/c4ab.txt
-for H in 5000 50000 250000; do
-  C4_ARGS="--head $H" REPS=3 bash tools/c4_ab.sh >> gpurun_out/c4ab.txt || exit 1
-done
-REPS=3 bash tools/c4_ab.sh >> gpurun_out/c4ab.txt || exit 1
-for H in 5000 50000 990002; do
-  timeout -k 10 100 python tools/run_one.py tsr kosarak --D 990002 --k 1000 --minconf 0.5 --head $H --reps 1 --verbose 2>&1 | grep -E "pair phase|child spec" | cut -c1-200 >> gpurun_out/c4ab.txt || exit 1
-done
-cat gpurun_out/c4ab.txt
+bash tools/ab_lib.sh spark-fsm_amd/build/var/noparsort/libfsm.so tsr kosarak --D 990002 --k 1000 --minconf 0.5 --reps 3 > gpurun_out/ab_sort.txt || exit 1
+bash tools/ab_lib.sh spark-fsm_amd/build/var/noparsort/libfsm.so tsr kosarak --D 990002 --k 1000 --minconf 0.5 --reps 3 --head 5000 >> gpurun_out/ab_sort.txt || exit 1
+cat gpurun_out/ab_sort.txt
