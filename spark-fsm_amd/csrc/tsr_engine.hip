@@ -2115,7 +2115,12 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         return v ? std::clamp<uint64_t>(std::strtoull(v, nullptr, 10), 1, 1u << 20) : uint64_t(kExpSpb);
     }();
     // per-kernel device time: every 16th launch records one set of events and reads
-    // them back when it finishes (ctx->kstats rows)
+    // them back when it finishes (ctx->kstats rows); FSM_TSR_TIME_EVERY=n times every n-th
+    // (1: every launch, the bench's roofline mine)
+    const int64_t time_every = [] {
+        const char* v = std::getenv("FSM_TSR_TIME_EVERY");
+        return v ? std::clamp<int64_t>(std::strtoll(v, nullptr, 10), 1, 1 << 20) : int64_t(16);
+    }();
     struct Seg {
         double ms = 0;  // over the timed launches
         int64_t n = 0, timed = 0, bytes = 0, survey = 0;  // survey: SURVEY §8(d) TSR units
@@ -2404,7 +2409,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         hipStream_t s = x.st;  // (shadows the context stream for this launch)
         FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, 2 * kOffB + size_t(nb) * sizeof(Side), hipMemcpyHostToDevice,
                                s));
-        x.timed = nb && (launches & 15) == 0;  // every 16th launch is timed (events cost host time)
+        x.timed = nb && launches % time_every == 0;  // every 16th launch is timed (events cost host time)
         const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
         if (nb) {  // (a rank may get no slot of a small sharded batch)
             if (use_bm && x.alive_t != rp.minsup) {  // minsup rose: the kids below it stop counting
