@@ -2840,30 +2840,31 @@ struct Miner {
         FSM_LAUNCHED("k_f2_tri", s);
         clk->end(tk_keys, db->E * 12 + int64_t(nd) * 12, int64_t(b.cls[0].cap) * 8);
         // count + frequent pairs (a retry when the first record buffer was too small)
+        // the records land in mapped pinned host memory, the counts in pinned slots: one sync
         uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * 2 * F, uint64_t(1) << 20));
-        DevBuf d_nrec(4), d_recs;
+        DevBuf d_nrec(4);
         size_t tk_cnt = 0;
         unsigned long long nkeys = 0;
         for (int attempt = 0;; ++attempt) {
-            d_recs.alloc(std::max<uint32_t>(cap_recs, 1) * sizeof(FreqRec));
+            PinnedBuf* pb = ctx->pinned_big(size_t(std::max<uint32_t>(cap_recs, 1)) * sizeof(FreqRec));
             FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
             tk_cnt = clk->begin("k_f2_count");
             hipLaunchKernelGGL((k_f2_count<false, true>), dim3(G), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
                                fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), 2 * F, 0u, 0u, rlo, rhi, minsup,
-                               d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u, gr, F);
+                               static_cast<FreqRec*>(pb->dev), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u,
+                               gr, F);
             FSM_LAUNCHED("k_f2_count", s);
             clk->end(tk_cnt, int64_t(G) * nblk * 12);
-            uint32_t nrec = 0;
-            FSM_HIP(hipMemcpyAsync(&nrec, d_nrec.p, 4, hipMemcpyDeviceToHost, s));
-            FSM_HIP(hipMemcpyAsync(&nkeys, nk.p, 8, hipMemcpyDeviceToHost, s));
+            pend[2] = pend[3] = 0;
+            FSM_HIP(hipMemcpyAsync(&pend[2], d_nrec.p, 4, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&pend[3], nk.p, 8, hipMemcpyDeviceToHost, s));
             sync();
+            const uint32_t nrec = uint32_t(pend[2]);
+            nkeys = pend[3];
             if (nrec <= cap_recs || attempt > 0) {
                 if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
-                recs.resize(nrec);
-                if (nrec)
-                    FSM_HIP(hipMemcpyAsync(recs.data(), d_recs.p, size_t(nrec) * sizeof(FreqRec), hipMemcpyDeviceToHost,
-                                           s));
-                sync();
+                const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
+                recs.assign(hr, hr + nrec);
                 break;
             }
             cap_recs = nrec;

@@ -1,6 +1,6 @@
-# host sampling profile of SIGN-shaped mines (line-table build of libfsm.so); THP state of the box
+# D1M: in-tree libfsm.so against the previous build (root F2 records through mapped memory)
 set -o pipefail
 mkdir -p gpurun_out
-cat /sys/kernel/mm/transparent_hugepage/enabled /sys/kernel/mm/transparent_hugepage/defrag > gpurun_out/thp.txt 2>&1 || true
-FSM_LIB_PATH=spark-fsm_amd/build/var/lines/libfsm.so FSM_HOST_PROF=gpurun_out/sign.prof FSM_HOST_TRACE=1 timeout -k 10 120 python tools/run_one.py spade sign --support 0.015 --reps 4 > gpurun_out/signprof.log 2>&1 || exit 1
-grep -c . gpurun_out/sign.prof
+bash tools/ab_lib.sh spark-fsm_amd/build/var/prev/libfsm.so spade quest --D 1000000 --support 0.001 --reps 12 > gpurun_out/ab_d1m.txt || exit 1
+bash tools/ab_lib.sh spark-fsm_amd/build/var/prev/libfsm.so spade quest --D 1000000 --support 0.001 --reps 12 >> gpurun_out/ab_d1m.txt || exit 1
+cat gpurun_out/ab_d1m.txt
