@@ -2982,6 +2982,27 @@ struct Miner {
     void count_and_freq(Batch& b) {
         const double tc0 = now_ms();
         double tl = tc0;
+        // FSM_HOST_TRACE=2: one line per batch with its host phases (diagnostics)
+        struct BatchTrace {
+            Miner* m;
+            Batch* b;
+            double h0[8], t0;
+            ~BatchTrace() {
+                std::fprintf(stderr, "[fsm batch] depth %lld root %d E %llu classes %zu children %zu: %.3f ms (", (long long)b->depth,
+                             int(b->root), (unsigned long long)b->E, b->cls.size(), b->children.size(), now_ms() - t0);
+                for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %.3f", m->hp[i] - h0[i]);
+                std::fprintf(stderr, " )\n");
+            }
+        };
+        static const bool btrace = [] { const char* v = std::getenv("FSM_HOST_TRACE"); return v && v[0] == '2'; }();
+        std::unique_ptr<BatchTrace> bt;
+        if (btrace) {
+            bt = std::make_unique<BatchTrace>();
+            bt->m = this;
+            bt->b = &b;
+            for (int i = 0; i < 8; ++i) bt->h0[i] = hp[i];
+            bt->t0 = tc0;
+        }
         dump(b);
         const int cmode = count_mode(b);
         lap(5, tl);

@@ -659,12 +659,13 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
     assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
 
 
-@pytest.mark.parametrize("batch", ["1", "7", "128"])
+@pytest.mark.parametrize("batch", ["1", "7", "128", "768"])
 @pytest.mark.parametrize("spb", ["default", "4", "100000"])
 def test_tsr_batch_sizes_agree(eng, batch, spb, monkeypatch):
-    """Rules expanded per launch (FSM_TSR_BATCH) and the domain sids per
-    expansion block (FSM_TSR_SPB: many small blocks, each slot in one block)
-    change only how much runs ahead speculatively and how the partial
+    """Rules expanded per launch (FSM_TSR_BATCH; 768: the wide batches c4-like
+    DBs take, here on a DB whose pair phase ends at a low minsup) and the domain
+    sids per expansion block (FSM_TSR_SPB: many small blocks, each slot in one
+    block) change only how much runs ahead speculatively and how the partial
     histograms are split: the rules and final minsup stay the oracle's."""
     from oracle import oracle
     from tools import gen

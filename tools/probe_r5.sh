@@ -1,6 +1,5 @@
-# D1M: in-tree libfsm.so against the previous build (root F2 records through mapped memory)
+# D1M per-batch host phases (FSM_HOST_TRACE=2)
 set -o pipefail
 mkdir -p gpurun_out
-bash tools/ab_lib.sh spark-fsm_amd/build/var/prev/libfsm.so spade quest --D 1000000 --support 0.001 --reps 12 > gpurun_out/ab_d1m.txt || exit 1
-bash tools/ab_lib.sh spark-fsm_amd/build/var/prev/libfsm.so spade quest --D 1000000 --support 0.001 --reps 12 >> gpurun_out/ab_d1m.txt || exit 1
-cat gpurun_out/ab_d1m.txt
+FSM_HOST_TRACE=2 timeout -k 10 200 python tools/run_one.py spade quest --D 1000000 --support 0.001 --reps 4 > gpurun_out/d1m_batches.log 2>&1 || exit 1
+grep "fsm batch" gpurun_out/d1m_batches.log | tail -5
