@@ -1,13 +1,5 @@
-# D1M: root F2 row blocks (FSM_F2_BLOCKS) for the unordered-pair kernel
+# c4 at the wide batches: per-launch grids (FSM_TSR_GRID = expand blocks per slot, reduce blocks, k_dl blocks)
 set -o pipefail
 mkdir -p gpurun_out
-: > gpurun_out/f2blocks.txt
-for b in 256 512 1024 2048 512 1024; do
-  FSM_F2_BLOCKS=$b timeout -k 10 120 python tools/run_one.py spade quest --D 1000000 --support 0.001 --reps 10 2>/dev/null | python3 -c "
-import json,sys
-rows=[json.loads(l) for l in sys.stdin if l.startswith('{')]
-ws=sorted(round(r['wall_ms'],2) for r in rows)
-k=[(q['name'],q['ms']) for q in rows[-1]['kernels'] if q['name'] in ('k_f2_keys','k_f2_count','k_f2_plan')]
-print('blocks $b', ws[:9], k)" >> gpurun_out/f2blocks.txt || exit 1
-done
-cat gpurun_out/f2blocks.txt
+C4_ENVS="- FSM_TSR_GRID=4096,8,1024 FSM_TSR_GRID=4096,8,2048 FSM_TSR_GRID=4096,4,1024 FSM_TSR_GRID=4096,8,256 -" REPS=3 bash tools/c4_ab.sh > gpurun_out/c4grid.txt || exit 1
+cat gpurun_out/c4grid.txt
