@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FSM_ABI_VERSION 6
+#define FSM_ABI_VERSION 7
 
 /* status codes */
 #define FSM_OK 0
@@ -87,10 +87,14 @@ typedef struct {
     int32_t rank;            /* this process's rank in [0, nranks) */
     int32_t verbose;         /* 1: per-level trace on stderr */
     uint8_t unique_id[128];  /* RCCL unique id (fsm_comm_unique_id on rank 0), nranks > 1 */
-    int64_t mem_budget;      /* device bytes for lattice frontier slabs; 0 = 1/2 of free HBM */
+    int64_t mem_budget;      /* device bytes for lattice frontier slabs; 0 = 1/2 of free HBM (divided
+                                among the in-process ranks that share a device) */
     const fsm_host_comm* host_comm; /* nranks > 1: NULL = RCCL over unique_id, else these callbacks
                                        (must outlive the context) */
-    int32_t ndevices;        /* > 1: in-process ranks on devices[0..ndevices) (nranks must be <= 1) */
+    int32_t ndevices;        /* > 1: in-process ranks on devices[0..ndevices) (nranks must be <= 1).
+                                The DB is parsed once (rank 0) and copied device to device to the
+                                other ranks.  A call waits at most FSM_COMM_TIMEOUT_S (default 300)
+                                for a rank, then returns FSM_ECOMM */
     int32_t devices[FSM_MAX_DEVICES]; /* HIP ordinals of the in-process ranks */
 } fsm_opts;
 
@@ -161,6 +165,12 @@ typedef struct {
     int64_t rank_root_owned;    /* SPADE: root entries this rank joined as the owner (F2 keys + root emit) */
     int64_t rank_root_slab;     /* SPADE: root entries this rank wrote to a root slab (0: DB-direct root) */
     int64_t rank_units;         /* TSR: expansion rule slots this rank counted */
+    /* DB build (kept across mines) */
+    int64_t db_parses;          /* passes over the caller's input of the last fsm_db_* (1; a group's DB is
+                                   parsed once on rank 0, every other rank copies the resident arrays) */
+    int64_t db_replicas;        /* group DBs: rank replicas made by device-to-device copy */
+    int64_t tsr_ring_waits;     /* TSR: launches in flight finished early to free their kept-row ring
+                                   positions before a later launch overwrote them */
 } fsm_stats;
 
 /* Per-kernel device time of the last fsm_*_mine call (HIP events on the

@@ -130,10 +130,6 @@ class ShmCounters {
     int64_t* ctr_ = nullptr;
 };
 
-double comm_timeout_ms(const char* var) {
-    const char* tv = std::getenv(var);
-    return 1000.0 * (tv ? std::max(1.0, std::atof(tv)) : 300.0);
-}
 
 // Whether every rank's ShmCounters are ONE segment (ranks on one node sharing /dev/shm):
 // rank 0 stores a nonce in the probe slot, the nonce is all-gathered, every rank reads
@@ -369,6 +365,11 @@ void rccl_unique_id(uint8_t out[128]) {
     std::memcpy(out, uid.internal, 128);
 }
 
+double comm_timeout_ms(const char* var) {
+    const char* tv = std::getenv(var);
+    return 1000.0 * (tv ? std::max(0.1, std::atof(tv)) : 300.0);
+}
+
 std::unique_ptr<Comm> make_comm(const fsm_opts& o) {
     if (o.nranks <= 1) return nullptr;
     if (o.rank < 0 || o.rank >= o.nranks) throw Error(FSM_EINVAL, "rank out of range");
@@ -414,7 +415,18 @@ void Agreement::check(const uint32_t* v) const {
                                "); the sharded mine is aborted on every rank");
 }
 
+void maybe_stall(int rank, const char* phase) {
+    const char* v = std::getenv("FSM_INJECT_STALL");
+    if (!v) return;
+    char ph[16] = {0};
+    int r = -1;
+    double sec = 0;
+    if (std::sscanf(v, "%d,%15[^,],%lf", &r, ph, &sec) == 3 && r == rank && !std::strcmp(ph, phase) && sec > 0)
+        std::this_thread::sleep_for(std::chrono::duration<double>(sec));
+}
+
 void Agreement::maybe_inject(const char* phase) const {
+    if (comm) maybe_stall(comm->rank(), phase);
     const char* v = std::getenv("FSM_INJECT_FAIL");
     if (!v || !comm) return;
     char ph[16] = {0};
@@ -466,7 +478,16 @@ class InProcHub {
             if (i > 256) std::this_thread::yield();
         }
         g.lock();
-        cv_.wait(g, [&] { return gen_ != my || broken_; });
+        const auto lim = std::chrono::duration<double, std::milli>(comm_timeout_ms("FSM_COMM_TIMEOUT_S"));
+        if (!cv_.wait_for(g, lim, [&] { return gen_ != my || broken_; })) {
+            // a peer never arrived: break the hub so every other waiter leaves too
+            broken_ = true;
+            abroken_.store(true);
+            g.unlock();
+            cv_.notify_all();
+            throw Error(FSM_ECOMM, "in-process rank group: rank " + std::to_string(rank) +
+                                       " timed out waiting for its peers (FSM_COMM_TIMEOUT_S); the call is aborted");
+        }
         if (gen_ == my) throw broken_error();
     }
     void abort() {

@@ -93,12 +93,19 @@ struct Agreement {
         if (code) f[std::clamp(code, 1, 7)] = 1u;
     }
     // FSM_INJECT_FAIL="<rank>,<phase>": throw FSM_ELIMIT on that rank at that phase
-    // (test hook for the agreement)
+    // (test hook for the agreement); FSM_INJECT_STALL (maybe_stall) at the same phases
     void maybe_inject(const char* phase) const;
 };
 
+// FSM_INJECT_STALL="<rank>,<phase>,<seconds>": that rank sleeps there (test hook for the
+// bounded waits of the in-process group: its peers must return FSM_ECOMM, not hang)
+void maybe_stall(int rank, const char* phase);
+
 std::unique_ptr<Comm> make_comm(const fsm_opts& o);
 void rccl_unique_id(uint8_t out[128]);
+// the limit (ms) of a wait on peer ranks: the environment variable `var` in seconds
+// (FSM_COMM_TIMEOUT_S, FSM_COMM_INIT_TIMEOUT_S), default 300 s
+double comm_timeout_ms(const char* var);
 
 // In-process ranks: one fsm_ctx driving fsm_opts.ndevices ranks, one host thread
 // per rank (fsm_api.cpp, Group).  The ranks' collectives meet in a hub in host
@@ -107,7 +114,9 @@ void rccl_unique_id(uint8_t out[128]);
 // exchanged data are KB-sized: F1 histograms, frequent-pair records, per-launch TSR
 // results).  abort() breaks every current and later barrier with FSM_ECOMM, so a
 // rank that fails outside a failure agreement cannot leave its peers blocked;
-// reset() re-arms the hub once every rank has returned.
+// reset() re-arms the hub once every rank has returned.  A barrier waits at most
+// FSM_COMM_TIMEOUT_S for its peers, then aborts the hub and throws FSM_ECOMM (a
+// stalled rank never leaves the others blocked without bound).
 class InProcHub;
 std::shared_ptr<InProcHub> make_inproc_hub(int nranks);
 std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<InProcHub>& hub, int rank);

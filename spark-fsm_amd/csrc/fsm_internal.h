@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -229,6 +230,7 @@ struct fsm_ctx {
     // fsm_opts.ndevices > 1: the rank contexts this context drives in-process (fsm_api.cpp)
     std::unique_ptr<fsm::Group> group;
     bool result_root_only = false;  // a rank context of a group: only rank 0's result is returned
+    int dev_share = 1;  // rank contexts of this group on the same device: default budgets are split
     std::shared_ptr<fsm::Pool> pool;  // device blocks of this context (see fsm::Pool)
     std::vector<fsm_kernel_stat> kstats;  // of the last mine call
     std::unique_ptr<fsm::PinnedBuf> pin;  // small mapped readback slots, made on first use
@@ -282,6 +284,7 @@ struct fsm_db {
     fsm_ctx* ctx = nullptr;
     int mode = 0;
     std::vector<fsm_db*> parts;  // a group context's DB: one replica per rank context (owned)
+    std::shared_ptr<std::atomic<bool>> group_stuck;  // the group's stalled-rank flag (group DBs)
     fsm::FlatSpade spade;
     fsm::FlatTsr tsr;
     SpadeDevDB* spade_dev = nullptr;

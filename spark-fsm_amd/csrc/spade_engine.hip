@@ -3519,10 +3519,12 @@ struct Miner {
     static constexpr uint64_t kClaimClassesPerRank = 64;
     // a rank's first claim takes this fraction of its fair share of the claimable volume
     // (FSM_CLAIM_FIRST); later claims half of the remaining volume's fair share, at least
-    // 1/8 of the fair share (guided self-scheduling: few claims, each an emit pass over the DB)
+    // 1/8 of the fair share (guided self-scheduling: few claims, each an emit pass over the DB).
+    // A value >= the rank count makes a first claim take every class (the regression test of
+    // a first claim that covers the whole class list)
     static double claim_first() {
         const char* v = std::getenv("FSM_CLAIM_FIRST");
-        return v ? std::clamp(std::atof(v), 0.01, 1.0) : 0.7;
+        return v ? std::clamp(std::atof(v), 0.01, 64.0) : 0.7;
     }
     // Claim the next range of first-level classes from the shared counter and append its
     // groups; false when every class is claimed.  Two atomics: a read of the counter to
@@ -4110,7 +4112,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     mn.minsup = none ? 0x7FFFFFFFu : (ms < 1.0 ? 1u : uint32_t(ms));
     size_t free_b = 0, total_b = 0;
     FSM_HIP(hipMemGetInfo(&free_b, &total_b));
-    mn.budget = ctx->opts.mem_budget > 0 ? uint64_t(ctx->opts.mem_budget) : uint64_t(free_b / 2);
+    mn.budget = ctx->opts.mem_budget > 0 ? uint64_t(ctx->opts.mem_budget) : uint64_t(free_b / 2) / uint64_t(ctx->dev_share);
     mn.pend = ctx->pinned_u64();
     mn.d_tests.alloc(8);
     FSM_HIP(hipMemsetAsync(mn.d_tests.p, 0, 8, ctx->stream));

@@ -1560,7 +1560,7 @@ void tsr_finish(fsm_ctx* ctx, TsrDevDB* d) {
     size_t free_b = 0, total_b = 0;
     FSM_HIP(hipMemGetInfo(&free_b, &total_b));
     const char* bm_env = std::getenv("FSM_TSR_BITMAP");
-    if (d->E && bm_bytes <= free_b / 4 && !(bm_env && bm_env[0] == '0')) {
+    if (d->E && bm_bytes <= free_b / (4 * uint64_t(ctx->dev_share)) && !(bm_env && bm_env[0] == '0')) {
         d->bm.alloc(bm_bytes);
         FSM_HIP(hipMemsetAsync(d->bm.p, 0, bm_bytes, s));
         const unsigned g = unsigned(std::min<int64_t>((d->E + kBlock - 1) / kBlock, 8192));
@@ -1957,13 +1957,21 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         FSM_HIP(hipMemGetInfo(&fr, &tot));
         // lists for about the whole mine: the rows where a rule holds summed over the expansions
         // reach a few thousand per sequence (c4: 2.0 G entries)
-        acap = std::min<uint64_t>({fr / 4, uint64_t(64) << 30,
+        acap = std::min<uint64_t>({fr / (4 * uint64_t(ctx->dev_share)), uint64_t(64) << 30,
                                    std::max<uint64_t>(uint64_t(64) << 20, uint64_t(d->NW) * 32 * 4096 * sizeof(uint4))}) /
                sizeof(uint4);
         if (const char* v = std::getenv("FSM_TSR_ARENA_MB"))
             acap = (std::strtoull(v, nullptr, 10) << 20) / sizeof(uint4);
         if (acap) arena.alloc(acap * sizeof(uint4));
     }
+    // a child reads its parent's list while it lies within this many entries of the head:
+    // acap / 2 by default, which keeps every list a launch in flight reads clear of the
+    // later launches' writes; FSM_TSR_PLIST_WINDOW=<sixteenths of the ring> (tests: 15 makes
+    // the in-flight guard below fire, and its waits show in fsm_stats.tsr_ring_waits)
+    const uint64_t plist_window = [&] {
+        const char* v = std::getenv("FSM_TSR_PLIST_WINDOW");
+        return acap / 16 * uint64_t(v ? std::clamp(std::atoi(v), 1, 15) : 8);
+    }();
     // |sids(X u {c})| memo (bitmap path; FSM_TSR_DLMEMO=0 turns it off): zeroed once per mine
     DevBuf memo_buf;
     DlMemo memo{nullptr, 0u};
@@ -2325,7 +2333,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             sd.ko = kNoList;
             sd.xid = r->xid;  // (the memo key of its left extensions)
             sd.klo = use_bm ? std::min(h_kid_of[rx[r->nx - 1]], h_kid_of[ry[r->ny - 1]]) + 1u : 0u;
-            if (use_bm && plist && r->ploff != kNoList && r->ploff + acap / 2 >= ahead) {
+            if (use_bm && plist && r->ploff != kNoList && r->ploff + plist_window >= ahead) {
                 // the parent's kept rows (still in the ring) are the domain: only the added item is
                 // probed there
                 wave_off[k + 1] = wave_off[k] + std::clamp<uint64_t>((uint64_t(r->pn) + pl_spb - 1) / pl_spb, 1,
@@ -2367,8 +2375,13 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         if (plist && acap) {  // the slots' kept-row lists at the ring's head, each at most the rule's support
             uint64_t need = 0;
             for (uint32_t k = 0; k < nb; ++k) need += bp[k]->sup;
-            if (need && need <= acap / (4 * uint64_t(nsets))) {
-                if (ahead % acap + need > acap) ahead += acap - ahead % acap;  // (a list never wraps)
+            // (the head skips to the ring's start when a list would wrap)
+            const uint64_t at = ahead % acap + need > acap ? ahead + acap - ahead % acap : ahead;
+            // a launch never overwrites the parent lists its own slots read (x.amin): it keeps
+            // no lists then (only a parent window wider than the default can come this close)
+            const bool own_ok = x.amin == kNoList || x.amin + acap >= at + need;
+            if (need && need <= acap / (4 * uint64_t(nsets)) && own_ok) {
+                ahead = at;
                 // positions below ahead + need - acap are overwritten now: a set still in flight
                 // that reads or writes one of them is finished first (its results are taken in)
                 for (int xi = 0; xi < nsets; ++xi) {
@@ -2697,6 +2710,7 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
     }
     for (int xi = 0; xi < nsets; ++xi)  // speculation still in flight when the replay ended
         if (xs[xi].busy) finish(xs[xi]);
+    ctx->stats.tsr_ring_waits = ring_waits;
     if (ctx->opts.verbose)
         std::fprintf(stderr,
                      "[fsm tsr] expansions %lld in %lld launches (%lld rules expanded, %lld pushed back), %.0f ms waiting on the "

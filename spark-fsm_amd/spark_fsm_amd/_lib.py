@@ -129,7 +129,8 @@ class Stats(ctypes.Structure):
         "count_launches", "mask_words", "bytes_count_alg")] + [(n, ctypes.c_double) for n in (
         "ms_gpu_wait", "ms_output")] + [(n, ctypes.c_int64) for n in (
         "joins_root", "root_keys", "pair_tests", "root_entries", "k0_device", "exp_domain", "exp_entries",
-        "exp_bitmap_bytes", "rank_claims", "rank_root_owned", "rank_root_slab", "rank_units")]
+        "exp_bitmap_bytes", "rank_claims", "rank_root_owned", "rank_root_slab", "rank_units",
+        "db_parses", "db_replicas", "tsr_ring_waits")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

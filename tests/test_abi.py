@@ -38,10 +38,10 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_sizes():
     L = _lib.load()
-    assert L.fsm_abi_version() == 6
+    assert L.fsm_abi_version() == 7
     assert ctypes.sizeof(_lib.Opts) == 4 * 4 + 128 + 8 + 8 + 4 + 16 * 4 + 4  # (+4: tail padding)
     assert ctypes.sizeof(_lib.Patterns) == 9 * 8  # 8 x 8-byte fields + int32 padded
-    assert ctypes.sizeof(_lib.Stats) == 9 * 8 + 8 * 8 + 3 * 8 + 2 * 8 + 8 * 8 + 4 * 8
+    assert ctypes.sizeof(_lib.Stats) == 9 * 8 + 8 * 8 + 3 * 8 + 2 * 8 + 8 * 8 + 4 * 8 + 3 * 8
     assert ctypes.sizeof(_lib.KernelStat) == 40 + 4 * 8
     assert ctypes.sizeof(_lib.HostComm) == 4 * 8
     assert ctypes.sizeof(_lib.DbImage) == 8 + 4 * 8 + 6 * 8

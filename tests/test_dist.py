@@ -138,3 +138,30 @@ def test_inproc_rejects_bad_device_lists():
     o.ndevices, o.nranks = 2, 2
     ctx = ctypes.c_void_p()
     assert L.fsm_ctx_create(ctypes.byref(o), ctypes.byref(ctx)) == _lib.FSM_EINVAL
+
+
+@pytest.mark.parametrize("stall_s", ["1", "6"])
+def test_inproc_stalled_rank_returns_ecomm(monkeypatch, stall_s):
+    """A rank that stalls (FSM_INJECT_STALL: it sleeps before its first collective) never
+    leaves the call hanging: its peers' barriers wait FSM_COMM_TIMEOUT_S, abort the hub and
+    the call returns FSM_ECOMM, within the limit plus the group's 2 s grace even while the
+    stalled rank is still asleep (6 s: the group is then reported stalled and leaked, so the
+    JVM actor records FAILURE instead of staying at MINING_STARTED, TrainActor.scala:56-67).
+    A new group works afterwards."""
+    import time
+    from spark_fsm_amd import FsmError, _lib
+    from spark_fsm_amd import dist as fdist
+    monkeypatch.setenv("FSM_COMM_TIMEOUT_S", "0.5")
+    monkeypatch.setenv("FSM_INJECT_STALL", "2,selftest,%s" % stall_s)
+    t0 = time.monotonic()
+    with pytest.raises(FsmError) as ei:
+        fdist.selftest_inproc(4)
+    dt = time.monotonic() - t0
+    assert ei.value.code == _lib.FSM_ECOMM, ei.value.msg
+    assert dt < 4.5, dt
+    if stall_s == "6":
+        assert "did not return" in ei.value.msg and "2" in ei.value.msg
+    else:
+        assert "timed out" in ei.value.msg or "peer rank failed" in ei.value.msg
+    monkeypatch.delenv("FSM_INJECT_STALL")
+    fdist.selftest_inproc(4)

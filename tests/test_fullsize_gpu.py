@@ -199,8 +199,16 @@ def test_bench_two_ranks_dry_run(tmp_path):
 # devices[r] as threads of this process.  On the one-GPU box every rank is device 0.
 
 @pytest.mark.parametrize("name,devices,claims", [("c3", (0, 0), "auto"), ("c3", (0, 0, 0), "forced"),
-                                                 ("c5-bible", (0, 0), "forced"), ("c5-bible", (0, 0, 0), "auto")])
+                                                 ("c5-bible", (0, 0), "forced"), ("c5-bible", (0, 0, 0), "auto"),
+                                                 ("c3", (0,) * 4, "auto"), ("c3", (0,) * 8, "auto"),
+                                                 ("c3", (0,) * 8, "forced"), ("c5-bible", (0,) * 4, "auto"),
+                                                 ("c5-bible", (0,) * 8, "auto")])
 def test_spade_fullsize_inproc(name, devices, claims, monkeypatch):
+    """Config 3 (and BIBLE) at the rank counts config 3 names (2, 3, 4 and 8; here all on
+    device 0): the F2 slices weighted by pair work, the 4- and 8-way static largest-first
+    plan or the claims, the heavy-class split, to the full-size digests.  The ranks share
+    the device's default memory budget (fsm_ctx::dev_share), and the DB is parsed once:
+    rank 0 builds it, the others copy its resident arrays device to device."""
     import spark_fsm_amd as fsm
     if claims == "forced":
         monkeypatch.setenv("FSM_SPADE_CLAIMS", "1")
@@ -208,6 +216,8 @@ def test_spade_fullsize_inproc(name, devices, claims, monkeypatch):
     ds = dataset(*SPADE_CFG[name])
     with fsm.Engine(devices=list(devices)) as e:
         db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+        st = e.stats()
+        assert st["db_parses"] == 1 and st["db_replicas"] == len(devices) - 1
         try:
             for _ in range(2):  # the group is re-armed between calls (counters, hub)
                 csr, meta = e.spade_csr(db, exp["support"])
@@ -224,8 +234,12 @@ def test_spade_fullsize_inproc(name, devices, claims, monkeypatch):
             db.free()
 
 
-@pytest.mark.parametrize("devices,shard_min", [((0, 0), "0"), ((0, 0, 0), "0"), ((0, 0, 0), "default")])
+@pytest.mark.parametrize("devices,shard_min", [((0, 0), "0"), ((0, 0, 0), "0"), ((0, 0, 0), "default"),
+                                                ((0,) * 4, "0"), ((0,) * 8, "0"), ((0,) * 8, "default")])
 def test_tsr_c4_prefix_inproc(devices, shard_min, monkeypatch):
+    """The c4 20K prefix over 2-8 in-process ranks: the pair phase by sequence range and the
+    launches' rule slots split over the ranks (every launch with FSM_TSR_SHARD_MIN=0), to the
+    exact prefix digest; the DB is parsed once and replicated device to device."""
     import spark_fsm_amd as fsm
     from tools import gen
     if shard_min != "default":
@@ -234,6 +248,8 @@ def test_tsr_c4_prefix_inproc(devices, shard_min, monkeypatch):
     ds = gen.kosarak(D=990002, seed=1).head(exp["sequences"])
     with fsm.Engine(devices=list(devices)) as e:
         db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_TSR)
+        bst = e.stats()
+        assert bst["db_parses"] == 1 and bst["db_replicas"] == len(devices) - 1
         try:
             rules, meta = e.tsr(db, exp["k"], exp["minconf"])
         finally:
@@ -266,3 +282,58 @@ def test_inproc_failure_agreement():
             assert pattern_digest(*csr) == exp["digest"]
         finally:
             db.free()
+
+
+def test_inproc_stalled_rank_returns_ecomm(monkeypatch):
+    """A rank that stalls inside a mine (FSM_INJECT_STALL: rank 2 sleeps 8 s at the root
+    phase) does not hang the caller: its peers' barriers time out (FSM_COMM_TIMEOUT_S = 1 s),
+    the call returns FSM_ECOMM within the limit and the 2 s grace, later calls return
+    FSM_ECOMM while the rank is still asleep, and once it has returned the same context
+    mines correctly again (the JNI shim throws, TrainActor records FAILURE, :65-67)."""
+    import time
+    import spark_fsm_amd as fsm
+    exp = FULL["c1"]
+    ds = dataset(*SPADE_CFG["c1"])
+    with fsm.Engine(devices=[0, 0, 0]) as e:
+        db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+        try:
+            monkeypatch.setenv("FSM_COMM_TIMEOUT_S", "1")
+            monkeypatch.setenv("FSM_INJECT_STALL", "2,root,8")
+            t0 = time.monotonic()
+            with pytest.raises(fsm.FsmError) as ei:
+                e.spade_csr(db, exp["support"])
+            dt = time.monotonic() - t0
+            monkeypatch.delenv("FSM_INJECT_STALL")
+            assert ei.value.code == 5 and dt < 6.0, (dt, ei.value.msg)
+            with pytest.raises(fsm.FsmError) as ei2:  # the rank is still asleep
+                e.spade_csr(db, exp["support"])
+            assert ei2.value.code == 5
+            time.sleep(max(0.0, 9.0 - (time.monotonic() - t0)))
+            monkeypatch.setenv("FSM_COMM_TIMEOUT_S", "60")
+            csr, meta = e.spade_csr(db, exp["support"])
+            assert pattern_digest(*csr) == exp["digest"]
+        finally:
+            db.free()
+
+
+@pytest.mark.parametrize("first", ["64", "0.01"])
+def test_inproc_whole_list_first_claim(first, monkeypatch):
+    """Regression for the claiming root (a first claim that covered every first-level class
+    handed the root's children over whole, so the rank's next claim read another batch's
+    children: gpurun_out/inproc2.log of round 5): FSM_CLAIM_FIRST=64 makes one rank's first
+    claim take every class and the others claim nothing; 0.01 makes many small claims.  Both
+    give the full-size digest, twice per context."""
+    import spark_fsm_amd as fsm
+    monkeypatch.setenv("FSM_SPADE_CLAIMS", "1")
+    monkeypatch.setenv("FSM_CLAIM_FIRST", first)
+    for name in ("c2", "c5-bible"):
+        exp = FULL[name]
+        ds = dataset(*SPADE_CFG[name])
+        with fsm.Engine(devices=[0, 0]) as e:
+            db = e.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, fsm.MODE_SPADE)
+            try:
+                for _ in range(2):
+                    csr, meta = e.spade_csr(db, exp["support"])
+                    assert pattern_digest(*csr) == exp["digest"] and e.stats()["joins"] == exp["joins"]
+            finally:
+                db.free()

@@ -612,7 +612,7 @@ def test_sharded_tsr_failure_reaches_every_rank(tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("bitmap", ["1", "0", "passes", "domain-bitmap", "domain-list", "max-kids", "max-pos",
                                     "plist-off", "dlmemo-off", "dlmemo-tiny", "ring-wrap",
-                                    "ring-wrap-2sets"])
+                                    "ring-wrap-2sets", "ring-guard", "ring-guard-2sets"])
 def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
     """TSR expansions over sid bitmaps (default: each slot's domain from the
     whole-bitmap AND or, for a rare item, from its sid list probed in the other
@@ -645,9 +645,14 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
         monkeypatch.setenv("FSM_TSR_DLMEMO", "0")
     if bitmap == "dlmemo-tiny":
         monkeypatch.setenv("FSM_TSR_DLMEMO_LOG2", "4")
-    if bitmap.startswith("ring-wrap"):
+    # ring-guard: children read parent lists up to 15/16 of the ring behind the head, so launches
+    # in flight hold positions that later launches reach: the guard must finish them first
+    # (fsm_stats.tsr_ring_waits > 0) and the rules stay the oracle's
+    if bitmap.startswith("ring-"):
         monkeypatch.setenv("FSM_TSR_ARENA_MB", "1")
         monkeypatch.setenv("FSM_TSR_SETS", "2" if bitmap.endswith("2sets") else "4")
+    if bitmap.startswith("ring-guard"):
+        monkeypatch.setenv("FSM_TSR_PLIST_WINDOW", "15")
     ds = gen.kosarak(D=6000, seed=3)
     o = oracle.tsr(ds.records(), 300, 0.4)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)  # bitmaps are built at upload
@@ -657,6 +662,8 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
         db.free()
     rules.sort(key=lambda t: (-t[2], t[0], t[1]))
     assert rules == o["rules"] and meta["final_minsup"] == o["final_minsup"]
+    if bitmap.startswith("ring-guard"):
+        assert eng.stats()["tsr_ring_waits"] > 0
 
 
 @pytest.mark.parametrize("batch", ["1", "7", "128", "768"])
