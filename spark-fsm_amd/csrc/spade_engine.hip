@@ -86,6 +86,25 @@ struct SlabPtrs {
     uint32_t* lim = nullptr;  // emit target: set when a child run exceeds 65535 entries (pos fields)
 };
 
+// W = 1 slabs keep no lohi word: an entry's first / last eid are the lowest / highest bit
+// of its one mask word (ctz / clz), 20 B per entry instead of 24.  FSM_W1_LOHI=1 (a build
+// flag, tools/build_variant.sh) stores it as the wider slabs do, for A/B runs.
+#ifndef FSM_W1_LOHI
+#define FSM_W1_LOHI 0
+#endif
+template <int W> constexpr bool kLhDerived = W == 1 && !FSM_W1_LOHI;
+inline bool lh_derived(int W) { return W == 1 && !FSM_W1_LOHI; }
+__device__ __forceinline__ uint32_t lh_of_word(uint64_t m) {
+    return uint32_t(__builtin_ctzll(m)) | ((63u - uint32_t(__builtin_clzll(m))) << 16);
+}
+// the lohi word of slab entry e (W: the slab's mask words; 0 = runtime width)
+template <int W>
+__device__ __forceinline__ uint32_t slab_lh(const uint32_t* __restrict__ lohi, const uint64_t* __restrict__ mask,
+                                            size_t e) {
+    if constexpr (kLhDerived<W>) return lh_of_word(mask[e]);
+    else return lohi[e];
+}
+
 // ------------------------------------------------------------------ kernels
 
 // K1: F1 histogram = distinct-sid support per item (entries are distinct per
@@ -150,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void k_root_write(const uint32_t* __restric
             } else {
                 uint64_t m[W];
                 load_mask<W>(mask + size_t(e) * W, m);
-                o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+                if constexpr (!kLhDerived<W>) o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
                 store_mask<W>(o.mask + size_t(d) * W, m);
             }
         }
@@ -187,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
         if (mi - mlo >= mhi - mlo) continue;  // member rows of another rank (sharded root)
         my_tests += p & 0xFFFFu;
         const DClass c = cls[cid[e]];
-        const uint32_t lh_i = lohi[e], lo_i = lh_i & 0xFFFFu;
+        const uint32_t lh_i = slab_lh<W>(lohi, mask, e), lo_i = lh_i & 0xFFFFu;
         const uint32_t ti = mi & 1u, ri = mi >> 1;
         const uint32_t rb = e - (p >> 16), rl = p & 0xFFFFu;
         MaskV<W> mk;
@@ -197,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_count(uint32_t E, const uint32_t* __
             const uint32_t f = rb + q;
             const uint32_t mj = mem[f];
             const uint32_t tj = mj & 1u, rj = mj >> 1;
-            const uint32_t lh_f = lohi[f];
+            const uint32_t lh_f = slab_lh<W>(lohi, mask, f);
             if (tj == kSeq) {
                 // P x -> y  /  P->x -> y : bits of L(j) strictly after first bit of L(i)
                 if ((lh_f >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
@@ -259,7 +278,7 @@ __device__ __forceinline__ void class_joins(uint32_t ti, uint32_t ri, uint32_t l
     const uint32_t mw = mask_words<W>(wd);
     const uint32_t mj = mem[f];
     const uint32_t tj = mj & 1u, rj = mj >> 1;
-    const uint32_t lh_f = lohi[f];
+    const uint32_t lh_f = slab_lh<W>(lohi, mask, f);
     if (tj == kSeq) {
         if ((lh_f >> 16) > lo_i) key(rj << 1);
         if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * mw, wd, lh_f)) key(rj << 1 | 1u);
@@ -299,7 +318,7 @@ __global__ __launch_bounds__(1024) void k_cnt_keys(uint32_t E, uint32_t epb, con
             const uint64_t rbase = row_base(cls[cid[e]], mi);
             g = uint32_t(rbase >> kGroupShift);
             kb = uint32_t(rbase) & (kGroupCounters - 1u);
-            const uint32_t lh_i = lohi[e];
+            const uint32_t lh_i = slab_lh<W>(lohi, mask, e);
             lo_i = lh_i & 0xFFFFu;
             ti = mi & 1u;
             ri = mi >> 1;
@@ -391,7 +410,7 @@ __global__ __launch_bounds__(kBlock) void k_sparse_keys(uint32_t E, const uint32
             rb = e - (p >> 16);
             my_tests += rl;
             slot = cls[cid[e]].cbase + mi;
-            const uint32_t lh_i = lohi[e];
+            const uint32_t lh_i = slab_lh<W>(lohi, mask, e);
             lo_i = lh_i & 0xFFFFu;
             ti = mi & 1u;
             ri = mi >> 1;
@@ -544,7 +563,7 @@ __global__ __launch_bounds__(kF2Threads) void k_root_write_plan(const uint32_t* 
                 } else {
                     uint64_t m[W];
                     load_mask<W>(mask + size_t(e) * W, m);
-                    o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
+                    if constexpr (!kLhDerived<W>) o.lohi[d] = mask_lo<W>(m) | (mask_hi<W>(m) << 16);
                     store_mask<W>(o.mask + size_t(d) * W, m);
                 }
                 if ((rk << 1) - mlo < mhi - mlo) atomicAdd(&h[group_of(rk, pm)], 2 * len - 1 - p);
@@ -577,7 +596,8 @@ template <int W> __device__ __forceinline__ uint32_t lohi_of(const uint64_t* __r
     return mask_lo<W>(m) | (mask_hi<W>(m) << 16);
 }
 // entry accessors of a batch slab (kRoot = false) or of the DB-direct root (kRoot = true)
-template <int W, bool kRoot> struct Ent {
+// (WL: the slab's own mask width for its lohi words, W's when W > 0)
+template <int W, bool kRoot, int WL = W> struct Ent {
     static constexpr bool kRootEnt = kRoot;
     const uint32_t* __restrict__ cid;
     const uint32_t* __restrict__ mem;
@@ -589,7 +609,7 @@ template <int W, bool kRoot> struct Ent {
     }
     __device__ __forceinline__ uint32_t m(size_t e) const { return mem[e]; }  // (DB-direct root: the plan's member ids)
     __device__ __forceinline__ uint32_t lh(size_t e) const {
-        if constexpr (kRoot) return lohi_of<W>(mask, e); else return lohi[e];
+        if constexpr (kRoot) return lohi_of<W>(mask, e); else return slab_lh<WL>(lohi, mask, e);
     }
 };
 // member ids in the wrapped order of the DB-direct root (identity order for batch slabs,
@@ -680,7 +700,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) cur[g] = uint32_t(base[f2_region(g, b, nblk)]);
     for (uint32_t r = r0 + threadIdx.x; r <= r1; r += blockDim.x) srow[r - r0] = kRoot ? row_off32[r] : uint32_t(roff[r]);
     if (threadIdx.x == 0) blk_keys = 0;
-    const Ent<W == 0 ? 1 : W, kRoot> en_{nullptr, mem, lohi, mask, rr};
+    const Ent<W == 0 ? 1 : W, kRoot, W> en_{nullptr, mem, lohi, mask, rr};
     __syncthreads();
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     F2Ent* stage = stage_all + wave * 64;
@@ -697,7 +717,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
         if (W == 1 && nrl <= 64 && lane < nrl) {
             nme = mem[nrb + lane];
             nmk = mask[nrb + lane];
-            if constexpr (kRoot) nlh = uint32_t(__builtin_ctzll(nmk)) | ((63u - uint32_t(__builtin_clzll(nmk))) << 16);
+            if constexpr (kRoot || kLhDerived<W>) nlh = lh_of_word(nmk);
             else nlh = lohi[nrb + lane];
         }
     };
@@ -768,7 +788,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                 const uint32_t me = rfl(kRoot ? en_.m(rb + i) : mem[rb + i]);
                 if ((me & 1u) || !(me - mlo < mhi - mlo)) continue;
                 const uint32_t ri = me >> 1, g = group_of(ri, pm);
-                const uint32_t li = rfl(kRoot ? en_.lh(rb + i) : lohi[rb + i]) & 0xFFFFu;
+                const uint32_t li = rfl(en_.lh(rb + i)) & 0xFFFFu;
                 const uint32_t kb = (ri - g * per) * D;
                 MaskV<W> mi;  // entry i's mask, wave-uniform (by address when W == 0)
                 if constexpr (W == 0) {
@@ -789,7 +809,7 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_keys(const uint64_t* __restri
                         const uint32_t mq = kRoot ? en_.m(rb + q) : mem[rb + q];
                         rq = mq >> 1;
                         if (!(mq & 1u)) {
-                            t_ok = ((kRoot ? en_.lh(rb + q) : lohi[rb + q]) >> 16) > li;
+                            t_ok = (en_.lh(rb + q) >> 16) > li;
                             if (q > i) e_ok = mi.and_any(mask + size_t(rb + q) * mask_words<W>(wd), wd);
                         }
                     }
@@ -1489,7 +1509,7 @@ __device__ __forceinline__ void emit_write(const SlabPtrs& o, uint64_t cap, uint
     }
     o.cid[d] = cc;
     o.mem[d] = kidc;
-    o.lohi[d] = lo2 | (hi2 << 16);
+    if constexpr (!kLhDerived<W>) o.lohi[d] = lo2 | (hi2 << 16);
     o.pos[d] = (k << 16) | n;
     store_mask<W>(o.mask + d * W, m);
     }
@@ -1536,7 +1556,7 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, RootRef rr, co
     __shared__ unsigned long long b_base;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
-    const Ent<W == 0 ? 1 : W, kRoot> en{cid, mem, lohi, mask, rr};
+    const Ent<W == 0 ? 1 : W, kRoot, W> en{cid, mem, lohi, mask, rr};
     // segments: the whole batch [0, E), or (runs != nullptr) each listed run, one block per run
     const uint32_t nseg = runs ? *nruns : 1u;
     for (uint32_t sg = runs ? blockIdx.x : 0u; sg < nseg; sg += runs ? gridDim.x : nseg) {
@@ -1703,8 +1723,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                     mi = en.m(e);
                     if constexpr (W == 1) {
                         mk = mask[e];
-                        if constexpr (kRoot) lh = uint32_t(__builtin_ctzll(mk)) | ((63u - uint32_t(__builtin_clzll(mk))) << 16);
-                        else lh = lohi[e];
+                        lh = kRoot || kLhDerived<W> ? lh_of_word(mk) : lohi[e];
                     } else {
                         lh = en.lh(e);
                     }
@@ -1899,12 +1918,12 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
                     if (!(mi - mlo < mhi - mlo)) continue;
                     my_tests += rl;
                     const DClass c = cls[cid[ei]];
-                    const uint32_t lh_i = lohi[ei], lo_i = lh_i & 0xFFFFu, ti = mi & 1u, ri = mi >> 1;
+                    const uint32_t lh_i = slab_lh<W>(lohi, mask, ei), lo_i = lh_i & 0xFFFFu, ti = mi & 1u, ri = mi >> 1;
                     MaskV<W> mk;
                     mk.load(mask + size_t(ei) * W, uint32_t(W), lh_i);
                     uint32_t* rowc = cnt + c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
                     for (uint32_t f = e0; f < e0 + rl; ++f) {
-                        const uint32_t mj = mem[f], tj = mj & 1u, rj = mj >> 1, lh_f = lohi[f];
+                        const uint32_t mj = mem[f], tj = mj & 1u, rj = mj >> 1, lh_f = slab_lh<W>(lohi, mask, f);
                         if (tj == kSeq) {
                             if ((lh_f >> 16) > lo_i) atomicAdd(rowc + (rj << 1), 1u);
                             if (ti == kSeq && rj > ri && mk.and_any(mask + size_t(f) * W, uint32_t(W), lh_f))
@@ -1929,8 +1948,8 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
             uint64_t mk = 0, rowa = 0;
             if (in) {
                 mi = mem[e];
-                lh = lohi[e];
                 if constexpr (W == 1) mk = mask[e];
+                lh = kLhDerived<W> ? lh_of_word(mk) : lohi[e];
                 if (mi - mlo < mhi - mlo) {  // (sharded root: this rank's member rows only)
                     const DClass c = cls[cid[e]];
                     rowa = c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
@@ -2008,7 +2027,7 @@ struct Slab {
     void alloc(uint64_t n, int W) {
         cid.alloc(n * 4);
         mem.alloc(n * 4);
-        lohi.alloc(n * 4);
+        if (!lh_derived(W)) lohi.alloc(n * 4);
         pos.alloc(n * 4);
         mask.alloc(n * 8 * uint64_t(W));
         cap = n;
@@ -2270,7 +2289,9 @@ struct Miner {
     uint64_t pend_total = 0;
     bool pend_check = false;
 
-    uint64_t entry_bytes() const { return 16ull + 8ull * uint64_t(W); }  // cid, mem, lohi, pos, mask
+    uint64_t entry_bytes() const {  // cid, mem, lohi (not at W = 1), pos, mask
+        return (lh_derived(W) ? 12ull : 16ull) + 8ull * uint64_t(W);
+    }
     // one (sid u32, eid mask) id-list entry, 4 + 8 ceil(E/64) bytes (12 B at W = 1)
     uint64_t survey_entry_bytes() const { return 4ull + 8ull * uint64_t(W); }
 
@@ -2556,10 +2577,13 @@ struct Miner {
         std::vector<uint64_t> mk(n * uint64_t(W));
         FSM_HIP(hipMemcpyAsync(cid.data(), b.slab.cid.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(mem.data(), b.slab.mem.p, n * 4, hipMemcpyDeviceToHost, s));
-        FSM_HIP(hipMemcpyAsync(lohi.data(), b.slab.lohi.p, n * 4, hipMemcpyDeviceToHost, s));
+        if (b.slab.lohi.p) FSM_HIP(hipMemcpyAsync(lohi.data(), b.slab.lohi.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(pos.data(), b.slab.pos.p, n * 4, hipMemcpyDeviceToHost, s));
         FSM_HIP(hipMemcpyAsync(mk.data(), b.slab.mask.p, n * 8 * W, hipMemcpyDeviceToHost, s));
         sync();
+        if (!b.slab.lohi.p)  // (W = 1: derived from the mask)
+            for (uint64_t e = 0; e < n; ++e)
+                lohi[e] = mk[e] ? uint32_t(__builtin_ctzll(mk[e])) | ((63u - uint32_t(__builtin_clzll(mk[e]))) << 16) : 0u;
         std::fprintf(stderr, "[dump] depth=%lld classes=%zu\n", (long long)b.depth, b.cls.size());
         for (uint64_t e = 0; e < n; ++e) {
             std::fprintf(stderr, "    e=%llu cls=%u mem=%u lo=%u hi=%u off=%u len=%u mask=", (unsigned long long)e,
