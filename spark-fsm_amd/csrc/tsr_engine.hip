@@ -1960,17 +1960,18 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
         acap = std::min<uint64_t>({fr / (4 * uint64_t(ctx->dev_share)), uint64_t(64) << 30,
                                    std::max<uint64_t>(uint64_t(64) << 20, uint64_t(d->NW) * 32 * 4096 * sizeof(uint4))}) /
                sizeof(uint4);
-        if (const char* v = std::getenv("FSM_TSR_ARENA_MB"))
-            acap = (std::strtoull(v, nullptr, 10) << 20) / sizeof(uint4);
+        if (const char* v = std::getenv("FSM_TSR_ARENA_MB"))  // (fractions of a MiB: tests)
+            acap = uint64_t(std::strtod(v, nullptr) * double(1u << 20)) / sizeof(uint4);
         if (acap) arena.alloc(acap * sizeof(uint4));
     }
-    // a child reads its parent's list while it lies within this many entries of the head:
-    // acap / 2 by default, which keeps every list a launch in flight reads clear of the
-    // later launches' writes; FSM_TSR_PLIST_WINDOW=<sixteenths of the ring> (tests: 15 makes
-    // the in-flight guard below fire, and its waits show in fsm_stats.tsr_ring_waits)
+    // a child reads its parent's list while it lies within this many entries of the head
+    // (16/16: while no later write has reached it yet): acap / 2 by default, which keeps every
+    // list a launch in flight reads clear of the later launches' writes;
+    // FSM_TSR_PLIST_WINDOW=<sixteenths of the ring> (tests: 16 makes the in-flight guard below
+    // fire, its waits counted in fsm_stats.tsr_ring_waits)
     const uint64_t plist_window = [&] {
         const char* v = std::getenv("FSM_TSR_PLIST_WINDOW");
-        return acap / 16 * uint64_t(v ? std::clamp(std::atoi(v), 1, 15) : 8);
+        return acap / 16 * uint64_t(v ? std::clamp(std::atoi(v), 1, 16) : 8);
     }();
     // |sids(X u {c})| memo (bitmap path; FSM_TSR_DLMEMO=0 turns it off): zeroed once per mine
     DevBuf memo_buf;

@@ -645,14 +645,15 @@ def test_tsr_expansion_domains_agree(eng, bitmap, monkeypatch):
         monkeypatch.setenv("FSM_TSR_DLMEMO", "0")
     if bitmap == "dlmemo-tiny":
         monkeypatch.setenv("FSM_TSR_DLMEMO_LOG2", "4")
-    # ring-guard: children read parent lists up to 15/16 of the ring behind the head, so launches
-    # in flight hold positions that later launches reach: the guard must finish them first
-    # (fsm_stats.tsr_ring_waits > 0) and the rules stay the oracle's
+    # ring-guard: children read parent lists anywhere in the ring not yet overwritten (window
+    # 16/16 instead of the default half), so a launch in flight can hold a position that a later
+    # launch is about to overwrite: the guard must finish it first (fsm_stats.tsr_ring_waits > 0;
+    # these two settings were found to fire it, tools/ring_probe.py) and the rules stay the oracle's
     if bitmap.startswith("ring-"):
-        monkeypatch.setenv("FSM_TSR_ARENA_MB", "1")
+        monkeypatch.setenv("FSM_TSR_ARENA_MB", "0.25" if bitmap == "ring-guard-2sets" else "1")
         monkeypatch.setenv("FSM_TSR_SETS", "2" if bitmap.endswith("2sets") else "4")
     if bitmap.startswith("ring-guard"):
-        monkeypatch.setenv("FSM_TSR_PLIST_WINDOW", "15")
+        monkeypatch.setenv("FSM_TSR_PLIST_WINDOW", "16")
     ds = gen.kosarak(D=6000, seed=3)
     o = oracle.tsr(ds.records(), 300, 0.4)
     db = eng.db_from_tokens(ds.sids, ds.seq_off, ds.tokens, MODE_TSR)  # bitmaps are built at upload
