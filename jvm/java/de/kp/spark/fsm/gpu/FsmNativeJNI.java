@@ -18,4 +18,8 @@ public final class FsmNativeJNI {
     /** [support int[], confidence double[], anteOff long[], ante int[], consOff long[], cons int[],
      *  {total, finalMinsup} long[]] */
     public static native Object[] tsr(int[] sids, String[] lines, int k, double minconf, int[] devices);
+
+    /** Destroys the contexts kept idle between requests (fsm_jni.c keeps up to 4, keyed by device
+     *  list, so a request does not rebuild its rank group); FsmNative registers it at JVM shutdown. */
+    public static native void release();
 }

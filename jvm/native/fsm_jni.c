@@ -15,6 +15,7 @@
  * it through an in-process JNIEnv (tests/jni_harness.c).
  */
 #include <jni.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -30,9 +31,10 @@ static void throw_exception(JNIEnv* env, const char* what, int rc, const char* d
 
 /* Collects the RDD's (sid, line) records the Scala side passes as arrays and
  * builds the flattened DB (parse + flatten + upload once).  NULL after a throw. */
-static fsm_db* make_db(JNIEnv* env, fsm_ctx* ctx, int32_t mode, jintArray jsids, jobjectArray jlines) {
+static fsm_db* make_db(JNIEnv* env, fsm_ctx* ctx, int32_t mode, jintArray jsids, jobjectArray jlines, int* rc_out) {
     const jsize n = (*env)->GetArrayLength(env, jsids);
     if ((*env)->GetArrayLength(env, jlines) != n) {
+        *rc_out = FSM_EINVAL;
         throw_exception(env, "fsm_db_from_spmf", FSM_EINVAL, "sids and lines differ in length");
         return NULL;
     }
@@ -45,6 +47,7 @@ static fsm_db* make_db(JNIEnv* env, fsm_ctx* ctx, int32_t mode, jintArray jsids,
         free(lines);
         free(lens);
         free(refs);
+        *rc_out = FSM_ENOMEM;
         throw_exception(env, "fsm_db_from_spmf", FSM_ENOMEM, "host allocation failed");
         return NULL;
     }
@@ -66,6 +69,7 @@ static fsm_db* make_db(JNIEnv* env, fsm_ctx* ctx, int32_t mode, jintArray jsids,
     free(lines);
     free(lens);
     free(refs);
+    *rc_out = got != n ? FSM_EINVAL : rc;
     if (got != n) {
         throw_exception(env, "fsm_db_from_spmf", FSM_EINVAL, "a null line in the dataset");
         return NULL;
@@ -77,15 +81,34 @@ static fsm_db* make_db(JNIEnv* env, fsm_ctx* ctx, int32_t mode, jintArray jsids,
     return db;
 }
 
-/* devices: the HIP ordinals of the request's ranks (FsmNative.devices, -Dfsm.devices).
- * One entry: the single-GPU context on that device.  More: ONE context that shards
- * the mine over in-process ranks, rank r on devices[r] (fsm_opts.ndevices, DESIGN.md
- * §6): the Spark driver thread (SPADE.scala:132-133, TSR.scala:102-103) makes one
- * call and gets the whole result back. */
-static fsm_ctx* make_ctx(JNIEnv* env, jintArray jdevices) {
-    fsm_opts o;
-    memset(&o, 0, sizeof o);
-    o.nranks = 1;
+/* The request's device list (FsmNative.devices, -Dfsm.devices).  One entry: the single-GPU
+ * context on that device.  More: ONE context that shards the mine over in-process ranks,
+ * rank r on devices[r] (fsm_opts.ndevices): the Spark driver thread
+ * (SPADE.scala:132-133, TSR.scala:102-103) makes one call and gets the whole result back. */
+typedef struct {
+    int32_t nd;
+    int32_t dev[FSM_MAX_DEVICES];
+} dev_list;
+
+/* Idle contexts kept between requests, keyed by device list: a context (and, for a device
+ * list, its rank threads, HIP streams, pools and pinned staging) is made once, not per
+ * request (each actor is per request and stops afterwards, FSMMiner.scala:77-83, but the
+ * process stays).  Concurrent requests take distinct contexts.  A context whose call failed
+ * with FSM_ECOMM / FSM_EDEVICE / FSM_ENOMEM is destroyed, not kept. */
+#define CTX_POOL_MAX 4
+static struct {
+    fsm_ctx* ctx;
+    dev_list dl;
+} g_idle[CTX_POOL_MAX];
+static int g_nidle;
+static pthread_mutex_t g_idle_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static int same_devices(const dev_list* a, const dev_list* b) {
+    return a->nd == b->nd && memcmp(a->dev, b->dev, sizeof(int32_t) * (size_t)a->nd) == 0;
+}
+
+static fsm_ctx* make_ctx(JNIEnv* env, jintArray jdevices, dev_list* dl) {
+    memset(dl, 0, sizeof *dl);
     const jsize nd = jdevices ? (*env)->GetArrayLength(env, jdevices) : 0;
     if (nd > FSM_MAX_DEVICES) {
         throw_exception(env, "fsm_ctx_create", FSM_EINVAL, "more devices than FSM_MAX_DEVICES");
@@ -97,12 +120,26 @@ static fsm_ctx* make_ctx(JNIEnv* env, jintArray jdevices) {
             throw_exception(env, "fsm_ctx_create", FSM_ENOMEM, "device list unavailable");
             return NULL;
         }
-        o.device = dv[0];
-        if (nd > 1) {
-            o.ndevices = nd;
-            for (jsize r = 0; r < nd; ++r) o.devices[r] = dv[r];
-        }
+        dl->nd = nd;
+        for (jsize r = 0; r < nd; ++r) dl->dev[r] = dv[r];
         (*env)->ReleaseIntArrayElements(env, jdevices, dv, JNI_ABORT);
+    }
+    pthread_mutex_lock(&g_idle_mu);
+    for (int i = 0; i < g_nidle; ++i)
+        if (same_devices(&g_idle[i].dl, dl)) {
+            fsm_ctx* ctx = g_idle[i].ctx;
+            g_idle[i] = g_idle[--g_nidle];
+            pthread_mutex_unlock(&g_idle_mu);
+            return ctx;
+        }
+    pthread_mutex_unlock(&g_idle_mu);
+    fsm_opts o;
+    memset(&o, 0, sizeof o);
+    o.nranks = 1;
+    if (dl->nd > 0) o.device = dl->dev[0];
+    if (dl->nd > 1) {
+        o.ndevices = dl->nd;
+        for (int32_t r = 0; r < dl->nd; ++r) o.devices[r] = dl->dev[r];
     }
     fsm_ctx* ctx = NULL;
     const int rc = fsm_ctx_create(&o, &ctx);
@@ -113,6 +150,35 @@ static fsm_ctx* make_ctx(JNIEnv* env, jintArray jdevices) {
     return ctx;
 }
 
+/* back to the idle list after a request (rc: the request's last libfsm status) */
+static void release_ctx(fsm_ctx* ctx, const dev_list* dl, int rc) {
+    if (!ctx) return;
+    if (rc == FSM_OK || rc == FSM_EINVAL || rc == FSM_EPARSE || rc == FSM_ELIMIT) {
+        pthread_mutex_lock(&g_idle_mu);
+        if (g_nidle < CTX_POOL_MAX) {
+            g_idle[g_nidle].ctx = ctx;
+            g_idle[g_nidle].dl = *dl;
+            ++g_nidle;
+            ctx = NULL;
+        }
+        pthread_mutex_unlock(&g_idle_mu);
+    }
+    if (ctx) fsm_ctx_destroy(ctx);
+}
+
+/* FsmNativeJNI.release(): destroy the idle contexts (the Scala side calls it at shutdown) */
+JNIEXPORT void JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_release(JNIEnv* env, jclass cls) {
+    (void)env;
+    (void)cls;
+    pthread_mutex_lock(&g_idle_mu);
+    const int n = g_nidle;
+    fsm_ctx* keep[CTX_POOL_MAX];
+    for (int i = 0; i < n; ++i) keep[i] = g_idle[i].ctx;
+    g_nidle = 0;
+    pthread_mutex_unlock(&g_idle_mu);
+    for (int i = 0; i < n; ++i) fsm_ctx_destroy(keep[i]);
+}
+
 /* de.kp.spark.fsm.gpu.FsmNativeJNI.spade(int[] sids, String[] lines, double support, boolean dfs,
  *                                        int[] devices): Object[] =
  *   [support: Array[Int], patOff: Array[Long], setOff: Array[Long], items: Array[Int], total+minsup: Array[Long]] */
@@ -120,15 +186,17 @@ JNIEXPORT jobjectArray JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(JNIEn
                                                                        jobjectArray jlines, jdouble support,
                                                                        jboolean dfs, jintArray jdevices) {
     (void)cls;
-    fsm_ctx* ctx = make_ctx(env, jdevices);
+    dev_list dl;
+    fsm_ctx* ctx = make_ctx(env, jdevices, &dl);
     if (!ctx) return NULL;
     jobjectArray res = NULL;
-    fsm_db* db = make_db(env, ctx, FSM_MODE_SPADE, jsids, jlines);
+    int rc = FSM_OK;
+    fsm_db* db = make_db(env, ctx, FSM_MODE_SPADE, jsids, jlines, &rc);
     fsm_patterns* p = NULL;
     if (db) {
         /* dfs as SpadeAlgorithm(support, dfs) takes it (SPADE.scala:132); SPADEActor passes the
          * default true (SPADE.scala:36, SPADEActor.scala:47) */
-        const int rc = fsm_spade_mine(ctx, db, support, dfs ? 1 : 0, &p);
+        rc = fsm_spade_mine(ctx, db, support, dfs ? 1 : 0, &p);
         if (rc != FSM_OK) throw_exception(env, "fsm_spade_mine", rc, fsm_last_error(ctx));
     }
     if (p) {
@@ -156,7 +224,7 @@ JNIEXPORT jobjectArray JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade(JNIEn
         fsm_patterns_free(p);
     }
     fsm_db_free(db);
-    fsm_ctx_destroy(ctx);
+    release_ctx(ctx, &dl, rc);
     return res;
 }
 
@@ -167,13 +235,15 @@ JNIEXPORT jobjectArray JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr(JNIEnv*
                                                                      jobjectArray jlines, jint k, jdouble minconf,
                                                                      jintArray jdevices) {
     (void)cls;
-    fsm_ctx* ctx = make_ctx(env, jdevices);
+    dev_list dl;
+    fsm_ctx* ctx = make_ctx(env, jdevices, &dl);
     if (!ctx) return NULL;
     jobjectArray res = NULL;
-    fsm_db* db = make_db(env, ctx, FSM_MODE_TSR, jsids, jlines);
+    int rc = FSM_OK;
+    fsm_db* db = make_db(env, ctx, FSM_MODE_TSR, jsids, jlines, &rc);
     fsm_rules* r = NULL;
     if (db) {
-        const int rc = fsm_tsr_mine(ctx, db, k, minconf, &r);
+        rc = fsm_tsr_mine(ctx, db, k, minconf, &r);
         if (rc != FSM_OK) throw_exception(env, "fsm_tsr_mine", rc, fsm_last_error(ctx));
     }
     if (r) {
@@ -204,6 +274,6 @@ JNIEXPORT jobjectArray JNICALL Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr(JNIEnv*
         fsm_rules_free(r);
     }
     fsm_db_free(db);
-    fsm_ctx_destroy(ctx);
+    release_ctx(ctx, &dl, rc);
     return res;
 }

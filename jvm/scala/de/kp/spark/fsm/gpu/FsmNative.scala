@@ -22,7 +22,12 @@ object FsmNative {
   /** System.loadLibrary("fsm_jni") once; a failure is kept and rethrown as Exception on every call. */
   private def ensureLoaded(): Unit = synchronized {
     if (loaded == null) {
-      loaded = try { System.loadLibrary("fsm_jni"); None } catch { case t: Throwable => Some(t) }
+      loaded = try {
+        System.loadLibrary("fsm_jni")
+        // the idle contexts the shim keeps between requests go with the JVM
+        Runtime.getRuntime.addShutdownHook(new Thread(new Runnable { def run(): Unit = FsmNativeJNI.release() }))
+        None
+      } catch { case t: Throwable => Some(t) }
     }
     loaded match {
       case Some(t) => throw new Exception("libfsm_jni could not be loaded: " + t.getMessage, t)

@@ -66,8 +66,10 @@ def test_shim_exports_the_bound_symbols(harness):
     out = subprocess.run(["nm", "-D", "--defined-only", harness.path], capture_output=True, text=True).stdout
     assert "Java_de_kp_spark_fsm_gpu_FsmNativeJNI_spade" in out
     assert "Java_de_kp_spark_fsm_gpu_FsmNativeJNI_tsr" in out
+    assert "Java_de_kp_spark_fsm_gpu_FsmNativeJNI_release" in out
     java = open(os.path.join(ROOT, "jvm", "java", "de", "kp", "spark", "fsm", "gpu", "FsmNativeJNI.java")).read()
     assert "static native Object[] spade(" in java and "static native Object[] tsr(" in java
+    assert "static native void release()" in java
 
 
 @pytest.mark.skipif(gpu_present(), reason="the no-device failure path needs a machine without a GPU")
@@ -109,6 +111,9 @@ def test_shim_spade_matches_golden(harness, devices):
     err = json.load(open(os.path.join(GOLD, "error_cases.json")))["spade"][0]
     assert call(harness, "harness_spade", [tuple(r) for r in err["records"]], 0.5, devices=devices).startswith(
         "EXCEPTION java/lang/Exception: libfsm fsm_db_from_spmf failed (FSM error 2)")
+    # every request above after the first reused the context (and rank group) the shim kept
+    # idle; FsmNative's shutdown hook destroys them
+    harness.Java_de_kp_spark_fsm_gpu_FsmNativeJNI_release(None, None)
 
 
 @pytest.mark.gpu
@@ -127,3 +132,4 @@ def test_shim_tsr_matches_golden(harness, devices):
     for err in json.load(open(os.path.join(GOLD, "error_cases.json")))["tsr"]:
         out = call(harness, "harness_tsr", [tuple(r) for r in err["records"]], 3, 0.5, devices=devices)
         assert out.startswith("EXCEPTION java/lang/Exception: libfsm ") and "(FSM error 2)" in out, err["name"]
+    harness.Java_de_kp_spark_fsm_gpu_FsmNativeJNI_release(None, None)
