@@ -250,6 +250,7 @@ size_t KernelClock::begin(const char* name) {
     for (size_t k = 0; k < recs.size(); ++k)
         if (recs[k].name == name) idx = k;
     if (idx == recs.size()) recs.push_back(Rec{name, {}, 0, 0});
+    if (!on) return idx;
     hipEvent_t a, b;
     FSM_HIP(hipEventCreate(&a));
     if (hipEventCreate(&b) != hipSuccess) {
@@ -262,7 +263,7 @@ size_t KernelClock::begin(const char* name) {
 }
 
 void KernelClock::end(size_t idx, int64_t alg_bytes, int64_t survey_bytes) {
-    FSM_HIP(hipEventRecord(recs[idx].ev.back().second, s));
+    if (on) FSM_HIP(hipEventRecord(recs[idx].ev.back().second, s));
     recs[idx].bytes += alg_bytes;
     recs[idx].survey += survey_bytes;
 }

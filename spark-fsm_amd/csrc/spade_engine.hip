@@ -2247,7 +2247,21 @@ struct Miner {
     uint64_t budget;
     ChunkedVec<PNode> nodes;
     KernelClock* clk = nullptr;
-    DevBuf d_tests;  // u64: (entry, partner) join tests of the class count kernels
+    // Per-mine zeroed device counters (slab cursors, record counts, the join-test total): ONE
+    // memset when the mine starts instead of a fill launch per counter; zslot(n) hands out
+    // 16-byte aligned slots, nullptr once the block is used up (the caller then allocates and
+    // zeroes its own)
+    DevBuf zblk;
+    uint32_t zused = 0;
+    static constexpr uint32_t kZBytes = 64u << 10;
+    void* zslot(size_t bytes) {
+        const uint32_t n = uint32_t((bytes + 15) & ~size_t(15));
+        if (!zblk.p || zused + n > kZBytes) return nullptr;
+        void* p = zblk.as<char>() + zused;
+        zused += n;
+        return p;
+    }
+    unsigned long long* d_tests = nullptr;  // u64 (a zslot): (entry, partner) join tests of the class count kernels
     // sharded mining (nranks > 1): this rank counts the root rows of ranks
     // [slice_lo, slice_hi) and mines the first-level classes shard_plan gives it
     Comm* comm = nullptr;
@@ -2467,7 +2481,7 @@ struct Miner {
 #define FSM_CK(WW)                                                                                                   \
     hipLaunchKernelGGL(k_cnt_keys<WW>, dim3(nblk), dim3(kF2Threads), size_t(G) * 4, s, E, epb, sp.cid,                \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, mlo, mhi, G, nblk, base.as<uint64_t>(), \
-                       fill.as<uint32_t>(), keys.as<uint16_t>(), d_tests.as<unsigned long long>(), uint32_t(W))
+                       fill.as<uint32_t>(), keys.as<uint16_t>(), d_tests, uint32_t(W))
         FSM_W_DISPATCH(W, FSM_CK)
 #undef FSM_CK
         FSM_LAUNCHED("k_cnt_keys", s);
@@ -2516,7 +2530,7 @@ struct Miner {
 #define FSM_SK(WW)                                                                                                  \
     hipLaunchKernelGGL(k_sparse_keys<WW>, dim3(grid), dim3(kBlock), 0, s, E, sp.cid, b.d_cls.as<DClass>(), sp.mem,   \
                        sp.lohi, sp.pos, sp.mask, mlo, mhi, uint32_t(W), keys.as<unsigned long long>(),              \
-                       cur.as<unsigned long long>(), d_tests.as<unsigned long long>())
+                       cur.as<unsigned long long>(), d_tests)
         FSM_W_DISPATCH(W, FSM_SK)
 #undef FSM_SK
         FSM_LAUNCHED("k_sparse_keys", s);
@@ -2758,13 +2772,20 @@ struct Miner {
 
         if (nslots >= (uint64_t(1) << 32) - 4096) return false;  // region cursors are u32
         // the one enumeration (keys padded: k_f2_count reads whole 16-byte words past a region's end)
-        DevBuf keys((nslots + 1024) * 2), nk(8);
-        FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
+        DevBuf keys((nslots + 1024) * 2), ctr_own;
+        // u64 key count | u32 frequent-record count, read back together
+        char* ctr = static_cast<char*>(zslot(16));
+        if (!ctr) {
+            ctr_own.alloc(16);
+            FSM_HIP(hipMemsetAsync(ctr_own.p, 0, 16, s));
+            ctr = ctr_own.as<char>();
+        }
+        unsigned long long* nk = reinterpret_cast<unsigned long long*>(ctr);
+        uint32_t* d_nrec = reinterpret_cast<uint32_t*>(ctr + 8);
         const size_t kshm = size_t(kF2Waves) * 64 * (sizeof(F2Ent) + sizeof(F2Act)) + size_t(kF2RowWords) * 4 + size_t(G) * 4;
         // count + frequent pairs of this rank's slice
         const uint32_t g0 = rlo / per, g1 = rhi == 0 ? 0u : (rhi - 1) / per + 1;
         uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * D, uint64_t(1) << 20));
-        DevBuf d_nrec(4);
         DevBuf d_recs;
         unsigned long long nkeys = 0;
         size_t tk_cnt = 0, tk_keys = 0;
@@ -2772,8 +2793,7 @@ struct Miner {
         // keys on-die, measured slower in round 4: each pass enumerates the rows again)
         for (int attempt = 0;; ++attempt) {
             d_recs.alloc(std::max<uint32_t>(cap_recs, 1) * sizeof(FreqRec));
-            FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
-            if (attempt == 0) FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
+            if (attempt > 0) FSM_HIP(hipMemsetAsync(d_nrec, 0, 4, s));
             {
                 const uint32_t pg0 = g0, pg1 = g1, prlo = rlo, prhi = rhi;
                 if (attempt == 0) {  // a retry (record overflow) counts from the keys already written
@@ -2783,13 +2803,13 @@ struct Miner {
     hipLaunchKernelGGL((k_f2_keys<WW, false>), dim3(nblk), dim3(kF2Threads), kshm, s, b.root_rows.as<uint64_t>(),      \
                        (const uint32_t*)nullptr, RootRef{nullptr, nullptr}, R, rpb, sp.mem, sp.lohi, sp.mask, D, per,  \
                        pm, G, nblk, pmlo, pmhi, base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(),        \
-                       nk.as<unsigned long long>(), uint32_t(W))
+                       nk, uint32_t(W))
 #define FSM_F2KD(WW)                                                                                                  \
     hipLaunchKernelGGL((k_f2_keys<WW, true>), dim3(nblk), dim3(kF2Threads), kshm, s, (const uint64_t*)nullptr,         \
                        db->row_off.as<uint32_t>(), RootRef{db->item.as<uint32_t>(), b.rk2.as<uint32_t>()}, R, rpb,     \
                        b.mem_db.as<uint32_t>(), (const uint32_t*)nullptr, db->mask.as<uint64_t>(), D, per, pm, G,      \
                        nblk, pmlo, pmhi, base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(),               \
-                       nk.as<unsigned long long>(), uint32_t(WW))
+                       nk, uint32_t(WW))
                     if (b.db_direct) {
                         switch (W) {
                             case 1: FSM_F2KD(1); break;
@@ -2813,14 +2833,15 @@ struct Miner {
                 if (pg1 > pg0)
                     hipLaunchKernelGGL(k_f2_count<false>, dim3(pg1 - pg0), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
                                        fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), D, per, pg0, prlo, prhi, minsup,
-                                       d_recs.as<FreqRec>(), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u);
+                                       d_recs.as<FreqRec>(), cap_recs, d_nrec, (uint32_t*)nullptr, 1u);
                 FSM_LAUNCHED("k_f2_count", s);
                 clk->end(tk_cnt, int64_t(pg1 - pg0) * nblk * 12);
             }
-            uint32_t nrec = 0;
-            FSM_HIP(hipMemcpyAsync(&nrec, d_nrec.p, 4, hipMemcpyDeviceToHost, s));
-            FSM_HIP(hipMemcpyAsync(&nkeys, nk.p, 8, hipMemcpyDeviceToHost, s));
+            pend[2] = pend[3] = 0;
+            FSM_HIP(hipMemcpyAsync(&pend[2], ctr, 16, hipMemcpyDeviceToHost, s));  // (one copy: both counts)
             sync();
+            nkeys = pend[2];
+            const uint32_t nrec = uint32_t(pend[3] & 0xFFFFFFFFu);
             if (nrec <= cap_recs || attempt > 0) {
                 if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
                 recs.resize(nrec);
@@ -2852,39 +2873,45 @@ struct Miner {
         DevBuf base = std::move(b.f2_base), fill(nd * 4);
         const uint64_t nslots = b.f2_nslots;
         if (nslots >= (uint64_t(1) << 32) - 4096) return false;
-        DevBuf keys((nslots + 1024) * 2), nk(8);
-        FSM_HIP(hipMemsetAsync(nk.p, 0, 8, s));
+        DevBuf keys((nslots + 1024) * 2), ctr_own;
+        // u64 key count | u32 frequent-record count, read back together
+        char* ctr = static_cast<char*>(zslot(16));
+        if (!ctr) {
+            ctr_own.alloc(16);
+            FSM_HIP(hipMemsetAsync(ctr_own.p, 0, 16, s));
+            ctr = ctr_own.as<char>();
+        }
+        unsigned long long* nk = reinterpret_cast<unsigned long long*>(ctr);
+        uint32_t* d_nrec = reinterpret_cast<uint32_t*>(ctr + 8);
         const uint32_t* gtab = b.f2_tri_tab.as<uint32_t>();
         const uint32_t* gr = gtab + F;
         const size_t kshm = size_t(kF2Waves) * 64 * 16 + size_t(kF2RowWords) * 4 + size_t(G) * 4;
         const size_t tk_keys = clk->begin("k_f2_keys");
         hipLaunchKernelGGL(k_f2_tri, dim3(nblk), dim3(kF2Threads), kshm, s, db->row_off.as<uint32_t>(),
                            b.mem_db.as<uint32_t>(), db->mask.as<uint64_t>(), R, rpb, gtab, G, nblk, geo.mlo, geo.mhi,
-                           base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(), nk.as<unsigned long long>());
+                           base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(), nk);
         FSM_LAUNCHED("k_f2_tri", s);
         clk->end(tk_keys, db->E * 12 + int64_t(nd) * 12, int64_t(b.cls[0].cap) * 8);
         // count + frequent pairs (a retry when the first record buffer was too small)
         // the records land in mapped pinned host memory, the counts in pinned slots: one sync
         uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * 2 * F, uint64_t(1) << 20));
-        DevBuf d_nrec(4);
         size_t tk_cnt = 0;
         unsigned long long nkeys = 0;
         for (int attempt = 0;; ++attempt) {
             PinnedBuf* pb = ctx->pinned_big(size_t(std::max<uint32_t>(cap_recs, 1)) * sizeof(FreqRec));
-            FSM_HIP(hipMemsetAsync(d_nrec.p, 0, 4, s));
+            if (attempt > 0) FSM_HIP(hipMemsetAsync(d_nrec, 0, 4, s));
             tk_cnt = clk->begin("k_f2_count");
             hipLaunchKernelGGL((k_f2_count<false, true>), dim3(G), dim3(kF2Threads), 0, s, base.as<uint64_t>(),
                                fill.as<uint32_t>(), nblk, keys.as<uint16_t>(), 2 * F, 0u, 0u, rlo, rhi, minsup,
-                               static_cast<FreqRec*>(pb->dev), cap_recs, d_nrec.as<uint32_t>(), (uint32_t*)nullptr, 1u,
+                               static_cast<FreqRec*>(pb->dev), cap_recs, d_nrec, (uint32_t*)nullptr, 1u,
                                gr, F);
             FSM_LAUNCHED("k_f2_count", s);
             clk->end(tk_cnt, int64_t(G) * nblk * 12);
             pend[2] = pend[3] = 0;
-            FSM_HIP(hipMemcpyAsync(&pend[2], d_nrec.p, 4, hipMemcpyDeviceToHost, s));
-            FSM_HIP(hipMemcpyAsync(&pend[3], nk.p, 8, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&pend[2], ctr, 16, hipMemcpyDeviceToHost, s));  // (one copy: both counts)
             sync();
-            const uint32_t nrec = uint32_t(pend[2]);
-            nkeys = pend[3];
+            nkeys = pend[2];
+            const uint32_t nrec = uint32_t(pend[3] & 0xFFFFFFFFu);
             if (nrec <= cap_recs || attempt > 0) {
                 if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
                 const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
@@ -3130,7 +3157,7 @@ struct Miner {
 #define FSM_COUNT(WW)                                                                                   \
     hipLaunchKernelGGL(k_count<WW>, dim3(unsigned((b.E + cchunk - 1) / cchunk)), dim3(kBlock), 0, s,   \
                        uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask,           \
-                       member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>(), d_tests.as<unsigned long long>(),    \
+                       member_lo(b), member_hi(b), cchunk, cnt.as<uint32_t>(), d_tests,    \
                        uint32_t(W))
                 const size_t tk = clk->begin("k_count");
                 if ((W == 1 || W == 2 || W == 4 || W == 8) && count_window()) {
@@ -3138,7 +3165,7 @@ struct Miner {
 #define FSM_COUNT2(WW)                                                                                  \
     hipLaunchKernelGGL(k_count2<WW>, dim3(g), dim3(kBlock), 0, s, uint32_t(b.E), sp.cid, b.d_cls.as<DClass>(), \
                        sp.mem, sp.lohi, sp.pos, sp.mask, member_lo(b), member_hi(b), cnt.as<uint32_t>(),      \
-                       d_tests.as<unsigned long long>())
+                       d_tests)
                     switch (W) {
                         case 1: FSM_COUNT2(1); break;
                         case 2: FSM_COUNT2(2); break;
@@ -3682,9 +3709,15 @@ struct Miner {
                 rr = RootRef{db->item.as<uint32_t>(), b.rk2.as<uint32_t>()};
             }
             SlabPtrs op = nb.slab.ptrs();
-            DevBuf cursor(16);  // u64 slab cursor | u32 long-run count (k_emit2) | u32 run-length flag
-            op.lim = reinterpret_cast<uint32_t*>(cursor.as<char>() + 12);
-            FSM_HIP(hipMemsetAsync(cursor.p, 0, 16, s));
+            // u64 slab cursor | u32 long-run count (k_emit2) | u32 run-length flag
+            DevBuf cursor_own;
+            char* cursor = static_cast<char*>(zslot(16));
+            if (!cursor) {
+                cursor_own.alloc(16);
+                FSM_HIP(hipMemsetAsync(cursor_own.p, 0, 16, s));
+                cursor = cursor_own.as<char>();
+            }
+            op.lim = reinterpret_cast<uint32_t*>(cursor + 12);
             const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
             const unsigned grid = unsigned(std::min<uint64_t>((Eg + chunk - 1) / chunk, emit_grid_cap()));
             const size_t tk = clk->begin("k_emit");
@@ -3697,13 +3730,13 @@ struct Miner {
 #define FSM_EMIT2(WW, RT)                                                                                       \
     hipLaunchKernelGGL((k_emit2<WW, RT>), dim3(g2), dim3(kE2Block), 0, s, uint32_t(Eg), rr, sp.cid,                  \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
-                       d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap, emit2_cap(),   \
-                       d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor.as<char>() + 8));               \
+                       d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op, nb.slab.cap, emit2_cap(),   \
+                       d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor + 8));               \
     FSM_LAUNCHED("k_emit2", s);                                                                                    \
     hipLaunchKernelGGL((k_emit1<WW, RT>), dim3(256), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,              \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
-                       d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op, nb.slab.cap, emit_cap(),    \
-                       uint32_t(WW), d_long.as<uint32_t>(), reinterpret_cast<const uint32_t*>(cursor.as<char>() + 8)); \
+                       d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op, nb.slab.cap, emit_cap(),    \
+                       uint32_t(WW), d_long.as<uint32_t>(), reinterpret_cast<const uint32_t*>(cursor + 8)); \
     FSM_LAUNCHED("k_emit1", s);
                 switch (W * 2 + (rootdb ? 1 : 0)) {
                     case 2: FSM_EMIT2(1, false) break;
@@ -3720,12 +3753,12 @@ struct Miner {
 #define FSM_EMIT1(WW)                                                                                               \
     hipLaunchKernelGGL((k_emit1<WW, false>), dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,                \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                   \
-                       b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
+                       b.kid_cid, d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op,  \
                        nb.slab.cap, emit_cap(), uint32_t(W), (const uint32_t*)nullptr, (const uint32_t*)nullptr)
 #define FSM_EMIT1R(WW)                                                                                              \
     hipLaunchKernelGGL((k_emit1<WW, true>), dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,                 \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                   \
-                       b.kid_cid, d_child_of.as<uint32_t>(), cursor.as<unsigned long long>(), op,  \
+                       b.kid_cid, d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op,  \
                        nb.slab.cap, emit_cap(), uint32_t(W), (const uint32_t*)nullptr, (const uint32_t*)nullptr)
                 if (rootdb) {
                     switch (W) {
@@ -3747,7 +3780,7 @@ struct Miner {
             clk->end(tk, int64_t(rd + total * entry_bytes()), int64_t((b.E + total) * survey_entry_bytes()));
             // the whole cursor block back in one copy: pend[6] = entries written, pend[7] = long
             // runs | run-length flag << 32
-            FSM_HIP(hipMemcpyAsync(&pend[6], cursor.p, 16, hipMemcpyDeviceToHost, s));
+            FSM_HIP(hipMemcpyAsync(&pend[6], cursor, 16, hipMemcpyDeviceToHost, s));
         } else {
             pend[6] = 0;
             pend[7] = 0;
@@ -4138,8 +4171,9 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     FSM_HIP(hipMemGetInfo(&free_b, &total_b));
     mn.budget = ctx->opts.mem_budget > 0 ? uint64_t(ctx->opts.mem_budget) : uint64_t(free_b / 2) / uint64_t(ctx->dev_share);
     mn.pend = ctx->pinned_u64();
-    mn.d_tests.alloc(8);
-    FSM_HIP(hipMemsetAsync(mn.d_tests.p, 0, 8, ctx->stream));
+    mn.zblk.alloc(Miner::kZBytes);
+    FSM_HIP(hipMemsetAsync(mn.zblk.p, 0, Miner::kZBytes, ctx->stream));
+    mn.d_tests = static_cast<unsigned long long*>(mn.zslot(8));
 
     // ---- F1 (K1)
     std::vector<uint32_t> f1(size_t(d->U), 0);
@@ -4256,7 +4290,7 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
     // sharded: a failure from here on is agreed on in the pattern gather (no round trip of its own)
     mn.run_or_defer([&] {
         unsigned long long tests = 0;
-        FSM_HIP(hipMemcpyAsync(&tests, mn.d_tests.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        FSM_HIP(hipMemcpyAsync(&tests, mn.d_tests, 8, hipMemcpyDeviceToHost, ctx->stream));
         mn.sync();
         ctx->stats.pair_tests = int64_t(tests);
     });
