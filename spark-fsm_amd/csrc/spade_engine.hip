@@ -1696,9 +1696,25 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
         // the windows of whole runs [e0, e0 + cut); pass 0 records, pass 1 (overflow) writes
         // at the bases in i_cc / i_n: on_ok(ok, f, q, owner slot, k)
         auto walk = [&](auto&& on_ok, bool keep) {
+            // the next window's entry words (pos, member, class, W = 1 mask) are loaded while the
+            // current window's pairs are joined: a window's dependent chain starts one load later
+            uint32_t np = 0, nmi = 0, ncid = 0;
+            uint64_t nmk = 0;
+            auto fetch = [&](uint32_t e0n) {
+                const uint32_t en_e = e0n + lane;
+                np = 0u;
+                if (en_e < E) {
+                    np = pos[en_e];
+                    nmi = en.m(en_e);
+                    if constexpr (W == 1) nmk = mask[en_e];
+                    if constexpr (!kRoot) ncid = cid[en_e];
+                }
+            };
+            if (ef < wz) fetch(ef);
             for (uint32_t e0 = ef; e0 < wz;) {
                 const uint32_t e = e0 + lane;
-                const uint32_t p = e < E ? pos[e] : 0u;
+                const uint32_t p = np, cmi = nmi, ccid = ncid;
+                const uint64_t cmk = nmk;
                 const uint32_t len = p & 0xFFFFu;
                 const bool st = e < E && (p >> 16) == 0u;
                 // a run starting at lane s is in this window iff it starts in [e0, wz) and fits
@@ -1708,6 +1724,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                 if (bad & 1ull) {  // lane 0 starts a run of more than 64 entries: k_emit1's list
                     if (keep && lane == 0) longl[atomicAdd(nlong, 1u)] = e0;
                     e0 += uint32_t(__shfl(int(len), 0, 64));
+                    if (e0 < wz) fetch(e0);
                     continue;
                 }
                 if (bad) {
@@ -1716,18 +1733,19 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                     const uint32_t ls = 63u - uint32_t(__clzll(sts));
                     cut = ls + uint32_t(__shfl(int(len), int(ls), 64));
                 }
+                if (e0 + cut < wz) fetch(e0 + cut);
                 const bool in = lane < cut;
                 uint32_t mi = 0, lh = 0, cc = kNone, k0 = 0, nk = 0, lt2 = 0;
                 uint64_t mk = 0;
                 if (in) {
-                    mi = en.m(e);
+                    mi = cmi;
                     if constexpr (W == 1) {
-                        mk = mask[e];
+                        mk = cmk;
                         lh = kRoot || kLhDerived<W> ? lh_of_word(mk) : lohi[e];
                     } else {
                         lh = en.lh(e);
                     }
-                    const DClass c = cls[en.c(e)];
+                    const DClass c = cls[kRoot ? 0u : ccid];
                     cc = kRoot && (mi & 1u) ? kNone : child_of[c.cbase + mi];  // (infrequent DB entry: no class)
                     if (cc != kNone) {
                         k0 = kid_off[c.cbase + mi];
@@ -1902,15 +1920,31 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
                 break;
             }
         }
+        // the next window's entry words are loaded while the current window's pairs are counted
+        uint32_t np = 0, nmi = 0, ncid = 0;
+        uint64_t nmk = 0;
+        auto fetch = [&](uint32_t e0n) {
+            const uint32_t en_e = e0n + lane;
+            np = 0u;
+            if (en_e < E) {
+                np = pos[en_e];
+                nmi = mem[en_e];
+                ncid = cid[en_e];
+                if constexpr (W == 1) nmk = mask[en_e];
+            }
+        };
+        if (e0 < wz) fetch(e0);
         while (e0 < wz) {
             const uint32_t e = e0 + lane;
-            const uint32_t p = e < E ? pos[e] : 0u;
+            const uint32_t p = np, cmi = nmi, ccid = ncid;
+            const uint64_t cmk = nmk;
             const uint32_t len = p & 0xFFFFu;
             const bool st = e < E && (p >> 16) == 0u;
             const uint64_t bad = ballot(st && (e >= wz || lane + len > 64u));
             const uint64_t sts = ballot(st);
             if (bad & 1ull) {  // lane 0 starts a run of more than 64 entries: thread per entry
                 const uint32_t rl = uint32_t(__shfl(int(len), 0, 64));
+                if (e0 + rl < wz) fetch(e0 + rl);
                 for (uint32_t i0 = e0; i0 < e0 + rl; i0 += 64) {
                     const uint32_t ei = i0 + lane;
                     if (ei >= e0 + rl) continue;
@@ -1943,22 +1977,23 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
                 const uint32_t ls = 63u - uint32_t(__clzll(sts));
                 cut = ls + uint32_t(__shfl(int(len), int(ls), 64));
             }
+            if (e0 + cut < wz) fetch(e0 + cut);
             const bool in = lane < cut;
-            uint32_t mi = 0, lh = 0, np = 0;
+            uint32_t mi = 0, lh = 0, npart = 0;
             uint64_t mk = 0, rowa = 0;
             if (in) {
-                mi = mem[e];
-                if constexpr (W == 1) mk = mask[e];
+                mi = cmi;
+                if constexpr (W == 1) mk = cmk;
                 lh = kLhDerived<W> ? lh_of_word(mk) : lohi[e];
                 if (mi - mlo < mhi - mlo) {  // (sharded root: this rank's member rows only)
-                    const DClass c = cls[cid[e]];
+                    const DClass c = cls[ccid];
                     rowa = c.cnt_off + uint64_t(mi >> c.mshift) * c.rstride;
-                    np = len;  // partners: every entry of its run
+                    npart = len;  // partners: every entry of its run
                     my_tests += len;
                 }
             }
             const uint32_t rs = lane - (p >> 16);  // first lane of the lane's run
-            const uint32_t incl = wave_incl_scan(np), excl = incl - np;
+            const uint32_t incl = wave_incl_scan(npart), excl = incl - npart;
             const uint32_t total = uint32_t(__shfl(int(incl), 63, 64));
             for (uint32_t p0 = 0; p0 < total; p0 += 64) {
                 const uint32_t pp = p0 + lane;
