@@ -2194,6 +2194,14 @@ void order_recs(std::vector<FreqRec>& recs, uint32_t nrows) {
 struct Batch {
     Slab slab;
     RawVec<ClassMeta> cls;
+    // unsharded batches whose children fit one emit group: the children (pattern nodes and
+    // the next batch's class tables) are built by emit() AFTER it has launched the emit
+    // kernels, from these records (valid until the next count_and_freq), so that host work
+    // overlaps the emit on the GPU instead of delaying its launch
+    bool defer_children = false;
+    const FreqRec* defer_R = nullptr;
+    uint64_t defer_n = 0, defer_total = 0;
+    const RawVec<DRow>* defer_rows = nullptr;
     DevBuf d_cls;
     DevBuf kid_tab;  // frequent children of every member (CSR over cbase + mi): offsets | slots | child ids
     const uint32_t* kid_off = nullptr;
@@ -2240,6 +2248,10 @@ struct Batch {
     void recycle() {
         slab = Slab{};
         cls.clear();
+        defer_children = false;
+        defer_R = nullptr;
+        defer_rows = nullptr;
+        defer_n = defer_total = 0;
         d_cls.release();
         kid_tab.release();
         child_pre.release();
@@ -3377,58 +3389,12 @@ struct Miner {
         }
         hp[1] += now_ms() - th;
         th = now_ms();
-        // children (new pattern nodes) in deterministic (row, slot) order
-        b.children.clear();
-        b.child_rank_item.clear();
-        b.child_node_of.clear();
-        b.children.reserve(nfreq);
-        b.child_rank_item.reserve(nfreq + 16);
-        b.child_node_of.reserve(2 * nfreq + 16);
-        if (!comm && nfreq >= par_min()) {
-            children_parallel(b, R, nfreq, rows);
-        } else
-        for (size_t q = 0; q < nfreq;) {
-            const uint32_t row = R[q].row;
-            const DRow pr = rows[row];
-            const ClassMeta& pm = b.cls[pr.cls];
-            size_t q2 = q;
-            uint32_t maxcid = 0;
-            while (q2 < nfreq && R[q2].row == row) { maxcid = std::max(maxcid, R[q2].cid); ++q2; }
-            ChildInfo ch;
-            ch.pcls = pr.cls;
-            ch.pmi = pr.mi;
-            const uint32_t R2 = (maxcid >> 1) + 1;
-            ch.D = 2 * R2;
-            ch.ri_off = b.child_rank_item.size();
-            ch.no_off = b.child_node_of.size();
-            b.child_rank_item.resize(ch.ri_off + R2, 0);
-            b.child_node_of.resize(ch.no_off + ch.D, -1);
-            const int32_t parent = b.node_of[pm.no_off + pr.mi];
-            const uint32_t pls = nodes[size_t(parent)].len_sets;
-            ch.psup = nodes[size_t(parent)].support;
-            if ((pls >> 16) >= 0xFFFFu) throw Error(FSM_ELIMIT, "SPADE: a pattern exceeds 65534 items");
-            const bool dup = comm && pm.split && comm->rank() != 0;  // a split class's nodes: rank 0 outputs them
-            uint32_t last_type = 0;
-            for (size_t k = q; k < q2; ++k) {
-                const FreqRec& fr = R[k];
-                const uint32_t item = b.rank_item[pm.ri_off + (fr.slot >> 1)];
-                const int32_t node = int32_t(nodes.size());
-                nodes.push_back(PNode{parent, item, fr.slot & 1u, fr.sup, pls + (1u << 16) + ((fr.slot & 1u) == kSeq)});
-                if (dup) {
-                    node_dup.resize(nodes.size(), 0);
-                    node_dup[size_t(node)] = 1;
-                }
-                b.child_rank_item[ch.ri_off + (fr.cid >> 1)] = item;
-                b.child_node_of[ch.no_off + fr.cid] = node;
-                ch.cap += fr.sup;
-                if ((fr.slot & 1u) == kSeq) { ++ch.nS; ch.sS += fr.sup; } else { ++ch.nI; ch.sI += fr.sup; }
-                if (!dup) st.bytes_join_equiv += int64_t(12ull * fr.sup);
-                last_type = fr.slot & 1u;
-            }
-            const size_t nch = q2 - q;
-            if (!(nch == 1 && last_type == kItm)) b.children.push_back(std::move(ch));
-            q = q2;
+        // emit() builds the children after launching its kernels (one group, unsharded)
+        if (defer_ok(b, R, nfreq, rows)) {
+            hp[2] += now_ms() - th;
+            return;
         }
+        make_children(b, R, nfreq, rows);
         if (shard) {
             // first-level classes: largest-first by estimated id-list volume (the
             // class's entries), same plan on every rank; keep this rank's share.
@@ -3573,6 +3539,104 @@ struct Miner {
                          b.children.size(), b.groups.size());
     }
 
+    // the children of a counted batch (new pattern nodes, the next batch's class records and
+    // member tables) in deterministic (row, slot) order
+    void make_children(Batch& b, const FreqRec* R, uint64_t nfreq, const RawVec<DRow>& rows) {
+        fsm_stats& st = ctx->stats;
+        b.children.clear();
+        b.child_rank_item.clear();
+        b.child_node_of.clear();
+        b.children.reserve(nfreq);
+        b.child_rank_item.reserve(nfreq + 16);
+        b.child_node_of.reserve(2 * nfreq + 16);
+        if (!comm && nfreq >= par_min()) {
+            children_parallel(b, R, nfreq, rows);
+        } else
+        for (size_t q = 0; q < nfreq;) {
+            const uint32_t row = R[q].row;
+            const DRow pr = rows[row];
+            const ClassMeta& pm = b.cls[pr.cls];
+            size_t q2 = q;
+            uint32_t maxcid = 0;
+            while (q2 < nfreq && R[q2].row == row) { maxcid = std::max(maxcid, R[q2].cid); ++q2; }
+            ChildInfo ch;
+            ch.pcls = pr.cls;
+            ch.pmi = pr.mi;
+            const uint32_t R2 = (maxcid >> 1) + 1;
+            ch.D = 2 * R2;
+            ch.ri_off = b.child_rank_item.size();
+            ch.no_off = b.child_node_of.size();
+            b.child_rank_item.resize(ch.ri_off + R2, 0);
+            b.child_node_of.resize(ch.no_off + ch.D, -1);
+            const int32_t parent = b.node_of[pm.no_off + pr.mi];
+            const uint32_t pls = nodes[size_t(parent)].len_sets;
+            ch.psup = nodes[size_t(parent)].support;
+            if ((pls >> 16) >= 0xFFFFu) throw Error(FSM_ELIMIT, "SPADE: a pattern exceeds 65534 items");
+            const bool dup = comm && pm.split && comm->rank() != 0;  // a split class's nodes: rank 0 outputs them
+            uint32_t last_type = 0;
+            for (size_t k = q; k < q2; ++k) {
+                const FreqRec& fr = R[k];
+                const uint32_t item = b.rank_item[pm.ri_off + (fr.slot >> 1)];
+                const int32_t node = int32_t(nodes.size());
+                nodes.push_back(PNode{parent, item, fr.slot & 1u, fr.sup, pls + (1u << 16) + ((fr.slot & 1u) == kSeq)});
+                if (dup) {
+                    node_dup.resize(nodes.size(), 0);
+                    node_dup[size_t(node)] = 1;
+                }
+                b.child_rank_item[ch.ri_off + (fr.cid >> 1)] = item;
+                b.child_node_of[ch.no_off + fr.cid] = node;
+                ch.cap += fr.sup;
+                if ((fr.slot & 1u) == kSeq) { ++ch.nS; ch.sS += fr.sup; } else { ++ch.nI; ch.sI += fr.sup; }
+                if (!dup) st.bytes_join_equiv += int64_t(12ull * fr.sup);
+                last_type = fr.slot & 1u;
+            }
+            const size_t nch = q2 - q;
+            if (!(nch == 1 && last_type == kItm)) b.children.push_back(std::move(ch));
+            q = q2;
+        }
+    }
+
+    // The one-group test of count_and_freq's group split, from the records alone (before the
+    // children exist): unsharded, no claims, every kept child in one group.  Then the batch
+    // records what emit() needs (the group, the child entry total) and defers the children.
+    bool defer_ok(Batch& b, const FreqRec* R, uint64_t nfreq, const RawVec<DRow>& rows) {
+        b.defer_children = false;
+        if (comm || b.claim_key >= 0 || nfreq == 0 || defer_env() == 0) return false;
+        uint64_t need = 0, ent = 0, nkept = 0;
+        for (uint64_t q = 0; q < nfreq;) {
+            const uint32_t row = R[q].row;
+            uint64_t q2 = q, sup = 0;
+            uint32_t maxcid = 0;
+            while (q2 < nfreq && R[q2].row == row) {
+                maxcid = std::max(maxcid, R[q2].cid);
+                sup += R[q2].sup;
+                ++q2;
+            }
+            if (!(q2 - q == 1 && (R[q].slot & 1u) == kItm)) {
+                const uint64_t D = 2ull * ((maxcid >> 1) + 1);
+                need += sup * entry_bytes() + D * D * 4;
+                ent += sup;
+                ++nkept;
+            }
+            q = q2;
+        }
+        if (need > budget || ent > (uint64_t(1) << 31) || nkept == 0) return false;
+        b.children.clear();
+        b.groups.assign(1, {size_t(0), size_t(nkept)});
+        b.next_group = 0;
+        b.defer_children = true;
+        b.defer_R = R;
+        b.defer_n = nfreq;
+        b.defer_total = ent;
+        b.defer_rows = &rows;
+        return true;
+    }
+    // FSM_EMIT_DEFER=0: children built before the emit launch (A/B)
+    static int defer_env() {
+        static const int v = [] { const char* e = std::getenv("FSM_EMIT_DEFER"); return e && e[0] == '0' ? 0 : 1; }();
+        return v;
+    }
+
     // groups of children [a, z) that fit the frontier budget, appended to b.groups
     void append_groups(Batch& b, size_t a, size_t z) {
         const uint64_t max_ent = uint64_t(1) << 31;
@@ -3657,14 +3721,33 @@ struct Miner {
         RawVec<uint32_t>& child_of = child_of_s;
         if (!dev_child_of) child_of.assign(b.cbase_total, kNone);
         uint64_t total = 0;
-        if (b.root)  // the root entries this rank joins as the owner: its first-level classes' prefix supports
+        const bool deferred = b.defer_children;  // (one group; the children are built after the launch)
+        if (deferred) {
+            total = b.defer_total;
+            if (!dev_child_of) {  // the member slots that open a class, numbered in record order
+                const FreqRec* R = b.defer_R;
+                const RawVec<DRow>& rows = *b.defer_rows;
+                uint32_t k = 0;
+                for (uint64_t q = 0; q < b.defer_n;) {
+                    uint64_t q2 = q;
+                    while (q2 < b.defer_n && R[q2].row == R[q].row) ++q2;
+                    if (!(q2 - q == 1 && (R[q].slot & 1u) == kItm)) {
+                        const DRow pr = rows[R[q].row];
+                        child_of[b.cls[pr.cls].cbase + pr.mi] = k++;
+                    }
+                    q = q2;
+                }
+            }
+        }
+        if (b.root && !deferred)  // the root entries this rank joins as the owner: its first-level classes' prefix supports
             for (size_t k = ga; k < gb; ++k) ctx->stats.rank_root_owned += int64_t(b.children[k].psup);
         // the only group: the children and their member tables move over whole (swapped:
         // the parent, released after this emit and recycled, keeps nb's old capacity)
         // (not a claiming root: it stays on the stack for its next claim, which reads its children;
         // a first claim covering every class would otherwise leave it with nb's old ones)
-        const bool whole = ga == 0 && gb == b.children.size() && b.groups.size() == 1 && b.claim_key < 0;
-        if (whole) {
+        const bool whole = !deferred && ga == 0 && gb == b.children.size() && b.groups.size() == 1 && b.claim_key < 0;
+        if (deferred) {
+        } else if (whole) {
             nb.cls.clear();
             nb.rank_item.clear();
             nb.node_of.clear();
@@ -3824,6 +3907,24 @@ struct Miner {
         // up exactly to the capacities (sum of child supports), checked at the next sync
         pend_total = total;
         pend_check = true;
+        if (deferred) {
+            // the children, while the emit runs: pattern nodes and the next batch's class tables,
+            // moved over whole (the only group)
+            const double td = now_ms();
+            b.defer_children = false;
+            make_children(b, b.defer_R, b.defer_n, *b.defer_rows);
+            if (b.children.size() != gb)
+                throw Error(FSM_EDEVICE, "SPADE internal error: deferred children do not match the emit group");
+            if (b.root)
+                for (const ChildInfo& c : b.children) ctx->stats.rank_root_owned += int64_t(c.psup);
+            nb.cls.clear();
+            nb.rank_item.clear();
+            nb.node_of.clear();
+            std::swap(nb.cls, b.children);
+            std::swap(nb.rank_item, b.child_rank_item);
+            std::swap(nb.node_of, b.child_node_of);
+            hp[2] += now_ms() - td;
+        }
     }
     // the deferred emit check (after a stream sync)
     void check_emit() {
