@@ -2168,11 +2168,14 @@ struct PNode {
 // the row's slots with a frequent temporal or equality candidate, << 1 | type (the ids
 // k_freq_write assigns in-kernel).  Counting sort by row, then the few slots of a row.
 void order_recs(std::vector<FreqRec>& recs, uint32_t nrows) {
-    std::vector<uint32_t> off(size_t(nrows) + 1, 0);
+    // (scratch kept per host thread: no fresh pages per batch)
+    thread_local std::vector<uint32_t> off, at;
+    thread_local std::vector<FreqRec> tmp;
+    off.assign(size_t(nrows) + 1, 0);
     for (const FreqRec& r : recs) ++off[size_t(r.row) + 1];
     for (uint32_t x = 0; x < nrows; ++x) off[x + 1] += off[x];
-    std::vector<FreqRec> tmp(recs.size());
-    std::vector<uint32_t> at(off.begin(), off.end() - 1);
+    tmp.resize(recs.size());
+    at.assign(off.begin(), off.end() - 1);
     for (const FreqRec& r : recs) tmp[at[r.row]++] = r;
     for (uint32_t x = 0; x < nrows; ++x)
         if (off[x + 1] - off[x] > 1)
@@ -3988,7 +3991,7 @@ struct Miner {
                 rk2[u] = 2 * below - 1u;  // wraps to 0xFFFFFFFF below the first frequent item
             }
         }
-        upload(root.rk2, rk2);
+        upload_staged(0, root.rk2, rk2.data(), rk2.size() * 4);  // (pinned: the copy does not block the host)
         // the unordered-pair layout (W = 1): its own groups over this rank's rows
         uint32_t G = geo.G;
         uint64_t nd = geo.nd;
@@ -3998,7 +4001,7 @@ struct Miner {
             const uint32_t rlo = geo.mlo / 2, rhi = geo.mhi == kNone ? F : std::min(geo.mhi / 2, F);
             const uint32_t TG = tri_tables(F, rlo, rhi, tab);
             if (TG) {
-                upload(root.f2_tri_tab, tab);
+                upload_staged(1, root.f2_tri_tab, tab.data(), tab.size() * 4);
                 root.f2_tri = true;
                 root.f2_tri_G = TG;
                 G = TG;
