@@ -2167,31 +2167,40 @@ struct PNode {
 // Frequent-pair records in (row, slot) order with their child member ids: rank among
 // the row's slots with a frequent temporal or equality candidate, << 1 | type (the ids
 // k_freq_write assigns in-kernel).  Counting sort by row, then the few slots of a row.
-void order_recs(std::vector<FreqRec>& recs, uint32_t nrows) {
+// Records in (row, slot) order with their child member ids: rank among the row's slots with
+// a frequent temporal or equality candidate, << 1 | type (as k_freq_write assigns them).
+// off (if given) receives the row offsets [nrows + 1] of the ordered records.
+void order_recs(std::vector<FreqRec>& recs, uint32_t nrows, std::vector<uint32_t>* off_out = nullptr) {
     // (scratch kept per host thread: no fresh pages per batch)
-    thread_local std::vector<uint32_t> off, at;
+    thread_local std::vector<uint32_t> off_s, at;
     thread_local std::vector<FreqRec> tmp;
+    std::vector<uint32_t>& off = off_out ? *off_out : off_s;
     off.assign(size_t(nrows) + 1, 0);
     for (const FreqRec& r : recs) ++off[size_t(r.row) + 1];
     for (uint32_t x = 0; x < nrows; ++x) off[x + 1] += off[x];
     tmp.resize(recs.size());
     at.assign(off.begin(), off.end() - 1);
     for (const FreqRec& r : recs) tmp[at[r.row]++] = r;
-    for (uint32_t x = 0; x < nrows; ++x)
-        if (off[x + 1] - off[x] > 1)
-            std::sort(tmp.begin() + off[x], tmp.begin() + off[x + 1],
-                      [](const FreqRec& a, const FreqRec& c) { return a.slot < c.slot; });
-    recs.swap(tmp);
-    for (size_t q = 0; q < recs.size();) {
-        size_t q2 = q;
-        uint32_t crank = 0;
-        while (q2 < recs.size() && recs[q2].row == recs[q].row) {
-            if (q2 > q && (recs[q2].slot >> 1) != (recs[q2 - 1].slot >> 1)) ++crank;
-            recs[q2].cid = crank << 1 | (recs[q2].slot & 1u);
-            ++q2;
+    for (uint32_t x = 0; x < nrows; ++x) {
+        FreqRec* a = tmp.data() + off[x];
+        const uint32_t n = off[x + 1] - off[x];
+        if (n > 16) {
+            std::sort(a, a + n, [](const FreqRec& u, const FreqRec& c) { return u.slot < c.slot; });
+        } else {
+            for (uint32_t i = 1; i < n; ++i) {  // (rows hold a few records: insertion sort)
+                const FreqRec v = a[i];
+                uint32_t j = i;
+                for (; j > 0 && a[j - 1].slot > v.slot; --j) a[j] = a[j - 1];
+                a[j] = v;
+            }
         }
-        q = q2;
+        uint32_t crank = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (i > 0 && (a[i].slot >> 1) != (a[i - 1].slot >> 1)) ++crank;
+            a[i].cid = crank << 1 | (a[i].slot & 1u);
+        }
     }
+    recs.swap(tmp);
 }
 
 struct Batch {
@@ -2323,6 +2332,8 @@ struct Miner {
     RawVec<DRow> rows_s;
     std::vector<FreqRec> recs_s;
     RawVec<uint32_t> ktab_s, child_of_s;
+    std::vector<uint32_t> rec_off_s;  // row offsets of the records order_recs ordered last (kid offsets)
+    bool rec_off_ok = false;
     RawVec<uint64_t> gs_s;
     RawVec<uint32_t> r2_s;
 
@@ -2909,7 +2920,8 @@ struct Miner {
         // (row, slot) order and child member ids: rank among the row's slots with a frequent
         // temporal or equality candidate, << 1 | type (as k_freq_write assigns them)
         const double th0 = now_ms();
-        order_recs(recs, F);
+        order_recs(recs, F, &rec_off_s);
+        rec_off_ok = true;
         hp[0] += now_ms() - th0;
         return true;
     }
@@ -2974,7 +2986,8 @@ struct Miner {
         clk->add_bytes(tk_cnt, int64_t(nkeys) * 2 + int64_t(recs.size() * sizeof(FreqRec)));
         ctx->stats.root_keys += int64_t(nkeys);
         const double th0 = now_ms();
-        order_recs(recs, F);
+        order_recs(recs, F, &rec_off_s);
+        rec_off_ok = true;
         hp[0] += now_ms() - th0;
         return true;
     }
@@ -3082,6 +3095,7 @@ struct Miner {
     // count kernel + frequent-candidate extraction; fills b.children / b.groups / kids
     void count_and_freq(Batch& b) {
         const double tc0 = now_ms();
+        rec_off_ok = false;
         double tl = tc0;
         // FSM_HOST_TRACE=2: one line per batch with its host phases (diagnostics)
         struct BatchTrace {
@@ -3190,7 +3204,8 @@ struct Miner {
         // huge, sparse counter matrices: the joins sorted instead (records in (row, slot) order)
         const bool sparse_done = !root_done && b.E && sparse_wanted(b) && sparse_count(b, recs, rows);
         if (sparse_done) {
-            order_recs(recs, uint32_t(rows.size()));
+            order_recs(recs, uint32_t(rows.size()), &rec_off_s);
+            rec_off_ok = true;
             return;
         }
         const bool keyed_done = !root_done && keyed_layout && keyed_count(b, cnt);
@@ -3308,7 +3323,8 @@ struct Miner {
                 if (attempt > 0) throw Error(FSM_EDEVICE, "SPADE: frequent candidate buffer overflow");
                 cap_recs = nf;
             }
-            order_recs(recs, rhi);
+            order_recs(recs, rhi, &rec_off_s);
+            rec_off_ok = rhi == rows.size();
         }
         };
         if (shard) {  // a failure here or in run_root reaches every rank in the gather below
@@ -3341,7 +3357,8 @@ struct Miner {
             // order and the child ids over the whole set.  Every rank orders them, whatever its
             // own F2 layout (a rank with an empty slice runs the ordered one): the ranks must
             // derive identical children, or their collective sequences part
-            order_recs(recs, uint32_t(rows.size()));
+            order_recs(recs, uint32_t(rows.size()), &rec_off_s);
+            rec_off_ok = true;
             R = recs.data();
         }
         double th = now_ms();
@@ -3353,30 +3370,40 @@ struct Miner {
             b.kid_slot = b.kid_off + nko;
             b.kid_cid = b.kid_slot + nfreq;
         } else {
-        RawVec<uint32_t>& ktab = ktab_s;
-        ktab.clear();  // (a growing resize then copies nothing over)
-        ktab.resize(nko + 2 * size_t(nfreq));
-        uint32_t* koff = ktab.data();
+        // the table is filled straight into the pinned staging slot it is DMA'd from
+        const size_t kbytes = (nko + 2 * size_t(nfreq)) * 4;
+        uint32_t* koff = static_cast<uint32_t*>(ctx->stage_host(2, kbytes));
         uint32_t* kslot = koff + nko;
         uint32_t* kcid = kslot + nfreq;
         double tl2 = th;
         lap(9, tl2);
         // records are in (row, slot) order, and a row's member slot cbase + mi ascends
-        // with the row: koff[x] = records of slots < x, by a merge (threads split x)
-        auto slot_of = [&](uint64_t q) { return uint64_t(b.cls[rows[R[q].row].cls].cbase) + rows[R[q].row].mi; };
+        // with the row: koff[x] = records of slots < x
         const int64_t nthk = nfreq >= par_min() ? host_threads() : 1;
-        par_slices(nthk, int64_t(nko), [&](int64_t, int64_t x0, int64_t x1) {
-            uint64_t lo = 0, hi = nfreq;  // first record with slot >= x0
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) / 2;
-                if (slot_of(mid) < uint64_t(x0)) lo = mid + 1; else hi = mid;
+        if (rec_off_ok && rec_off_s.size() == rows.size() + 1) {
+            // from the row offsets of the ordering: slots (s(r-1), s(r)] take off[r]
+            uint64_t x = 0;
+            for (size_t r = 0; r < rows.size(); ++r) {
+                const uint64_t sr = uint64_t(b.cls[rows[r].cls].cbase) + rows[r].mi;
+                const uint32_t o = rec_off_s[r];
+                for (; x <= sr && x < nko; ++x) koff[x] = o;
             }
-            uint64_t q = lo;
-            for (int64_t x = x0; x < x1; ++x) {
-                while (q < nfreq && slot_of(q) < uint64_t(x)) ++q;
-                koff[x] = uint32_t(q);
-            }
-        });
+            for (; x < nko; ++x) koff[x] = uint32_t(nfreq);
+        } else {  // (records ordered on the device: a merge, threads split x)
+            auto slot_of = [&](uint64_t q) { return uint64_t(b.cls[rows[R[q].row].cls].cbase) + rows[R[q].row].mi; };
+            par_slices(nthk, int64_t(nko), [&](int64_t, int64_t x0, int64_t x1) {
+                uint64_t lo = 0, hi = nfreq;  // first record with slot >= x0
+                while (lo < hi) {
+                    const uint64_t mid = (lo + hi) / 2;
+                    if (slot_of(mid) < uint64_t(x0)) lo = mid + 1; else hi = mid;
+                }
+                uint64_t q = lo;
+                for (int64_t x = x0; x < x1; ++x) {
+                    while (q < nfreq && slot_of(q) < uint64_t(x)) ++q;
+                    koff[x] = uint32_t(q);
+                }
+            });
+        }
         par_slices(nthk, int64_t(nfreq), [&](int64_t, int64_t q0, int64_t q1) {
             for (int64_t q = q0; q < q1; ++q) {  // recs are ordered by (row, slot) = CSR order
                 kslot[q] = R[q].slot;
@@ -3384,7 +3411,8 @@ struct Miner {
             }
         });
         lap(10, tl2);
-        upload_staged(2, b.kid_tab, ktab.data(), ktab.size() * 4);
+        b.kid_tab.alloc(std::max<size_t>(kbytes, 4));
+        ctx->stage_copy(2, b.kid_tab.p, kbytes);
         lap(11, tl2);
         b.kid_off = b.kid_tab.as<uint32_t>();
         b.kid_slot = b.kid_off + nko;
