@@ -226,6 +226,22 @@ void DevBuf::alloc(size_t n) {
     pool = std::move(q);
 }
 
+__global__ __launch_bounds__(256) void k_copy_mapped(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16,
+                                                    const uint32_t* __restrict__ src4, uint32_t* __restrict__ dst4,
+                                                    size_t n4) {
+    const size_t stride = size_t(gridDim.x) * blockDim.x;
+    for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+    for (size_t i = 4 * n16 + size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) dst4[i] = src4[i];
+}
+
+void copy_from_mapped(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    const size_t n4 = bytes / 4, n16 = bytes / 16;
+    const unsigned grid = unsigned(std::min<size_t>((std::max<size_t>(n16, 1) + 255) / 256, 1024));
+    hipLaunchKernelGGL(k_copy_mapped, dim3(grid), dim3(256), 0, s, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), n16, static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), n4);
+    FSM_LAUNCHED("k_copy_mapped", s);
+}
+
 bool debug_sync() {
     static const bool on = [] {
         const char* v = std::getenv("FSM_DEBUG_SYNC");

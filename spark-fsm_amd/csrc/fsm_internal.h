@@ -127,6 +127,10 @@ struct PoolScope {
     PoolScope& operator=(const PoolScope&) = delete;
 };
 
+// dst (device) <- src (a mapped pinned host pointer's device address), `bytes` a multiple of 4:
+// a copy kernel on stream s (device_util.hip)
+void copy_from_mapped(void* dst, const void* src, size_t bytes, hipStream_t s);
+
 // Mapped pinned host memory (kernels write results straight into it; the host
 // reads them after a stream sync, with no copy launch).
 struct PinnedBuf {
@@ -242,8 +246,8 @@ struct fsm_ctx {
     std::shared_ptr<fsm::Pool> pool;  // device blocks of this context (see fsm::Pool)
     std::vector<fsm_kernel_stat> kstats;  // of the last mine call
     std::unique_ptr<fsm::PinnedBuf> pin;  // small mapped readback slots, made on first use
-    uint64_t* pinned_u64() {              // 8 u64 slots of pinned host memory
-        if (!pin) pin = std::make_unique<fsm::PinnedBuf>(64);
+    uint64_t* pinned_u64() {              // 16 u64 slots of pinned host memory
+        if (!pin) pin = std::make_unique<fsm::PinnedBuf>(128);
         return static_cast<uint64_t*>(pin->host);
     }
     // mapped pinned host memory of at least `bytes` (kernels write results straight into it);
@@ -279,10 +283,16 @@ struct fsm_ctx {
         }
         return stage[i]->host;
     }
-    void stage_copy(int i, void* dst, size_t bytes) {  // async H2D of the slot's first `bytes`
+    // Async H2D of the slot's first `bytes`.  Up to kStageKernelMax bytes (a multiple of 4) go
+    // through a copy kernel on the stream that reads the mapped slot over PCIe: an SDMA copy
+    // costs the next kernel a cross-engine wait of about 20 us (the gaps after every small
+    // upload in the D1M kernel timeline), a kernel on the same queue none.
+    static constexpr size_t kStageKernelMax = size_t(2) << 20;
+    void stage_copy(int i, void* dst, size_t bytes) {
         if (!bytes) return;
         if (!stage_ev[i]) FSM_HIP(hipEventCreateWithFlags(&stage_ev[i], hipEventDisableTiming));
-        FSM_HIP(hipMemcpyAsync(dst, stage[i]->host, bytes, hipMemcpyHostToDevice, stream));
+        if (bytes <= kStageKernelMax && bytes % 4 == 0) fsm::copy_from_mapped(dst, stage[i]->dev, bytes, stream);
+        else FSM_HIP(hipMemcpyAsync(dst, stage[i]->host, bytes, hipMemcpyHostToDevice, stream));
         FSM_HIP(hipEventRecord(stage_ev[i], stream));
         stage_pending[i] = true;
     }

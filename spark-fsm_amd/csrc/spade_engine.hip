@@ -2214,6 +2214,13 @@ struct Batch {
     const FreqRec* defer_R = nullptr;
     uint64_t defer_n = 0, defer_total = 0;
     const RawVec<DRow>* defer_rows = nullptr;
+    const uint32_t* child_of_pre = nullptr;  // deferred, host child_of: uploaded with the kid table
+    // the root's unordered-pair F2 keys, launched by run_root_db right after its plan (the host's
+    // root bookkeeping then overlaps them): keys, region fills, the counters block
+    bool f2_launched = false;
+    DevBuf f2_keys, f2_fill, f2_ctr_own;
+    char* f2_ctr = nullptr;
+    size_t f2_tk = 0;
     DevBuf d_cls;
     DevBuf kid_tab;  // frequent children of every member (CSR over cbase + mi): offsets | slots | child ids
     const uint32_t* kid_off = nullptr;
@@ -2263,6 +2270,12 @@ struct Batch {
         defer_children = false;
         defer_R = nullptr;
         defer_rows = nullptr;
+        child_of_pre = nullptr;
+        f2_launched = false;
+        f2_keys.release();
+        f2_fill.release();
+        f2_ctr_own.release();
+        f2_ctr = nullptr;
         defer_n = defer_total = 0;
         d_cls.release();
         kid_tab.release();
@@ -2355,12 +2368,19 @@ struct Miner {
     void maybe_inject(const char* phase) const { agr.maybe_inject(phase); }
     void agree() { agr.agree(s); }
     void sync() {
+        if (pend_check && emit_blk && !emit_copied) {  // the last emit's cursor block (check_emit)
+            FSM_HIP(hipMemcpyAsync(&pend[8], emit_blk, 16, hipMemcpyDeviceToHost, s));
+            emit_copied = true;
+        }
         const double t = now_ms();
         FSM_HIP(hipStreamSynchronize(s));
         wait_ms += now_ms() - t;
         check_emit();
     }
-    uint64_t* pend = nullptr;  // pinned slot: the last emit's slab cursor (ctx->pinned_u64())
+    uint64_t* pend = nullptr;  // pinned slots (ctx->pinned_u64()): [8..10] the last emit's cursor block
+    char* emit_blk = nullptr;  // the last emit's 32-byte device block (cursor, long runs, flag, next count)
+    bool emit_copied = false;  // its read-back is enqueued
+    DevBuf emit_own;           // (the block when the zeroed slots are used up)
     uint64_t pend_total = 0;
     bool pend_check = false;
 
@@ -2929,31 +2949,45 @@ struct Miner {
     // k_f2_count<false, true>): the frequent ordered pairs of the rows [rlo, rhi), as records
     // in (row, slot) order.  A pair (i, j) counts where the lower rank i is owned, so a rank's
     // records also hold rows j above its slice (the sharded gather orders them again).
-    bool root_f2_tri(Batch& b, std::vector<FreqRec>& recs, const F2Geo& geo, uint32_t rlo, uint32_t rhi) {
-        const uint32_t F = geo.F, G = b.f2_tri_G, R = geo.R, rpb = geo.rpb, nblk = geo.nblk;
+    // the k_f2_tri launch of the root (once; false: the slot count exceeds the u32 cursors)
+    bool launch_f2_tri(Batch& b, const F2Geo& geo) {
+        if (b.f2_launched) return true;
+        const uint32_t G = b.f2_tri_G, R = geo.R, rpb = geo.rpb, nblk = geo.nblk;
         const uint64_t nd = uint64_t(G) * nblk;
-        DevBuf base = std::move(b.f2_base), fill(nd * 4);
         const uint64_t nslots = b.f2_nslots;
         if (nslots >= (uint64_t(1) << 32) - 4096) return false;
-        DevBuf keys((nslots + 1024) * 2), ctr_own;
+        b.f2_fill.alloc(nd * 4);
+        b.f2_keys.alloc((nslots + 1024) * 2);
         // u64 key count | u32 frequent-record count, read back together
-        char* ctr = static_cast<char*>(zslot(16));
-        if (!ctr) {
-            ctr_own.alloc(16);
-            FSM_HIP(hipMemsetAsync(ctr_own.p, 0, 16, s));
-            ctr = ctr_own.as<char>();
+        b.f2_ctr = static_cast<char*>(zslot(16));
+        if (!b.f2_ctr) {
+            b.f2_ctr_own.alloc(16);
+            FSM_HIP(hipMemsetAsync(b.f2_ctr_own.p, 0, 16, s));
+            b.f2_ctr = b.f2_ctr_own.as<char>();
         }
-        unsigned long long* nk = reinterpret_cast<unsigned long long*>(ctr);
+        const uint32_t* gtab = b.f2_tri_tab.as<uint32_t>();
+        const size_t kshm = size_t(kF2Waves) * 64 * 16 + size_t(kF2RowWords) * 4 + size_t(G) * 4;
+        b.f2_tk = clk->begin("k_f2_keys");
+        hipLaunchKernelGGL(k_f2_tri, dim3(nblk), dim3(kF2Threads), kshm, s, db->row_off.as<uint32_t>(),
+                           b.mem_db.as<uint32_t>(), db->mask.as<uint64_t>(), R, rpb, gtab, G, nblk, geo.mlo, geo.mhi,
+                           b.f2_base.as<uint64_t>(), b.f2_fill.as<uint32_t>(), b.f2_keys.as<uint16_t>(),
+                           reinterpret_cast<unsigned long long*>(b.f2_ctr));
+        FSM_LAUNCHED("k_f2_tri", s);
+        clk->end(b.f2_tk, db->E * 12 + int64_t(nd) * 12, int64_t(b.cls[0].cap) * 8);
+        b.f2_launched = true;
+        return true;
+    }
+
+    bool root_f2_tri(Batch& b, std::vector<FreqRec>& recs, const F2Geo& geo, uint32_t rlo, uint32_t rhi) {
+        const uint32_t F = geo.F, G = b.f2_tri_G, nblk = geo.nblk;
+        if (!launch_f2_tri(b, geo)) return false;
+        DevBuf base = std::move(b.f2_base), fill = std::move(b.f2_fill), keys = std::move(b.f2_keys),
+               ctr_own = std::move(b.f2_ctr_own);
+        char* ctr = b.f2_ctr;
+        const size_t tk_keys = b.f2_tk;
         uint32_t* d_nrec = reinterpret_cast<uint32_t*>(ctr + 8);
         const uint32_t* gtab = b.f2_tri_tab.as<uint32_t>();
         const uint32_t* gr = gtab + F;
-        const size_t kshm = size_t(kF2Waves) * 64 * 16 + size_t(kF2RowWords) * 4 + size_t(G) * 4;
-        const size_t tk_keys = clk->begin("k_f2_keys");
-        hipLaunchKernelGGL(k_f2_tri, dim3(nblk), dim3(kF2Threads), kshm, s, db->row_off.as<uint32_t>(),
-                           b.mem_db.as<uint32_t>(), db->mask.as<uint64_t>(), R, rpb, gtab, G, nblk, geo.mlo, geo.mhi,
-                           base.as<uint64_t>(), fill.as<uint32_t>(), keys.as<uint16_t>(), nk);
-        FSM_LAUNCHED("k_f2_tri", s);
-        clk->end(tk_keys, db->E * 12 + int64_t(nd) * 12, int64_t(b.cls[0].cap) * 8);
         // count + frequent pairs (a retry when the first record buffer was too small)
         // the records land in mapped pinned host memory, the counts in pinned slots: one sync
         uint32_t cap_recs = uint32_t(std::min<uint64_t>(uint64_t(rhi - rlo) * 2 * F, uint64_t(1) << 20));
@@ -3299,6 +3333,9 @@ struct Miner {
             // the records land in mapped pinned host memory: one stream sync per batch
             DevBuf d_n;
             uint32_t* dn = d_nz;  // zeroed with the counters (a retry or the keyed count: its own)
+            // the last emit's block has a zeroed counter for this count: both come back in one copy
+            const bool ride = pend_check && emit_blk && !emit_copied;
+            if (ride) dn = reinterpret_cast<uint32_t*>(emit_blk + 16);
             for (int attempt = 0; nrows; ++attempt) {
                 PinnedBuf* pb = ctx->pinned_big(size_t(std::max<uint32_t>(cap_recs, 1)) * sizeof(FreqRec));
                 if (attempt > 0 || dn == nullptr) {
@@ -3312,9 +3349,17 @@ struct Miner {
                                    static_cast<FreqRec*>(pb->dev), cap_recs, dn);
                 FSM_LAUNCHED("k_freq_recs", s);
                 clk->end(tk, int64_t(uint64_t(nrows) * (b.n_cnt / std::max<uint64_t>(rows.size(), 1)) * 4));
-                FSM_HIP(hipMemcpyAsync(&pend[1], dn, 4, hipMemcpyDeviceToHost, s));
-                sync();
-                const uint32_t nf = uint32_t(pend[1] & 0xFFFFFFFFu);
+                uint32_t nf = 0;
+                if (ride && attempt == 0) {
+                    FSM_HIP(hipMemcpyAsync(&pend[8], emit_blk, 24, hipMemcpyDeviceToHost, s));
+                    emit_copied = true;
+                    sync();
+                    nf = uint32_t(pend[10] & 0xFFFFFFFFu);
+                } else {
+                    FSM_HIP(hipMemcpyAsync(&pend[1], dn, 4, hipMemcpyDeviceToHost, s));
+                    sync();
+                    nf = uint32_t(pend[1] & 0xFFFFFFFFu);
+                }
                 if (nf <= cap_recs) {
                     const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
                     recs.assign(hr, hr + nf);
@@ -3365,13 +3410,21 @@ struct Miner {
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
         // one table, one H2D copy: [koff: cbase_total + 1 | kslot: nfreq | kcid: nfreq]
         const size_t nko = size_t(b.cbase_total) + 1;
+        bool defer_checked = false;
         if (kids_dev) {
             b.kid_off = b.kid_tab.as<uint32_t>();
             b.kid_slot = b.kid_off + nko;
             b.kid_cid = b.kid_slot + nfreq;
         } else {
+        // deferred children (one group, unsharded; decided here, the children are built by emit()):
+        // the host child_of table (member slot -> child class) rides in the same upload
+        b.child_of_pre = nullptr;
+        const bool defer = defer_ok(b, R, nfreq, rows);
+        defer_checked = true;
+        const bool pre_co = defer && !child_of_device(b.cbase_total);
+        const size_t nco = pre_co ? size_t(b.cbase_total) : 0;
         // the table is filled straight into the pinned staging slot it is DMA'd from
-        const size_t kbytes = (nko + 2 * size_t(nfreq)) * 4;
+        const size_t kbytes = (nko + 2 * size_t(nfreq) + nco) * 4;
         uint32_t* koff = static_cast<uint32_t*>(ctx->stage_host(2, kbytes));
         uint32_t* kslot = koff + nko;
         uint32_t* kcid = kslot + nfreq;
@@ -3410,6 +3463,20 @@ struct Miner {
                 kcid[q] = R[q].cid;
             }
         });
+        if (pre_co) {  // the member slots that open a class, numbered in record order (as emit's)
+            uint32_t* co = kcid + nfreq;
+            std::fill(co, co + nco, kNone);
+            uint32_t k = 0;
+            for (uint64_t q = 0; q < nfreq;) {
+                uint64_t q2 = q;
+                while (q2 < nfreq && R[q2].row == R[q].row) ++q2;
+                if (!(q2 - q == 1 && (R[q].slot & 1u) == kItm)) {
+                    const DRow pr = rows[R[q].row];
+                    co[b.cls[pr.cls].cbase + pr.mi] = k++;
+                }
+                q = q2;
+            }
+        }
         lap(10, tl2);
         b.kid_tab.alloc(std::max<size_t>(kbytes, 4));
         ctx->stage_copy(2, b.kid_tab.p, kbytes);
@@ -3417,11 +3484,16 @@ struct Miner {
         b.kid_off = b.kid_tab.as<uint32_t>();
         b.kid_slot = b.kid_off + nko;
         b.kid_cid = b.kid_slot + nfreq;
+        if (pre_co) b.child_of_pre = b.kid_cid + nfreq;
+        if (defer) {  // emit() builds the children after launching its kernels
+            hp[1] += now_ms() - th;
+            return;
+        }
         }
         hp[1] += now_ms() - th;
         th = now_ms();
         // emit() builds the children after launching its kernels (one group, unsharded)
-        if (defer_ok(b, R, nfreq, rows)) {
+        if (!defer_checked && defer_ok(b, R, nfreq, rows)) {
             hp[2] += now_ms() - th;
             return;
         }
@@ -3750,12 +3822,12 @@ struct Miner {
         // children, so the host builds the table
         const bool dev_child_of = comm == nullptr && child_of_device(b.cbase_total);
         RawVec<uint32_t>& child_of = child_of_s;
-        if (!dev_child_of) child_of.assign(b.cbase_total, kNone);
+        if (!dev_child_of && !(b.defer_children && b.child_of_pre)) child_of.assign(b.cbase_total, kNone);
         uint64_t total = 0;
         const bool deferred = b.defer_children;  // (one group; the children are built after the launch)
         if (deferred) {
             total = b.defer_total;
-            if (!dev_child_of) {  // the member slots that open a class, numbered in record order
+            if (!dev_child_of && !b.child_of_pre) {  // the member slots that open a class, numbered in record order
                 const FreqRec* R = b.defer_R;
                 const RawVec<DRow>& rows = *b.defer_rows;
                 uint32_t k = 0;
@@ -3841,9 +3913,11 @@ struct Miner {
                                    b.child_pre.as<uint64_t>(), n, uint32_t(ga), uint32_t(gb), d_child_of.as<uint32_t>());
                 FSM_LAUNCHED("k_child_of", s);
             }
-        } else {
+        } else if (!(deferred && b.child_of_pre)) {
             upload_staged(3, d_child_of, child_of.data(), child_of.size() * 4);
         }
+        // (deferred with the host table: it came up with the kid table)
+        const uint32_t* cof = deferred && b.child_of_pre ? b.child_of_pre : d_child_of.as<uint32_t>();
         ctx->stats.bytes_streamed += int64_t((total + b.E) * entry_bytes());
         if (b.E) {
             // the DB-direct root is read from the DB rows themselves (pos: the DB's row
@@ -3859,12 +3933,12 @@ struct Miner {
             }
             SlabPtrs op = nb.slab.ptrs();
             // u64 slab cursor | u32 long-run count (k_emit2) | u32 run-length flag
-            DevBuf cursor_own;
-            char* cursor = static_cast<char*>(zslot(16));
+            // (32 bytes: the next count's record counter rides along, read back with it)
+            char* cursor = static_cast<char*>(zslot(32));
             if (!cursor) {
-                cursor_own.alloc(16);
-                FSM_HIP(hipMemsetAsync(cursor_own.p, 0, 16, s));
-                cursor = cursor_own.as<char>();
+                emit_own.alloc(32);
+                FSM_HIP(hipMemsetAsync(emit_own.p, 0, 32, s));
+                cursor = emit_own.as<char>();
             }
             op.lim = reinterpret_cast<uint32_t*>(cursor + 12);
             const uint64_t chunk = uint64_t(kEmitBlock) * kEmitRounds;
@@ -3879,12 +3953,12 @@ struct Miner {
 #define FSM_EMIT2(WW, RT)                                                                                       \
     hipLaunchKernelGGL((k_emit2<WW, RT>), dim3(g2), dim3(kE2Block), 0, s, uint32_t(Eg), rr, sp.cid,                  \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
-                       d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op, nb.slab.cap, emit2_cap(),   \
+                       cof, reinterpret_cast<unsigned long long*>(cursor), op, nb.slab.cap, emit2_cap(),   \
                        d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor + 8));               \
     FSM_LAUNCHED("k_emit2", s);                                                                                    \
     hipLaunchKernelGGL((k_emit1<WW, RT>), dim3(256), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,              \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
-                       d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op, nb.slab.cap, emit_cap(),    \
+                       cof, reinterpret_cast<unsigned long long*>(cursor), op, nb.slab.cap, emit_cap(),    \
                        uint32_t(WW), d_long.as<uint32_t>(), reinterpret_cast<const uint32_t*>(cursor + 8)); \
     FSM_LAUNCHED("k_emit1", s);
                 switch (W * 2 + (rootdb ? 1 : 0)) {
@@ -3902,12 +3976,12 @@ struct Miner {
 #define FSM_EMIT1(WW)                                                                                               \
     hipLaunchKernelGGL((k_emit1<WW, false>), dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,                \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                   \
-                       b.kid_cid, d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op,  \
+                       b.kid_cid, cof, reinterpret_cast<unsigned long long*>(cursor), op,  \
                        nb.slab.cap, emit_cap(), uint32_t(W), (const uint32_t*)nullptr, (const uint32_t*)nullptr)
 #define FSM_EMIT1R(WW)                                                                                              \
     hipLaunchKernelGGL((k_emit1<WW, true>), dim3(grid), dim3(kEmitBlock), 0, s, uint32_t(Eg), rr, sp.cid,                 \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot,                   \
-                       b.kid_cid, d_child_of.as<uint32_t>(), reinterpret_cast<unsigned long long*>(cursor), op,  \
+                       b.kid_cid, cof, reinterpret_cast<unsigned long long*>(cursor), op,  \
                        nb.slab.cap, emit_cap(), uint32_t(W), (const uint32_t*)nullptr, (const uint32_t*)nullptr)
                 if (rootdb) {
                     switch (W) {
@@ -3927,12 +4001,14 @@ struct Miner {
             // writes every child entry once
             const uint64_t rd = rootdb ? Eg * (8 + 8 * uint64_t(W)) : b.E * entry_bytes();
             clk->end(tk, int64_t(rd + total * entry_bytes()), int64_t((b.E + total) * survey_entry_bytes()));
-            // the whole cursor block back in one copy: pend[6] = entries written, pend[7] = long
-            // runs | run-length flag << 32
-            FSM_HIP(hipMemcpyAsync(&pend[6], cursor, 16, hipMemcpyDeviceToHost, s));
+            // the cursor block is read back with the next count's record count (or at the next
+            // sync): pend[8] = entries written, pend[9] = long runs | run-length flag << 32
+            emit_blk = cursor;
+            emit_copied = false;
         } else {
-            pend[6] = 0;
-            pend[7] = 0;
+            emit_blk = nullptr;
+            pend[8] = 0;
+            pend[9] = 0;
         }
         // no sync: the host prepares the next count while the emit runs; the runs must add
         // up exactly to the capacities (sum of child supports), checked at the next sync
@@ -3961,8 +4037,8 @@ struct Miner {
     void check_emit() {
         if (!pend_check) return;
         pend_check = false;
-        const uint64_t written = pend[6];
-        if (pend[7] >> 32)
+        const uint64_t written = pend[8];
+        if (pend[9] >> 32)
             throw Error(FSM_ELIMIT, "SPADE: a class holds more than 65535 entries of one sequence");
         if (written != pend_total)
             throw Error(FSM_EDEVICE, "SPADE emit: wrote " + std::to_string(written) + " child entries, expected " +
@@ -4067,6 +4143,9 @@ struct Miner {
         root.f2_planned = true;
         root.f2_nslots = pend[2];
         root.db_direct = true;
+        // the pair keys start now: the host's root bookkeeping (class record, member rows,
+        // descriptors) overlaps them (count_and_freq -> root_f2_tri takes the count from here)
+        if (root.f2_tri && !comm) (void)launch_f2_tri(root, f2_geometry(root, 2 * F, E0, uint64_t(db->R)));
         return true;
     }
 
@@ -4360,8 +4439,11 @@ void spade_mine(fsm_ctx* ctx, fsm_db* db, double support, fsm_patterns** out) {
             clock.end(tk, int64_t((e1 - e0) * 4 + uint64_t(d->U) * 4), int64_t((e1 - e0) * 4));
         }
         if (comm) comm->allreduce_u32(d_f1.as<uint32_t>(), size_t(d->U), ctx->stream);
-        if (d->U) FSM_HIP(hipMemcpyAsync(f1.data(), d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));
+        // (through pinned memory: a pageable read-back is staged by the runtime)
+        PinnedBuf* pb = ctx->pinned_big(std::max<size_t>(size_t(d->U) * 4, 4));
+        if (d->U) FSM_HIP(hipMemcpyAsync(pb->host, d_f1.p, size_t(d->U) * 4, hipMemcpyDeviceToHost, ctx->stream));
         FSM_HIP(hipStreamSynchronize(ctx->stream));
+        if (d->U) std::memcpy(f1.data(), pb->host, size_t(d->U) * 4);
     }
     std::vector<uint32_t> freq;
     if (!none)

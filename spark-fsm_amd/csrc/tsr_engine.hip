@@ -2421,8 +2421,10 @@ void tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules** o
             x.dom.alloc(std::max<uint64_t>(drv_off[nb] * 4 * 5 / 4, uint64_t(1) << 20));
         fill_ms += now_ms() - tl0;
         hipStream_t s = x.st;  // (shadows the context stream for this launch)
-        FSM_HIP(hipMemcpyAsync(x.d_stage.p, x.stage->host, 2 * kOffB + size_t(nb) * sizeof(Side), hipMemcpyHostToDevice,
-                               s));
+        // the descriptors by a copy kernel on the set's stream (reading the mapped staging over PCIe:
+        // an SDMA copy would cost the launch's first kernel a cross-engine wait)
+        static_assert(sizeof(Side) % 4 == 0, "Side: whole words");
+        copy_from_mapped(x.d_stage.p, x.stage->dev, 2 * kOffB + size_t(nb) * sizeof(Side), s);
         x.timed = nb && launches % time_every == 0;  // every 16th launch is timed (events cost host time)
         const ExpGeo geo{K, KP, uint32_t(wave_off[nb]), rp.minsup};
         if (nb) {  // (a rank may get no slot of a small sharded batch)
