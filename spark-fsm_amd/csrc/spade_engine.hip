@@ -3011,7 +3011,9 @@ struct Miner {
             if (nrec <= cap_recs || attempt > 0) {
                 if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
                 const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
+                double tr = now_ms();
                 recs.assign(hr, hr + nrec);
+                lap(14, tr);
                 break;
             }
             cap_recs = nrec;
@@ -3020,7 +3022,9 @@ struct Miner {
         clk->add_bytes(tk_cnt, int64_t(nkeys) * 2 + int64_t(recs.size() * sizeof(FreqRec)));
         ctx->stats.root_keys += int64_t(nkeys);
         const double th0 = now_ms();
+        double to_ = now_ms();
         order_recs(recs, F, &rec_off_s);
+        lap(15, to_);
         rec_off_ok = true;
         hp[0] += now_ms() - th0;
         return true;
@@ -3419,7 +3423,9 @@ struct Miner {
         // deferred children (one group, unsharded; decided here, the children are built by emit()):
         // the host child_of table (member slot -> child class) rides in the same upload
         b.child_of_pre = nullptr;
+        double tl3 = now_ms();
         const bool defer = defer_ok(b, R, nfreq, rows);
+        lap(12, tl3);
         defer_checked = true;
         const bool pre_co = defer && !child_of_device(b.cbase_total);
         const size_t nco = pre_co ? size_t(b.cbase_total) : 0;
@@ -3463,6 +3469,7 @@ struct Miner {
                 kcid[q] = R[q].cid;
             }
         });
+        lap(10, tl2);
         if (pre_co) {  // the member slots that open a class, numbered in record order (as emit's)
             uint32_t* co = kcid + nfreq;
             std::fill(co, co + nco, kNone);
@@ -3477,7 +3484,7 @@ struct Miner {
                 q = q2;
             }
         }
-        lap(10, tl2);
+        lap(13, tl2);
         b.kid_tab.alloc(std::max<size_t>(kbytes, 4));
         ctx->stage_copy(2, b.kid_tab.p, kbytes);
         lap(11, tl2);
