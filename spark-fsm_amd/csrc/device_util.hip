@@ -1,5 +1,7 @@
 // device_util.hip — single-pass exclusive scan (decoupled look-back), the
 // device memory pool and kernel timing.
+#include <sys/mman.h>
+
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -240,6 +242,82 @@ void copy_from_mapped(void* dst, const void* src, size_t bytes, hipStream_t s) {
     hipLaunchKernelGGL(k_copy_mapped, dim3(grid), dim3(256), 0, s, static_cast<const uint4*>(src),
                        static_cast<uint4*>(dst), n16, static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), n4);
     FSM_LAUNCHED("k_copy_mapped", s);
+}
+
+// Big host blocks (>= 4 MiB: the member tables, class records and pattern-node chunks of
+// deep lattices) are kept after a mine instead of returned to the OS, up to kCacheCap bytes
+// per process, and handed to the next mine: a fresh block costs its first touch (the kernel
+// zeroes every transparent huge page on its first fault), about a third of SIGN's host time
+// (5.9M pattern nodes, hundreds of MB of tables per mine).  Blocks are 2 MiB aligned and
+// marked MADV_HUGEPAGE.
+#ifndef FSM_BIGBLOCK_MIN_MB
+#define FSM_BIGBLOCK_MIN_MB 32
+#endif
+struct BigBlocks {
+    static constexpr size_t kHuge = size_t(2) << 20;
+    static constexpr size_t kCacheCap = size_t(1) << 30;
+    // below this size glibc's own heap already recycles freed blocks (its mmap threshold
+    // rises to 32 MiB after the first free): only larger ones come through the cache
+    static constexpr size_t kMin = size_t(FSM_BIGBLOCK_MIN_MB) << 20;
+    static BigBlocks& get() {
+        static BigBlocks* b = new BigBlocks();  // (leaked on exit on purpose)
+        return *b;
+    }
+    void* take(size_t bytes) {  // bytes: a multiple of kHuge
+        if (bytes < kMin) {
+            void* q = std::aligned_alloc(kHuge, bytes);
+            if (!q) throw std::bad_alloc();
+            (void)madvise(q, bytes, MADV_HUGEPAGE);
+            return q;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto it = free_.lower_bound(bytes);
+            if (it != free_.end() && it->first <= 2 * bytes) {
+                void* p = it->second;
+                const size_t sz = it->first;
+                held_ -= sz;
+                free_.erase(it);
+                sizes_[p] = sz;
+                return p;
+            }
+        }
+        void* p = std::aligned_alloc(kHuge, bytes);
+        if (!p) throw std::bad_alloc();
+        (void)madvise(p, bytes, MADV_HUGEPAGE);
+        std::lock_guard<std::mutex> g(mu_);
+        sizes_[p] = bytes;
+        return p;
+    }
+    void give(void* p) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = sizes_.find(p);
+        const size_t sz = it == sizes_.end() ? 0 : it->second;
+        if (it != sizes_.end()) sizes_.erase(it);
+        if (sz == 0 || sz > kCacheCap) {
+            std::free(p);
+            return;
+        }
+        while (held_ + sz > kCacheCap && !free_.empty()) {  // the largest cached ones go first
+            auto last = std::prev(free_.end());
+            held_ -= last->first;
+            std::free(last->second);
+            free_.erase(last);
+        }
+        free_.emplace(sz, p);
+        held_ += sz;
+    }
+
+  private:
+    std::mutex mu_;
+    std::multimap<size_t, void*> free_;
+    std::map<void*, size_t> sizes_;  // blocks handed out (their granted size)
+    size_t held_ = 0;
+};
+
+void* big_take(size_t bytes) { return BigBlocks::get().take(bytes); }
+void big_give(void* p) {
+    if (p) BigBlocks::get().give(p);
 }
 
 bool debug_sync() {

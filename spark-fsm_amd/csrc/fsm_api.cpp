@@ -937,23 +937,24 @@ int fsm_tsr_mine(fsm_ctx* ctx, fsm_db* db, int32_t k, double minconf, fsm_rules*
     });
 }
 
+// (result arrays may be big host blocks: fsm::big_give frees malloc'ed ones, caches the others)
 void fsm_patterns_free(fsm_patterns* p) {
     if (!p) return;
-    std::free(p->support);
-    std::free(p->pat_off);
-    std::free(p->set_off);
-    std::free(p->items);
+    fsm::big_give(p->support);
+    fsm::big_give(p->pat_off);
+    fsm::big_give(p->set_off);
+    fsm::big_give(p->items);
     std::free(p);
 }
 
 void fsm_rules_free(fsm_rules* r) {
     if (!r) return;
-    std::free(r->support);
-    std::free(r->confidence);
-    std::free(r->ante_off);
-    std::free(r->ante);
-    std::free(r->cons_off);
-    std::free(r->cons);
+    fsm::big_give(r->support);
+    fsm::big_give(r->confidence);
+    fsm::big_give(r->ante_off);
+    fsm::big_give(r->ante);
+    fsm::big_give(r->cons_off);
+    fsm::big_give(r->cons);
     std::free(r);
 }
 

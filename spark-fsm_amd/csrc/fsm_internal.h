@@ -131,6 +131,13 @@ struct PoolScope {
 // a copy kernel on stream s (device_util.hip)
 void copy_from_mapped(void* dst, const void* src, size_t bytes, hipStream_t s);
 
+// Big host blocks (device_util.hip): 2 MiB aligned, MADV_HUGEPAGE; blocks of 32 MiB and more
+// are cached across mines (1 GiB per process) instead of returned to the OS.  big_take(bytes):
+// bytes a multiple of kHugeBlock; big_give(p): any pointer from big_take or malloc (freed then)
+constexpr size_t kHugeBlock = size_t(2) << 20;
+void* big_take(size_t bytes);
+void big_give(void* p);
+
 // Mapped pinned host memory (kernels write results straight into it; the host
 // reads them after a stream sync, with no copy launch).
 struct PinnedBuf {

@@ -2078,90 +2078,19 @@ struct Slab {
 // value-initialising resize would write every byte once more, serially)
 // Arrays of 4 MiB and more come 2 MiB aligned and marked for transparent huge pages
 // (a mine's Miner and batches are fresh: their tables fault in 2 MiB at a time).
-// Big host blocks (>= 4 MiB: the member tables, class records and pattern-node chunks of
-// deep lattices) are kept after a mine instead of returned to the OS, up to kCacheCap bytes
-// per process, and handed to the next mine: a fresh block costs its first touch (the kernel
-// zeroes every transparent huge page on its first fault), about a third of SIGN's host time
-// (5.9M pattern nodes, hundreds of MB of tables per mine).  Blocks are 2 MiB aligned and
-// marked MADV_HUGEPAGE.
-#ifndef FSM_BIGBLOCK_MIN_MB
-#define FSM_BIGBLOCK_MIN_MB 32
-#endif
-struct BigBlocks {
-    static constexpr size_t kHuge = size_t(2) << 20;
-    static constexpr size_t kCacheCap = size_t(1) << 30;
-    // below this size glibc's own heap already recycles freed blocks (its mmap threshold
-    // rises to 32 MiB after the first free): only larger ones come through the cache
-    static constexpr size_t kMin = size_t(FSM_BIGBLOCK_MIN_MB) << 20;
-    static BigBlocks& get() {
-        static BigBlocks* b = new BigBlocks();  // (leaked on exit on purpose)
-        return *b;
-    }
-    void* take(size_t bytes) {  // bytes: a multiple of kHuge
-        if (bytes < kMin) {
-            void* q = std::aligned_alloc(kHuge, bytes);
-            if (!q) throw std::bad_alloc();
-            (void)madvise(q, bytes, MADV_HUGEPAGE);
-            return q;
-        }
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            auto it = free_.lower_bound(bytes);
-            if (it != free_.end() && it->first <= 2 * bytes) {
-                void* p = it->second;
-                const size_t sz = it->first;
-                held_ -= sz;
-                free_.erase(it);
-                sizes_[p] = sz;
-                return p;
-            }
-        }
-        void* p = std::aligned_alloc(kHuge, bytes);
-        if (!p) throw std::bad_alloc();
-        (void)madvise(p, bytes, MADV_HUGEPAGE);
-        std::lock_guard<std::mutex> g(mu_);
-        sizes_[p] = bytes;
-        return p;
-    }
-    void give(void* p) {
-        std::lock_guard<std::mutex> g(mu_);
-        auto it = sizes_.find(p);
-        const size_t sz = it == sizes_.end() ? 0 : it->second;
-        if (it != sizes_.end()) sizes_.erase(it);
-        if (sz == 0 || sz > kCacheCap) {
-            std::free(p);
-            return;
-        }
-        while (held_ + sz > kCacheCap && !free_.empty()) {  // the largest cached ones go first
-            auto last = std::prev(free_.end());
-            held_ -= last->first;
-            std::free(last->second);
-            free_.erase(last);
-        }
-        free_.emplace(sz, p);
-        held_ += sz;
-    }
-
-  private:
-    std::mutex mu_;
-    std::multimap<size_t, void*> free_;
-    std::map<void*, size_t> sizes_;  // blocks handed out (their granted size)
-    size_t held_ = 0;
-};
-
 template <class T> struct NoInitAlloc : std::allocator<T> {
     template <class U> struct rebind { using other = NoInitAlloc<U>; };
     NoInitAlloc() = default;
     template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
-    static constexpr size_t kHuge = BigBlocks::kHuge;
+    static constexpr size_t kHuge = kHugeBlock;
     T* allocate(size_t n) {
         const size_t bytes = n * sizeof(T);
         if (bytes < 2 * kHuge) return std::allocator<T>::allocate(n);
-        return static_cast<T*>(BigBlocks::get().take((bytes + kHuge - 1) & ~(kHuge - 1)));
+        return static_cast<T*>(big_take((bytes + kHuge - 1) & ~(kHuge - 1)));
     }
     void deallocate(T* p, size_t n) {
         if (n * sizeof(T) < 2 * kHuge) std::allocator<T>::deallocate(p, n);
-        else BigBlocks::get().give(p);
+        else big_give(p);
     }
     template <class U> void construct(U*) noexcept {}
     template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
@@ -2195,7 +2124,7 @@ using ChildInfo = ClassMeta;
 // pages: the host threads that fill a fresh chunk fault it in 2 MiB at a time)
 template <class T, int kShift = 20> struct ChunkedVec {
     struct Free {
-        void operator()(T* p) const { BigBlocks::get().give(p); }
+        void operator()(T* p) const { big_give(p); }
     };
     std::vector<std::unique_ptr<T[], Free>> ch;
     size_t n = 0;
@@ -2204,9 +2133,9 @@ template <class T, int kShift = 20> struct ChunkedVec {
     T& operator[](size_t i) { return ch[i >> kShift][i & kMask]; }
     const T& operator[](size_t i) const { return ch[i >> kShift][i & kMask]; }
     void add_chunk() {
-        constexpr size_t kHuge = BigBlocks::kHuge;
+        constexpr size_t kHuge = kHugeBlock;
         const size_t bytes = ((sizeof(T) << kShift) + kHuge - 1) & ~(kHuge - 1);
-        ch.emplace_back(static_cast<T*>(BigBlocks::get().take(bytes)));
+        ch.emplace_back(static_cast<T*>(big_take(bytes)));
     }
     void push_back(const T& v) {
         if ((n >> kShift) == ch.size()) add_chunk();
@@ -4332,26 +4261,20 @@ template <class T> struct MallocArr {
     MallocArr() = default;
     explicit MallocArr(size_t n_) { alloc(n_); }
     void alloc(size_t n_) {
-        std::free(p);
+        big_give(p);
         p = nullptr;
         n = n_;
-        // large result arrays: 2 MiB aligned and marked for transparent huge pages, so
-        // the threads that fill them fault in 2 MiB at a time instead of 4 KiB (a dense
-        // mine's CSR is hundreds of MB of fresh pages); free()-compatible either way
-        static const bool thp = [] { const char* v = std::getenv("FSM_OUTPUT_THP"); return !(v && v[0] == '0'); }();
+        // large result arrays: big host blocks (2 MiB aligned, transparent huge pages, the
+        // largest reused from earlier mines: a dense mine's CSR is hundreds of MB of pages);
+        // fsm_patterns_free / fsm_rules_free hand them back through big_give
         const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-        constexpr size_t kHuge = size_t(2) << 20;
-        if (thp && bytes >= 4 * kHuge) {
-            p = static_cast<T*>(std::aligned_alloc(kHuge, (bytes + kHuge - 1) & ~(kHuge - 1)));
-            if (p) (void)madvise(p, (bytes + kHuge - 1) & ~(kHuge - 1), MADV_HUGEPAGE);
-        } else {
-            p = static_cast<T*>(std::malloc(bytes));
-        }
+        if (bytes >= 4 * kHugeBlock) p = static_cast<T*>(big_take((bytes + kHugeBlock - 1) & ~(kHugeBlock - 1)));
+        else p = static_cast<T*>(std::malloc(bytes));
         if (!p) throw Error(FSM_ENOMEM, "malloc failed");
     }
     MallocArr(const MallocArr&) = delete;
     MallocArr& operator=(const MallocArr&) = delete;
-    ~MallocArr() { std::free(p); }
+    ~MallocArr() { big_give(p); }
     T& operator[](size_t i) { return p[i]; }
     T* release() {
         T* r = p;
