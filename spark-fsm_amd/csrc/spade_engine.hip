@@ -2042,6 +2042,171 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
     if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
 }
 
+// ---- The root's frequent pairs in (row, slot) order on the device (unsharded tri F2),
+// with each record's child member id (rank of its partner item among its row's partners,
+// << 1 | type), the kid table [koff | kslot | kcid] and the member slot -> child class table,
+// so the root emit launches with no host step between the F2 count and it.  A row's
+// records have distinct slots < 2F: a bitmap of them in LDS and two prefix popcounts
+// (slots, partner items) give every record its rank, so nothing is sorted.  Four
+// launches: histogram, the row tables, bucket scatter, one block per row.
+// (No last-block fusion: the agent-scope fences it needs write back the XCD's L2 in
+// every block, which cost 0.3 ms over ~1000 row blocks.)
+
+// exclusive scan over the block (kBlock threads) of one u32 per thread; tot = the sum
+__device__ __forceinline__ uint32_t rk_block_scan(uint32_t v, uint32_t* wsum, uint32_t& tot) {
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    __syncthreads();  // (wsum's previous readers are done)
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+        before += w < wv ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    return before + inc - v;
+}
+// exclusive scan of get(0..m) by one block in per-thread chunks: put(i, prefix, get(i)); returns the sum
+template <class Get, class Put>
+__device__ uint32_t rk_scan_range(uint32_t m, uint32_t* wsum, Get get, Put put) {
+    const uint32_t ch = (m + kBlock - 1) / kBlock;
+    const uint32_t a = min(m, threadIdx.x * ch), z = min(m, a + ch);
+    uint32_t s = 0;
+    for (uint32_t i = a; i < z; ++i) s += get(i);
+    uint32_t tot;
+    uint32_t run = rk_block_scan(s, wsum, tot);
+    for (uint32_t i = a; i < z; ++i) {
+        const uint32_t g = get(i);
+        put(i, run, g);
+        run += g;
+    }
+    return tot;
+}
+__global__ __launch_bounds__(kBlock) void k_rk_hist(const FreqRec* __restrict__ R, uint32_t n,
+                                                    FreqRec* __restrict__ Rd, uint32_t* __restrict__ rowcnt,
+                                                    uint32_t* __restrict__ roweven) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const FreqRec r = R[p];  // (mapped pinned memory: read once, kept in HBM)
+        Rd[p] = r;
+        atomicAdd(&rowcnt[r.row], 1u);
+        if (!(r.slot & 1u)) roweven[r.row] = 1u;
+    }
+}
+// one tile of kRkTile rows per block: the block sums the rows before its tile itself (all
+// loads independent, no cross-block wait), then scans its tile staged through LDS.  Per row
+// one packed value: records | kept << 32 (a row opens a child class unless it is empty or
+// one lone itemset extension).  Out: row offsets, koff and the child-class table.
+constexpr uint32_t kRkV = 8, kRkTile = kBlock * kRkV;
+__global__ __launch_bounds__(kBlock) void k_rk_tables(const uint32_t* __restrict__ rowcnt,
+                                                      const uint32_t* __restrict__ roweven, uint32_t F,
+                                                      uint32_t* __restrict__ rowoff, uint32_t* __restrict__ koff,
+                                                      uint32_t* __restrict__ child_of) {
+    __shared__ uint64_t tileb[kRkTile];
+    __shared__ uint64_t wsum[kBlock / 64];
+    auto get = [&](uint32_t r) {
+        const uint32_t c = rowcnt[r];
+        return uint64_t(c) | uint64_t(c > 1u || (c == 1u && roweven[r])) << 32;
+    };
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, t0 = blockIdx.x * kRkTile;
+    uint64_t acc = 0;
+    for (uint32_t i = threadIdx.x; i < t0; i += kBlock) acc += get(i);
+#pragma unroll
+    for (uint32_t k = 0; k < kRkV; ++k) {
+        const uint32_t i = t0 + k * kBlock + threadIdx.x;
+        tileb[k * kBlock + threadIdx.x] = i < F ? get(i) : 0ull;
+    }
+    acc = wave_incl_scan(acc);
+    if (lane == 63) wsum[wv] = acc;
+    __syncthreads();
+    uint64_t carry = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w) carry += wsum[w];
+    uint64_t v[kRkV], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kRkV; ++k) sum += (v[k] = tileb[threadIdx.x * kRkV + k]);
+    const uint64_t inc = wave_incl_scan(sum);
+    __syncthreads();  // (wsum is reused)
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint64_t run = carry, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+        run += w < wv ? wsum[w] : 0ull;
+        tot += wsum[w];
+    }
+    run += inc - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < kRkV; ++k) {
+        const uint32_t r = t0 + threadIdx.x * kRkV + k;
+        if (r < F) {
+            const uint32_t off = uint32_t(run), c = uint32_t(v[k]);
+            rowoff[r] = off;
+            // a root row r is member 2r of the root class: records with slot_of < x are those of rows < (x + 1) / 2
+            koff[2 * r] = off;
+            koff[2 * r + 1] = off + c;
+            child_of[2 * r] = (v[k] >> 32) ? uint32_t(run >> 32) : kNone;
+            child_of[2 * r + 1] = kNone;
+        }
+        run += v[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        rowoff[F] = uint32_t(carry + tot);
+        koff[2 * F] = uint32_t(carry + tot);
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_rk_scatter(const FreqRec* __restrict__ Rd, uint32_t n,
+                                                       const uint32_t* __restrict__ rowoff, uint32_t* __restrict__ rowcnt,
+                                                       uint32_t* __restrict__ idx) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const uint32_t row = Rd[p].row;
+        idx[rowoff[row] + atomicSub(&rowcnt[row], 1u) - 1u] = p;  // (bucket order is free: ranks come from slots)
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_rk_row(const FreqRec* __restrict__ Rd, const uint32_t* __restrict__ idx,
+                                                   const uint32_t* __restrict__ rowoff, uint32_t F,
+                                                   FreqRec* __restrict__ out, uint32_t* __restrict__ kslot,
+                                                   uint32_t* __restrict__ kcid) {
+    extern __shared__ uint32_t rk_sm[];
+    __shared__ uint32_t wsum[kBlock / 64];
+    const uint32_t nw = (2 * F + 31) / 32;
+    uint32_t* bm = rk_sm;      // the row's slots
+    uint32_t* ps = bm + nw;    // slots in words < w
+    uint32_t* pi = ps + nw;    // partner items in words < w
+    const uint32_t r = blockIdx.x, beg = rowoff[r], c = rowoff[r + 1] - beg;
+    if (c == 0) return;  // (block-uniform)
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) bm[w] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+        const uint32_t slot = Rd[idx[beg + i]].slot;
+        atomicOr(&bm[slot >> 5], 1u << (slot & 31u));
+    }
+    __syncthreads();
+    // one scan of (slots | partner items << 16) per word: both sums <= 2F < 2^16
+    rk_scan_range(
+        nw, wsum,
+        [&](uint32_t w) {
+            const uint32_t m = bm[w];
+            return uint32_t(__popc(m)) | uint32_t(__popc((m | m >> 1) & 0x55555555u)) << 16;
+        },
+        [&](uint32_t w, uint32_t pre, uint32_t) {
+            ps[w] = pre & 0xFFFFu;
+            pi[w] = pre >> 16;
+        });
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+        FreqRec rec = Rd[idx[beg + i]];
+        const uint32_t w = rec.slot >> 5, bt = rec.slot & 31u, m = bm[w];
+        const uint32_t rank = ps[w] + uint32_t(__popc(m & ((1u << bt) - 1u)));
+        const uint32_t crank = pi[w] + uint32_t(__popc((m | m >> 1) & 0x55555555u & ((1u << (bt & ~1u)) - 1u)));
+        rec.cid = crank << 1 | (rec.slot & 1u);
+        out[beg + rank] = rec;
+        kslot[beg + rank] = rec.slot;
+        kcid[beg + rank] = rec.cid;
+    }
+}
+
 // ------------------------------------------------------------- host side
 
 #define FSM_W_DISPATCH(W_, MACRO) \
@@ -2210,6 +2375,11 @@ struct Batch {
     const uint32_t* child_of_pre = nullptr;  // deferred, host child_of: uploaded with the kid table
     // the root's unordered-pair F2 keys, launched by run_root_db right after its plan (the host's
     // root bookkeeping then overlaps them): keys, region fills, the counters block
+    // the root's records ordered on the device (root_order_device): the kid and child-class
+    // tables are device-built; the ordered records reach pinned host memory at rec_ev
+    bool dev_order = false;
+    DevBuf root_child_of;
+    hipEvent_t rec_ev = nullptr;
     bool f2_launched = false;
     DevBuf f2_keys, f2_fill, f2_ctr_own;
     char* f2_ctr = nullptr;
@@ -2264,6 +2434,10 @@ struct Batch {
         defer_R = nullptr;
         defer_rows = nullptr;
         child_of_pre = nullptr;
+        dev_order = false;
+        root_child_of.release();
+        if (rec_ev) (void)hipEventDestroy(rec_ev);
+        rec_ev = nullptr;
         f2_launched = false;
         f2_keys.release();
         f2_fill.release();
@@ -3005,6 +3179,14 @@ struct Miner {
                 if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
                 const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
                 double tr = now_ms();
+                if (root_order_device(b, pb, nrec, F)) {
+                    recs.clear();
+                    lap(14, tr);
+                    clk->add_bytes(tk_keys, int64_t(nkeys) * 2);
+                    clk->add_bytes(tk_cnt, int64_t(nkeys) * 2 + int64_t(nrec) * int64_t(sizeof(FreqRec)));
+                    ctx->stats.root_keys += int64_t(nkeys);
+                    return true;
+                }
                 recs.assign(hr, hr + nrec);
                 lap(14, tr);
                 break;
@@ -3022,6 +3204,65 @@ struct Miner {
         hp[0] += now_ms() - th0;
         return true;
     }
+    // FSM_ROOT_DEVORDER=0: the root's records ordered on the host (A/B)
+    static bool root_devorder_env() {
+        static const bool on = [] { const char* v = std::getenv("FSM_ROOT_DEVORDER"); return !(v && v[0] == '0'); }();
+        return on;
+    }
+    // The root's nrec frequent pair records (unordered, mapped pinned memory pb) ordered on the
+    // device with the kid table and the child-class table (k_rk_*), the ordered records copied
+    // back into pb (event b.rec_ev), and the batch set up for a deferred emit whose slab is sized
+    // by every record's support (the lone itemset extensions' entries are counted out when the
+    // children are built).  false: the host orders them (sharded, too many ranks, over budget).
+    bool root_order_device(Batch& b, PinnedBuf* pb, uint32_t nrec, uint32_t F) {
+        if (comm || !b.f2_tri || F >= (1u << 15) || nrec == 0 || !root_devorder_env() || b.claim_key >= 0) return false;
+        const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
+        uint64_t sumsup = 0;
+        for (uint32_t q = 0; q < nrec; ++q) sumsup += hr[q].sup;
+        const uint64_t dn = 2ull * nrec + 2ull * F;  // bounds the next batch's member id spaces
+        if (sumsup * entry_bytes() + dn * dn * 4 > budget || sumsup > (uint64_t(1) << 31)) return false;
+        const uint32_t n = nrec;
+        const FreqRec* R = static_cast<const FreqRec*>(pb->dev);
+        const size_t nko = size_t(2) * F + 1;
+        DevBuf Rd(size_t(n) * sizeof(FreqRec)), rowcnt(size_t(2) * F * 4), rowoff(size_t(F + 1) * 4),
+            idx(size_t(n) * 4), out(size_t(n) * sizeof(FreqRec));
+        b.kid_tab.alloc((nko + 2 * size_t(n)) * 4);
+        b.root_child_of.alloc(size_t(2) * F * 4);
+        uint32_t* cnt = rowcnt.as<uint32_t>();  // [F row counts | F rows-with-an-even-slot flags]
+        FSM_HIP(hipMemsetAsync(cnt, 0, size_t(2) * F * 4, s));
+        const unsigned gn = unsigned(std::min<uint64_t>((uint64_t(n) + kBlock - 1) / kBlock, 1024));
+        hipLaunchKernelGGL(k_rk_hist, dim3(gn), dim3(kBlock), 0, s, R, n, Rd.as<FreqRec>(), cnt, cnt + F);
+        FSM_LAUNCHED("k_rk_hist", s);
+        uint32_t* koff = b.kid_tab.as<uint32_t>();
+        hipLaunchKernelGGL(k_rk_tables, dim3((F + kRkTile - 1) / kRkTile), dim3(kBlock), 0, s, cnt, cnt + F, F, rowoff.as<uint32_t>(), koff,
+                           b.root_child_of.as<uint32_t>());
+        FSM_LAUNCHED("k_rk_tables", s);
+        hipLaunchKernelGGL(k_rk_scatter, dim3(gn), dim3(kBlock), 0, s, Rd.as<FreqRec>(), n, rowoff.as<uint32_t>(), cnt,
+                           idx.as<uint32_t>());
+        FSM_LAUNCHED("k_rk_scatter", s);
+        const size_t lds = size_t(3) * ((2 * F + 31) / 32) * 4;  // (F < 2^15: at most 24 KiB)
+        hipLaunchKernelGGL(k_rk_row, dim3(F), dim3(kBlock), lds, s, Rd.as<FreqRec>(), idx.as<uint32_t>(),
+                           rowoff.as<uint32_t>(), F, out.as<FreqRec>(), koff + nko, koff + nko + n);
+        FSM_LAUNCHED("k_rk_row", s);
+        FSM_HIP(hipMemcpyAsync(pb->host, out.p, size_t(n) * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
+        if (!b.rec_ev) FSM_HIP(hipEventCreateWithFlags(&b.rec_ev, hipEventDisableTiming));
+        FSM_HIP(hipEventRecord(b.rec_ev, s));
+        b.kid_off = b.kid_tab.as<uint32_t>();
+        b.kid_slot = b.kid_off + nko;
+        b.kid_cid = b.kid_slot + n;
+        b.child_of_pre = b.root_child_of.as<uint32_t>();
+        b.dev_order = true;
+        b.defer_children = true;
+        b.defer_R = hr;
+        b.defer_n = nrec;
+        b.defer_total = sumsup;  // (an upper bound: emit() counts the children's entries exactly)
+        b.defer_rows = &rows_s;
+        b.children.clear();
+        b.groups.assign(1, {size_t(0), size_t(0)});  // (the child count: set by emit())
+        b.next_group = 0;
+        return true;
+    }
+
     // The children loop of count_and_freq split over host threads (unsharded, large
     // batches; same tables, same node ids: node of record q = first + q).  Every step
     // runs over the same host-thread slices: row groups of the records (counts, then
@@ -3406,6 +3647,10 @@ struct Miner {
         double th = now_ms();
         // kids CSR over (cbase + mi): the frequent children of every member, by slot
         // one table, one H2D copy: [koff: cbase_total + 1 | kslot: nfreq | kcid: nfreq]
+        if (b.dev_order) {  // kid and child-class tables built on the device; emit() builds the children
+            hp[1] += now_ms() - th;
+            return;
+        }
         const size_t nko = size_t(b.cbase_total) + 1;
         bool defer_checked = false;
         if (kids_dev) {
@@ -4019,9 +4264,20 @@ struct Miner {
             // moved over whole (the only group)
             const double td = now_ms();
             b.defer_children = false;
+            if (b.dev_order) FSM_HIP(hipEventSynchronize(b.rec_ev));  // the ordered records (pinned)
             make_children(b, b.defer_R, b.defer_n, *b.defer_rows);
-            if (b.children.size() != gb)
+            if (b.dev_order) {
+                // the exact child entries (the slab was sized by every record's support)
+                uint64_t exact = 0;
+                for (const ChildInfo& c : b.children) exact += c.cap;
+                if (exact > nb.slab.cap)
+                    throw Error(FSM_EDEVICE, "SPADE internal error: root children exceed their slab");
+                nb.E = exact;
+                pend_total = exact;
+                b.groups[0].second = b.children.size();
+            } else if (b.children.size() != gb) {
                 throw Error(FSM_EDEVICE, "SPADE internal error: deferred children do not match the emit group");
+            }
             if (b.root)
                 for (const ChildInfo& c : b.children) ctx->stats.rank_root_owned += int64_t(c.psup);
             nb.cls.clear();
