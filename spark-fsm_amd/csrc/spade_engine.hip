@@ -897,26 +897,30 @@ __device__ __forceinline__ void tri_keys(uint64_t M0, uint64_t M1, uint64_t M2, 
 }
 
 // The pair (ie, je) of a row staged in LDS (je == ie: the repeat), okm the lanes with a pair,
-// lanes [st, en] sharing ie.  A staged entry: x = 3 rank | group << 16, y = lo | hi << 8 |
-// (A + kTriA) << 16 with A = (first counter of its row) - 3 rank - 2, z / w its mask: the key of
-// (i -> j) is then A_i + 3 rank_j, that of the repeat A_i + 3 rank_i + 2 (the row's first counter).
+// lanes [st, en] sharing ie.  A staged entry is two 8-byte words (two arrays, so the lanes'
+// consecutive je read consecutive 8-byte slots, and a 16-byte AoS entry's bank aliasing
+// between the folded segments is gone): d.x = 3 rank (mod 2^16) | lo << 16 | hi << 24,
+// d.y = (A + kTriA) | group << 16 with A = (first counter of its row) - 3 rank - 2, and the
+// mask: the key of (i -> j) is then A_i + 3 rank_j, that of the repeat A_i + 3 rank_i + 2 (the
+// row's first counter).
 constexpr uint32_t kTriA = 32770u;
 __device__ __forceinline__ void tri_pair(uint64_t okm, uint32_t ie, uint32_t je, uint32_t st, uint32_t en,
-                                         const uint4* __restrict__ stage, uint32_t* __restrict__ cur,
-                                         uint16_t* __restrict__ keys) {
+                                         const uint2* __restrict__ sd, const uint64_t* __restrict__ smk,
+                                         uint32_t* __restrict__ cur, uint16_t* __restrict__ keys) {
     const bool ok = (okm >> lane_id()) & 1ull;
-    const uint4 Ei = stage[ok ? ie : 0], Ej = stage[ok ? je : 0];
-    const uint32_t lo_i = Ei.y & 0xFFu, hi_i = (Ei.y >> 8) & 0xFFu, lo_j = Ej.y & 0xFFu, hi_j = (Ej.y >> 8) & 0xFFu;
+    const uint32_t qi = ok ? ie : 0u, qj = ok ? je : 0u;
+    const uint2 Di = sd[qi], Dj = sd[qj];
+    const uint64_t mm = smk[qi], mj = smk[qj];
+    const uint32_t lo_i = (Di.x >> 16) & 0xFFu, hi_i = Di.x >> 24, lo_j = (Dj.x >> 16) & 0xFFu, hi_j = Dj.x >> 24;
     const bool self = je == ie;
     const uint64_t sm = eq_mask(je, ie);
     const uint32_t hs = self ? hi_i : hi_j;
-    const uint64_t mm = Ei.z | (uint64_t(Ei.w) << 32), mj = Ej.z | (uint64_t(Ej.w) << 32);
     const uint64_t M0 = okm & lt_mask(lo_i, hs);
     const uint64_t M1 = okm & ~sm & lt_mask(lo_j, hi_i);
     const uint64_t M2 = okm & ~sm & nz_mask(mm & mj);
     const bool t0 = ok && lo_i < hs, t1 = ok && !self && lo_j < hi_i, t2 = ok && !self && (mm & mj) != 0ull;
-    const uint32_t key0 = (Ei.y >> 16) - kTriA + (Ej.x & 0xFFFFu) + (self ? 2u : 0u);
-    tri_keys(M0, M1, M2, t0, t1, t2, key0, Ei.x >> 16, st, en, cur, keys);
+    const uint32_t key0 = (Di.y & 0xFFFFu) - kTriA + (Dj.x & 0xFFFFu) + (self ? 2u : 0u);
+    tri_keys(M0, M1, M2, t0, t1, t2, key0, Di.y >> 16, st, en, cur, keys);
 }
 
 __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restrict__ row_off32,
@@ -927,7 +931,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
                                                       uint32_t* __restrict__ fill, uint16_t* __restrict__ keys,
                                                       unsigned long long* __restrict__ nkeys_total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint4* stage_all = reinterpret_cast<uint4*>(smem);            // kF2Waves x 64 staged entries (tri_pair)
+    uint2* sd_all = reinterpret_cast<uint2*>(smem);               // kF2Waves x 64 staged entries (tri_pair):
+    uint64_t* smk_all = reinterpret_cast<uint64_t*>(sd_all + kF2Waves * 64);  // words, then masks
     uint32_t* srow = smem + kF2Waves * 64 * 4;                     // row offsets of the block [rpb + 1]
     uint32_t* cur = srow + kF2RowWords;                            // region cursors [G]
     __shared__ uint32_t blk_keys;
@@ -938,7 +943,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
     if (threadIdx.x == 0) blk_keys = 0;
     __syncthreads();
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    uint4* stage = stage_all + wave * 64;
+    uint2* sd = sd_all + wave * 64;
+    uint64_t* smk = smk_all + wave * 64;
     const uint64_t lt = lanemask_lt();
     // the next row's entries are loaded while the current row is enumerated
     uint32_t nrb = 0, nrl = 0, nme = 0;
@@ -973,8 +979,8 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
                 const uint32_t gt = act ? gtab[rk] : 0u;
                 const uint32_t A = (gt & (kGroupCounters - 1u)) - 3u * rk - 2u + kTriA;  // (active entries only)
                 const uint32_t lh = uint32_t(__builtin_ctzll(mk)) | ((63u - uint32_t(__builtin_clzll(mk))) << 8);
-                stage[p] = make_uint4(3u * rk | ((gt >> kGroupShift) << 16), lh | (A << 16), uint32_t(mk),
-                                      uint32_t(mk >> 32));
+                sd[p] = make_uint2(((3u * rk) & 0xFFFFu) | (lh << 16), (A & 0xFFFFu) | ((gt >> kGroupShift) << 16));
+                smk[p] = mk;
             }
             __builtin_amdgcn_wave_barrier();
             const uint32_t need = 2u * n + 1u - a0 - a1;  // partners of a folded pair of entries
@@ -992,13 +998,13 @@ __global__ __launch_bounds__(kF2Threads) void k_f2_tri(const uint32_t* __restric
                     const uint64_t okm = lt_mask(fp, npairs) & lt_mask(je, n) & (~sec | lt_mask(iA, iB));
                     // the run of lanes of ie: [s0, s0 + cA) for iA, [s0 + cA, s0 + S) for iB
                     const uint32_t st = second ? s0 + cA : s0, en = second ? s0 + S - 1u : s0 + cA - 1u;
-                    tri_pair(okm, ie, je, st, en, stage, cur, keys);
+                    tri_pair(okm, ie, je, st, en, sd, smk, cur, keys);
                 }
             } else {
                 for (uint32_t i = a0; i < a1; ++i)
                     for (uint32_t c0 = 0; i + c0 < n; c0 += 64) {
                         const uint32_t je = i + c0 + lane;
-                        tri_pair(lt_mask(je, n), i, je, 0u, 63u, stage, cur, keys);
+                        tri_pair(lt_mask(je, n), i, je, 0u, 63u, sd, smk, cur, keys);
                     }
             }
             __builtin_amdgcn_wave_barrier();
