@@ -2048,15 +2048,27 @@ __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* _
     if (threadIdx.x == 0 && blk_tests) atomicAdd(tests, (unsigned long long)blk_tests);
 }
 
-// ---- The root's frequent pairs in (row, slot) order on the device (unsharded tri F2),
-// with each record's child member id (rank of its partner item among its row's partners,
+// ---- A batch's frequent records in (row, slot) order on the device (unsharded, one emit
+// group): each record's child member id (rank of its partner item among its row's partners,
 // << 1 | type), the kid table [koff | kslot | kcid] and the member slot -> child class table,
-// so the root emit launches with no host step between the F2 count and it.  A row's
-// records have distinct slots < 2F: a bitmap of them in LDS and two prefix popcounts
-// (slots, partner items) give every record its rank, so nothing is sorted.  Four
-// launches: histogram, the row tables, bucket scatter, one block per row.
-// (No last-block fusion: the agent-scope fences it needs write back the XCD's L2 in
-// every block, which cost 0.3 ms over ~1000 row blocks.)
+// so the next emit launches with no host ordering between the count and it.  A row's
+// records have distinct slots below its class's member id space D: a bitmap of them in LDS
+// and two prefix popcounts (slots, partner items) give every record its rank, so nothing
+// is sorted.  Four launches: histogram, the row tables, bucket scatter, one block per row.
+// (No last-block fusion: the agent-scope fences it needs write back the XCD's L2 in every
+// block, which cost 0.3 ms over ~1000 row blocks.)  Rows: the root's (row r = member 2r of
+// the one root class, D = 2F) or a batch's counter rows (RkRows: class and member per row).
+struct RkRows {
+    const DRow* rows;     // nullptr: the root (row r: member slot 2r, D = 2F)
+    const DClass* cls;
+    uint32_t F;
+    __device__ __forceinline__ uint32_t slot(uint32_t r) const {
+        if (!rows) return 2u * r;
+        const DRow d = rows[r];
+        return cls[d.cls].cbase + d.mi;
+    }
+    __device__ __forceinline__ uint32_t width(uint32_t r) const { return rows ? cls[rows[r].cls].D : 2u * F; }
+};
 
 // exclusive scan over the block (kBlock threads) of one u32 per thread; tot = the sum
 __device__ __forceinline__ uint32_t rk_block_scan(uint32_t v, uint32_t* wsum, uint32_t& tot) {
@@ -2090,38 +2102,42 @@ __device__ uint32_t rk_scan_range(uint32_t m, uint32_t* wsum, Get get, Put put) 
     }
     return tot;
 }
+// rowcnt[r]: the row's records | 1 << 31 if one of them has an even slot (a sequence extension)
+constexpr uint32_t kRkEven = 1u << 31;
 __global__ __launch_bounds__(kBlock) void k_rk_hist(const FreqRec* __restrict__ R, uint32_t n,
-                                                    FreqRec* __restrict__ Rd, uint32_t* __restrict__ rowcnt,
-                                                    uint32_t* __restrict__ roweven) {
+                                                    FreqRec* __restrict__ Rd, uint32_t* __restrict__ rowcnt) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const FreqRec r = R[p];  // (mapped pinned memory: read once, kept in HBM)
         Rd[p] = r;
-        atomicAdd(&rowcnt[r.row], 1u);
-        if (!(r.slot & 1u)) roweven[r.row] = 1u;
+        atomicAdd(&rowcnt[r.row], (r.slot & 1u) ? 1u : 1u | kRkEven);
     }
 }
 // one tile of kRkTile rows per block: the block sums the rows before its tile itself (all
 // loads independent, no cross-block wait), then scans its tile staged through LDS.  Per row
 // one packed value: records | kept << 32 (a row opens a child class unless it is empty or
-// one lone itemset extension).  Out: row offsets, koff and the child-class table.
+// one lone itemset extension).  Out: row offsets; over the member slots x in (slot(r - 1),
+// slot(r)] koff[x] = the row's offset and child_of[x] = its class at slot(r), else none
+// (the last row also fills the slots above it up to nko).
 constexpr uint32_t kRkV = 8, kRkTile = kBlock * kRkV;
-__global__ __launch_bounds__(kBlock) void k_rk_tables(const uint32_t* __restrict__ rowcnt,
-                                                      const uint32_t* __restrict__ roweven, uint32_t F,
-                                                      uint32_t* __restrict__ rowoff, uint32_t* __restrict__ koff,
-                                                      uint32_t* __restrict__ child_of) {
+__global__ __launch_bounds__(kBlock) void k_rk_tables(const uint32_t* __restrict__ rowcnt, uint32_t nrows,
+                                                      RkRows rr, uint32_t nko, uint32_t* __restrict__ rowoff,
+                                                      uint32_t* __restrict__ koff, uint32_t* __restrict__ child_of) {
     __shared__ uint64_t tileb[kRkTile];
+    __shared__ uint32_t sslot[kRkTile];  // the tile's member slots (loaded with the counts)
     __shared__ uint64_t wsum[kBlock / 64];
     auto get = [&](uint32_t r) {
-        const uint32_t c = rowcnt[r];
-        return uint64_t(c) | uint64_t(c > 1u || (c == 1u && roweven[r])) << 32;
+        const uint32_t w = rowcnt[r], c = w & ~kRkEven;
+        return uint64_t(c) | uint64_t(c > 1u || (c == 1u && (w & kRkEven))) << 32;
     };
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, t0 = blockIdx.x * kRkTile;
     uint64_t acc = 0;
+#pragma unroll 8
     for (uint32_t i = threadIdx.x; i < t0; i += kBlock) acc += get(i);
 #pragma unroll
     for (uint32_t k = 0; k < kRkV; ++k) {
         const uint32_t i = t0 + k * kBlock + threadIdx.x;
-        tileb[k * kBlock + threadIdx.x] = i < F ? get(i) : 0ull;
+        tileb[k * kBlock + threadIdx.x] = i < nrows ? get(i) : 0ull;
+        sslot[k * kBlock + threadIdx.x] = i < nrows ? rr.slot(i) : 0u;
     }
     acc = wave_incl_scan(acc);
     if (lane == 63) wsum[wv] = acc;
@@ -2136,30 +2152,36 @@ __global__ __launch_bounds__(kBlock) void k_rk_tables(const uint32_t* __restrict
     __syncthreads();  // (wsum is reused)
     if (lane == 63) wsum[wv] = inc;
     __syncthreads();
-    uint64_t run = carry, tot = 0;
+    uint64_t run = carry;
 #pragma unroll
-    for (uint32_t w = 0; w < kBlock / 64; ++w) {
-        run += w < wv ? wsum[w] : 0ull;
-        tot += wsum[w];
-    }
+    for (uint32_t w = 0; w < kBlock / 64; ++w) run += w < wv ? wsum[w] : 0ull;
     run += inc - sum;
+    const uint32_t first = t0 + threadIdx.x * kRkV;
+    // the first member slot after row first - 1 (read only for a thread that has rows)
+    uint32_t prev = first == 0 || first >= nrows ? 0u : (first > t0 ? sslot[first - 1u - t0] : rr.slot(first - 1u)) + 1u;
 #pragma unroll
     for (uint32_t k = 0; k < kRkV; ++k) {
-        const uint32_t r = t0 + threadIdx.x * kRkV + k;
-        if (r < F) {
-            const uint32_t off = uint32_t(run), c = uint32_t(v[k]);
+        const uint32_t r = first + k;
+        if (r < nrows) {
+            const uint32_t off = uint32_t(run), sr = sslot[r - t0];
+            for (uint32_t x = prev; x < sr; ++x) {  // member slots without a counter row
+                koff[x] = off;
+                child_of[x] = kNone;
+            }
             rowoff[r] = off;
-            // a root row r is member 2r of the root class: records with slot_of < x are those of rows < (x + 1) / 2
-            koff[2 * r] = off;
-            koff[2 * r + 1] = off + c;
-            child_of[2 * r] = (v[k] >> 32) ? uint32_t(run >> 32) : kNone;
-            child_of[2 * r + 1] = kNone;
+            koff[sr] = off;
+            child_of[sr] = (v[k] >> 32) ? uint32_t(run >> 32) : kNone;
+            prev = sr + 1u;
+            if (r == nrows - 1u) {
+                const uint32_t n = uint32_t(run + v[k]);
+                rowoff[nrows] = n;
+                for (uint32_t x = prev; x < nko; ++x) {
+                    koff[x] = n;
+                    if (x < nko - 1u) child_of[x] = kNone;
+                }
+            }
         }
         run += v[k];
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
-        rowoff[F] = uint32_t(carry + tot);
-        koff[2 * F] = uint32_t(carry + tot);
     }
 }
 __global__ __launch_bounds__(kBlock) void k_rk_scatter(const FreqRec* __restrict__ Rd, uint32_t n,
@@ -2167,21 +2189,22 @@ __global__ __launch_bounds__(kBlock) void k_rk_scatter(const FreqRec* __restrict
                                                        uint32_t* __restrict__ idx) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const uint32_t row = Rd[p].row;
-        idx[rowoff[row] + atomicSub(&rowcnt[row], 1u) - 1u] = p;  // (bucket order is free: ranks come from slots)
+        // (bucket order is free: ranks come from slots)
+        idx[rowoff[row] + (atomicSub(&rowcnt[row], 1u) & ~kRkEven) - 1u] = p;
     }
 }
 __global__ __launch_bounds__(kBlock) void k_rk_row(const FreqRec* __restrict__ Rd, const uint32_t* __restrict__ idx,
-                                                   const uint32_t* __restrict__ rowoff, uint32_t F,
+                                                   const uint32_t* __restrict__ rowoff, RkRows rr, uint32_t nwmax,
                                                    FreqRec* __restrict__ out, uint32_t* __restrict__ kslot,
                                                    uint32_t* __restrict__ kcid) {
     extern __shared__ uint32_t rk_sm[];
     __shared__ uint32_t wsum[kBlock / 64];
-    const uint32_t nw = (2 * F + 31) / 32;
-    uint32_t* bm = rk_sm;      // the row's slots
-    uint32_t* ps = bm + nw;    // slots in words < w
-    uint32_t* pi = ps + nw;    // partner items in words < w
     const uint32_t r = blockIdx.x, beg = rowoff[r], c = rowoff[r + 1] - beg;
     if (c == 0) return;  // (block-uniform)
+    const uint32_t nw = (rr.width(r) + 31) / 32;  // (<= nwmax: the LDS the host sized)
+    uint32_t* bm = rk_sm;       // the row's slots
+    uint32_t* ps = bm + nwmax;  // slots in words < w
+    uint32_t* pi = ps + nwmax;  // partner items in words < w
     for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) bm[w] = 0;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
@@ -2189,7 +2212,7 @@ __global__ __launch_bounds__(kBlock) void k_rk_row(const FreqRec* __restrict__ R
         atomicOr(&bm[slot >> 5], 1u << (slot & 31u));
     }
     __syncthreads();
-    // one scan of (slots | partner items << 16) per word: both sums <= 2F < 2^16
+    // one scan of (slots | partner items << 16) per word: both sums <= D < 2^16
     rk_scan_range(
         nw, wsum,
         [&](uint32_t w) {
@@ -2381,10 +2404,10 @@ struct Batch {
     const uint32_t* child_of_pre = nullptr;  // deferred, host child_of: uploaded with the kid table
     // the root's unordered-pair F2 keys, launched by run_root_db right after its plan (the host's
     // root bookkeeping then overlaps them): keys, region fills, the counters block
-    // the root's records ordered on the device (root_order_device): the kid and child-class
-    // tables are device-built; the ordered records reach pinned host memory at rec_ev
+    // the records ordered on the device (order_device): the kid and child-class tables are
+    // device-built; the ordered records reach pinned host memory at rec_ev
     bool dev_order = false;
-    DevBuf root_child_of;
+    DevBuf ord_child_of;
     hipEvent_t rec_ev = nullptr;
     bool f2_launched = false;
     DevBuf f2_keys, f2_fill, f2_ctr_own;
@@ -2441,7 +2464,7 @@ struct Batch {
         defer_rows = nullptr;
         child_of_pre = nullptr;
         dev_order = false;
-        root_child_of.release();
+        ord_child_of.release();
         if (rec_ev) (void)hipEventDestroy(rec_ev);
         rec_ev = nullptr;
         f2_launched = false;
@@ -3185,7 +3208,7 @@ struct Miner {
                 if (nrec > cap_recs) throw Error(FSM_EDEVICE, "SPADE root F2: frequent pair buffer overflow");
                 const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
                 double tr = now_ms();
-                if (root_order_device(b, pb, nrec, F)) {
+                if (b.f2_tri && F < (1u << 15) && order_device(b, pb, nrec, F, RkRows{nullptr, nullptr, F}, 2 * F, 2 * size_t(F) + 1)) {
                     recs.clear();
                     lap(14, tr);
                     clk->add_bytes(tk_keys, int64_t(nkeys) * 2);
@@ -3210,53 +3233,57 @@ struct Miner {
         hp[0] += now_ms() - th0;
         return true;
     }
-    // FSM_ROOT_DEVORDER=0: the root's records ordered on the host (A/B)
-    static bool root_devorder_env() {
-        static const bool on = [] { const char* v = std::getenv("FSM_ROOT_DEVORDER"); return !(v && v[0] == '0'); }();
+    // FSM_DEVORDER=0: a batch's records ordered on the host (A/B)
+    static bool devorder_env() {
+        static const bool on = [] { const char* v = std::getenv("FSM_DEVORDER"); return !(v && v[0] == '0'); }();
         return on;
     }
-    // The root's nrec frequent pair records (unordered, mapped pinned memory pb) ordered on the
-    // device with the kid table and the child-class table (k_rk_*), the ordered records copied
-    // back into pb (event b.rec_ev), and the batch set up for a deferred emit whose slab is sized
-    // by every record's support (the lone itemset extensions' entries are counted out when the
-    // children are built).  false: the host orders them (sharded, too many ranks, over budget).
-    bool root_order_device(Batch& b, PinnedBuf* pb, uint32_t nrec, uint32_t F) {
-        if (comm || !b.f2_tri || F >= (1u << 15) || nrec == 0 || !root_devorder_env() || b.claim_key >= 0) return false;
+    // A batch's nrec frequent records (unordered, mapped pinned memory pb) ordered on the device
+    // with the kid table [koff: nko | kslot | kcid] and the child-class table (k_rk_*), written
+    // back into pb in order (event b.rec_ev), and the batch set up for a deferred emit whose slab
+    // is sized by every record's support (the lone itemset extensions' entries are counted out
+    // when the children are built).  rr: the counter rows (nrows), dmax: the largest member id
+    // space of a row's class.  false: the host orders them (sharded, claims, over budget).
+    bool order_device(Batch& b, PinnedBuf* pb, uint32_t nrec, uint32_t nrows, RkRows rr, uint32_t dmax, size_t nko) {
+        if (comm || nrec == 0 || nrows == 0 || !devorder_env() || defer_env() == 0 || b.claim_key >= 0 ||
+            dmax >= (1u << 16) || nko >= kNone)
+            return false;
         const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
         uint64_t sumsup = 0;
         for (uint32_t q = 0; q < nrec; ++q) sumsup += hr[q].sup;
-        const uint64_t dn = 2ull * nrec + 2ull * F;  // bounds the next batch's member id spaces
-        if (sumsup * entry_bytes() + dn * dn * 4 > budget || sumsup > (uint64_t(1) << 31)) return false;
+        // a row's c records give its child class D <= 2c <= 2 dmax members: sum (2c)^2 4 B <= 16 nrec dmax
+        if (sumsup * entry_bytes() + 16ull * nrec * dmax > budget || sumsup > (uint64_t(1) << 31)) return false;
         const uint32_t n = nrec;
-        const FreqRec* R = static_cast<const FreqRec*>(pb->dev);
-        const size_t nko = size_t(2) * F + 1;
-        DevBuf Rd(size_t(n) * sizeof(FreqRec)), rowcnt(size_t(2) * F * 4), rowoff(size_t(F + 1) * 4),
-            idx(size_t(n) * 4), out(size_t(n) * sizeof(FreqRec));
+        FreqRec* R = static_cast<FreqRec*>(pb->dev);
+        DevBuf Rd(size_t(n) * sizeof(FreqRec)), rowcnt(size_t(nrows) * 4), rowoff(size_t(nrows + 1) * 4),
+            idx(size_t(n) * 4);
         b.kid_tab.alloc((nko + 2 * size_t(n)) * 4);
-        b.root_child_of.alloc(size_t(2) * F * 4);
-        uint32_t* cnt = rowcnt.as<uint32_t>();  // [F row counts | F rows-with-an-even-slot flags]
-        FSM_HIP(hipMemsetAsync(cnt, 0, size_t(2) * F * 4, s));
+        b.ord_child_of.alloc(std::max<size_t>(nko - 1, 1) * 4);
+        uint32_t* cnt = rowcnt.as<uint32_t>();  // row counts | kRkEven
+        FSM_HIP(hipMemsetAsync(cnt, 0, size_t(nrows) * 4, s));
         const unsigned gn = unsigned(std::min<uint64_t>((uint64_t(n) + kBlock - 1) / kBlock, 1024));
-        hipLaunchKernelGGL(k_rk_hist, dim3(gn), dim3(kBlock), 0, s, R, n, Rd.as<FreqRec>(), cnt, cnt + F);
+        hipLaunchKernelGGL(k_rk_hist, dim3(gn), dim3(kBlock), 0, s, R, n, Rd.as<FreqRec>(), cnt);
         FSM_LAUNCHED("k_rk_hist", s);
         uint32_t* koff = b.kid_tab.as<uint32_t>();
-        hipLaunchKernelGGL(k_rk_tables, dim3((F + kRkTile - 1) / kRkTile), dim3(kBlock), 0, s, cnt, cnt + F, F, rowoff.as<uint32_t>(), koff,
-                           b.root_child_of.as<uint32_t>());
+        hipLaunchKernelGGL(k_rk_tables, dim3((nrows + kRkTile - 1) / kRkTile), dim3(kBlock), 0, s, cnt, nrows, rr,
+                           uint32_t(nko), rowoff.as<uint32_t>(), koff, b.ord_child_of.as<uint32_t>());
         FSM_LAUNCHED("k_rk_tables", s);
         hipLaunchKernelGGL(k_rk_scatter, dim3(gn), dim3(kBlock), 0, s, Rd.as<FreqRec>(), n, rowoff.as<uint32_t>(), cnt,
                            idx.as<uint32_t>());
         FSM_LAUNCHED("k_rk_scatter", s);
-        const size_t lds = size_t(3) * ((2 * F + 31) / 32) * 4;  // (F < 2^15: at most 24 KiB)
-        hipLaunchKernelGGL(k_rk_row, dim3(F), dim3(kBlock), lds, s, Rd.as<FreqRec>(), idx.as<uint32_t>(),
-                           rowoff.as<uint32_t>(), F, out.as<FreqRec>(), koff + nko, koff + nko + n);
+        const uint32_t nwmax = (dmax + 31) / 32;
+        const size_t lds = size_t(3) * nwmax * 4;  // (dmax < 2^16: at most 24 KiB)
+        // the ordered records go straight back over the unordered ones in pinned memory
+        // (k_rk_hist has copied those into HBM)
+        hipLaunchKernelGGL(k_rk_row, dim3(nrows), dim3(kBlock), lds, s, Rd.as<FreqRec>(), idx.as<uint32_t>(),
+                           rowoff.as<uint32_t>(), rr, nwmax, R, koff + nko, koff + nko + n);
         FSM_LAUNCHED("k_rk_row", s);
-        FSM_HIP(hipMemcpyAsync(pb->host, out.p, size_t(n) * sizeof(FreqRec), hipMemcpyDeviceToHost, s));
         if (!b.rec_ev) FSM_HIP(hipEventCreateWithFlags(&b.rec_ev, hipEventDisableTiming));
         FSM_HIP(hipEventRecord(b.rec_ev, s));
         b.kid_off = b.kid_tab.as<uint32_t>();
         b.kid_slot = b.kid_off + nko;
         b.kid_cid = b.kid_slot + n;
-        b.child_of_pre = b.root_child_of.as<uint32_t>();
+        b.child_of_pre = b.ord_child_of.as<uint32_t>();
         b.dev_order = true;
         b.defer_children = true;
         b.defer_R = hr;
@@ -3605,6 +3632,16 @@ struct Miner {
                     nf = uint32_t(pend[1] & 0xFFFFFFFFu);
                 }
                 if (nf <= cap_recs) {
+                    // unsharded, one emit group: ordered on the device, the children deferred to emit()
+                    if (nf && rlo == 0 && nrows == rows.size() && !comm && !kids_host()) {
+                        uint32_t dmax = 0;
+                        for (const ClassMeta& m : b.cls) dmax = std::max(dmax, m.D);
+                        if (order_device(b, pb, nf, nrows, RkRows{d_rows.as<DRow>(), b.d_cls.as<DClass>(), 0u}, dmax,
+                                         size_t(b.cbase_total) + 1)) {
+                            recs.clear();
+                            return;
+                        }
+                    }
                     const FreqRec* hr = static_cast<const FreqRec*>(pb->host);
                     recs.assign(hr, hr + nf);
                     break;
@@ -4071,7 +4108,7 @@ struct Miner {
         // unsharded, large batches: the child class of each member slot comes from the kids
         // CSR on the device (k_child_of); sharded runs keep only their share of the
         // children, so the host builds the table
-        const bool dev_child_of = comm == nullptr && child_of_device(b.cbase_total);
+        const bool dev_child_of = comm == nullptr && !b.dev_order && child_of_device(b.cbase_total);
         RawVec<uint32_t>& child_of = child_of_s;
         if (!dev_child_of && !(b.defer_children && b.child_of_pre)) child_of.assign(b.cbase_total, kNone);
         uint64_t total = 0;
