@@ -3993,23 +3993,40 @@ struct Miner {
     bool defer_ok(Batch& b, const FreqRec* R, uint64_t nfreq, const RawVec<DRow>& rows) {
         b.defer_children = false;
         if (comm || b.claim_key >= 0 || nfreq == 0 || defer_env() == 0) return false;
+        // the rows' sums over host-thread slices of the records (a slice takes the rows that start
+        // in it, whole; SIGN-shaped batches hold millions of records)
+        const int64_t nthr = nfreq >= par_min() ? host_threads() : 1;
+        std::vector<uint64_t> sl(size_t(nthr) * 3, 0);  // need, ent, nkept per slice
+        const size_t eb = entry_bytes();
+        par_slices(nthr, int64_t(nfreq), [&](int64_t t, int64_t q0, int64_t q1) {
+            uint64_t q = uint64_t(q0), need = 0, ent = 0, nkept = 0;
+            while (q0 > 0 && q < uint64_t(q1) && R[q].row == R[q - 1].row) ++q;  // (a row that started before)
+            while (q < uint64_t(q1)) {
+                const uint32_t row = R[q].row;
+                uint64_t q2 = q, sup = 0;
+                uint32_t maxcid = 0;
+                while (q2 < nfreq && R[q2].row == row) {
+                    maxcid = std::max(maxcid, R[q2].cid);
+                    sup += R[q2].sup;
+                    ++q2;
+                }
+                if (!(q2 - q == 1 && (R[q].slot & 1u) == kItm)) {
+                    const uint64_t D = 2ull * ((maxcid >> 1) + 1);
+                    need += sup * eb + D * D * 4;
+                    ent += sup;
+                    ++nkept;
+                }
+                q = q2;
+            }
+            sl[size_t(t) * 3] = need;
+            sl[size_t(t) * 3 + 1] = ent;
+            sl[size_t(t) * 3 + 2] = nkept;
+        });
         uint64_t need = 0, ent = 0, nkept = 0;
-        for (uint64_t q = 0; q < nfreq;) {
-            const uint32_t row = R[q].row;
-            uint64_t q2 = q, sup = 0;
-            uint32_t maxcid = 0;
-            while (q2 < nfreq && R[q2].row == row) {
-                maxcid = std::max(maxcid, R[q2].cid);
-                sup += R[q2].sup;
-                ++q2;
-            }
-            if (!(q2 - q == 1 && (R[q].slot & 1u) == kItm)) {
-                const uint64_t D = 2ull * ((maxcid >> 1) + 1);
-                need += sup * entry_bytes() + D * D * 4;
-                ent += sup;
-                ++nkept;
-            }
-            q = q2;
+        for (int64_t t = 0; t < nthr; ++t) {
+            need += sl[size_t(t) * 3];
+            ent += sl[size_t(t) * 3 + 1];
+            nkept += sl[size_t(t) * 3 + 2];
         }
         if (need > budget || ent > (uint64_t(1) << 31) || nkept == 0) return false;
         b.children.clear();
