@@ -3234,9 +3234,9 @@ struct Miner {
         return true;
     }
     // FSM_DEVORDER=0: a batch's records ordered on the host (A/B)
-    static bool devorder_env() {
-        static const bool on = [] { const char* v = std::getenv("FSM_DEVORDER"); return !(v && v[0] == '0'); }();
-        return on;
+    static bool devorder_env() {  // (read per batch: the tests switch it within one process)
+        const char* v = std::getenv("FSM_DEVORDER");
+        return !(v && v[0] == '0');
     }
     // A batch's nrec frequent records (unordered, mapped pinned memory pb) ordered on the device
     // with the kid table [koff: nko | kslot | kcid] and the child-class table (k_rk_*), written
@@ -4040,9 +4040,9 @@ struct Miner {
         return true;
     }
     // FSM_EMIT_DEFER=0: children built before the emit launch (A/B)
-    static int defer_env() {
-        static const int v = [] { const char* e = std::getenv("FSM_EMIT_DEFER"); return e && e[0] == '0' ? 0 : 1; }();
-        return v;
+    static int defer_env() {  // (read per batch: the tests switch it within one process)
+        const char* e = std::getenv("FSM_EMIT_DEFER");
+        return e && e[0] == '0' ? 0 : 1;
     }
 
     // groups of children [a, z) that fit the frontier budget, appended to b.groups

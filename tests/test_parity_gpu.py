@@ -424,7 +424,8 @@ def _wide_runs_db(seed=5, n=600):
     return gen.DataSet(np.array(so, dtype=np.int64), np.array(tk, dtype=np.int64), "wide-runs")
 
 
-@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some", "chunk", "host-child-of", "device-child-of", "host-kids"])
+@pytest.mark.parametrize("path", ["onepass", "overflow-all", "overflow-some", "chunk", "host-child-of", "device-child-of", "host-kids",
+                                  "host-order", "no-defer"])
 @pytest.mark.parametrize("shape", ["quest", "sign", "bible", "wide"])
 def test_emit_paths_agree(eng, path, shape, monkeypatch):
     """Child-run emission: the window kernel k_emit2 (W = 1: runs of <= 64
@@ -432,7 +433,10 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
     kernel k_emit1 (FSM_EMIT_PATH=chunk; every W), and their overflow paths
     (records capped at 0 / 17 per wave, so waves join again while writing)
     give the oracle's patterns and joins; so do both builds of the child class
-    table (FSM_CHILD_OF=host, or device: k_child_flag / scan / k_child_of)."""
+    table (FSM_CHILD_OF=host, or device: k_child_flag / scan / k_child_of), and
+    both orderings of a one-group batch's records (default: on the device, k_rk_*;
+    FSM_DEVORDER=0: on the host) with the children built after the emit launch or,
+    FSM_EMIT_DEFER=0, before it."""
     from oracle import oracle
     from tools import gen
     if path == "overflow-all":
@@ -447,6 +451,10 @@ def test_emit_paths_agree(eng, path, shape, monkeypatch):
         monkeypatch.setenv("FSM_CHILD_OF", "device")
     elif path == "host-kids":  # the kid table from the host records (default: k_freq_write + k_kid_off)
         monkeypatch.setenv("FSM_KIDS", "host")
+    elif path == "host-order":
+        monkeypatch.setenv("FSM_DEVORDER", "0")
+    elif path == "no-defer":
+        monkeypatch.setenv("FSM_EMIT_DEFER", "0")
     ds, sup, o = shape_case(shape)
     pats, meta, st = gpu_spade(eng, None, sup, tokens=ds)
     assert pats == o["patterns"] and st["joins"] == o["joins"]
