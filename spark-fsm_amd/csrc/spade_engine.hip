@@ -1654,15 +1654,23 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, RootRef rr, co
 // the partner's masks at their known slab slots (no search), after the eid-range
 // overlap test on the lohi words it already holds.
 #ifndef FSM_E2_RANGE
-#define FSM_E2_RANGE 128
+#define FSM_E2_RANGE 192
+#endif
+#ifndef FSM_E2_RANGE_ROOT
+#define FSM_E2_RANGE_ROOT 128
 #endif
 #ifndef FSM_E2_CAP
 #define FSM_E2_CAP 192
 #endif
 constexpr int kE2Block = 256;                   // 4 waves
 constexpr uint32_t kE2Waves = kE2Block / 64;
-constexpr uint32_t kE2Range = FSM_E2_RANGE;     // entries per wave range (runs starting in it)
-constexpr uint32_t kE2Own = kE2Range + 64;      // owner slots per wave (a run may end 63 past the range)
+// entries per wave range (runs starting in it; a multiple of 64): the DB-direct root's rows are
+// short runs of one class, best at 128; a lattice batch's at 192 (round 6: rocprof per kernel,
+// root 0.55 vs 0.60 ms, lattice 0.41 vs 0.32 ms per D1M mine)
+static_assert(FSM_E2_RANGE % 64 == 0 && FSM_E2_RANGE_ROOT % 64 == 0, "k_emit2 wave ranges are whole lane steps");
+template <bool kRoot> constexpr uint32_t e2_range() { return kRoot ? FSM_E2_RANGE_ROOT : FSM_E2_RANGE; }
+// owner slots per wave (a run may end 63 past the range)
+template <bool kRoot> constexpr uint32_t e2_own() { return e2_range<kRoot>() + 64; }
 constexpr uint32_t kE2Cap = FSM_E2_CAP;         // LDS join records per wave
 
 template <int W, bool kRoot>
@@ -1678,6 +1686,7 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                                                     uint32_t rcap, uint32_t* __restrict__ longl,
                                                     uint32_t* __restrict__ nlong) {
     __shared__ uint32_t r_f[kE2Waves][kE2Cap], r_q[kE2Waves][kE2Cap], r_ek[kE2Waves][kE2Cap];
+    constexpr uint32_t kE2Range = e2_range<kRoot>(), kE2Own = e2_own<kRoot>();
     __shared__ uint32_t i_n[kE2Waves][kE2Own], i_off[kE2Waves][kE2Own], i_cc[kE2Waves][kE2Own], i_lt[kE2Waves][kE2Own];
     __shared__ uint32_t w_tot[kE2Waves];
     __shared__ unsigned long long b_base;
@@ -4252,7 +4261,7 @@ struct Miner {
             if ((W == 1 || W == 2 || W == 4 || W == 8) && emit_window()) {
                 // windows of whole runs in registers; the runs of more than 64 entries go to
                 // k_emit1's run list (device-side count: no host round trip)
-                const uint64_t ce = uint64_t(kE2Waves) * kE2Range;
+                const uint64_t ce = uint64_t(kE2Waves) * (rootdb ? e2_range<true>() : e2_range<false>());
                 const unsigned g2 = unsigned(std::min<uint64_t>((Eg + ce - 1) / ce, emit_grid_cap()));
                 d_long.alloc(std::max<uint64_t>(Eg / 65 + 1, 1) * 4);
 #define FSM_EMIT2(WW, RT)                                                                                       \
