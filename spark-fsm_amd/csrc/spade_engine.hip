@@ -1910,7 +1910,12 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
 // by shuffle.  Runs longer than 64 entries are counted thread-per-entry.
 // W > 1 (up to 8 words): equality tests read both masks at their slab slots after
 // the eid-range overlap test (as k_emit2).
-constexpr uint32_t kC2Range = 128;  // entries per wave range (runs starting in it)
+#ifndef FSM_C2_RANGE
+#define FSM_C2_RANGE 256
+#endif
+// entries per wave range (runs starting in it; round 6, rocprof per D1M mine: 64 0.88 ms,
+// 128 0.57-0.60, 256 0.54-0.55, 384 / 512 0.55)
+constexpr uint32_t kC2Range = FSM_C2_RANGE;
 
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_count2(uint32_t E, const uint32_t* __restrict__ cid,
