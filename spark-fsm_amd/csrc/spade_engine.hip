@@ -1662,19 +1662,27 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, RootRef rr, co
 #ifndef FSM_E2_CAP
 #define FSM_E2_CAP 192
 #endif
-constexpr int kE2Block = 256;                   // 4 waves
-constexpr uint32_t kE2Waves = kE2Block / 64;
+#ifndef FSM_E2_BLOCK
+#define FSM_E2_BLOCK 512
+#endif
+#ifndef FSM_E2_BLOCK_ROOT
+#define FSM_E2_BLOCK_ROOT 256
+#endif
+// threads per block, by kind (round 6, rocprof per D1M mine: the root 0.56 ms at 256 vs 0.61 at
+// 512; W = 1 lattice batches 0.32 at 256 vs 0.29 at 512; 128 is slower for both; BIBLE's W = 8
+// batches are slower at 512: 256 kept there)
+template <bool kRoot, int W> constexpr int e2_block() { return kRoot || W != 1 ? FSM_E2_BLOCK_ROOT : FSM_E2_BLOCK; }
 // entries per wave range (runs starting in it; a multiple of 64): the DB-direct root's rows are
-// short runs of one class, best at 128; a lattice batch's at 192 (round 6: rocprof per kernel,
-// root 0.55 vs 0.60 ms, lattice 0.41 vs 0.32 ms per D1M mine)
+// short runs of one class, best at 128; a W = 1 lattice batch's at 192 (round 6: rocprof per
+// kernel, root 0.55 vs 0.60 ms, lattice 0.41 vs 0.32 ms per D1M mine); W > 1 keeps 128
 static_assert(FSM_E2_RANGE % 64 == 0 && FSM_E2_RANGE_ROOT % 64 == 0, "k_emit2 wave ranges are whole lane steps");
-template <bool kRoot> constexpr uint32_t e2_range() { return kRoot ? FSM_E2_RANGE_ROOT : FSM_E2_RANGE; }
+template <bool kRoot, int W> constexpr uint32_t e2_range() { return kRoot || W != 1 ? FSM_E2_RANGE_ROOT : FSM_E2_RANGE; }
 // owner slots per wave (a run may end 63 past the range)
-template <bool kRoot> constexpr uint32_t e2_own() { return e2_range<kRoot>() + 64; }
+template <bool kRoot, int W> constexpr uint32_t e2_own() { return e2_range<kRoot, W>() + 64; }
 constexpr uint32_t kE2Cap = FSM_E2_CAP;         // LDS join records per wave
 
 template <int W, bool kRoot>
-__global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, const uint32_t* __restrict__ cid,
+__global__ __launch_bounds__((e2_block<kRoot, W>())) void k_emit2(uint32_t E, RootRef rr, const uint32_t* __restrict__ cid,
                                                     const DClass* __restrict__ cls, const uint32_t* __restrict__ mem,
                                                     const uint32_t* __restrict__ lohi, const uint32_t* __restrict__ pos,
                                                     const uint64_t* __restrict__ mask,
@@ -1685,8 +1693,9 @@ __global__ __launch_bounds__(kE2Block) void k_emit2(uint32_t E, RootRef rr, cons
                                                     unsigned long long* __restrict__ cursor, SlabPtrs o, uint64_t cap,
                                                     uint32_t rcap, uint32_t* __restrict__ longl,
                                                     uint32_t* __restrict__ nlong) {
+    constexpr uint32_t kE2Waves = uint32_t(e2_block<kRoot, W>()) / 64;
     __shared__ uint32_t r_f[kE2Waves][kE2Cap], r_q[kE2Waves][kE2Cap], r_ek[kE2Waves][kE2Cap];
-    constexpr uint32_t kE2Range = e2_range<kRoot>(), kE2Own = e2_own<kRoot>();
+    constexpr uint32_t kE2Range = e2_range<kRoot, W>(), kE2Own = e2_own<kRoot, W>();
     __shared__ uint32_t i_n[kE2Waves][kE2Own], i_off[kE2Waves][kE2Own], i_cc[kE2Waves][kE2Own], i_lt[kE2Waves][kE2Own];
     __shared__ uint32_t w_tot[kE2Waves];
     __shared__ unsigned long long b_base;
@@ -4266,11 +4275,13 @@ struct Miner {
             if ((W == 1 || W == 2 || W == 4 || W == 8) && emit_window()) {
                 // windows of whole runs in registers; the runs of more than 64 entries go to
                 // k_emit1's run list (device-side count: no host round trip)
-                const uint64_t ce = uint64_t(kE2Waves) * (rootdb ? e2_range<true>() : e2_range<false>());
-                const unsigned g2 = unsigned(std::min<uint64_t>((Eg + ce - 1) / ce, emit_grid_cap()));
+                // (grid: the entries over one block's wave ranges, per kernel kind, capped)
                 d_long.alloc(std::max<uint64_t>(Eg / 65 + 1, 1) * 4);
 #define FSM_EMIT2(WW, RT)                                                                                       \
-    hipLaunchKernelGGL((k_emit2<WW, RT>), dim3(g2), dim3(kE2Block), 0, s, uint32_t(Eg), rr, sp.cid,                  \
+    hipLaunchKernelGGL((k_emit2<WW, RT>), dim3(unsigned(std::min<uint64_t>(                                         \
+                           (Eg + uint64_t(e2_block<RT, WW>() / 64) * e2_range<RT, WW>() - 1) /                     \
+                           (uint64_t(e2_block<RT, WW>() / 64) * e2_range<RT, WW>()), emit_grid_cap()))),           \
+                       dim3(e2_block<RT, WW>()), 0, s, uint32_t(Eg), rr, sp.cid,                                     \
                        b.d_cls.as<DClass>(), sp.mem, sp.lohi, sp.pos, sp.mask, b.kid_off, b.kid_slot, b.kid_cid,   \
                        cof, reinterpret_cast<unsigned long long*>(cursor), op, nb.slab.cap, emit2_cap(),   \
                        d_long.as<uint32_t>(), reinterpret_cast<uint32_t*>(cursor + 8));               \
