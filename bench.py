@@ -375,6 +375,13 @@ def main():
     # over the launches of the last step); the same time over the kernel's own slab bytes
     # (24-B entries: cid, mem, lohi, pos + mask) is `roofline_slab`
     dom = max(ks, key=lambda k: k["ms"])
+    # (the dominant kernel is k_emit or the root F2's k_f2_tri, named k_f2_keys in the table: their
+    # times are within a few percent since round 6, so the line also carries k_emit's own object)
+    dom_basis = ("SURVEY §8(d) F2 unit: 8 B per root (item, sid) entry read per F2 pass"
+                 if dom["name"] in ROOT_F2_KERNELS else
+                 "SURVEY §8(d): one 12-B (sid u32, eid mask u64) id-list entry per parent entry "
+                 "read and per child entry written (4 + 8W B for W mask words)")
+    emit = next((k for k in ks if k["name"] == "k_emit"), None)
     achieved = (dom["survey_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
     achieved_slab = (dom["alg_bytes"] / 1e9) / (dom["ms"] / 1000.0) if dom["ms"] > 0 else 0.0
     traffic = pmc_traffic(dom["name"])  # per step
@@ -408,9 +415,17 @@ def main():
                      "traffic_per_step": traffic,
                      "traffic_basis": "HBM bytes per launch (average over the step's launches) = "
                                       "(2 x FETCH_SIZE + WRITE_SIZE) / launches from the committed PMC passes",
-                     "bytes_basis": "SURVEY §8(d): one 12-B (sid u32, eid mask u64) id-list entry per parent entry "
-                                    "read and per child entry written (4 + 8W B for W mask words)",
+                     "bytes_basis": dom_basis,
                      "traffic_source": PMC_FILE if traffic is not None else None},
+        "roofline_k_emit": None if emit is None or emit["ms"] <= 0 else {
+            "bound": "hbm", "kernel": "k_emit", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "kernel_ms_per_step": emit["ms"], "launches_per_step": emit["launches"],
+            "alg_bytes_per_step": emit["survey_bytes"],
+            "achieved": (emit["survey_bytes"] / 1e9) / (emit["ms"] / 1000.0),
+            "frac": ((emit["survey_bytes"] / 1e9) / (emit["ms"] / 1000.0)) / HBM_PEAK_GBS,
+            "traffic_per_step": pmc_traffic("k_emit"),
+            "bytes_basis": "SURVEY §8(d): one 12-B (sid u32, eid mask u64) id-list entry per parent entry "
+                           "read and per child entry written (4 + 8W B for W mask words)"},
         "roofline_slab": {"bound": "hbm", "achieved": achieved_slab, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": achieved_slab / HBM_PEAK_GBS, "kernel": dom["name"],
                           "alg_bytes_per_step": dom["alg_bytes"],
