@@ -1671,12 +1671,23 @@ __global__ __launch_bounds__(kEmitBlock) void k_emit1(uint32_t E, RootRef rr, co
 // threads per block, by kind (round 6, rocprof per D1M mine: the root 0.56 ms at 256 vs 0.61 at
 // 512; W = 1 lattice batches 0.32 at 256 vs 0.29 at 512; 128 is slower for both; BIBLE's W = 8
 // batches are slower at 512: 256 kept there)
-template <bool kRoot, int W> constexpr int e2_block() { return kRoot || W != 1 ? FSM_E2_BLOCK_ROOT : FSM_E2_BLOCK; }
+#ifndef FSM_E2_BLOCK_W
+#define FSM_E2_BLOCK_W FSM_E2_BLOCK_ROOT
+#endif
+#ifndef FSM_E2_RANGE_W
+#define FSM_E2_RANGE_W 64  // W > 1 lattice batches (BIBLE k_emit2<8>: 64 -6 % vs 128, 192 +6 %; rocprof)
+#endif
+template <bool kRoot, int W> constexpr int e2_block() {
+    return kRoot ? FSM_E2_BLOCK_ROOT : (W != 1 ? FSM_E2_BLOCK_W : FSM_E2_BLOCK);
+}
 // entries per wave range (runs starting in it; a multiple of 64): the DB-direct root's rows are
 // short runs of one class, best at 128; a W = 1 lattice batch's at 192 (round 6: rocprof per
-// kernel, root 0.55 vs 0.60 ms, lattice 0.41 vs 0.32 ms per D1M mine); W > 1 keeps 128
+// kernel, root 0.55 vs 0.60 ms, lattice 0.41 vs 0.32 ms per D1M mine); W > 1 lattice batches 64
 static_assert(FSM_E2_RANGE % 64 == 0 && FSM_E2_RANGE_ROOT % 64 == 0, "k_emit2 wave ranges are whole lane steps");
-template <bool kRoot, int W> constexpr uint32_t e2_range() { return kRoot || W != 1 ? FSM_E2_RANGE_ROOT : FSM_E2_RANGE; }
+static_assert(FSM_E2_RANGE_W % 64 == 0, "k_emit2 wave ranges are whole lane steps");
+template <bool kRoot, int W> constexpr uint32_t e2_range() {
+    return kRoot ? FSM_E2_RANGE_ROOT : (W != 1 ? FSM_E2_RANGE_W : FSM_E2_RANGE);
+}
 // owner slots per wave (a run may end 63 past the range)
 template <bool kRoot, int W> constexpr uint32_t e2_own() { return e2_range<kRoot, W>() + 64; }
 constexpr uint32_t kE2Cap = FSM_E2_CAP;         // LDS join records per wave
@@ -2760,7 +2771,10 @@ struct Miner {
         const uint64_t G64 = (b.n_cnt + kGroupCounters - 1) >> kGroupShift;
         if (G64 == 0 || G64 > kMaxGroups) return false;
         const uint32_t G = uint32_t(G64), E = uint32_t(b.E);
-        const uint32_t nblk = uint32_t(std::min<uint64_t>(kF2MaxBlocks, std::max<uint64_t>(1, (b.E + 8191) / 8192)));
+#ifndef FSM_CK_EPB
+#define FSM_CK_EPB 8192
+#endif
+        const uint32_t nblk = uint32_t(std::min<uint64_t>(kF2MaxBlocks, std::max<uint64_t>(1, (b.E + FSM_CK_EPB - 1) / FSM_CK_EPB)));
         const uint32_t epb = (E + nblk - 1) / nblk;
         const uint64_t nd = uint64_t(G) * nblk;
         const SlabPtrs sp = b.slab.ptrs();
